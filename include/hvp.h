@@ -1,0 +1,153 @@
+/*
+ * hvp.h -- C ABI of libhvpsolve.so, the MI355X batched hybrid-MPC (MLD MIQP) solver.
+ *
+ * This is the drop-in boundary for the reference's per-timestep local MIQP solve:
+ *
+ *   reference call site                                   replaced by
+ *   ----------------------------------------------------  ----------------------------------
+ *   MpcMld.__init__(system, N, thread_limit,               hvp_create()   (model build, once)
+ *     constrain_first_state=False)  [EXT dmpcpwa]
+ *     called from fleet_decent_mld.py:46-48
+ *   LocalMpcMld.setup_cost_and_constraints                 hvp_problem + HVP_ROLE_* flags
+ *     fleet_decent_mld.py:61-208
+ *   LocalMpcMld.set_leader_x / set_x_front / set_x_back    the params block of each instance
+ *     fleet_decent_mld.py:210-223
+ *   MpcMld.solve_mpc(state) -> gp.Model.optimize()         hvp_solve_batch() (B instances at once)
+ *     [EXT], called via MldAgent.get_control at
+ *     fleet_decent_mld.py:316
+ *   gurobi Status / Runtime / NodeCount / NumBinVars       status_out / timing / nodes_out / 7N
+ *     read at fleet_decent_mld.py:336-337, mpcs/mpc_gear.py:119
+ *
+ * Conventions
+ *   - Plain C types only; every array is caller-owned.  hvp_solve_batch takes DEVICE pointers
+ *     (e.g. torch tensors on the GPU) and is asynchronous on `stream` (a hipStream_t, NULL =
+ *     the null stream); hvp_solve_batch_host takes host pointers and is synchronous.
+ *   - Return value: 0 = ok, < 0 = error (HVP_E_*); the message is kept per thread and read
+ *     with hvp_last_error().  No exception crosses the ABI.
+ *   - One handle per host thread / stream; handles are independent.
+ *   - All arithmetic is IEEE float64.  Region indices are 0-based; gears are the 1-based
+ *     labels given in hvp_system.gear (PwaGearVehicle: 1,2,3,4,4,5,6).
+ */
+#ifndef HVP_H
+#define HVP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HVP_ABI_VERSION 1
+#define HVP_MAX_REGIONS 8
+#define HVP_MAX_N 8 /* horizon supported by the enumeration path */
+
+/* Discrete-time PWA model of one vehicle, velocity-partitioned (the form every system dict of
+ * models.py:370-492 has): region r holds for vlo[r] <= v <= vhi[r] (closed; overlapping
+ * boundaries are feasible for both regions, as in the MLD big-M model) and then
+ *     p+ = p + ts * v,        v+ = a[r] * v + b[r] * u + c[r].
+ * hvp/tables.py builds it from the reference's {S,R,T,A,B,c,D,E,F,G} dict and rejects any dict
+ * that is not of that form. */
+typedef struct hvp_system {
+    int32_t n_regions;
+    int32_t gear[HVP_MAX_REGIONS]; /* gear label of each region                       */
+    int32_t pad_;
+    double ts;                     /* Ad[0][1]                                          */
+    double a[HVP_MAX_REGIONS];     /* Ad[1][1]                                          */
+    double b[HVP_MAX_REGIONS];     /* Bd[1][0]  (> 0)                                   */
+    double c[HVP_MAX_REGIONS];     /* cd[1][0]                                          */
+    double vlo[HVP_MAX_REGIONS];   /* region velocity interval (+-1e300 = unbounded)    */
+    double vhi[HVP_MAX_REGIONS];
+    double pmin, pmax, vmin, vmax; /* D x <= E, applied for k = 1..N                    */
+    double umin, umax;             /* F u <= G, applied for k = 0..N-1                  */
+} hvp_system;
+
+/* Cost and constraint constants shared by every local MPC of one controller
+ * (misc/common_controller_params.py:14-23, fleet_decent_mld.py:61-208). */
+typedef struct hvp_problem {
+    int32_t N;              /* prediction horizon (2..HVP_MAX_N)                      */
+    int32_t quadratic_cost; /* 1 = min_2_norm (only form supported on the GPU)         */
+    double Qx[4];           /* 2x2 row-major state-tracking weight                     */
+    double Qu;              /* control weight                                          */
+    double Qdu;             /* control-variation weight                                */
+    double w;               /* slack weight                                            */
+    double a_acc, a_dec;    /* acceleration limits (per unit of ts_acc)                */
+    double ts_acc;          /* Params.ts used in the accel rows                        */
+    double d_safe;          /* safe distance                                           */
+    double accel_tightening;
+    double spacing_d0;      /* spacing(x) = [-d0 - t0 * v, 0]                          */
+    double spacing_t0;
+    int32_t max_iter;       /* IPM iteration cap per candidate (<=0: default 60)       */
+    int32_t pad_;
+    double tol;             /* relative IPM tolerance (<=0: default 1e-10)             */
+} hvp_problem;
+
+/* Role of one local MPC (is_front / is_trailer / is_leader / real_vehicle_as_reference). */
+enum {
+    HVP_ROLE_SAFE_FRONT = 1,     /* not is_front : p_k - s_f,k <= pf_k - d_safe, s_f >= 0  */
+    HVP_ROLE_SAFE_BACK = 2,      /* not is_trailer: p_k + s_b,k >= pb_k + d_safe, s_b >= 0 */
+    HVP_ROLE_TRACK_FRONT = 4,    /* not is_front and not is_leader                         */
+    HVP_ROLE_TRACK_BACK = 8,     /* not is_trailer and not is_leader                       */
+    HVP_ROLE_TRACK_LEADER = 16,  /* is_leader                                              */
+    HVP_ROLE_LEADER_SPACING = 32 /* is_leader and real_vehicle_as_reference                */
+};
+
+/* Per-instance status (Gurobi Status 2 <-> HVP_OPTIMAL). */
+enum {
+    HVP_OPTIMAL = 0,
+    HVP_INFEASIBLE = 1,      /* no region sequence is feasible                          */
+    HVP_MAXITER = 2,         /* no candidate converged within max_iter                  */
+    HVP_OVERFLOW = 3         /* candidate workspace exhausted (raise hvp_reserve)        */
+};
+
+/* Error codes. */
+enum {
+    HVP_OK = 0,
+    HVP_E_ARG = -1,
+    HVP_E_HIP = -2,
+    HVP_E_UNSUPPORTED = -3,
+    HVP_E_NOMEM = -4
+};
+
+/* Instance parameter block, stride hvp_params_stride(N) doubles:
+ *   [0..1]                x0 = (p0, v0)                      (solve_mpc(state))
+ *   [2 .. 2+2(N+1))       x_front (2, N+1) row-major          (set_x_front)
+ *   next 2(N+1)           x_back  (2, N+1) row-major          (set_x_back)
+ *   next 2(N+1)           leader_x (2, N+1) row-major         (set_leader_x)
+ * Blocks a role does not use are ignored. */
+static inline int hvp_params_stride(int N) { return 2 + 6 * (N + 1); }
+
+typedef struct hvp_handle hvp_handle;
+
+typedef struct hvp_stats {
+    int64_t n_instances;    /* instances in the last solve                            */
+    int64_t n_candidates;   /* region sequences (QPs) solved in the last solve         */
+    int64_t ipm_iterations; /* sum of IPM iterations over those QPs                    */
+    int64_t capacity;       /* candidate workspace                                     */
+    double last_ms;         /* device time of the last solve (event-timed), ms         */
+} hvp_stats;
+
+int hvp_create(hvp_handle** out, const hvp_problem* problem, const hvp_system* systems,
+               int n_systems, int device);
+int hvp_reserve(hvp_handle* h, int max_batch, int64_t candidate_capacity);
+/* Device-pointer entry point (async on stream).  Outputs may be NULL except cost/status. */
+int hvp_solve_batch(hvp_handle* h, int B, const int32_t* sys, const int32_t* role,
+                    const double* params, double* u_out, double* x_out, int8_t* region_out,
+                    int8_t* gear_out, double* cost_out, int32_t* status_out,
+                    int32_t* nodes_out, int32_t* iters_out, void* stream);
+/* Host-pointer entry point (copies in, solves, copies out, synchronises). */
+int hvp_solve_batch_host(hvp_handle* h, int B, const int32_t* sys, const int32_t* role,
+                         const double* params, double* u_out, double* x_out,
+                         int8_t* region_out, int8_t* gear_out, double* cost_out,
+                         int32_t* status_out, int32_t* nodes_out, int32_t* iters_out);
+int hvp_sync(hvp_handle* h, void* stream);
+int hvp_get_stats(hvp_handle* h, hvp_stats* out); /* synchronises the handle's last stream */
+void hvp_destroy(hvp_handle* h);
+int hvp_last_error(char* buf, size_t len);
+int hvp_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HVP_H */

@@ -1,0 +1,886 @@
+/*
+ * hvp_oracle.c -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the reference's local hybrid-MPC solve, used as the parity checker for
+ * libhvpsolve.so (tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg are the
+ * only code allowed to load it).  It is never part of the product path.
+ *
+ * What it restates (reference file:line; [EXT] = dmpcpwa/gurobipy, absent from the container,
+ * behaviour inferred from the call sites -- see DESIGN.md "Oracle"):
+ *   - MLD model of MpcMld [EXT] as used by LocalMpcMld (fleet_decent_mld.py:46-48,
+ *     constrain_first_state=False): x(2,N+1), u(1,N); D x_k <= E for k = 1..N; F u_k <= G for
+ *     k = 0..N-1; one region per step with S_r x_k + R_r u_k <= T_r (closed regions, exact MLD,
+ *     i.e. no strictness epsilon) and x_{k+1} = A_r x_k + B_r u_k + c_r; x_0 = state (IC).
+ *   - cost / constraints of LocalMpcMld.setup_cost_and_constraints (fleet_decent_mld.py:61-208):
+ *     front/back/leader tracking with the spacing policy (misc/spacing_policy.py:14-37),
+ *     Q_u u^2, Q_du (du)^2, w (s_f + s_b); accel rows with tightening (:172-188); soft safe
+ *     distance rows (:190-208); s >= 0 and s == 0 for the front / trailer vehicle (:100-105).
+ *     min_2_norm (x' Q x) or min_1_norm (sum_i Q_ii |x_i|, diagonal Q) [EXT].
+ *   - MpcMld.solve_mpc -> Gurobi MIQP optimum [EXT]: restated as  min over region sequences
+ *     sigma of the convex QP with sigma fixed (exact: the MLD big-M model with delta fixed IS
+ *     that QP).  Sequences are enumerated depth-first in lexicographic order; a sequence is
+ *     kept when the velocity constraints admit a trajectory, decided per step by an exact 2-D
+ *     vertex enumeration of the (v_k, v_{k+1}) polygon.  Ties (costs within 1e-9 relative)
+ *     go to the lexicographically smallest sequence.
+ *
+ * Independent of the product kernel on purpose: the QP here is posed in the full (x, u, s)
+ * space with the dynamics as equality constraints and assembled term by term from the
+ * reference's expressions; it is solved by a dense Mehrotra primal-dual interior point method
+ * with LU-factored KKT systems, then polished on the identified active set and certified by
+ * its KKT conditions.  The product condenses to velocity space and runs a structured IPM.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define OR_MAX_N 16
+#define OR_MAX_REG 8
+#define OR_MAX_NZ 200
+#define OR_MAX_EQ 40
+#define OR_MAX_M 420
+#define OR_MAX_KKT (OR_MAX_NZ + OR_MAX_EQ + OR_MAX_M)
+#define OR_BIG 1e6
+
+/* ------------------------------------------------------------------ model description */
+typedef struct {
+    int nreg, nsr, nd, nf;
+    double S[OR_MAX_REG][4][2], R[OR_MAX_REG][4], T[OR_MAX_REG][4];
+    double A[OR_MAX_REG][2][2], B[OR_MAX_REG][2], c[OR_MAX_REG][2];
+    double D[8][2], E[8], F[4], G[4];
+} or_model;
+
+typedef struct {
+    int N;
+    int quadratic;
+    double Qx[2][2], Qu, Qdu, w, a_acc, a_dec, ts, d_safe, tight, d0, t0;
+    int role; /* HVP_ROLE_* bits, see include/hvp.h */
+} or_cfg;
+
+enum { R_SF = 1, R_SB = 2, R_TF = 4, R_TB = 8, R_TL = 16, R_LSP = 32 };
+
+/* ------------------------------------------------------------------ linear expressions */
+typedef struct {
+    int n;
+    int idx[8];
+    double cf[8];
+    double cst;
+} lin;
+
+static lin lin_const(double c) { lin e; e.n = 0; e.cst = c; return e; }
+static void lin_add(lin* e, int idx, double cf) {
+    if (cf == 0.0) return;
+    for (int i = 0; i < e->n; ++i)
+        if (e->idx[i] == idx) { e->cf[i] += cf; return; }
+    e->idx[e->n] = idx; e->cf[e->n] = cf; e->n++;
+}
+static lin lin_axpy(double a, const lin* x, const lin* y) { /* a*x + y */
+    lin r = *y;
+    for (int i = 0; i < x->n; ++i) lin_add(&r, x->idx[i], a * x->cf[i]);
+    r.cst += a * x->cst;
+    return r;
+}
+
+/* ------------------------------------------------------------------ QP container */
+typedef struct {
+    int nz, neq, m;
+    double P[OR_MAX_NZ][OR_MAX_NZ];
+    double q[OR_MAX_NZ];
+    double r0;
+    double Aeq[OR_MAX_EQ][OR_MAX_NZ], beq[OR_MAX_EQ];
+    double G[OR_MAX_M][OR_MAX_NZ], h[OR_MAX_M];
+    int infeasible_const; /* a variable-free row was violated */
+} or_qp;
+
+static void qp_add_prod(or_qp* qp, double wgt, const lin* a, const lin* b) { /* wgt * a * b */
+    for (int i = 0; i < a->n; ++i)
+        for (int j = 0; j < b->n; ++j) {
+            double v = wgt * a->cf[i] * b->cf[j];
+            qp->P[a->idx[i]][b->idx[j]] += v;
+            qp->P[b->idx[j]][a->idx[i]] += v;
+        }
+    for (int i = 0; i < a->n; ++i) qp->q[a->idx[i]] += wgt * a->cf[i] * b->cst;
+    for (int j = 0; j < b->n; ++j) qp->q[b->idx[j]] += wgt * b->cf[j] * a->cst;
+    qp->r0 += wgt * a->cst * b->cst;
+}
+static void qp_add_lin(or_qp* qp, const lin* a) {
+    for (int i = 0; i < a->n; ++i) qp->q[a->idx[i]] += a->cf[i];
+    qp->r0 += a->cst;
+}
+static void qp_add_le(or_qp* qp, const lin* e, double rhs) { /* e <= rhs */
+    if (e->n == 0) {
+        if (e->cst > rhs + 1e-9 * (1.0 + fabs(rhs))) qp->infeasible_const = 1;
+        return;
+    }
+    int r = qp->m++;
+    memset(qp->G[r], 0, sizeof(double) * OR_MAX_NZ);
+    for (int i = 0; i < e->n; ++i) qp->G[r][e->idx[i]] += e->cf[i];
+    qp->h[r] = rhs - e->cst;
+}
+static void qp_add_eq(or_qp* qp, const lin* e, double rhs) { /* e == rhs */
+    int r = qp->neq++;
+    memset(qp->Aeq[r], 0, sizeof(double) * OR_MAX_NZ);
+    for (int i = 0; i < e->n; ++i) qp->Aeq[r][e->idx[i]] += e->cf[i];
+    qp->beq[r] = rhs - e->cst;
+}
+
+/* ------------------------------------------------------------------ problem assembly */
+typedef struct {
+    int N, nx_idx, nu_idx, nsf_idx, nsb_idx, naux;
+    const double *x0, *xf, *xb, *xl; /* (2, N+1) row-major */
+} or_layout;
+
+/* state component i of x_k as an expression (x_0 is the fixed initial state) */
+static lin X(const or_layout* L, int k, int i) {
+    if (k == 0) return lin_const(L->x0[i]);
+    lin e = lin_const(0.0);
+    lin_add(&e, L->nx_idx + 2 * (k - 1) + i, 1.0);
+    return e;
+}
+static lin U(const or_layout* L, int k) {
+    lin e = lin_const(0.0);
+    lin_add(&e, L->nu_idx + k, 1.0);
+    return e;
+}
+static double par(const double* M, int N, int i, int k) { return M[i * (N + 1) + k]; }
+
+/* sum_ij Q_ij e_i e_j  (min_2_norm)  or  sum_i Q_ii |e_i|  (min_1_norm, via aux >= +-Q_ii e_i) */
+static void add_norm(or_qp* qp, or_layout* L, const or_cfg* cf, const lin e[2], const double Q[2][2],
+                     int dim) {
+    if (cf->quadratic) {
+        for (int i = 0; i < dim; ++i)
+            for (int j = 0; j < dim; ++j)
+                if (Q[i][j] != 0.0) qp_add_prod(qp, Q[i][j], &e[i], &e[j]);
+        return;
+    }
+    for (int i = 0; i < dim; ++i) {
+        int a = L->nsb_idx + L->naux++;
+        lin y = lin_const(0.0);
+        lin_add(&y, a, 1.0);
+        lin pos = lin_axpy(Q[i][i], &e[i], &(lin){.n = 0, .cst = 0.0}); /* Q_ii e_i */
+        lin t1 = lin_axpy(-1.0, &y, &pos);                          /* Q e - y <= 0 */
+        qp_add_le(qp, &t1, 0.0);
+        lin neg = lin_axpy(-1.0, &pos, &(lin){.n = 0, .cst = 0.0});
+        lin t2 = lin_axpy(-1.0, &y, &neg); /* -Q e - y <= 0 */
+        qp_add_le(qp, &t2, 0.0);
+        qp_add_lin(qp, &y);
+    }
+}
+
+/* Builds the fixed-sigma QP. Returns number of variables (0 on layout overflow). */
+static int build_qp(or_qp* qp, const or_model* md, const or_cfg* cf, const int* sigma, const double* x0,
+                    const double* xf, const double* xb, const double* xl) {
+    const int N = cf->N;
+    or_layout L;
+    L.N = N; L.x0 = x0; L.xf = xf; L.xb = xb; L.xl = xl;
+    L.nx_idx = 0;
+    L.nu_idx = 2 * N;
+    int nz = 3 * N;
+    L.nsf_idx = nz;
+    if (cf->role & R_SF) nz += N + 1;
+    int sb0 = nz;
+    if (cf->role & R_SB) nz += N + 1;
+    L.nsb_idx = nz; /* aux (L1) variables are appended after the slacks */
+    L.naux = 0;
+    int aux_needed = cf->quadratic ? 0 : (N + 1) * 2 * 3 + N * 2;
+    if (nz + aux_needed > OR_MAX_NZ) return 0;
+    memset(qp->P, 0, sizeof(qp->P));
+    memset(qp->q, 0, sizeof(qp->q));
+    qp->r0 = 0.0; qp->neq = 0; qp->m = 0; qp->infeasible_const = 0;
+
+    /* dynamics of the selected region (MLD with delta fixed) */
+    for (int k = 0; k < N; ++k) {
+        int r = sigma[k];
+        for (int i = 0; i < 2; ++i) {
+            lin e = X(&L, k + 1, i);
+            for (int j = 0; j < 2; ++j) { lin xj = X(&L, k, j); e = lin_axpy(-md->A[r][i][j], &xj, &e); }
+            lin uk = U(&L, k);
+            e = lin_axpy(-md->B[r][i], &uk, &e);
+            qp_add_eq(qp, &e, md->c[r][i]);
+        }
+    }
+    /* region rows S x_k + R u_k <= T (k = 0..N-1) */
+    for (int k = 0; k < N; ++k) {
+        int r = sigma[k];
+        for (int row = 0; row < md->nsr; ++row) {
+            lin e = lin_const(0.0);
+            for (int j = 0; j < 2; ++j) { lin xj = X(&L, k, j); e = lin_axpy(md->S[r][row][j], &xj, &e); }
+            lin uk = U(&L, k);
+            e = lin_axpy(md->R[r][row], &uk, &e);
+            qp_add_le(qp, &e, md->T[r][row]);
+        }
+    }
+    /* state box k = 1..N, input box k = 0..N-1 */
+    for (int k = 1; k <= N; ++k)
+        for (int row = 0; row < md->nd; ++row) {
+            lin e = lin_const(0.0);
+            for (int j = 0; j < 2; ++j) { lin xj = X(&L, k, j); e = lin_axpy(md->D[row][j], &xj, &e); }
+            qp_add_le(qp, &e, md->E[row]);
+        }
+    for (int k = 0; k < N; ++k)
+        for (int row = 0; row < md->nf; ++row) {
+            lin uk = U(&L, k);
+            lin e = lin_axpy(md->F[row], &uk, &(lin){.n = 0, .cst = 0.0});
+            qp_add_le(qp, &e, md->G[row]);
+        }
+    /* acceleration rows: a_dec*ts <= v_{k+1}-v_k - k*tight ; v_{k+1}-v_k <= a_acc*ts - k*tight */
+    for (int k = 0; k < N; ++k) {
+        lin v1 = X(&L, k + 1, 1), v0 = X(&L, k, 1);
+        lin dv = lin_axpy(-1.0, &v0, &v1);
+        lin ndv = lin_axpy(-1.0, &dv, &(lin){.n = 0, .cst = 0.0});
+        qp_add_le(qp, &ndv, -(cf->a_dec * cf->ts) - k * cf->tight);
+        qp_add_le(qp, &dv, cf->a_acc * cf->ts - k * cf->tight);
+    }
+    /* slacks: s >= 0 and the soft safe-distance rows */
+    for (int k = 0; k <= N; ++k) {
+        lin pk = X(&L, k, 0);
+        if (cf->role & R_SF) {
+            lin s = lin_const(0.0);
+            lin_add(&s, L.nsf_idx + k, 1.0);
+            lin ns = lin_axpy(-1.0, &s, &(lin){.n = 0, .cst = 0.0});
+            qp_add_le(qp, &ns, 0.0);
+            lin e = lin_axpy(-1.0, &s, &pk); /* p_k - s_f <= pf_k - d_safe */
+            qp_add_le(qp, &e, par(xf, N, 0, k) - cf->d_safe);
+            lin ws = lin_axpy(cf->w, &s, &(lin){.n = 0, .cst = 0.0});
+            qp_add_lin(qp, &ws);
+        }
+        if (cf->role & R_SB) {
+            lin s = lin_const(0.0);
+            lin_add(&s, sb0 + k, 1.0);
+            lin ns = lin_axpy(-1.0, &s, &(lin){.n = 0, .cst = 0.0});
+            qp_add_le(qp, &ns, 0.0);
+            lin e = lin_axpy(-1.0, &pk, &ns); /* -p_k - s_b <= -(pb_k + d_safe) */
+            qp_add_le(qp, &e, -(par(xb, N, 0, k) + cf->d_safe));
+            lin ws = lin_axpy(cf->w, &s, &(lin){.n = 0, .cst = 0.0});
+            qp_add_lin(qp, &ws);
+        }
+    }
+    /* tracking costs, k = 0..N */
+    for (int k = 0; k <= N; ++k) {
+        lin p = X(&L, k, 0), v = X(&L, k, 1);
+        lin e[2];
+        if (cf->role & R_TF) { /* x_k - xf_k - spacing(x_k) ; spacing(x) = [-d0 - t0 v, 0] */
+            e[0] = lin_axpy(cf->t0, &v, &p);
+            e[0].cst += cf->d0 - par(xf, N, 0, k);
+            e[1] = v; e[1].cst -= par(xf, N, 1, k);
+            add_norm(qp, &L, cf, e, cf->Qx, 2);
+        }
+        if (cf->role & R_TB) { /* xb_k - x_k - spacing(xb_k) */
+            double pb = par(xb, N, 0, k), vb = par(xb, N, 1, k);
+            e[0] = lin_axpy(-1.0, &p, &(lin){.n = 0, .cst = pb + cf->d0 + cf->t0 * vb});
+            e[1] = lin_axpy(-1.0, &v, &(lin){.n = 0, .cst = vb});
+            add_norm(qp, &L, cf, e, cf->Qx, 2);
+        }
+        if (cf->role & R_TL) { /* x_k - xl_k (- spacing(x_k) for real_vehicle_as_reference) */
+            if (cf->role & R_LSP) { e[0] = lin_axpy(cf->t0, &v, &p); e[0].cst += cf->d0; }
+            else e[0] = p;
+            e[0].cst -= par(xl, N, 0, k);
+            e[1] = v; e[1].cst -= par(xl, N, 1, k);
+            add_norm(qp, &L, cf, e, cf->Qx, 2);
+        }
+    }
+    /* control effort and variation */
+    double Qu[2][2] = {{cf->Qu, 0}, {0, 0}}, Qdu[2][2] = {{cf->Qdu, 0}, {0, 0}};
+    for (int k = 0; k < N; ++k) {
+        lin e[2]; e[0] = U(&L, k); e[1] = lin_const(0.0);
+        add_norm(qp, &L, cf, e, Qu, 1);
+    }
+    for (int k = 0; k + 1 < N; ++k) {
+        lin e[2];
+        lin a = U(&L, k + 1), b = U(&L, k);
+        e[0] = lin_axpy(-1.0, &b, &a); e[1] = lin_const(0.0);
+        if (cf->Qdu != 0.0) add_norm(qp, &L, cf, e, Qdu, 1);
+    }
+    qp->nz = L.nsb_idx + L.naux;
+    return qp->nz;
+}
+
+/* ------------------------------------------------------------------ dense LU */
+static int lu_factor(int n, double* M, int ld, int* piv) {
+    double big = 0.0;
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) big = fmax(big, fabs(M[i * ld + j]));
+    if (big == 0.0) return -1;
+    for (int k = 0; k < n; ++k) {
+        int p = k;
+        double mx = fabs(M[k * ld + k]);
+        for (int i = k + 1; i < n; ++i)
+            if (fabs(M[i * ld + k]) > mx) { mx = fabs(M[i * ld + k]); p = i; }
+        piv[k] = p;
+        if (mx <= 1e-300 * big || !isfinite(mx)) return -1;
+        if (p != k)
+            for (int j = 0; j < n; ++j) { double t = M[k * ld + j]; M[k * ld + j] = M[p * ld + j]; M[p * ld + j] = t; }
+        double inv = 1.0 / M[k * ld + k];
+        for (int i = k + 1; i < n; ++i) {
+            double f = M[i * ld + k] * inv;
+            M[i * ld + k] = f;
+            if (f != 0.0)
+                for (int j = k + 1; j < n; ++j) M[i * ld + j] -= f * M[k * ld + j];
+        }
+    }
+    return 0;
+}
+static void lu_solve(int n, const double* M, int ld, const int* piv, double* x) {
+    for (int k = 0; k < n; ++k)
+        if (piv[k] != k) { double t = x[k]; x[k] = x[piv[k]]; x[piv[k]] = t; }
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < i; ++j) x[i] -= M[i * ld + j] * x[j];
+    for (int i = n - 1; i >= 0; --i) {
+        for (int j = i + 1; j < n; ++j) x[i] -= M[i * ld + j] * x[j];
+        x[i] /= M[i * ld + i];
+    }
+}
+
+/* ------------------------------------------------------------------ IPM */
+typedef struct {
+    double z[OR_MAX_NZ], nu[OR_MAX_EQ], lam[OR_MAX_M], t[OR_MAX_M];
+    double K[OR_MAX_KKT * OR_MAX_KKT];
+    int piv[OR_MAX_KKT];
+    double rhs[OR_MAX_KKT];
+} or_work;
+
+static double vmaxabs(const double* v, int n) {
+    double m = 0.0;
+    for (int i = 0; i < n; ++i) m = fmax(m, fabs(v[i]));
+    return m;
+}
+static double objective(const or_qp* qp, const double* z) {
+    double f = qp->r0;
+    for (int i = 0; i < qp->nz; ++i) {
+        double pz = 0.0;
+        for (int j = 0; j < qp->nz; ++j) pz += qp->P[i][j] * z[j];
+        f += 0.5 * z[i] * pz + qp->q[i] * z[i];
+    }
+    return f;
+}
+
+/* Solves the KKT system [[P + G'DG, A'], [A, 0]] [dz; dnu] = rhs ; factorises once per call. */
+static int ipm_factor(const or_qp* qp, or_work* w, const double* d) {
+    const int nz = qp->nz, ne = qp->neq, n = nz + ne, ld = n;
+    for (int i = 0; i < nz; ++i)
+        for (int j = 0; j < nz; ++j) w->K[i * ld + j] = qp->P[i][j];
+    for (int r = 0; r < qp->m; ++r) {
+        const double* g = qp->G[r];
+        for (int i = 0; i < nz; ++i) {
+            if (g[i] == 0.0) continue;
+            double gi = d[r] * g[i];
+            for (int j = 0; j < nz; ++j) w->K[i * ld + j] += gi * g[j];
+        }
+    }
+    for (int e = 0; e < ne; ++e)
+        for (int j = 0; j < nz; ++j) { w->K[(nz + e) * ld + j] = qp->Aeq[e][j]; w->K[j * ld + nz + e] = qp->Aeq[e][j]; }
+    for (int e = 0; e < ne; ++e)
+        for (int f = 0; f < ne; ++f) w->K[(nz + e) * ld + nz + f] = 0.0;
+    return lu_factor(n, w->K, ld, w->piv);
+}
+
+/* Newton direction for residuals (rd, re, rp, rc). Outputs dz, dnu, dlam, dt. */
+static void ipm_direction(const or_qp* qp, or_work* w, const double* d, const double* rd, const double* re,
+                          const double* rp, const double* rc, double* dz, double* dnu, double* dl, double* dt) {
+    const int nz = qp->nz, ne = qp->neq, m = qp->m;
+    double tmp[OR_MAX_M];
+    for (int i = 0; i < m; ++i) tmp[i] = d[i] * rp[i] - rc[i] / w->t[i];
+    for (int j = 0; j < nz; ++j) {
+        double s = -rd[j];
+        for (int i = 0; i < m; ++i) s -= qp->G[i][j] * tmp[i];
+        w->rhs[j] = s;
+    }
+    for (int e = 0; e < ne; ++e) w->rhs[nz + e] = -re[e];
+    lu_solve(nz + ne, w->K, nz + ne, w->piv, w->rhs);
+    for (int j = 0; j < nz; ++j) dz[j] = w->rhs[j];
+    for (int e = 0; e < ne; ++e) dnu[e] = w->rhs[nz + e];
+    for (int i = 0; i < m; ++i) {
+        double gdz = 0.0;
+        for (int j = 0; j < nz; ++j) gdz += qp->G[i][j] * dz[j];
+        dl[i] = d[i] * (gdz + rp[i]) - rc[i] / w->t[i];
+        dt[i] = -rp[i] - gdz;
+    }
+}
+
+static double max_step(const double* v, const double* dv, int n) {
+    double a = 1.0;
+    for (int i = 0; i < n; ++i)
+        if (dv[i] < 0.0) a = fmin(a, -v[i] / dv[i]);
+    return a;
+}
+
+typedef struct {
+    int converged, certified, iters;
+    double obj;
+} or_result;
+
+static void residuals(const or_qp* qp, const or_work* w, double* rd, double* re, double* rp) {
+    for (int j = 0; j < qp->nz; ++j) {
+        double s = qp->q[j];
+        for (int k = 0; k < qp->nz; ++k) s += qp->P[j][k] * w->z[k];
+        for (int e = 0; e < qp->neq; ++e) s += qp->Aeq[e][j] * w->nu[e];
+        for (int i = 0; i < qp->m; ++i) s += qp->G[i][j] * w->lam[i];
+        rd[j] = s;
+    }
+    for (int e = 0; e < qp->neq; ++e) {
+        double s = -qp->beq[e];
+        for (int j = 0; j < qp->nz; ++j) s += qp->Aeq[e][j] * w->z[j];
+        re[e] = s;
+    }
+    for (int i = 0; i < qp->m; ++i) {
+        double s = w->t[i] - qp->h[i];
+        for (int j = 0; j < qp->nz; ++j) s += qp->G[i][j] * w->z[j];
+        rp[i] = s;
+    }
+}
+
+/* Active-set polish: solve the equality QP on {rows with lam > t} and accept it when it is
+ * primal and dual feasible -- then it satisfies the KKT conditions exactly (certificate). */
+static int polish(const or_qp* qp, or_work* w) {
+    const int nz = qp->nz, ne = qp->neq, m = qp->m;
+    int act[OR_MAX_M], na = 0;
+    for (int i = 0; i < m; ++i)
+        if (w->lam[i] > w->t[i]) act[na++] = i;
+    const int n = nz + ne + na, ld = n;
+    if (n > OR_MAX_KKT) return 0;
+    double* K = w->K;
+    memset(K, 0, sizeof(double) * (size_t)n * (size_t)n);
+    for (int i = 0; i < nz; ++i)
+        for (int j = 0; j < nz; ++j) K[i * ld + j] = qp->P[i][j];
+    for (int e = 0; e < ne; ++e)
+        for (int j = 0; j < nz; ++j) { K[(nz + e) * ld + j] = qp->Aeq[e][j]; K[j * ld + nz + e] = qp->Aeq[e][j]; }
+    for (int a = 0; a < na; ++a)
+        for (int j = 0; j < nz; ++j) { K[(nz + ne + a) * ld + j] = qp->G[act[a]][j]; K[j * ld + nz + ne + a] = qp->G[act[a]][j]; }
+    double* x = w->rhs;
+    for (int j = 0; j < nz; ++j) x[j] = -qp->q[j];
+    for (int e = 0; e < ne; ++e) x[nz + e] = qp->beq[e];
+    for (int a = 0; a < na; ++a) x[nz + ne + a] = qp->h[act[a]];
+    if (lu_factor(n, K, ld, w->piv) != 0) return 0;
+    lu_solve(n, K, ld, w->piv, x);
+    double scale_h = 1.0 + vmaxabs(qp->h, m), scale_l = 1.0 + vmaxabs(w->lam, m);
+    for (int a = 0; a < na; ++a)
+        if (x[nz + ne + a] < -1e-9 * scale_l) return 0;
+    for (int i = 0; i < m; ++i) {
+        double g = 0.0;
+        for (int j = 0; j < nz; ++j) g += qp->G[i][j] * x[j];
+        if (g > qp->h[i] + 1e-9 * scale_h) return 0;
+    }
+    for (int j = 0; j < nz; ++j) w->z[j] = x[j];
+    return 1;
+}
+
+static or_result ipm_solve(const or_qp* qp, or_work* w, int maxit) {
+    const int nz = qp->nz, ne = qp->neq, m = qp->m;
+    double rd[OR_MAX_NZ], re[OR_MAX_EQ], rp[OR_MAX_M], rc[OR_MAX_M], d[OR_MAX_M];
+    double dz[OR_MAX_NZ], dnu[OR_MAX_EQ], dl[OR_MAX_M], dt[OR_MAX_M];
+    double dza[OR_MAX_NZ], dnua[OR_MAX_EQ], dla[OR_MAX_M], dta[OR_MAX_M];
+    or_result res = {0, 0, 0, 0.0};
+    /* initial point (CVXOPT-style): minimise 1/2 z'Pz + q'z + 1/2 |h - Gz|^2 s.t. Az = b, then
+     * t = h - Gz, lam = -t, both shifted into the interior (Mehrotra's heuristic). */
+    for (int i = 0; i < m; ++i) d[i] = 1.0;
+    if (ipm_factor(qp, w, d) != 0) return res;
+    for (int j = 0; j < nz; ++j) {
+        double s = -qp->q[j];
+        for (int i = 0; i < m; ++i) s += qp->G[i][j] * qp->h[i];
+        w->rhs[j] = s;
+    }
+    for (int e = 0; e < ne; ++e) w->rhs[nz + e] = qp->beq[e];
+    lu_solve(nz + ne, w->K, nz + ne, w->piv, w->rhs);
+    for (int j = 0; j < nz; ++j) w->z[j] = w->rhs[j];
+    for (int e = 0; e < ne; ++e) w->nu[e] = w->rhs[nz + e];
+    {
+        double tmin = INFINITY, lmin = INFINITY;
+        for (int i = 0; i < m; ++i) {
+            double g = 0.0;
+            for (int j = 0; j < nz; ++j) g += qp->G[i][j] * w->z[j];
+            w->t[i] = qp->h[i] - g;
+            w->lam[i] = -w->t[i];
+            tmin = fmin(tmin, w->t[i]);
+            lmin = fmin(lmin, w->lam[i]);
+        }
+        double st = fmax(-1.5 * tmin, 0.0), sl = fmax(-1.5 * lmin, 0.0), tl = 0.0, ssum = 0.0, lsum = 0.0;
+        for (int i = 0; i < m; ++i) { w->t[i] += st; w->lam[i] += sl; }
+        for (int i = 0; i < m; ++i) { tl += w->t[i] * w->lam[i]; ssum += w->t[i]; lsum += w->lam[i]; }
+        double dt0 = lsum > 0 ? 0.5 * tl / lsum : 1.0, dl0 = ssum > 0 ? 0.5 * tl / ssum : 1.0;
+        for (int i = 0; i < m; ++i) {
+            w->t[i] += dt0; w->lam[i] += dl0;
+            if (!(w->t[i] > 0)) w->t[i] = 1.0;
+            if (!(w->lam[i] > 0)) w->lam[i] = 1.0;
+        }
+    }
+    double sq = 1.0 + vmaxabs(qp->q, nz), sb = 1.0 + vmaxabs(qp->beq, ne), sh = 1.0 + vmaxabs(qp->h, m);
+    for (int it = 0; it < maxit; ++it) {
+        residuals(qp, w, rd, re, rp);
+        double mu = 0.0;
+        for (int i = 0; i < m; ++i) mu += w->lam[i] * w->t[i];
+        double gap = mu;
+        mu /= (m > 0 ? m : 1);
+        double obj = objective(qp, w->z);
+        res.iters = it;
+        if (vmaxabs(rd, nz) <= 1e-10 * sq && vmaxabs(re, ne) <= 1e-10 * sb && vmaxabs(rp, m) <= 1e-10 * sh &&
+            gap <= 1e-11 * fmax(1.0, fabs(obj))) {
+            res.converged = 1;
+            break;
+        }
+        for (int i = 0; i < m; ++i) d[i] = w->lam[i] / w->t[i];
+        if (ipm_factor(qp, w, d) != 0) break;
+        /* predictor */
+        for (int i = 0; i < m; ++i) rc[i] = w->lam[i] * w->t[i];
+        ipm_direction(qp, w, d, rd, re, rp, rc, dza, dnua, dla, dta);
+        double ap = max_step(w->t, dta, m), ad = max_step(w->lam, dla, m);
+        double alpha = fmin(ap, ad);
+        double mua = 0.0;
+        for (int i = 0; i < m; ++i) mua += (w->lam[i] + alpha * dla[i]) * (w->t[i] + alpha * dta[i]);
+        mua /= (m > 0 ? m : 1);
+        double sigma = mu > 0 ? pow(mua / mu, 3.0) : 0.0;
+        /* corrector */
+        for (int i = 0; i < m; ++i) rc[i] = w->lam[i] * w->t[i] + dla[i] * dta[i] - sigma * mu;
+        ipm_direction(qp, w, d, rd, re, rp, rc, dz, dnu, dl, dt);
+        ap = max_step(w->t, dt, m);
+        ad = max_step(w->lam, dl, m);
+        alpha = fmin(1.0, 0.99 * fmin(ap, ad));
+        for (int j = 0; j < nz; ++j) w->z[j] += alpha * dz[j];
+        for (int e = 0; e < ne; ++e) w->nu[e] += alpha * dnu[e];
+        for (int i = 0; i < m; ++i) { w->lam[i] += alpha * dl[i]; w->t[i] += alpha * dt[i]; }
+        res.iters = it + 1;
+    }
+    if (res.converged) res.certified = polish(qp, w);
+    res.obj = objective(qp, w->z);
+    return res;
+}
+
+/* ------------------------------------------------------------------ sigma enumeration */
+/* velocity interval of a region / the state box from rows acting on v only */
+static int v_interval(const double (*S)[2], const double* T, int nrows, double* lo, double* hi) {
+    *lo = -OR_BIG; *hi = OR_BIG;
+    for (int r = 0; r < nrows; ++r) {
+        if (S[r][0] != 0.0) continue; /* position rows are handled by the QP */
+        double s = S[r][1];
+        if (s > 0) *hi = fmin(*hi, T[r] / s);
+        else if (s < 0) *lo = fmax(*lo, T[r] / s);
+        else if (T[r] < 0) return 0;
+    }
+    return *lo <= *hi;
+}
+
+/* Exact projection onto v' of the polygon {(v, v'): lo<=v<=hi, v' = a v + b u + c for some
+ * u in [ul, uh], dec <= v'-v <= acc, blo <= v' <= bhi} by vertex enumeration. */
+static int next_interval(double lo, double hi, double a, double b, double c, double ul, double uh, double dec,
+                         double acc, double blo, double bhi, double* nlo, double* nhi) {
+    /* half-planes  n0*v + n1*v' <= r */
+    double H[8][3];
+    int nh = 0;
+    double bl = fmin(b * ul, b * uh), bu = fmax(b * ul, b * uh);
+    H[nh][0] = -1; H[nh][1] = 0; H[nh++][2] = -lo;
+    H[nh][0] = 1; H[nh][1] = 0; H[nh++][2] = hi;
+    H[nh][0] = a; H[nh][1] = -1; H[nh++][2] = -(c + bl);  /* v' >= a v + c + bl */
+    H[nh][0] = -a; H[nh][1] = 1; H[nh++][2] = c + bu;     /* v' <= a v + c + bu */
+    H[nh][0] = 1; H[nh][1] = -1; H[nh++][2] = -dec;       /* v' - v >= dec */
+    H[nh][0] = -1; H[nh][1] = 1; H[nh++][2] = acc;        /* v' - v <= acc */
+    H[nh][0] = 0; H[nh][1] = -1; H[nh++][2] = -blo;
+    H[nh][0] = 0; H[nh][1] = 1; H[nh++][2] = bhi;
+    int found = 0;
+    double mn = OR_BIG, mx = -OR_BIG;
+    for (int i = 0; i < nh; ++i)
+        for (int j = i + 1; j < nh; ++j) {
+            double det = H[i][0] * H[j][1] - H[i][1] * H[j][0];
+            if (fabs(det) < 1e-14) continue;
+            double v = (H[i][2] * H[j][1] - H[i][1] * H[j][2]) / det;
+            double vp = (H[i][0] * H[j][2] - H[i][2] * H[j][0]) / det;
+            int ok = 1;
+            for (int k = 0; k < nh && ok; ++k) {
+                double tol = 1e-9 * (1.0 + fabs(H[k][2]));
+                if (H[k][0] * v + H[k][1] * vp > H[k][2] + tol) ok = 0;
+            }
+            if (ok) { found = 1; mn = fmin(mn, vp); mx = fmax(mx, vp); }
+        }
+    if (!found) return 0;
+    *nlo = mn; *nhi = mx;
+    return 1;
+}
+
+typedef struct {
+    double a[OR_MAX_REG], b[OR_MAX_REG], c[OR_MAX_REG], rlo[OR_MAX_REG], rhi[OR_MAX_REG];
+    int rok[OR_MAX_REG];
+    double blo, bhi, ul, uh;
+} or_vmodel;
+
+static int make_vmodel(const or_model* md, or_vmodel* vm) {
+    for (int r = 0; r < md->nreg; ++r) {
+        if (md->A[r][1][0] != 0.0) return -1; /* velocity dynamics must not depend on p */
+        for (int row = 0; row < md->nsr; ++row)
+            if (md->S[r][row][0] != 0.0 || md->R[r][row] != 0.0) return -1;
+        vm->a[r] = md->A[r][1][1]; vm->b[r] = md->B[r][1]; vm->c[r] = md->c[r][1];
+        vm->rok[r] = v_interval((const double(*)[2])md->S[r], md->T[r], md->nsr, &vm->rlo[r], &vm->rhi[r]);
+    }
+    if (!v_interval((const double(*)[2])md->D, md->E, md->nd, &vm->blo, &vm->bhi)) return -1;
+    vm->ul = -OR_BIG; vm->uh = OR_BIG;
+    for (int row = 0; row < md->nf; ++row) {
+        if (md->F[row] > 0) vm->uh = fmin(vm->uh, md->G[row] / md->F[row]);
+        else if (md->F[row] < 0) vm->ul = fmax(vm->ul, md->G[row] / md->F[row]);
+    }
+    return 0;
+}
+
+typedef void (*or_visit)(const int* sigma, void* ctx);
+
+static void dfs(const or_vmodel* vm, int nreg, const or_cfg* cf, int k, double lo, double hi, int* sigma,
+                or_visit visit, void* ctx, int* count) {
+    const int N = cf->N;
+    if (k == N) { (*count)++; if (visit) visit(sigma, ctx); return; }
+    double dec = cf->a_dec * cf->ts + k * cf->tight, acc = cf->a_acc * cf->ts - k * cf->tight;
+    for (int r = 0; r < nreg; ++r) {
+        if (!vm->rok[r]) continue;
+        double ilo = fmax(lo, vm->rlo[r]), ihi = fmin(hi, vm->rhi[r]);
+        if (ilo > ihi + 1e-9 * (1.0 + fabs(ihi))) continue;
+        if (ilo > ihi) ilo = ihi = 0.5 * (ilo + ihi);
+        double nlo, nhi;
+        if (!next_interval(ilo, ihi, vm->a[r], vm->b[r], vm->c[r], vm->ul, vm->uh, dec, acc, vm->blo, vm->bhi,
+                           &nlo, &nhi))
+            continue;
+        sigma[k] = r;
+        dfs(vm, nreg, cf, k + 1, nlo, nhi, sigma, visit, ctx, count);
+    }
+}
+
+/* ------------------------------------------------------------------ public API */
+typedef struct {
+    const or_model* md;
+    const or_cfg* cf;
+    const double *x0, *xf, *xb, *xl;
+    or_qp* qp;
+    or_work* w;
+    int maxit;
+    int n_conv, n_cert, iters;
+    /* every candidate in DFS (= lexicographic) order */
+    int ncand, cap;
+    double* obj;
+    int* sig;
+    unsigned char* cert;
+} or_ctx;
+
+static void visit_qp(const int* sigma, void* vctx) {
+    or_ctx* C = (or_ctx*)vctx;
+    const int N = C->cf->N;
+    if (C->ncand == C->cap) {
+        int nc = C->cap ? 2 * C->cap : 64;
+        C->obj = (double*)realloc(C->obj, sizeof(double) * nc);
+        C->sig = (int*)realloc(C->sig, sizeof(int) * (size_t)nc * N);
+        C->cert = (unsigned char*)realloc(C->cert, (size_t)nc);
+        C->cap = nc;
+    }
+    double obj = INFINITY;
+    int cert = 0;
+    if (build_qp(C->qp, C->md, C->cf, sigma, C->x0, C->xf, C->xb, C->xl) > 0 && !C->qp->infeasible_const) {
+        or_result r = ipm_solve(C->qp, C->w, C->maxit);
+        C->iters += r.iters;
+        if (r.converged) { obj = r.obj; cert = r.certified; C->n_conv++; C->n_cert += cert; }
+    }
+    C->obj[C->ncand] = obj;
+    C->cert[C->ncand] = (unsigned char)cert;
+    memcpy(C->sig + (size_t)C->ncand * N, sigma, sizeof(int) * N);
+    C->ncand++;
+}
+
+/* Winner: the minimum objective; among candidates within 1e-9 relative of it the first in
+ * lexicographic sequence order.  Returns -1 when no candidate converged. */
+static int select_winner(const double* obj, int n) {
+    double best = INFINITY;
+    for (int i = 0; i < n; ++i) best = fmin(best, obj[i]);
+    if (!isfinite(best)) return -1;
+    double tol = 1e-9 * fmax(1.0, fabs(best));
+    for (int i = 0; i < n; ++i)
+        if (obj[i] <= best + tol) return i;
+    return -1;
+}
+
+typedef struct { int* out; int cap, n, N; } or_collect;
+static void collect_visit(const int* s, void* p) {
+    or_collect* c = (or_collect*)p;
+    if (c->out && c->n < c->cap) memcpy(c->out + (size_t)c->n * c->N, s, sizeof(int) * c->N);
+    c->n++;
+}
+
+static int unpack_model(or_model* md, int nreg, int nsr, const double* S, const double* R, const double* T,
+                        const double* A, const double* B, const double* c, int nd, const double* D,
+                        const double* E, int nf, const double* F, const double* G) {
+    if (nreg > OR_MAX_REG || nsr > 4 || nd > 8 || nf > 4) return -1;
+    md->nreg = nreg; md->nsr = nsr; md->nd = nd; md->nf = nf;
+    for (int r = 0; r < nreg; ++r) {
+        for (int i = 0; i < nsr; ++i) {
+            md->S[r][i][0] = S[(r * nsr + i) * 2]; md->S[r][i][1] = S[(r * nsr + i) * 2 + 1];
+            md->R[r][i] = R[r * nsr + i]; md->T[r][i] = T[r * nsr + i];
+        }
+        for (int i = 0; i < 2; ++i) {
+            md->A[r][i][0] = A[r * 4 + i * 2]; md->A[r][i][1] = A[r * 4 + i * 2 + 1];
+            md->B[r][i] = B[r * 2 + i]; md->c[r][i] = c[r * 2 + i];
+        }
+    }
+    for (int i = 0; i < nd; ++i) { md->D[i][0] = D[2 * i]; md->D[i][1] = D[2 * i + 1]; md->E[i] = E[i]; }
+    for (int i = 0; i < nf; ++i) { md->F[i] = F[i]; md->G[i] = G[i]; }
+    return 0;
+}
+
+static void unpack_cfg(or_cfg* cf, int N, int quadratic, int role, const double* p) {
+    /* p = [Qx00 Qx01 Qx10 Qx11 Qu Qdu w a_acc a_dec ts d_safe tight d0 t0] */
+    cf->N = N; cf->quadratic = quadratic; cf->role = role;
+    cf->Qx[0][0] = p[0]; cf->Qx[0][1] = p[1]; cf->Qx[1][0] = p[2]; cf->Qx[1][1] = p[3];
+    cf->Qu = p[4]; cf->Qdu = p[5]; cf->w = p[6]; cf->a_acc = p[7]; cf->a_dec = p[8]; cf->ts = p[9];
+    cf->d_safe = p[10]; cf->tight = p[11]; cf->d0 = p[12]; cf->t0 = p[13];
+}
+
+/* Number of candidate region sequences (DFS order) for one instance; -1 on bad model. */
+int oracle_count_candidates(int N, int nreg, int nsr, const double* S, const double* R, const double* T,
+                            const double* A, const double* B, const double* c, int nd, const double* D,
+                            const double* E, int nf, const double* F, const double* G, const double* cfgp,
+                            const double* x0, int* sigmas_out, int cap) {
+    or_model md;
+    or_cfg cf;
+    or_vmodel vm;
+    if (N > OR_MAX_N || unpack_model(&md, nreg, nsr, S, R, T, A, B, c, nd, D, E, nf, F, G)) return -1;
+    unpack_cfg(&cf, N, 1, 0, cfgp);
+    if (make_vmodel(&md, &vm)) return -1;
+    int sigma[OR_MAX_N], count = 0;
+    or_collect sc = {sigmas_out, cap, 0, N};
+    dfs(&vm, md.nreg, &cf, 0, x0[1], x0[1], sigma, collect_visit, &sc, &count);
+    return count;
+}
+
+/* Solves one local MIQP.  x_out (2, N+1) row-major, u_out (N), sigma_out (N),
+ * info_out = [cost, n_candidates, n_converged, n_certified, best_certified, status, iters].
+ * cand_obj / cand_sigma (optional) receive every candidate's objective (inf = not converged). */
+int oracle_solve_miqp(int N, int nreg, int nsr, const double* S, const double* R, const double* T, const double* A,
+                      const double* B, const double* c, int nd, const double* D, const double* E, int nf,
+                      const double* F, const double* G, const double* cfgp, int quadratic, int role,
+                      const double* x0, const double* xf, const double* xb, const double* xl, int maxit,
+                      double* x_out, double* u_out, int* sigma_out, double* info_out, double* cand_obj,
+                      int* cand_sigma, int cand_cap) {
+    or_model md;
+    or_cfg cf;
+    or_vmodel vm;
+    if (N > OR_MAX_N || unpack_model(&md, nreg, nsr, S, R, T, A, B, c, nd, D, E, nf, F, G)) return -1;
+    unpack_cfg(&cf, N, quadratic, role, cfgp);
+    if (make_vmodel(&md, &vm)) return -2;
+    or_qp* qp = (or_qp*)malloc(sizeof(or_qp));
+    or_work* w = (or_work*)malloc(sizeof(or_work));
+    if (!qp || !w) { free(qp); free(w); return -3; }
+    or_ctx C;
+    memset(&C, 0, sizeof(C));
+    C.md = &md; C.cf = &cf; C.x0 = x0; C.xf = xf; C.xb = xb; C.xl = xl; C.qp = qp; C.w = w;
+    C.maxit = maxit > 0 ? maxit : 200;
+    int sigma[OR_MAX_N], count = 0;
+    dfs(&vm, md.nreg, &cf, 0, x0[1], x0[1], sigma, visit_qp, &C, &count);
+    int win = select_winner(C.obj, C.ncand);
+    int status = win >= 0 ? 0 : (count == 0 ? 1 : 2);
+    int best_cert = 0;
+    double best_obj = INFINITY;
+    if (win >= 0) {
+        /* re-solve the winner to recover its trajectory */
+        const int* ws = C.sig + (size_t)win * N;
+        build_qp(qp, &md, &cf, ws, x0, xf, xb, xl);
+        or_result r = ipm_solve(qp, w, C.maxit);
+        best_obj = r.obj;
+        best_cert = r.certified;
+        for (int i = 0; i < 2; ++i) x_out[i * (N + 1)] = x0[i];
+        for (int k = 1; k <= N; ++k)
+            for (int i = 0; i < 2; ++i) x_out[i * (N + 1) + k] = w->z[2 * (k - 1) + i];
+        for (int k = 0; k < N; ++k) u_out[k] = w->z[2 * N + k];
+        for (int k = 0; k < N; ++k) sigma_out[k] = ws[k];
+    }
+    for (int i = 0; i < C.ncand && i < cand_cap; ++i) {
+        if (cand_obj) cand_obj[i] = C.obj[i];
+        if (cand_sigma) memcpy(cand_sigma + (size_t)i * N, C.sig + (size_t)i * N, sizeof(int) * N);
+    }
+    free(C.obj); free(C.sig); free(C.cert);
+    info_out[0] = best_obj;
+    info_out[1] = count;
+    info_out[2] = C.n_conv;
+    info_out[3] = C.n_cert;
+    info_out[4] = best_cert;
+    info_out[5] = status;
+    info_out[6] = C.iters;
+    free(qp);
+    free(w);
+    return 0;
+}
+
+/* Batch of independent instances sharing one model table set (models indexed per instance).
+ * Model arrays are stacked per system: S[nsys][nreg][nsr][2] etc.  OpenMP over instances. */
+int oracle_solve_batch(int B, int N, int nsys, int nreg, int nsr, const double* S, const double* R,
+                       const double* T, const double* A, const double* B_, const double* c, int nd,
+                       const double* D, const double* E, int nf, const double* F, const double* G,
+                       const double* cfgp, int quadratic, const int* sys, const int* role, const double* params,
+                       int maxit, double* x_out, double* u_out, int* sigma_out, double* info_out, int nthreads) {
+    const int P = 2 + 6 * (N + 1);
+    int err = 0;
+    (void)nsys;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1) reduction(| : err)
+    for (int i = 0; i < B; ++i) {
+        const int s = sys[i];
+        const double* p = params + (size_t)i * P;
+        int rc = oracle_solve_miqp(
+            N, nreg, nsr, S + (size_t)s * nreg * nsr * 2, R + (size_t)s * nreg * nsr, T + (size_t)s * nreg * nsr,
+            A + (size_t)s * nreg * 4, B_ + (size_t)s * nreg * 2, c + (size_t)s * nreg * 2, nd, D + (size_t)s * nd * 2,
+            E + (size_t)s * nd, nf, F + (size_t)s * nf, G + (size_t)s * nf, cfgp, quadratic, role[i], p, p + 2,
+            p + 2 + 2 * (N + 1), p + 2 + 4 * (N + 1), maxit, x_out + (size_t)i * 2 * (N + 1), u_out + (size_t)i * N,
+            sigma_out + (size_t)i * N, info_out + (size_t)i * 7, NULL, NULL, 0);
+        if (rc) err |= 1;
+    }
+    return err ? -1 : 0;
+}
+
+/* Solve ONE fixed-sigma QP (exposed for the tests that cross-check against scipy). */
+int oracle_solve_qp(int N, int nreg, int nsr, const double* S, const double* R, const double* T, const double* A,
+                    const double* B, const double* c, int nd, const double* D, const double* E, int nf,
+                    const double* F, const double* G, const double* cfgp, int quadratic, int role, const int* sigma,
+                    const double* x0, const double* xf, const double* xb, const double* xl, double* z_out,
+                    double* info_out) {
+    or_model md;
+    or_cfg cf;
+    if (N > OR_MAX_N || unpack_model(&md, nreg, nsr, S, R, T, A, B, c, nd, D, E, nf, F, G)) return -1;
+    unpack_cfg(&cf, N, quadratic, role, cfgp);
+    or_qp* qp = (or_qp*)malloc(sizeof(or_qp));
+    or_work* w = (or_work*)malloc(sizeof(or_work));
+    if (!qp || !w) { free(qp); free(w); return -3; }
+    int nz = build_qp(qp, &md, &cf, sigma, x0, xf, xb, xl);
+    or_result r = {0, 0, 0, INFINITY};
+    if (nz > 0 && !qp->infeasible_const) r = ipm_solve(qp, w, 200);
+    if (nz > 0) memcpy(z_out, w->z, sizeof(double) * nz);
+    info_out[0] = r.converged ? r.obj : INFINITY;
+    info_out[1] = r.converged;
+    info_out[2] = r.certified;
+    info_out[3] = r.iters;
+    info_out[4] = nz;
+    info_out[5] = qp->m;
+    info_out[6] = qp->neq;
+    free(qp);
+    free(w);
+    return 0;
+}
+
+/* Dense export of one fixed-sigma QP (tests only): P[nz*nz], q[nz], Aeq[neq*nz], beq, G[m*nz], h,
+ * dims_out = [nz, neq, m, r0, infeasible_const]. Capacity of each buffer given by cap_* . */
+int oracle_export_qp(int N, int nreg, int nsr, const double* S, const double* R, const double* T, const double* A,
+                     const double* B, const double* c, int nd, const double* D, const double* E, int nf,
+                     const double* F, const double* G, const double* cfgp, int quadratic, int role, const int* sigma,
+                     const double* x0, const double* xf, const double* xb, const double* xl, double* P_out,
+                     double* q_out, double* A_out, double* b_out, double* G_out, double* h_out, double* dims_out) {
+    or_model md;
+    or_cfg cf;
+    if (N > OR_MAX_N || unpack_model(&md, nreg, nsr, S, R, T, A, B, c, nd, D, E, nf, F, G)) return -1;
+    unpack_cfg(&cf, N, quadratic, role, cfgp);
+    or_qp* qp = (or_qp*)malloc(sizeof(or_qp));
+    if (!qp) return -3;
+    int nz = build_qp(qp, &md, &cf, sigma, x0, xf, xb, xl);
+    for (int i = 0; i < nz; ++i) {
+        q_out[i] = qp->q[i];
+        for (int j = 0; j < nz; ++j) P_out[i * nz + j] = qp->P[i][j];
+    }
+    for (int e = 0; e < qp->neq; ++e) {
+        b_out[e] = qp->beq[e];
+        for (int j = 0; j < nz; ++j) A_out[e * nz + j] = qp->Aeq[e][j];
+    }
+    for (int r = 0; r < qp->m; ++r) {
+        h_out[r] = qp->h[r];
+        for (int j = 0; j < nz; ++j) G_out[r * nz + j] = qp->G[r][j];
+    }
+    dims_out[0] = nz; dims_out[1] = qp->neq; dims_out[2] = qp->m; dims_out[3] = qp->r0;
+    dims_out[4] = qp->infeasible_const;
+    free(qp);
+    return 0;
+}

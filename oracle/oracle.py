@@ -1,0 +1,355 @@
+"""TEST INFRASTRUCTURE ONLY -- Python face of the CPU parity oracle (oracle/hvp_oracle.c).
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may
+import this module; the product (``hybrid-vehicle-platoon_amd/``) never does.
+
+Besides the ctypes binding it restates, independently of the product package, the pieces of
+the reference the checker needs as inputs:
+
+* ``gear_pwa_system(m, ts)``   <- models.py:390-492 (PwaGearVehicle.build_gear_pwa_system)
+                                  + models.py:370-387 (forward-Euler discretisation)
+* ``friction_pwa_system(m, ts)`` <- models.py:272-332
+* ``env_initial_state(n, seed)`` <- env.py:79-101 with the mpcrl seed derivation
+                                  (SeedSequence(seed).generate_state(1)[0], model_validation.py:76)
+* ``constant_velocity_prediction`` <- fleet_decent_mld.py:421-428
+
+Parity status: pinned to the reference's constants through the known answers listed in
+SURVEY.md 8(c) (discretised tables, seed derivation, env init at seed 0) and, for the MIQP
+layer, cross-checked against HiGHS (scipy.optimize.milp) on the reference's own big-M MLD
+formulation with the L1 cost; the reference solver (Gurobi) itself cannot run here, so the
+quadratic-cost MIQP optimum is "parity unpinned" against Gurobi and certified instead by
+exhaustive sequence enumeration + per-QP KKT certificates.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(_HERE, "liboracle.so")
+_lib = None
+
+# ------------------------------------------------------------------ reference constants
+_B_GEAR = (4057, 2945, 2116, 1607, 1166, 838)
+_VL = (3.94, 5.43, 7.56, 9.96, 13.70, 19.10)
+_VH = (9.46, 13.04, 18.15, 23.90, 32.93, 45.84)
+_CF, _MU, _G = 0.5, 0.01, 9.8
+_VMIN, _VMAX = _VL[0], _VH[-1]
+
+
+def _friction_constants():
+    beta = 3 * _CF * _VMAX**2 / 16
+    alpha = _VMAX / 2
+    c1 = beta / alpha
+    c2 = (_CF * _VMAX**2 - beta) / (_VMAX - alpha)
+    return alpha, c1, c2, beta - alpha * c2
+
+
+def _box():
+    D = np.array([[1.0, 0], [-1, 0], [0, 1], [0, -1]])
+    E = np.array([10000.0, -0.0, _VMAX, -_VMIN])
+    F = np.array([1.0, -1.0])
+    G = np.array([1.0, 1.0])
+    return D, E, F, G
+
+
+def gear_pwa_system(mass: float, ts: float = 1.0) -> dict:
+    """Discrete 7-region gear PWA model as flat arrays (S[r][2][2], T[r][2], A[r][2][2], ...)."""
+    alpha, c1, c2, d = _friction_constants()
+    lim = [(_VH[i] - _VL[i]) / 2 + _VL[i] for i in range(1, 6)]
+    cuts = [lim[0], lim[1], lim[2], alpha, lim[3], lim[4]]
+    S = np.zeros((7, 2, 2))
+    T = np.zeros((7, 2))
+    for r in range(7):
+        if r == 0:
+            S[r] = [[0, 1], [0, 0]]
+            T[r] = [cuts[0], 0]
+        elif r == 6:
+            S[r] = [[0, 0], [0, -1]]
+            T[r] = [0, -cuts[5]]
+        else:
+            S[r] = [[0, 1], [0, -1]]
+            T[r] = [cuts[r], -cuts[r - 1]]
+    gear_of_region = [0, 1, 2, 3, 3, 4, 5]
+    A = np.zeros((7, 2, 2))
+    B = np.zeros((7, 2))
+    c = np.zeros((7, 2))
+    for r in range(7):
+        fr = c2 if r >= 4 else c1
+        A[r] = np.eye(2) + ts * np.array([[0, 1], [0, -fr / mass]])
+        B[r] = ts * np.array([0, _B_GEAR[gear_of_region[r]] / mass])
+        c[r] = ts * np.array([0, -_MU * _G - (d / mass if r >= 4 else 0.0)])
+    D, E, F, G = _box()
+    return dict(S=S, R=np.zeros((7, 2)), T=T, A=A, B=B, c=c, D=D, E=E, F=F, G=G,
+                gear=np.array([1, 2, 3, 4, 4, 5, 6]))
+
+
+def friction_pwa_system(mass: float, ts: float = 1.0) -> dict:
+    alpha, c1, c2, d = _friction_constants()
+    S = np.array([[[0, 1], [0, 0]], [[0, 0], [0, -1]]], dtype=float)
+    T = np.array([[alpha, 0], [0, -alpha]])
+    A = np.stack([np.eye(2) + ts * np.array([[0, 1], [0, -f / mass]]) for f in (c1, c2)])
+    B = np.stack([ts * np.array([0, 1 / mass])] * 2)
+    c = np.stack([ts * np.array([0, -_MU * _G]), ts * np.array([0, -_MU * _G - d / mass])])
+    D, E, F, G = _box()
+    return dict(S=S, R=np.zeros((2, 2)), T=T, A=A, B=B, c=c, D=D, E=E, F=F, G=G, gear=np.array([1, 2]))
+
+
+def env_seed(seed: int) -> int:
+    return int(np.random.SeedSequence(seed).generate_state(1)[0])
+
+
+def env_initial_state(n: int, seed: int) -> np.ndarray:
+    """(2n,) int64 initial state of env.reset for the derived seed of `seed`."""
+    rs = np.random.RandomState(env_seed(seed))
+    vel = [30 * rs.random_sample() + 5 for _ in range(100)]
+    pos = [3000.0]
+    for _ in range(99):
+        pos.append(-100 * rs.random_sample() + pos[-1] - 60)
+    x = np.zeros(2 * n, dtype=np.int64)
+    for i in range(n):
+        p = max(pos)
+        x[2 * i] = p
+        x[2 * i + 1] = vel[i]
+        pos.remove(p)
+    return x
+
+
+def constant_velocity_prediction(p: float, v: float, N: int, ts: float = 1.0) -> np.ndarray:
+    out = np.zeros((2, N + 1))
+    out[:, 0] = (p, v)
+    for k in range(N):
+        out[0, k + 1] = out[0, k] + ts * out[1, k]
+        out[1, k + 1] = out[1, k]
+    return out
+
+
+# ------------------------------------------------------------------ controller constants
+@dataclass
+class Cfg:
+    """Params of misc/common_controller_params.py:14-23 + spacing policy (d0, t0)."""
+
+    Qx: tuple = (1.0, 0.0, 0.0, 0.1)
+    Qu: float = 1.0
+    Qdu: float = 0.0
+    w: float = 1e4
+    a_acc: float = 2.5
+    a_dec: float = -2.0
+    ts: float = 1.0
+    d_safe: float = 25.0
+    tight: float = 0.0
+    d0: float = 50.0
+    t0: float = 0.0
+
+    def vector(self) -> np.ndarray:
+        return np.array(list(self.Qx) + [self.Qu, self.Qdu, self.w, self.a_acc, self.a_dec, self.ts,
+                                         self.d_safe, self.tight, self.d0, self.t0], dtype=np.float64)
+
+
+ROLE_SAFE_FRONT, ROLE_SAFE_BACK, ROLE_TRACK_FRONT, ROLE_TRACK_BACK, ROLE_TRACK_LEADER, ROLE_LEADER_SPACING = (
+    1, 2, 4, 8, 16, 32)
+
+
+def role_bits(i: int, n: int, leader_index: int = 0, real_vehicle_as_reference: bool = False) -> int:
+    """Role of vehicle i as set up in fleet_decent_mld.py:506-518 / :100-153."""
+    is_front, is_trailer, is_leader = i == 0, i == n - 1, i == leader_index
+    r = 0
+    if not is_front:
+        r |= ROLE_SAFE_FRONT
+    if not is_trailer:
+        r |= ROLE_SAFE_BACK
+    if not is_front and not is_leader:
+        r |= ROLE_TRACK_FRONT
+    if not is_trailer and not is_leader:
+        r |= ROLE_TRACK_BACK
+    if is_leader:
+        r |= ROLE_TRACK_LEADER
+        if real_vehicle_as_reference:
+            r |= ROLE_LEADER_SPACING
+    return r
+
+
+# ------------------------------------------------------------------ ctypes binding
+def build(force: bool = False) -> str:
+    if force or not os.path.exists(_LIB) or os.path.getmtime(_LIB) < os.path.getmtime(
+        os.path.join(_HERE, "hvp_oracle.c")
+    ):
+        subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(_LIB)
+        dp = ctypes.POINTER(ctypes.c_double)
+        ip = ctypes.POINTER(ctypes.c_int)
+        c_int = ctypes.c_int
+        model_args = [c_int, c_int, c_int, dp, dp, dp, dp, dp, dp, c_int, dp, dp, c_int, dp, dp]
+        L.oracle_solve_miqp.argtypes = model_args + [dp, c_int, c_int, dp, dp, dp, dp, c_int, dp, dp, ip, dp, dp, ip,
+                                                     c_int]
+        L.oracle_solve_miqp.restype = c_int
+        L.oracle_count_candidates.argtypes = model_args + [dp, dp, ip, c_int]
+        L.oracle_count_candidates.restype = c_int
+        L.oracle_solve_qp.argtypes = model_args + [dp, c_int, c_int, ip, dp, dp, dp, dp, dp, dp]
+        L.oracle_solve_qp.restype = c_int
+        L.oracle_solve_batch.argtypes = [c_int, c_int, c_int, c_int, c_int, dp, dp, dp, dp, dp, dp, c_int, dp, dp,
+                                         c_int, dp, dp, dp, c_int, ip, ip, dp, c_int, dp, dp, ip, dp, c_int]
+        L.oracle_solve_batch.restype = c_int
+        _lib = L
+    return _lib
+
+
+def _d(a) -> ctypes.POINTER(ctypes.c_double):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+def _i(a) -> ctypes.POINTER(ctypes.c_int):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_int))
+
+
+def _model_arrays(sysd: dict):
+    arr = {k: np.ascontiguousarray(np.asarray(sysd[k], dtype=np.float64)) for k in "SRTABcDEFG"}
+    nreg = arr["S"].shape[0]
+    nsr = arr["S"].shape[1]
+    return nreg, nsr, arr
+
+
+def _model_args(sysd: dict):
+    nreg, nsr, a = _model_arrays(sysd)
+    keep = a
+    args = [nreg, nsr, _d(a["S"]), _d(a["R"]), _d(a["T"]), _d(a["A"]), _d(a["B"]), _d(a["c"]),
+            a["D"].shape[0], _d(a["D"]), _d(a["E"]), a["F"].shape[0], _d(a["F"]), _d(a["G"])]
+    return args, keep
+
+
+@dataclass
+class MiqpResult:
+    x: np.ndarray  # (2, N+1)
+    u: np.ndarray  # (N,)
+    sigma: np.ndarray  # (N,) region indices
+    cost: float
+    n_candidates: int
+    n_converged: int
+    n_certified: int
+    best_certified: bool
+    status: int
+    iters: int
+    cand_obj: np.ndarray | None = None
+    cand_sigma: np.ndarray | None = None
+
+
+def solve_miqp(sysd: dict, cfg: Cfg, N: int, role: int, x0, xf, xb, xl, quadratic: bool = True,
+               maxit: int = 200, want_candidates: bool = False) -> MiqpResult:
+    L = lib()
+    args, keep = _model_args(sysd)
+    cv = cfg.vector()
+    f = lambda a: np.ascontiguousarray(np.asarray(a, dtype=np.float64))  # noqa: E731
+    x0, xf, xb, xl = f(x0).ravel(), f(xf), f(xb), f(xl)
+    x_out = np.zeros((2, N + 1))
+    u_out = np.zeros(N)
+    sig = np.zeros(N, dtype=np.int32)
+    info = np.zeros(7)
+    cap = 20000 if want_candidates else 0
+    cobj = np.zeros(max(cap, 1))
+    csig = np.zeros((max(cap, 1), N), dtype=np.int32)
+    rc = L.oracle_solve_miqp(N, *args, _d(cv), int(quadratic), int(role), _d(x0), _d(xf), _d(xb), _d(xl), maxit,
+                             _d(x_out), _d(u_out), _i(sig), _d(info), _d(cobj), _i(csig), cap)
+    del keep
+    if rc != 0:
+        raise RuntimeError(f"oracle_solve_miqp failed ({rc})")
+    n = int(info[1])
+    res = MiqpResult(x_out, u_out, sig, float(info[0]), n, int(info[2]), int(info[3]), bool(info[4]), int(info[5]),
+                     int(info[6]))
+    if want_candidates:
+        res.cand_obj = cobj[:n].copy()
+        res.cand_sigma = csig[:n].copy()
+    return res
+
+
+def candidates(sysd: dict, cfg: Cfg, N: int, x0, cap: int = 200000) -> np.ndarray:
+    L = lib()
+    args, keep = _model_args(sysd)
+    cv = cfg.vector()
+    x0 = np.ascontiguousarray(np.asarray(x0, dtype=np.float64)).ravel()
+    out = np.zeros((cap, N), dtype=np.int32)
+    n = L.oracle_count_candidates(N, *args, _d(cv), _d(x0), _i(out), cap)
+    del keep
+    if n < 0:
+        raise RuntimeError("oracle_count_candidates: unsupported model")
+    return out[: min(n, cap)].copy()
+
+
+def solve_qp(sysd: dict, cfg: Cfg, N: int, role: int, sigma, x0, xf, xb, xl, quadratic: bool = True):
+    """One fixed-sequence QP: returns (objective, converged, certified, z, (nz, m, neq))."""
+    L = lib()
+    args, keep = _model_args(sysd)
+    cv = cfg.vector()
+    f = lambda a: np.ascontiguousarray(np.asarray(a, dtype=np.float64))  # noqa: E731
+    sig = np.ascontiguousarray(np.asarray(sigma, dtype=np.int32))
+    z = np.zeros(256)
+    info = np.zeros(8)
+    L.oracle_solve_qp(N, *args, _d(cv), int(quadratic), int(role), _i(sig), _d(f(x0).ravel()), _d(f(xf)),
+                      _d(f(xb)), _d(f(xl)), _d(z), _d(info))
+    del keep
+    nz = int(info[4])
+    return float(info[0]), bool(info[1]), bool(info[2]), z[:nz].copy(), (nz, int(info[5]), int(info[6]))
+
+
+def solve_batch(systems: list[dict], cfg: Cfg, N: int, sys_idx, roles, params, quadratic: bool = True,
+                maxit: int = 200, nthreads: int = 1):
+    """Batch of instances (params rows laid out as include/hvp.h hvp_params_stride)."""
+    L = lib()
+    nreg = np.asarray(systems[0]["S"]).shape[0]
+    nsr = np.asarray(systems[0]["S"]).shape[1]
+    st = {k: np.ascontiguousarray(np.stack([np.asarray(s[k], dtype=np.float64) for s in systems])) for k in
+          "SRTABcDEFG"}
+    B = len(sys_idx)
+    sys_idx = np.ascontiguousarray(np.asarray(sys_idx, dtype=np.int32))
+    roles = np.ascontiguousarray(np.asarray(roles, dtype=np.int32))
+    params = np.ascontiguousarray(np.asarray(params, dtype=np.float64))
+    cv = cfg.vector()
+    x_out = np.zeros((B, 2, N + 1))
+    u_out = np.zeros((B, N))
+    sig = np.zeros((B, N), dtype=np.int32)
+    info = np.zeros((B, 7))
+    rc = L.oracle_solve_batch(B, N, len(systems), nreg, nsr, _d(st["S"]), _d(st["R"]), _d(st["T"]), _d(st["A"]),
+                              _d(st["B"]), _d(st["c"]), st["D"].shape[1], _d(st["D"]), _d(st["E"]), st["F"].shape[1],
+                              _d(st["F"]), _d(st["G"]), _d(cv), int(quadratic), _i(sys_idx), _i(roles), _d(params),
+                              maxit, _d(x_out), _d(u_out), _i(sig), _d(info), nthreads)
+    if rc != 0:
+        raise RuntimeError("oracle_solve_batch failed")
+    return x_out, u_out, sig, info
+
+
+def export_qp(sysd: dict, cfg: Cfg, N: int, role: int, sigma, x0, xf, xb, xl, quadratic: bool = True):
+    """Dense (P, q, r0, Aeq, beq, G, h) of one fixed-sequence QP, for independent cross-checks."""
+    L = lib()
+    if not hasattr(L, "_export_set"):
+        dp = ctypes.POINTER(ctypes.c_double)
+        ip = ctypes.POINTER(ctypes.c_int)
+        c_int = ctypes.c_int
+        L.oracle_export_qp.argtypes = [c_int, c_int, c_int, dp, dp, dp, dp, dp, dp, c_int, dp, dp, c_int, dp, dp, dp,
+                                       c_int, c_int, ip, dp, dp, dp, dp, dp, dp, dp, dp, dp, dp, dp]
+        L.oracle_export_qp.restype = c_int
+        L._export_set = True
+    args, keep = _model_args(sysd)
+    cv = cfg.vector()
+    f = lambda a: np.ascontiguousarray(np.asarray(a, dtype=np.float64))  # noqa: E731
+    sig = np.ascontiguousarray(np.asarray(sigma, dtype=np.int32))
+    P = np.zeros(200 * 200); q = np.zeros(200); A = np.zeros(40 * 200); b = np.zeros(40)
+    G = np.zeros(420 * 200); h = np.zeros(420); dims = np.zeros(5)
+    rc = L.oracle_export_qp(N, *args, _d(cv), int(quadratic), int(role), _i(sig), _d(f(x0).ravel()), _d(f(xf)),
+                            _d(f(xb)), _d(f(xl)), _d(P), _d(q), _d(A), _d(b), _d(G), _d(h), _d(dims))
+    del keep
+    if rc != 0:
+        raise RuntimeError("export failed")
+    nz, ne, m = int(dims[0]), int(dims[1]), int(dims[2])
+    return (P[: nz * nz].reshape(nz, nz), q[:nz].copy(), float(dims[3]), A[: ne * nz].reshape(ne, nz), b[:ne].copy(),
+            G[: m * nz].reshape(m, nz), h[:m].copy())
