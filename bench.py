@@ -1,0 +1,221 @@
+#!/usr/bin/env python3
+"""Throughput benchmark of the decentralised hybrid-MPC hot path on MI355X.
+
+Metric (BASELINE.json): MPC timesteps/s for whole platoons, decentralised MLD, n = 10, N = 5
+(configs[1]).  One *step* = one pass of the hot path over one batch: every vehicle of
+``--platoons`` platoons (per GPU) solves its local MIQP (fleet_decent_mld.py:314-326) for one
+platoon timestep.  ``value`` = platoon-timesteps solved by all ranks / wall time of the timed
+region (max over ranks).  Inputs are synthetic random-init platoon states (env.py:70-116
+distribution, seed s -> SeedSequence(s) derived env seed), constant-velocity neighbour
+predictions and the constant-velocity leader window, resident in HBM before timing starts.
+
+Multi-GPU: one process per GPU (torch.distributed.run); every rank owns a disjoint range of
+seeds (weak scaling, no collective in the data path -- the platoons are independent); the
+barrier / MAX-reduction only brackets the timing.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "hybrid-vehicle-platoon_amd"))
+
+HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: 8.0 TB/s spec
+FP64_PEAK_TFLOPS = 78.6     # MI355X FP64 vector peak (spec)
+
+
+def dense_qp_bytes(N: int) -> int:
+    """bytes of one dense fixed-sequence QP, 8 (n_w^2 + m n_w + m + n_w)."""
+    nw, m = 3 * N + 2, 14 * N + 4
+    return 8 * (nw * nw + m * nw + m + nw)
+
+
+def instance_io_bytes(N: int) -> int:
+    """params in + u, x, cost out per local MIQP (+ N bytes of sigma)."""
+    return 8 * (2 + 6 * (N + 1) + N + 2 * (N + 1) + 1) + N
+
+
+def make_inputs(seeds, n: int, N: int):
+    """(params, roles, sys) for n-vehicle platoons at t = 0 (vectorised over seeds)."""
+    from hvp.batched import decent_params_from_states
+    from hvp.env import derive_env_seed, initial_platoon_state
+
+    states = np.stack([initial_platoon_state(n, derive_env_seed(int(s))).reshape(-1).astype(np.float64)
+                       for s in seeds])
+    lead = np.stack([3000.0 + 20.0 * np.arange(N + 1), np.full(N + 1, 20.0)])
+    params, roles = decent_params_from_states(states, N, lead)
+    return params, roles
+
+
+def cpu_baseline(n: int, N: int, budget_s: float, threads: int):
+    """The CPU oracle (oracle/hvp_oracle.c, OpenMP over instances) on a bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    sysd = O.gear_pwa_system(800.0)
+    done = 0
+    t0 = time.perf_counter()
+    chunk = max(threads, 1) * 2
+    seed = 10_000_000
+    while time.perf_counter() - t0 < budget_s:
+        params, roles = make_inputs(range(seed, seed + chunk), n, N)
+        seed += chunk
+        O.solve_batch([sysd], O.Cfg(), N, np.zeros(len(roles), np.int32), roles, params, nthreads=threads)
+        done += chunk
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "platoon-timesteps/s", "cores": threads, "kind": "port",
+            "sample": f"{done} platoons x {n} local MIQPs (N={N}) by oracle/hvp_oracle.c, {dt:.1f} s"}
+
+
+def hostref_baseline(n: int, N: int, budget_s: float, threads: int):
+    """The product's lane algorithm compiled for the host cores (extra, fairer CPU number)."""
+    import ctypes
+
+    from hvp import _abi, tables
+    from hvp.models import PwaGearVehicle
+
+    if not os.path.exists(_abi.HOSTREF_PATH):
+        return None
+    L = ctypes.CDLL(_abi.HOSTREF_PATH)
+    veh = PwaGearVehicle(800)
+    S = (_abi.HvpSystem * 1)(tables.system_from_dict(veh.get_discrete_system(1), tables.gears_of(veh)))
+    prob = tables.problem(N)
+    done, seed = 0, 20_000_000
+    chunk = max(threads, 1) * 16
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        params, roles = make_inputs(range(seed, seed + chunk), n, N)
+        seed += chunk
+        B = len(roles)
+        bufs = [np.zeros((B, N)), np.zeros((B, 2, N + 1)), np.zeros((B, N), np.int8), np.zeros(B),
+                np.zeros(B, np.int32), np.zeros(B, np.int32), np.zeros(B, np.int32)]
+        f = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+        L.hvp_hostref_solve_batch(ctypes.byref(prob), S, B, f(np.zeros(B, np.int32)), f(roles),
+                                  f(np.ascontiguousarray(params)), *[f(b) for b in bufs], threads)
+        done += chunk
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "platoon-timesteps/s", "cores": threads,
+            "sample": f"{done} platoons, same lane algorithm built with g++ -O2 -fopenmp"}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--platoons", type=int, default=16384, help="platoons per GPU per step")
+    ap.add_argument("--n", type=int, default=10)
+    ap.add_argument("--N", type=int, default=5)
+    ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-oracle baseline (0 = skip)")
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from hvp import tables
+    from hvp.models import PwaGearVehicle
+    from hvp.solver import BatchSolver
+
+    n, N, S = args.n, args.N, args.platoons
+    veh = PwaGearVehicle(800)
+    system = tables.system_from_dict(veh.get_discrete_system(1), tables.gears_of(veh))
+    solver = BatchSolver(tables.problem(N), [system], device=local)
+    # each rank owns a disjoint seed range: platoons are independent (weak scaling)
+    params, roles = make_inputs(range(rank * S, (rank + 1) * S), n, N)
+    B = len(roles)
+    solver.reserve(B)
+    dev = torch.device("cuda", local)
+    t_params = torch.from_numpy(params).to(dev)
+    t_roles = torch.from_numpy(roles).to(dev)
+    t_sys = torch.zeros(B, dtype=torch.int32, device=dev)
+    out = solver.alloc_outputs(B, dev)
+
+    for _ in range(args.warmup):
+        solver.solve_device(t_sys, t_roles, t_params, out)
+    torch.cuda.synchronize()
+    st0 = solver.stats()
+
+    qp_ms, cand, iters = [], 0, 0
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        solver.solve_device(t_sys, t_roles, t_params, out)
+        s = solver.stats()  # event times of this step (syncs the stream: per-step host sync)
+        qp_ms.append(s.qp_ms)
+        cand += s.n_candidates
+        iters += s.ipm_iterations
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist:
+        tt = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+
+    ok = bool((out["status"] == 0).all().item())
+    steps_total = S * world * args.steps
+    value = steps_total / dt
+    qp_avg_ms = float(np.mean(qp_ms))
+    cand_per_launch = cand / args.steps
+    alg_bytes = cand_per_launch * dense_qp_bytes(N) + B * instance_io_bytes(N)
+    achieved = alg_bytes / (qp_avg_ms * 1e-3) / 1e9
+
+    result = {
+        "metric": "MPC timesteps/sec (whole platoon) at n=10 N=5 decent_mld",
+        "value": value,
+        "unit": "platoon-timesteps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic: env.reset random-init platoon states (seeded), constant-velocity neighbour "
+                "predictions, constant-velocity leader",
+        "config": {"workload": "fleet_decent_mld n=10 N=5 pwa_gear (configs[1])", "n_vehicles": n, "horizon": N,
+                   "platoons_per_gpu": S, "local_miqps_per_step": B * world, "parallelism": f"seeds-sharded x{world}"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "k_qp", "kernel_avg_ms": qp_avg_ms,
+                     "note": "achieved = SURVEY 8(d) dense-QP bytes of the sequences solved per launch / K_qp time; "
+                             "the kernel builds its QPs in registers (FP64-VALU bound), see DESIGN.md"},
+        "candidates_per_step": cand_per_launch,
+        "ipm_iters_per_candidate": iters / max(cand, 1),
+        "all_optimal": ok,
+    }
+    if rank == 0 and not args.no_cpu and args.cpu_budget > 0 and world == 1:
+        threads = min(len(os.sched_getaffinity(0)), 16)
+        result["cpu_baseline"] = cpu_baseline(n, N, args.cpu_budget, threads)
+        hr = hostref_baseline(n, N, min(args.cpu_budget, 10.0), threads)
+        if hr:
+            result["cpu_same_algorithm"] = hr
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,154 @@
+// hvp_hostref.cpp -- TEST-ONLY host build of the lane algorithm in hvp_ipm.h.
+//
+// Compiled with g++ into lib/libhvp_hostref.so and loaded only by tests/ (to exercise the
+// enumeration + per-lane IPM logic on a machine without a GPU) and by bench.py's extra
+// "same algorithm on the host cores" baseline.  The product entry points live in
+// libhvpsolve.so (hvp_kernels.hip) and never call into this library.
+#include <string.h>
+
+#include <vector>
+
+#include "hvp_ipm.h"
+
+namespace {
+
+hvp::Consts make_consts(const hvp_problem& p) {
+    hvp::Consts C;
+    memset(&C, 0, sizeof(C));
+    C.Qpp = p.Qx[0];
+    C.Qpv = 0.5 * (p.Qx[1] + p.Qx[2]);
+    C.Qvv = p.Qx[3];
+    C.Qu = p.Qu;
+    C.Qdu = p.Qdu;
+    C.w = p.w;
+    C.d_safe = p.d_safe;
+    C.d0 = p.spacing_d0;
+    C.t0 = p.spacing_t0;
+    for (int k = 0; k < HVP_MAX_N; ++k) {
+        C.dec[k] = p.a_dec * p.ts_acc + k * p.accel_tightening;
+        C.acc[k] = p.a_acc * p.ts_acc - k * p.accel_tightening;
+    }
+    C.tol = p.tol > 0 ? p.tol : 1e-12;
+    C.max_iter = p.max_iter > 0 ? p.max_iter : 60;
+    C.N = p.N;
+    return C;
+}
+
+template <int N>
+void solve_one(const hvp_system& S, const hvp::Consts& C, int role, const double* prm, double* u, double* x,
+               int8_t* region, double* cost, int32_t* status, int32_t* nodes, int32_t* iters, double* cand_cost,
+               uint32_t* cand_code, int cand_cap) {
+    struct Cand {
+        uint32_t code;
+        double cost;
+        int status, iters;
+        double y[N];
+    };
+    std::vector<Cand> cands;
+    hvp::LaneQp<N> probe;
+    const bool ok = hvp::setup_lane<N>(probe, S, C, role, prm, 0u);
+    int n = 0;
+    if (ok) {
+        n = hvp::enumerate_sequences(S, C, prm[1], [&](uint32_t code, int) {
+            hvp::LaneQp<N> q;
+            hvp::setup_lane<N>(q, S, C, role, prm, code);
+            hvp::QpOut o = hvp::solve_lane<N>(q, C);
+            Cand c;
+            c.code = code;
+            c.cost = o.status == 0 ? hvp::direct_cost<N>(q, S, C, role, prm, code) : o.cost;
+            c.status = o.status;
+            c.iters = o.iters;
+            for (int i = 0; i < N; ++i) c.y[i] = q.y[i];
+            cands.push_back(c);
+        });
+    }
+    double best = 1e300;
+    int tot = 0;
+    for (const Cand& c : cands) {
+        tot += c.iters;
+        if (c.status == 0 && c.cost < best) best = c.cost;
+    }
+    int win = -1;
+    if (best < 1e300) {
+        const double tol = 1e-9 * fmax(1.0, fabs(best));
+        for (size_t i = 0; i < cands.size(); ++i)
+            if (cands[i].status == 0 && cands[i].cost <= best + tol) { win = (int)i; break; }
+    }
+    for (int i = 0; i < (int)cands.size() && i < cand_cap; ++i) {
+        if (cand_cost) cand_cost[i] = cands[i].status == 0 ? cands[i].cost : 1e300;
+        if (cand_code) cand_code[i] = cands[i].code;
+    }
+    *nodes = n;
+    *iters = tot;
+    if (win < 0) {
+        *status = (!ok || n == 0) ? HVP_INFEASIBLE : HVP_MAXITER;
+        *cost = 1e300;
+        return;
+    }
+    const Cand& c = cands[win];
+    *status = HVP_OPTIMAL;
+    *cost = c.cost;
+    const double p0 = prm[0], v0 = prm[1];
+    x[0] = p0;
+    x[N + 1] = v0;
+    double p = p0, v = v0;
+    for (int k = 0; k < N; ++k) {
+        const int r = (c.code >> (3 * k)) & 7;
+        region[k] = (int8_t)r;
+        const double vn = c.y[k];
+        u[k] = (vn - S.a[r] * v - S.c[r]) / S.b[r];
+        p = p + S.ts * v;
+        v = vn;
+        x[k + 1] = p;
+        x[N + 1 + k + 1] = v;
+    }
+}
+
+template <int N>
+void solve_range(const hvp_problem& P, const hvp_system* systems, int B, const int32_t* sys, const int32_t* role,
+                 const double* params, double* u, double* x, int8_t* region, double* cost, int32_t* status,
+                 int32_t* nodes, int32_t* iters, int nthreads) {
+    const hvp::Consts C = make_consts(P);
+    const int stride = hvp_params_stride(N);
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1)
+    for (int i = 0; i < B; ++i)
+        solve_one<N>(systems[sys[i]], C, role[i], params + (size_t)i * stride, u + (size_t)i * N,
+                     x + (size_t)i * 2 * (N + 1), region + (size_t)i * N, cost + i, status + i, nodes + i, iters + i,
+                     nullptr, nullptr, 0);
+}
+
+}  // namespace
+
+extern "C" {
+
+// Same outputs as hvp_solve_batch (host pointers); test / baseline use only.
+int hvp_hostref_solve_batch(const hvp_problem* P, const hvp_system* systems, int B, const int32_t* sys,
+                            const int32_t* role, const double* params, double* u, double* x, int8_t* region,
+                            double* cost, int32_t* status, int32_t* nodes, int32_t* iters, int nthreads) {
+    switch (P->N) {
+#define HVP_CASE(n) \
+    case n: solve_range<n>(*P, systems, B, sys, role, params, u, x, region, cost, status, nodes, iters, nthreads); return 0;
+        HVP_CASE(2) HVP_CASE(3) HVP_CASE(4) HVP_CASE(5) HVP_CASE(6) HVP_CASE(7) HVP_CASE(8)
+#undef HVP_CASE
+        default: return HVP_E_UNSUPPORTED;
+    }
+}
+
+// Per-candidate costs of one instance in enumeration order (debugging / parity of every QP).
+int hvp_hostref_candidates(const hvp_problem* P, const hvp_system* S, int role, const double* prm,
+                           double* cand_cost, uint32_t* cand_code, int cap) {
+    const hvp::Consts C = make_consts(*P);
+    int n = 0;
+    double u[HVP_MAX_N], x[2 * (HVP_MAX_N + 1)], cost;
+    int8_t reg[HVP_MAX_N];
+    int32_t st, nodes, it;
+    switch (P->N) {
+#define HVP_CASE(k) \
+    case k: solve_one<k>(*S, C, role, prm, u, x, reg, &cost, &st, &nodes, &it, cand_cost, cand_code, cap); n = nodes; break;
+        HVP_CASE(2) HVP_CASE(3) HVP_CASE(4) HVP_CASE(5) HVP_CASE(6) HVP_CASE(7) HVP_CASE(8)
+#undef HVP_CASE
+        default: return HVP_E_UNSUPPORTED;
+    }
+    return n;
+}
+}

@@ -1,0 +1,475 @@
+// hvp_kernels.hip -- MI355X (gfx950) batched hybrid-MPC solver and its C ABI (include/hvp.h).
+//
+// One hvp_solve_batch call solves B independent local MIQPs (fleet_decent_mld.py:316: the n
+// agents of a platoon step, times any number of platoons / seeds / sweep points) in three
+// launches on the caller's stream:
+//
+//   K_enum   one thread per instance: depth-first enumeration of the velocity-feasible region
+//            sequences (exact interval reachability), reservation of a contiguous slice of the
+//            global candidate list with ONE atomicAdd per instance, and the candidate codes
+//            (3 bits per step) written in lexicographic order.
+//   K_qp     one LANE per candidate (instance, sigma): the condensed velocity-space QP is built
+//            and solved by a Mehrotra IPM entirely in registers (hvp_ipm.h); writes cost, status,
+//            iteration count and v_1..v_N.  Grid-stride over the candidate count read on the
+//            device, so no host round trip sits between K_enum and K_qp.  Consecutive lanes carry
+//            consecutive candidates of the same instance: the instance block (38 doubles) is read
+//            once per wave from L1/L2 and the lanes of a wave share the iteration count closely.
+//   K_select one thread per instance: min over its candidates, tie rule (first sequence within
+//            1e-9 relative of the minimum), reconstruction of u and x, status / node counts.
+//
+// Memory: everything lives in caller-owned device buffers plus a handle-owned workspace sized
+// once by hvp_reserve (no allocation inside hvp_solve_batch, so a call can be graph-captured).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#define HVP_HD __host__ __device__
+#include "hvp.h"
+#include "hvp_ipm.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                                     \
+    do {                                                                                                  \
+        hipError_t e_ = (expr);                                                                           \
+        if (e_ != hipSuccess) return fail(HVP_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+constexpr int kBlock = 256;
+
+struct Workspace {
+    int max_batch = 0;
+    int64_t cap = 0;
+    int32_t* inst_off = nullptr;   // [max_batch] first candidate slot (-1: overflow)
+    int32_t* inst_cnt = nullptr;   // [max_batch] candidates of the instance
+    int32_t* inst_flag = nullptr;  // [max_batch] 0 ok, 1 infeasible constant rows
+    unsigned long long* counter = nullptr;  // [2] reserved slots, ipm iteration total
+    int32_t* task_inst = nullptr;  // [cap]
+    uint32_t* task_code = nullptr; // [cap]
+    double* task_cost = nullptr;   // [cap]
+    int32_t* task_stat = nullptr;  // [cap] status | iters << 8
+    double* task_y = nullptr;      // [cap * N]
+};
+
+}  // namespace
+
+struct hvp_handle {
+    int device = 0;
+    hvp_problem prob{};
+    hvp::Consts C{};
+    int n_systems = 0;
+    hvp_system* d_sys = nullptr;
+    Workspace ws;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;  // around the whole solve
+    hipEvent_t evq0 = nullptr, evq1 = nullptr; // around K_qp (the dominant kernel)
+    hipStream_t last_stream = nullptr;
+    int last_B = 0;
+    int n_cu = 256;
+    // host-pointer entry point staging (grown on demand)
+    size_t stage_bytes = 0;
+    char* d_stage = nullptr;
+};
+
+namespace {
+
+hvp::Consts make_consts(const hvp_problem& p) {
+    hvp::Consts C;
+    std::memset(&C, 0, sizeof(C));
+    C.Qpp = p.Qx[0];
+    C.Qpv = 0.5 * (p.Qx[1] + p.Qx[2]);
+    C.Qvv = p.Qx[3];
+    C.Qu = p.Qu;
+    C.Qdu = p.Qdu;
+    C.w = p.w;
+    C.d_safe = p.d_safe;
+    C.d0 = p.spacing_d0;
+    C.t0 = p.spacing_t0;
+    for (int k = 0; k < HVP_MAX_N; ++k) {
+        C.dec[k] = p.a_dec * p.ts_acc + k * p.accel_tightening;
+        C.acc[k] = p.a_acc * p.ts_acc - k * p.accel_tightening;
+    }
+    C.tol = p.tol > 0 ? p.tol : 1e-12;
+    C.max_iter = p.max_iter > 0 ? p.max_iter : 60;
+    C.N = p.N;
+    return C;
+}
+
+// ------------------------------------------------------------------ K_enum
+template <int N>
+__global__ __launch_bounds__(kBlock) void k_enum(int B, const hvp_system* __restrict__ systems,
+                                                 const int32_t* __restrict__ sys, const int32_t* __restrict__ role,
+                                                 const double* __restrict__ params, hvp::Consts C, Workspace ws) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B) return;
+    const hvp_system& S = systems[sys[i]];
+    const double* prm = params + (size_t)i * (2 + 6 * (N + 1));
+    const double p0 = prm[0], v0 = prm[1];
+    const double P1 = p0 + S.ts * v0;
+    // sigma-independent constant row: p_1 = p_0 + ts v_0 inside the position box
+    const bool ok = P1 >= S.pmin - 1e-9 * (1.0 + fabs(S.pmin)) && P1 <= S.pmax + 1e-9 * (1.0 + fabs(S.pmax));
+    int cnt = 0;
+    if (ok) cnt = hvp::enumerate_sequences(S, C, v0, [](uint32_t, int) {});
+    ws.inst_cnt[i] = cnt;
+    ws.inst_flag[i] = ok ? 0 : 1;
+    int off = -1;
+    if (cnt > 0) {
+        const unsigned long long o = atomicAdd(&ws.counter[0], (unsigned long long)cnt);
+        if ((long long)o + cnt <= ws.cap) off = (int)o;
+    }
+    ws.inst_off[i] = off;
+    if (off < 0) return;
+    hvp::enumerate_sequences(S, C, v0, [&](uint32_t code, int j) {
+        ws.task_inst[off + j] = i;
+        ws.task_code[off + j] = code;
+    });
+    (void)role;
+}
+
+// ------------------------------------------------------------------ K_qp
+template <int N>
+__global__ __launch_bounds__(kBlock) void k_qp(const hvp_system* __restrict__ systems, const int32_t* __restrict__ sys,
+                                               const int32_t* __restrict__ role, const double* __restrict__ params,
+                                               hvp::Consts C, Workspace ws) {
+    const unsigned long long reserved = ws.counter[0];
+    const long long total = (long long)(reserved < (unsigned long long)ws.cap ? reserved : ws.cap);
+    unsigned long long iter_sum = 0;
+    for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (long long)gridDim.x * blockDim.x) {
+        const int inst = ws.task_inst[t];
+        const uint32_t code = ws.task_code[t];
+        const hvp_system& S = systems[sys[inst]];
+        const int rl = role[inst];
+        const double* prm = params + (size_t)inst * (2 + 6 * (N + 1));
+        hvp::LaneQp<N> q;
+        hvp::setup_lane<N>(q, S, C, rl, prm, code);
+        hvp::QpOut o = hvp::solve_lane<N>(q, C);
+        ws.task_cost[t] = o.status == 0 ? hvp::direct_cost<N>(q, S, C, rl, prm, code) : 1e300;
+        ws.task_stat[t] = o.status | (o.iters << 8);
+#pragma unroll
+        for (int k = 0; k < N; ++k) ws.task_y[t * N + k] = q.y[k];
+        iter_sum += (unsigned long long)o.iters;
+    }
+    // one atomic per wave for the iteration statistics
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) iter_sum += __shfl_down(iter_sum, off, 64);
+    if ((threadIdx.x & 63) == 0 && iter_sum) atomicAdd(&ws.counter[1], iter_sum);
+}
+
+// ------------------------------------------------------------------ K_select
+template <int N>
+__global__ __launch_bounds__(kBlock) void k_select(int B, const hvp_system* __restrict__ systems,
+                                                   const int32_t* __restrict__ sys, const double* __restrict__ params,
+                                                   Workspace ws, double* __restrict__ u_out, double* __restrict__ x_out,
+                                                   int8_t* __restrict__ region_out, int8_t* __restrict__ gear_out,
+                                                   double* __restrict__ cost_out, int32_t* __restrict__ status_out,
+                                                   int32_t* __restrict__ nodes_out, int32_t* __restrict__ iters_out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B) return;
+    const int cnt = ws.inst_cnt[i], off = ws.inst_off[i];
+    const hvp_system& S = systems[sys[i]];
+    const double* prm = params + (size_t)i * (2 + 6 * (N + 1));
+    int status;
+    int win = -1;
+    int iters = 0;
+    if (ws.inst_flag[i] != 0 || cnt == 0) {
+        status = HVP_INFEASIBLE;
+    } else if (off < 0) {
+        status = HVP_OVERFLOW;
+    } else {
+        double best = 1e300;
+        for (int j = 0; j < cnt; ++j) {
+            const int st = ws.task_stat[off + j];
+            iters += st >> 8;
+            if ((st & 0xff) == 0) best = fmin(best, ws.task_cost[off + j]);
+        }
+        if (best < 1e300) {
+            const double tol = 1e-9 * fmax(1.0, fabs(best));
+            for (int j = 0; j < cnt; ++j)
+                if ((ws.task_stat[off + j] & 0xff) == 0 && ws.task_cost[off + j] <= best + tol) {
+                    win = off + j;
+                    break;
+                }
+        }
+        status = win >= 0 ? HVP_OPTIMAL : HVP_MAXITER;
+    }
+    if (status_out) status_out[i] = status;
+    if (nodes_out) nodes_out[i] = cnt;
+    if (iters_out) iters_out[i] = iters;
+    if (cost_out) cost_out[i] = win >= 0 ? ws.task_cost[win] : 1e300;
+    const uint32_t code = win >= 0 ? ws.task_code[win] : 0u;
+    double p = prm[0], v = prm[1];
+    if (x_out) {
+        x_out[(size_t)i * 2 * (N + 1)] = p;
+        x_out[(size_t)i * 2 * (N + 1) + N + 1] = v;
+    }
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        const int r = (code >> (3 * k)) & 7;
+        const double vn = win >= 0 ? ws.task_y[(size_t)win * N + k] : v;
+        const double u = win >= 0 ? (vn - S.a[r] * v - S.c[r]) / S.b[r] : 0.0;
+        p = p + S.ts * v;
+        v = vn;
+        if (u_out) u_out[(size_t)i * N + k] = u;
+        if (x_out) {
+            x_out[(size_t)i * 2 * (N + 1) + k + 1] = p;
+            x_out[(size_t)i * 2 * (N + 1) + N + 1 + k + 1] = v;
+        }
+        if (region_out) region_out[(size_t)i * N + k] = (int8_t)(win >= 0 ? r : -1);
+        if (gear_out) gear_out[(size_t)i * N + k] = (int8_t)(win >= 0 ? S.gear[r] : 0);
+    }
+}
+
+int grid_for(long long n) { return (int)std::max<long long>(1, (n + kBlock - 1) / kBlock); }
+
+template <int N>
+int launch_all(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, const double* params, double* u_out,
+               double* x_out, int8_t* region_out, int8_t* gear_out, double* cost_out, int32_t* status_out,
+               int32_t* nodes_out, int32_t* iters_out, hipStream_t st) {
+    Workspace ws = h->ws;
+    HIP_TRY(hipMemsetAsync(ws.counter, 0, 2 * sizeof(unsigned long long), st));
+    HIP_TRY(hipEventRecord(h->ev0, st));
+    hipLaunchKernelGGL(k_enum<N>, dim3(grid_for(B)), dim3(kBlock), 0, st, B, h->d_sys, sys, role, params, h->C, ws);
+    HIP_TRY(hipGetLastError());
+    // the candidate count is only known on the device: size the grid for the capacity bound
+    // (≈ every CU x 8 blocks) and let the kernel grid-stride over the real count
+    const long long want = std::min<long long>(grid_for(h->ws.cap), (long long)h->n_cu * 8);
+    HIP_TRY(hipEventRecord(h->evq0, st));
+    hipLaunchKernelGGL(k_qp<N>, dim3((int)want), dim3(kBlock), 0, st, h->d_sys, sys, role, params, h->C, ws);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(h->evq1, st));
+    hipLaunchKernelGGL(k_select<N>, dim3(grid_for(B)), dim3(kBlock), 0, st, B, h->d_sys, sys, params, ws, u_out,
+                       x_out, region_out, gear_out, cost_out, status_out, nodes_out, iters_out);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(h->ev1, st));
+    h->last_stream = st;
+    h->last_B = B;
+    return 0;
+}
+
+void free_ws(Workspace& w) {
+    (void)hipFree(w.inst_off);
+    (void)hipFree(w.inst_cnt);
+    (void)hipFree(w.inst_flag);
+    (void)hipFree(w.counter);
+    (void)hipFree(w.task_inst);
+    (void)hipFree(w.task_code);
+    (void)hipFree(w.task_cost);
+    (void)hipFree(w.task_stat);
+    (void)hipFree(w.task_y);
+    w = Workspace{};
+}
+
+int64_t default_capacity(int N, int B) {
+    // per-instance average budget: 7^N capped (N = 5: mean ~30, max ~85 region sequences)
+    int64_t per = 1;
+    for (int k = 0; k < N; ++k) per = std::min<int64_t>(per * 7, 1 << 20);
+    per = std::min<int64_t>(per, N <= 5 ? 256 : (N <= 6 ? 1024 : 4096));
+    return per * (int64_t)std::max(B, 1);
+}
+
+bool valid_system(const hvp_system& s, std::string* why) {
+    if (s.n_regions < 1 || s.n_regions > HVP_MAX_REGIONS) { *why = "n_regions out of range"; return false; }
+    if (!(s.ts > 0)) { *why = "ts must be > 0"; return false; }
+    for (int r = 0; r < s.n_regions; ++r) {
+        if (!(s.b[r] > 0)) { *why = "input gain b must be > 0"; return false; }
+        if (s.vlo[r] > s.vhi[r]) { *why = "empty region interval"; return false; }
+    }
+    if (!(s.umin <= s.umax) || !(s.vmin <= s.vmax) || !(s.pmin <= s.pmax)) { *why = "empty box"; return false; }
+    return true;
+}
+
+}  // namespace
+
+// ===================================================================== C ABI
+extern "C" {
+
+int hvp_abi_version(void) { return HVP_ABI_VERSION; }
+
+int hvp_last_error(char* buf, size_t len) {
+    if (!buf || len == 0) return HVP_E_ARG;
+    std::snprintf(buf, len, "%s", g_err.c_str());
+    return 0;
+}
+
+int hvp_create(hvp_handle** out, const hvp_problem* problem, const hvp_system* systems, int n_systems, int device) {
+    if (!out || !problem || !systems || n_systems <= 0) return fail(HVP_E_ARG, "hvp_create: null argument");
+    *out = nullptr;
+    if (problem->N < 2 || problem->N > HVP_MAX_N)
+        return fail(HVP_E_UNSUPPORTED, "hvp_create: horizon N must be in [2, " + std::to_string(HVP_MAX_N) + "]");
+    if (problem->quadratic_cost != 1)
+        return fail(HVP_E_UNSUPPORTED, "hvp_create: only the quadratic cost (min_2_norm) runs on the GPU");
+    for (int i = 0; i < n_systems; ++i) {
+        std::string why;
+        if (!valid_system(systems[i], &why)) return fail(HVP_E_ARG, "hvp_create: system " + std::to_string(i) + ": " + why);
+    }
+    HIP_TRY(hipSetDevice(device));
+    hvp_handle* h = new hvp_handle();
+    h->device = device;
+    h->prob = *problem;
+    h->C = make_consts(*problem);
+    h->n_systems = n_systems;
+    (void)hipDeviceGetAttribute(&h->n_cu, hipDeviceAttributeMultiprocessorCount, device);
+    if (hipMalloc(&h->d_sys, sizeof(hvp_system) * n_systems) != hipSuccess ||
+        hipMemcpy(h->d_sys, systems, sizeof(hvp_system) * n_systems, hipMemcpyHostToDevice) != hipSuccess ||
+        hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess ||
+        hipEventCreate(&h->evq0) != hipSuccess || hipEventCreate(&h->evq1) != hipSuccess) {
+        hvp_destroy(h);
+        return fail(HVP_E_HIP, "hvp_create: device allocation failed");
+    }
+    *out = h;
+    return 0;
+}
+
+int hvp_reserve(hvp_handle* h, int max_batch, int64_t cap) {
+    if (!h || max_batch <= 0) return fail(HVP_E_ARG, "hvp_reserve: bad argument");
+    if (cap <= 0) cap = default_capacity(h->prob.N, max_batch);
+    if (max_batch <= h->ws.max_batch && cap <= h->ws.cap) return 0;
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(hipDeviceSynchronize());
+    max_batch = std::max(max_batch, h->ws.max_batch);
+    cap = std::max<int64_t>(cap, h->ws.cap);
+    free_ws(h->ws);
+    Workspace& w = h->ws;
+    const int N = h->prob.N;
+    bool ok = hipMalloc(&w.inst_off, sizeof(int32_t) * max_batch) == hipSuccess &&
+              hipMalloc(&w.inst_cnt, sizeof(int32_t) * max_batch) == hipSuccess &&
+              hipMalloc(&w.inst_flag, sizeof(int32_t) * max_batch) == hipSuccess &&
+              hipMalloc(&w.counter, sizeof(unsigned long long) * 2) == hipSuccess &&
+              hipMalloc(&w.task_inst, sizeof(int32_t) * cap) == hipSuccess &&
+              hipMalloc(&w.task_code, sizeof(uint32_t) * cap) == hipSuccess &&
+              hipMalloc(&w.task_cost, sizeof(double) * cap) == hipSuccess &&
+              hipMalloc(&w.task_stat, sizeof(int32_t) * cap) == hipSuccess &&
+              hipMalloc(&w.task_y, sizeof(double) * cap * N) == hipSuccess;
+    if (!ok) {
+        free_ws(w);
+        return fail(HVP_E_NOMEM, "hvp_reserve: device allocation failed");
+    }
+    w.max_batch = max_batch;
+    w.cap = cap;
+    return 0;
+}
+
+int hvp_solve_batch(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, const double* params,
+                    double* u_out, double* x_out, int8_t* region_out, int8_t* gear_out, double* cost_out,
+                    int32_t* status_out, int32_t* nodes_out, int32_t* iters_out, void* stream) {
+    if (!h || B < 0 || (B > 0 && (!sys || !role || !params || !cost_out || !status_out)))
+        return fail(HVP_E_ARG, "hvp_solve_batch: bad argument");
+    if (B == 0) return 0;
+    if (B > h->ws.max_batch) {
+        int rc = hvp_reserve(h, B, default_capacity(h->prob.N, B));
+        if (rc) return rc;
+    }
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t st = (hipStream_t)stream;
+    switch (h->prob.N) {
+#define HVP_CASE(n) \
+    case n: return launch_all<n>(h, B, sys, role, params, u_out, x_out, region_out, gear_out, cost_out, status_out, nodes_out, iters_out, st);
+        HVP_CASE(2) HVP_CASE(3) HVP_CASE(4) HVP_CASE(5) HVP_CASE(6) HVP_CASE(7) HVP_CASE(8)
+#undef HVP_CASE
+        default: return fail(HVP_E_UNSUPPORTED, "hvp_solve_batch: unsupported N");
+    }
+}
+
+int hvp_sync(hvp_handle* h, void* stream) {
+    if (!h) return fail(HVP_E_ARG, "hvp_sync: null handle");
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    return 0;
+}
+
+int hvp_get_stats(hvp_handle* h, hvp_stats* out) {
+    if (!h || !out) return fail(HVP_E_ARG, "hvp_get_stats: bad argument");
+    HIP_TRY(hipStreamSynchronize(h->last_stream));
+    unsigned long long c[2] = {0, 0};
+    if (h->ws.counter) HIP_TRY(hipMemcpy(c, h->ws.counter, sizeof(c), hipMemcpyDeviceToHost));
+    float ms = 0.f, qms = 0.f;
+    if (h->last_B > 0) {
+        HIP_TRY(hipEventElapsedTime(&ms, h->ev0, h->ev1));
+        HIP_TRY(hipEventElapsedTime(&qms, h->evq0, h->evq1));
+    }
+    out->qp_ms = qms;
+    out->n_instances = h->last_B;
+    out->n_candidates = (int64_t)c[0];
+    out->ipm_iterations = (int64_t)c[1];
+    out->capacity = h->ws.cap;
+    out->last_ms = ms;
+    return 0;
+}
+
+int hvp_solve_batch_host(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, const double* params,
+                         double* u_out, double* x_out, int8_t* region_out, int8_t* gear_out, double* cost_out,
+                         int32_t* status_out, int32_t* nodes_out, int32_t* iters_out) {
+    if (!h || B < 0) return fail(HVP_E_ARG, "hvp_solve_batch_host: bad argument");
+    if (B == 0) return 0;
+    const int N = h->prob.N;
+    const size_t P = (2 + 6 * (N + 1));
+    // staging layout (8-byte aligned pieces)
+    const size_t s_sys = sizeof(int32_t) * B, s_role = s_sys, s_prm = sizeof(double) * P * B;
+    const size_t s_u = sizeof(double) * N * B, s_x = sizeof(double) * 2 * (N + 1) * B;
+    const size_t s_reg = (size_t)N * B, s_gear = s_reg, s_cost = sizeof(double) * B, s_i32 = sizeof(int32_t) * B;
+    auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    const size_t total = al(s_sys) + al(s_role) + al(s_prm) + al(s_u) + al(s_x) + al(s_reg) + al(s_gear) + al(s_cost) +
+                         3 * al(s_i32);
+    HIP_TRY(hipSetDevice(h->device));
+    if (total > h->stage_bytes) {
+        if (h->d_stage) (void)hipFree(h->d_stage);
+        h->d_stage = nullptr;
+        h->stage_bytes = 0;
+        HIP_TRY(hipMalloc(&h->d_stage, total));
+        h->stage_bytes = total;
+    }
+    char* p = h->d_stage;
+    auto take = [&](size_t n) { char* r = p; p += al(n); return r; };
+    int32_t* d_sys = (int32_t*)take(s_sys);
+    int32_t* d_role = (int32_t*)take(s_role);
+    double* d_prm = (double*)take(s_prm);
+    double* d_u = (double*)take(s_u);
+    double* d_x = (double*)take(s_x);
+    int8_t* d_reg = (int8_t*)take(s_reg);
+    int8_t* d_gear = (int8_t*)take(s_gear);
+    double* d_cost = (double*)take(s_cost);
+    int32_t* d_stat = (int32_t*)take(s_i32);
+    int32_t* d_nodes = (int32_t*)take(s_i32);
+    int32_t* d_iters = (int32_t*)take(s_i32);
+    HIP_TRY(hipMemcpy(d_sys, sys, s_sys, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(d_role, role, s_role, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(d_prm, params, s_prm, hipMemcpyHostToDevice));
+    int rc = hvp_solve_batch(h, B, d_sys, d_role, d_prm, d_u, d_x, d_reg, d_gear, d_cost, d_stat, d_nodes, d_iters,
+                             nullptr);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(nullptr));
+    if (u_out) HIP_TRY(hipMemcpy(u_out, d_u, s_u, hipMemcpyDeviceToHost));
+    if (x_out) HIP_TRY(hipMemcpy(x_out, d_x, s_x, hipMemcpyDeviceToHost));
+    if (region_out) HIP_TRY(hipMemcpy(region_out, d_reg, s_reg, hipMemcpyDeviceToHost));
+    if (gear_out) HIP_TRY(hipMemcpy(gear_out, d_gear, s_gear, hipMemcpyDeviceToHost));
+    if (cost_out) HIP_TRY(hipMemcpy(cost_out, d_cost, s_cost, hipMemcpyDeviceToHost));
+    if (status_out) HIP_TRY(hipMemcpy(status_out, d_stat, s_i32, hipMemcpyDeviceToHost));
+    if (nodes_out) HIP_TRY(hipMemcpy(nodes_out, d_nodes, s_i32, hipMemcpyDeviceToHost));
+    if (iters_out) HIP_TRY(hipMemcpy(iters_out, d_iters, s_i32, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+void hvp_destroy(hvp_handle* h) {
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    (void)hipDeviceSynchronize();
+    free_ws(h->ws);
+    if (h->d_sys) (void)hipFree(h->d_sys);
+    if (h->d_stage) (void)hipFree(h->d_stage);
+    if (h->ev0) (void)hipEventDestroy(h->ev0);
+    if (h->ev1) (void)hipEventDestroy(h->ev1);
+    if (h->evq0) (void)hipEventDestroy(h->evq0);
+    if (h->evq1) (void)hipEventDestroy(h->evq1);
+    delete h;
+}
+
+}  // extern "C"

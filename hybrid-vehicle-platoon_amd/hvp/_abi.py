@@ -1,0 +1,146 @@
+"""ctypes mirror of include/hvp.h and the loader of libhvpsolve.so.
+
+The product path has exactly one backend: the HIP library built from csrc/hvp_kernels.hip.
+If it is missing, :func:`load` raises -- there is no CPU fallback.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+
+MAX_REGIONS = 8
+MAX_N = 8
+ABI_VERSION = 1
+
+ROLE_SAFE_FRONT = 1
+ROLE_SAFE_BACK = 2
+ROLE_TRACK_FRONT = 4
+ROLE_TRACK_BACK = 8
+ROLE_TRACK_LEADER = 16
+ROLE_LEADER_SPACING = 32
+
+OPTIMAL, INFEASIBLE, MAXITER, OVERFLOW = 0, 1, 2, 3
+STATUS_NAMES = {OPTIMAL: "OPTIMAL", INFEASIBLE: "INFEASIBLE", MAXITER: "MAXITER", OVERFLOW: "OVERFLOW"}
+
+_D8 = ctypes.c_double * MAX_REGIONS
+
+
+class HvpSystem(ctypes.Structure):
+    _fields_ = [
+        ("n_regions", ctypes.c_int32),
+        ("gear", ctypes.c_int32 * MAX_REGIONS),
+        ("pad_", ctypes.c_int32),
+        ("ts", ctypes.c_double),
+        ("a", _D8),
+        ("b", _D8),
+        ("c", _D8),
+        ("vlo", _D8),
+        ("vhi", _D8),
+        ("pmin", ctypes.c_double),
+        ("pmax", ctypes.c_double),
+        ("vmin", ctypes.c_double),
+        ("vmax", ctypes.c_double),
+        ("umin", ctypes.c_double),
+        ("umax", ctypes.c_double),
+    ]
+
+
+class HvpProblem(ctypes.Structure):
+    _fields_ = [
+        ("N", ctypes.c_int32),
+        ("quadratic_cost", ctypes.c_int32),
+        ("Qx", ctypes.c_double * 4),
+        ("Qu", ctypes.c_double),
+        ("Qdu", ctypes.c_double),
+        ("w", ctypes.c_double),
+        ("a_acc", ctypes.c_double),
+        ("a_dec", ctypes.c_double),
+        ("ts_acc", ctypes.c_double),
+        ("d_safe", ctypes.c_double),
+        ("accel_tightening", ctypes.c_double),
+        ("spacing_d0", ctypes.c_double),
+        ("spacing_t0", ctypes.c_double),
+        ("max_iter", ctypes.c_int32),
+        ("pad_", ctypes.c_int32),
+        ("tol", ctypes.c_double),
+    ]
+
+
+class HvpStats(ctypes.Structure):
+    _fields_ = [
+        ("n_instances", ctypes.c_int64),
+        ("n_candidates", ctypes.c_int64),
+        ("ipm_iterations", ctypes.c_int64),
+        ("capacity", ctypes.c_int64),
+        ("last_ms", ctypes.c_double),
+        ("qp_ms", ctypes.c_double),
+    ]
+
+
+def params_stride(N: int) -> int:
+    return 2 + 6 * (N + 1)
+
+
+_PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_DIR = os.path.join(_PKG_ROOT, "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libhvpsolve.so")
+HOSTREF_PATH = os.path.join(LIB_DIR, "libhvp_hostref.so")
+
+_lib = None
+
+_P = ctypes.c_void_p
+_I32P = ctypes.POINTER(ctypes.c_int32)
+_DP = ctypes.POINTER(ctypes.c_double)
+_I8P = ctypes.POINTER(ctypes.c_int8)
+
+# exported symbol -> (argtypes, restype); also the list the CPU tests check
+EXPORTS = {
+    "hvp_create": ([ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(HvpProblem), ctypes.POINTER(HvpSystem),
+                    ctypes.c_int, ctypes.c_int], ctypes.c_int),
+    "hvp_reserve": ([_P, ctypes.c_int, ctypes.c_int64], ctypes.c_int),
+    "hvp_solve_batch": ([_P, ctypes.c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
+    "hvp_solve_batch_host": ([_P, ctypes.c_int, _I32P, _I32P, _DP, _DP, _DP, _I8P, _I8P, _DP, _I32P, _I32P,
+                              _I32P], ctypes.c_int),
+    "hvp_sync": ([_P, _P], ctypes.c_int),
+    "hvp_get_stats": ([_P, ctypes.POINTER(HvpStats)], ctypes.c_int),
+    "hvp_destroy": ([_P], None),
+    "hvp_last_error": ([ctypes.c_char_p, ctypes.c_size_t], ctypes.c_int),
+    "hvp_abi_version": ([], ctypes.c_int),
+}
+
+
+class HvpError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libhvpsolve.so (built by ``make -C hybrid-vehicle-platoon_amd``); raises if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise HvpError(
+            f"{LIB_PATH} not found: build the HIP library first (python -c 'import __graft_entry__ as g; g.build()' "
+            "or make -C hybrid-vehicle-platoon_amd). There is no CPU fallback."
+        )
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (argt, rest) in EXPORTS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argt
+        fn.restype = rest
+    if lib.hvp_abi_version() != ABI_VERSION:
+        raise HvpError(f"libhvpsolve ABI {lib.hvp_abi_version()} != expected {ABI_VERSION}")
+    _lib = lib
+    return lib
+
+
+def last_error() -> str:
+    buf = ctypes.create_string_buffer(1024)
+    load().hvp_last_error(buf, len(buf))
+    return buf.value.decode(errors="replace")
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise HvpError(f"{what} failed ({rc}): {last_error()}")

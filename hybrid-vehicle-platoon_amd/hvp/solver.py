@@ -1,0 +1,138 @@
+"""Batched local-MIQP solver: the Python face of libhvpsolve.so (include/hvp.h).
+
+:class:`BatchSolver` owns one ``hvp_handle`` (the compiled problem: horizon, weights, the
+vehicles' PWA tables) and solves any number of instances per call:
+
+* ``solve_device(...)`` takes torch tensors already on the GPU (zero-copy device pointers, the
+  throughput path: bench.py, batched coordinators), asynchronous on the current torch stream;
+* ``solve(...)`` takes numpy arrays (host pointers; one synchronous call, PCIe included) -- the
+  path behind the per-agent ``solve_mpc`` drop-in.
+
+There is no CPU fallback: constructing a solver without the HIP library raises.
+"""
+
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _abi
+
+
+@dataclass
+class BatchResult:
+    u: np.ndarray        # (B, N)     control sequence
+    x: np.ndarray        # (B, 2, N+1) predicted state trajectory
+    region: np.ndarray   # (B, N)     PWA region (= MLD delta) per step, -1 if no solution
+    gear: np.ndarray     # (B, N)     gear label implied by the region
+    cost: np.ndarray     # (B,)       optimal objective (Gurobi ObjVal equivalent)
+    status: np.ndarray   # (B,)       HVP_* status
+    nodes: np.ndarray    # (B,)       region sequences solved (Gurobi NodeCount analogue)
+    iters: np.ndarray    # (B,)       IPM iterations summed over the sequences
+
+
+class BatchSolver:
+    def __init__(self, problem: _abi.HvpProblem, systems: list[_abi.HvpSystem], device: int = 0,
+                 max_batch: int = 0, candidate_capacity: int = 0) -> None:
+        self._lib = _abi.load()
+        self.N = int(problem.N)
+        self.problem = problem
+        self.n_systems = len(systems)
+        arr = (_abi.HvpSystem * len(systems))(*systems)
+        h = ctypes.c_void_p()
+        _abi.check(self._lib.hvp_create(ctypes.byref(h), ctypes.byref(problem), arr, len(systems), device), "hvp_create")
+        self._h = h
+        self.device = device
+        if max_batch > 0:
+            self.reserve(max_batch, candidate_capacity)
+
+    # -------------------------------------------------------------- lifecycle
+    def reserve(self, max_batch: int, candidate_capacity: int = 0) -> None:
+        _abi.check(self._lib.hvp_reserve(self._h, int(max_batch), int(candidate_capacity)), "hvp_reserve")
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._lib.hvp_destroy(self._h)
+            self._h = None
+
+    def __del__(self) -> None:  # pragma: no cover - interpreter shutdown order
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def params_stride(self) -> int:
+        return _abi.params_stride(self.N)
+
+    def stats(self) -> _abi.HvpStats:
+        s = _abi.HvpStats()
+        _abi.check(self._lib.hvp_get_stats(self._h, ctypes.byref(s)), "hvp_get_stats")
+        return s
+
+    # -------------------------------------------------------------- host path
+    def solve(self, sys_idx, roles, params) -> BatchResult:
+        N = self.N
+        sys_idx = np.ascontiguousarray(np.asarray(sys_idx, dtype=np.int32).reshape(-1))
+        roles = np.ascontiguousarray(np.asarray(roles, dtype=np.int32).reshape(-1))
+        params = np.ascontiguousarray(np.asarray(params, dtype=np.float64).reshape(len(roles), -1))
+        B = len(roles)
+        if params.shape[1] != self.params_stride or len(sys_idx) != B:
+            raise ValueError(f"params must be (B, {self.params_stride}) and sys_idx (B,)")
+        if B and (sys_idx.min() < 0 or sys_idx.max() >= self.n_systems):
+            raise ValueError("system index out of range")
+        out = BatchResult(
+            u=np.zeros((B, N)), x=np.zeros((B, 2, N + 1)), region=np.zeros((B, N), np.int8),
+            gear=np.zeros((B, N), np.int8), cost=np.zeros(B), status=np.zeros(B, np.int32),
+            nodes=np.zeros(B, np.int32), iters=np.zeros(B, np.int32),
+        )
+        if B == 0:
+            return out
+        P = lambda a, t: a.ctypes.data_as(ctypes.POINTER(t))  # noqa: E731
+        d, i32, i8 = ctypes.c_double, ctypes.c_int32, ctypes.c_int8
+        rc = self._lib.hvp_solve_batch_host(
+            self._h, B, P(sys_idx, i32), P(roles, i32), P(params, d), P(out.u, d), P(out.x, d), P(out.region, i8),
+            P(out.gear, i8), P(out.cost, d), P(out.status, i32), P(out.nodes, i32), P(out.iters, i32))
+        _abi.check(rc, "hvp_solve_batch_host")
+        return out
+
+    # -------------------------------------------------------------- device path
+    def alloc_outputs(self, B: int, device=None) -> dict:
+        import torch
+
+        dev = device or torch.device("cuda", self.device)
+        N = self.N
+        return {
+            "u": torch.empty((B, N), dtype=torch.float64, device=dev),
+            "x": torch.empty((B, 2, N + 1), dtype=torch.float64, device=dev),
+            "region": torch.empty((B, N), dtype=torch.int8, device=dev),
+            "gear": torch.empty((B, N), dtype=torch.int8, device=dev),
+            "cost": torch.empty((B,), dtype=torch.float64, device=dev),
+            "status": torch.empty((B,), dtype=torch.int32, device=dev),
+            "nodes": torch.empty((B,), dtype=torch.int32, device=dev),
+            "iters": torch.empty((B,), dtype=torch.int32, device=dev),
+        }
+
+    def solve_device(self, sys_idx, roles, params, out: dict | None = None, stream=None) -> dict:
+        """Asynchronous solve of device-resident tensors; returns (and fills) the output dict."""
+        import torch
+
+        B = int(roles.shape[0])
+        for name, t, dt in (("sys_idx", sys_idx, torch.int32), ("roles", roles, torch.int32),
+                            ("params", params, torch.float64)):
+            if not t.is_cuda or t.dtype != dt or not t.is_contiguous():
+                raise ValueError(f"{name} must be a contiguous CUDA tensor of dtype {dt}")
+        if params.numel() != B * self.params_stride or sys_idx.numel() != B:
+            raise ValueError("params must be (B, params_stride), sys_idx (B,)")
+        out = out or self.alloc_outputs(B, params.device)
+        if stream is None:
+            stream = torch.cuda.current_stream(params.device)
+        ptr = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        rc = self._lib.hvp_solve_batch(
+            self._h, B, ptr(sys_idx), ptr(roles), ptr(params), ptr(out["u"]), ptr(out["x"]), ptr(out["region"]),
+            ptr(out["gear"]), ptr(out["cost"]), ptr(out["status"]), ptr(out["nodes"]), ptr(out["iters"]),
+            ctypes.c_void_p(stream.cuda_stream))
+        _abi.check(rc, "hvp_solve_batch")
+        return out

@@ -125,6 +125,7 @@ typedef struct hvp_stats {
     int64_t ipm_iterations; /* sum of IPM iterations over those QPs                    */
     int64_t capacity;       /* candidate workspace                                     */
     double last_ms;         /* device time of the last solve (event-timed), ms         */
+    double qp_ms;           /* device time of its QP kernel (K_qp), ms                 */
 } hvp_stats;
 
 int hvp_create(hvp_handle** out, const hvp_problem* problem, const hvp_system* systems,

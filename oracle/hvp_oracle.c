@@ -544,6 +544,47 @@ static or_result ipm_solve(const or_qp* qp, or_work* w, int maxit) {
     return res;
 }
 
+/* Objective evaluated term by term on the trajectory (the form of fleet_decent_mld.py:107-169):
+ * sums of squared tracking errors, control terms and w * slack with the slacks at their optimal
+ * value max(0, .).  Avoids the cancellation of 1/2 z'Pz + q'z + r0 (positions ~3e3). */
+static double direct_objective(const or_cfg* cf, const double* x0, const double* xf, const double* xb,
+                               const double* xl, const double* z) {
+    const int N = cf->N;
+    double J = 0.0;
+    for (int k = 0; k <= N; ++k) {
+        double p = k == 0 ? x0[0] : z[2 * (k - 1)], v = k == 0 ? x0[1] : z[2 * (k - 1) + 1];
+        double e[3][2];
+        int ne = 0;
+        if (cf->role & R_TF) { e[ne][0] = p + cf->t0 * v + cf->d0 - par(xf, N, 0, k); e[ne][1] = v - par(xf, N, 1, k); ne++; }
+        if (cf->role & R_TB) {
+            double pb = par(xb, N, 0, k), vb = par(xb, N, 1, k);
+            e[ne][0] = pb + cf->t0 * vb + cf->d0 - p; e[ne][1] = vb - v; ne++;
+        }
+        if (cf->role & R_TL) {
+            e[ne][0] = p - par(xl, N, 0, k) + ((cf->role & R_LSP) ? cf->t0 * v + cf->d0 : 0.0);
+            e[ne][1] = v - par(xl, N, 1, k); ne++;
+        }
+        for (int t = 0; t < ne; ++t) {
+            if (cf->quadratic)
+                J += cf->Qx[0][0] * e[t][0] * e[t][0] + (cf->Qx[0][1] + cf->Qx[1][0]) * e[t][0] * e[t][1] +
+                     cf->Qx[1][1] * e[t][1] * e[t][1];
+            else
+                J += fabs(cf->Qx[0][0] * e[t][0]) + fabs(cf->Qx[1][1] * e[t][1]);
+        }
+        if (cf->role & R_SF) J += cf->w * fmax(0.0, p - par(xf, N, 0, k) + cf->d_safe);
+        if (cf->role & R_SB) J += cf->w * fmax(0.0, par(xb, N, 0, k) + cf->d_safe - p);
+    }
+    for (int k = 0; k < N; ++k) {
+        double u = z[2 * N + k];
+        J += cf->quadratic ? cf->Qu * u * u : fabs(cf->Qu * u);
+        if (k + 1 < N) {
+            double du = z[2 * N + k + 1] - u;
+            J += cf->quadratic ? cf->Qdu * du * du : fabs(cf->Qdu * du);
+        }
+    }
+    return J;
+}
+
 /* ------------------------------------------------------------------ sigma enumeration */
 /* velocity interval of a region / the state box from rows acting on v only */
 static int v_interval(const double (*S)[2], const double* T, int nrows, double* lo, double* hi) {
@@ -669,7 +710,10 @@ static void visit_qp(const int* sigma, void* vctx) {
     if (build_qp(C->qp, C->md, C->cf, sigma, C->x0, C->xf, C->xb, C->xl) > 0 && !C->qp->infeasible_const) {
         or_result r = ipm_solve(C->qp, C->w, C->maxit);
         C->iters += r.iters;
-        if (r.converged) { obj = r.obj; cert = r.certified; C->n_conv++; C->n_cert += cert; }
+        if (r.converged) {
+            obj = direct_objective(C->cf, C->x0, C->xf, C->xb, C->xl, C->w->z);
+            cert = r.certified; C->n_conv++; C->n_cert += cert;
+        }
     }
     C->obj[C->ncand] = obj;
     C->cert[C->ncand] = (unsigned char)cert;
@@ -774,7 +818,7 @@ int oracle_solve_miqp(int N, int nreg, int nsr, const double* S, const double* R
         const int* ws = C.sig + (size_t)win * N;
         build_qp(qp, &md, &cf, ws, x0, xf, xb, xl);
         or_result r = ipm_solve(qp, w, C.maxit);
-        best_obj = r.obj;
+        best_obj = direct_objective(&cf, x0, xf, xb, xl, w->z);
         best_cert = r.certified;
         for (int i = 0; i < 2; ++i) x_out[i * (N + 1)] = x0[i];
         for (int k = 1; k <= N; ++k)

@@ -1,0 +1,75 @@
+"""GPU parity: libhvpsolve.so (HIP, gfx950) against the CPU oracle, through the C ABI.
+
+Bar: region sequence (= MLD binaries) and gear labels bit-exact; cost within 1e-9 relative;
+u and x within 1e-6 (the north-star KKT tolerance); node counts (sequences enumerated) equal.
+"""
+
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import oracle as O
+from instances import decent_instances, leader_window, oracle_solve
+
+pytestmark = pytest.mark.gpu
+
+N = 5
+
+
+def _solver(systems, N=N, **kw):
+    from hvp import tables
+    from hvp.solver import BatchSolver
+
+    return BatchSolver(tables.problem(N, **kw), systems)
+
+
+def _gear_system(mass=800.0):
+    from hvp import tables
+    from hvp.models import PwaGearVehicle
+
+    veh = PwaGearVehicle(mass)
+    return tables.system_from_dict(veh.get_discrete_system(1), tables.gears_of(veh))
+
+
+def _compare(res, ref, params, tol_c=1e-9, tol_u=1e-6):
+    gear_of = np.array([1, 2, 3, 4, 4, 5, 6])
+    for i, r in enumerate(ref):
+        assert res.status[i] == 0, (i, res.status[i])
+        assert list(res.region[i]) == list(r.sigma), (i, res.region[i], r.sigma, res.cost[i], r.cost)
+        assert list(res.gear[i]) == list(gear_of[r.sigma]), i
+        assert res.nodes[i] == r.n_candidates, (i, res.nodes[i], r.n_candidates)
+        assert abs(res.cost[i] - r.cost) <= tol_c * max(1.0, abs(r.cost)), (i, res.cost[i], r.cost)
+        assert np.abs(res.u[i] - r.u).max() <= tol_u, (i, res.u[i], r.u)
+        assert np.abs(res.x[i] - r.x).max() <= tol_u * 100, i  # positions ~3e3: 1e-4 absolute
+
+
+@pytest.mark.parametrize("n", [2, 10])
+def test_decent_seeds_match_oracle(gpu_available, n):
+    s = _solver([_gear_system()])
+    sysd = O.gear_pwa_system(800.0)
+    lead = leader_window(N)
+    for seed in range(10):
+        params, roles = decent_instances(O.env_initial_state(n, seed), N, lead)
+        res = s.solve(np.zeros(n, np.int32), roles, params)
+        _compare(res, oracle_solve(sysd, O.Cfg(), N, params, roles), params)
+
+
+def test_device_path_matches_host_path(gpu_available):
+    import torch
+
+    s = _solver([_gear_system()])
+    lead = leader_window(N)
+    P, R = [], []
+    for seed in range(64):
+        p, r = decent_instances(O.env_initial_state(10, seed), N, lead)
+        P.append(p)
+        R.append(r)
+    params, roles = np.concatenate(P), np.concatenate(R)
+    host = s.solve(np.zeros(len(roles), np.int32), roles, params)
+    dev = s.solve_device(torch.zeros(len(roles), dtype=torch.int32, device="cuda"),
+                         torch.from_numpy(roles).cuda(), torch.from_numpy(params).cuda())
+    torch.cuda.synchronize()
+    assert np.array_equal(dev["region"].cpu().numpy(), host.region)
+    assert np.array_equal(dev["cost"].cpu().numpy(), host.cost)
+    assert np.array_equal(dev["u"].cpu().numpy(), host.u)
