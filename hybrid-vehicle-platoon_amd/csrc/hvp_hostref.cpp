@@ -52,7 +52,14 @@ void solve_one(const hvp_system& S, const hvp::Consts& C, int role, const double
         n = hvp::enumerate_sequences(S, C, prm[1], [&](uint32_t code, int) {
             hvp::LaneQp<N> q;
             hvp::setup_lane<N>(q, S, C, role, prm, code);
-            hvp::QpOut o = hvp::solve_lane<N>(q, C);
+            hvp::QpOut o = hvp::Solver<N, false>::solve(q, C);
+            if (o.status == 0 && !hvp::pbox_ok<N>(q)) {
+                // relaxed optimum leaves the position box: solve the full QP (exact fallback)
+                hvp::setup_lane<N>(q, S, C, role, prm, code);
+                const int it0 = o.iters;
+                o = hvp::Solver<N, true>::solve(q, C);
+                o.iters += it0;
+            }
             Cand c;
             c.code = code;
             c.cost = o.status == 0 ? hvp::direct_cost<N>(q, S, C, role, prm, code) : o.cost;

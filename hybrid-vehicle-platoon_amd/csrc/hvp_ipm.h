@@ -60,12 +60,25 @@ struct QpOut {
 // packed lower-triangular index
 HVP_HD constexpr int tri(int i, int j) { return i * (i + 1) / 2 + j; }
 
+// Refined hardware reciprocal: v_rcp_f64 estimate + two Newton steps (full double accuracy
+// in 1 + 4 FMA instead of the ~12-instruction IEEE division sequence).
+HVP_HD inline double frcp(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    double r = __builtin_amdgcn_rcp(x);
+    r = fma(r, fma(-x, r, 1.0), r);
+    r = fma(r, fma(-x, r, 1.0), r);
+    return r;
+#else
+    return 1.0 / x;
+#endif
+}
+
 template <int N>
 struct LaneQp {
-    static constexpr int NP = N - 1;        // position-type rows exist for k = 2..N
+    static constexpr int NP = N - 1;              // position-type groups exist for k = 2..N
+    static constexpr int NPX = N > 1 ? N - 1 : 1;
     static constexpr int NT = N * (N + 1) / 2;
-    static constexpr int RV = 6 * N;        // V/U/A rows: 6 per k = 1..N
-    static constexpr int R = RV + 6 * NP;   // + P/SF/SB rows: 6 per k = 2..N
+    static constexpr int NPAIR = 3 * N + NP;      // two-sided rows: V,U,A (k = 1..N), P (k = 2..N)
 
     // ---------------- problem data
     double v0, P1, ts;
@@ -73,164 +86,121 @@ struct LaneQp {
     double vlo[N], vhi[N];    // bounds on v_k
     double ulo[N], uhi[N];    // bounds on v_k - a v_{k-1}
     double pmin, pmax;
-    double hf[NP > 0 ? NP : 1], hb[NP > 0 ? NP : 1];  // pf_k - d_safe, pb_k + d_safe (k = 2..N)
+    double hf[NPX], hb[NPX];  // pf_k - d_safe, pb_k + d_safe (k = 2..N)
     bool has_sf, has_sb;
     double H[NT], f[N], C0;
 
-    // ---------------- iterate
-    double y[N], sf[NP > 0 ? NP : 1], sb[NP > 0 ? NP : 1];
-    double lam[R], t[R];
+    // ---------------- iterate: slack t and multiplier l of both sides of every two-sided row;
+    // for a safe row pair {sgn*p_k - s <= h, -s <= 0} the slack variable s (which is also the
+    // second row's t), the first row's t and both multipliers.
+    double y[N];
+    double tlo[NPAIR], thi[NPAIR], llo[NPAIR], lhi[NPAIR];
+    double sf[NPX], tf[NPX], lf[NPX], lf2[NPX];
+    double sb[NPX], tb[NPX], lb[NPX], lb2[NPX];
 };
 
-// Row layout: for k = 1..N  base 6(k-1): Vlo Vhi Ulo Uhi Alo Ahi
-//             for k = 2..N  base 6N + 6(k-2): Plo Phi SF SF0 SB SB0
-enum { VLO = 0, VHI, ULO, UHI, ALO, AHI };
-enum { PLO = 0, PHI, SFR, SF0, SBR, SB0 };
-
+// bounds of pair p (V,U,A of step k = p/3 + 1; P of step k = p - 3N + 2)
 template <int N>
-HVP_HD inline bool row_active(const LaneQp<N>& q, int i) {
-    if (i < LaneQp<N>::RV) return true;
-    int r = (i - LaneQp<N>::RV) % 6;
-    if (r == SFR || r == SF0) return q.has_sf;
-    if (r == SBR || r == SB0) return q.has_sb;
-    return true;
+HVP_HD inline void pair_bounds(const LaneQp<N>& q, const Consts& C, int p, double& lo, double& hi) {
+    if (p < 3 * N) {
+        const int j = p / 3, r = p % 3;
+        if (r == 0) { lo = q.vlo[j]; hi = q.vhi[j]; }
+        else if (r == 1) { lo = q.ulo[j]; hi = q.uhi[j]; }
+        else { lo = C.dec[j]; hi = C.acc[j]; }
+    } else {
+        lo = q.pmin;
+        hi = q.pmax;
+    }
 }
 
-// Affine row values G z (+ constants when with_const) for z = (y, sf, sb).
-// Calls emit(i, value) for every row.  v_prev of step 1 is the constant v0 (0 for directions),
-// p_k = P1 + ts * cum (P1 -> 0 for directions).
-template <int N, class F>
-HVP_HD inline void for_rows(const LaneQp<N>& q, const double* y, const double* sf, const double* sb, bool with_const,
-                            F&& emit) {
-    double vprev = with_const ? q.v0 : 0.0;
-    double cum = 0.0;
-    const double p1 = with_const ? q.P1 : 0.0;
+// Row-group traversal over three vectors at once: y (with the constants v0 / P1), a and b
+// (directions, no constants).  emit_pair(p, g.y, g.a, g.b); emit_safe(j, p_k(y), g.a, g.b)
+// with g the prefix gradient ts * (e_0 + .. + e_j) of p_{j+2}.
+template <int N, class FP, class FS>
+HVP_HD inline void for_groups3(const LaneQp<N>& q, const double* y, const double* a, const double* b, FP&& emit_pair,
+                               FS&& emit_safe) {
+    double yp = q.v0, ap = 0.0, bp = 0.0;
+    double cy = 0.0, ca = 0.0, cb = 0.0;
 #pragma unroll
     for (int k = 1; k <= N; ++k) {
-        const double vk = y[k - 1];
-        const int b = 6 * (k - 1);
-        const double du = vk - q.am[k - 1] * vprev;
-        const double da = vk - vprev;
-        emit(b + VLO, -vk);
-        emit(b + VHI, vk);
-        emit(b + ULO, -du);
-        emit(b + UHI, du);
-        emit(b + ALO, -da);
-        emit(b + AHI, da);
+        const double yk = y[k - 1], ak = a[k - 1], bk = b[k - 1], am = q.am[k - 1];
+        emit_pair(3 * (k - 1) + 0, yk, ak, bk);
+        emit_pair(3 * (k - 1) + 1, yk - am * yp, ak - am * ap, bk - am * bp);
+        emit_pair(3 * (k - 1) + 2, yk - yp, ak - ap, bk - bp);
         if (k >= 2) {
-            cum += y[k - 2];
-            const double pk = p1 + q.ts * cum;
-            const int c = LaneQp<N>::RV + 6 * (k - 2);
-            emit(c + PLO, -pk);
-            emit(c + PHI, pk);
-            emit(c + SFR, pk - sf[k - 2]);
-            emit(c + SF0, -sf[k - 2]);
-            emit(c + SBR, -pk - sb[k - 2]);
-            emit(c + SB0, -sb[k - 2]);
+            cy += y[k - 2];
+            ca += a[k - 2];
+            cb += b[k - 2];
+            const double py = q.P1 + q.ts * cy, pa = q.ts * ca, pb = q.ts * cb;
+            emit_pair(3 * N + (k - 2), py, pa, pb);
+            emit_safe(k - 2, py, pa, pb);
         }
-        vprev = vk;
+        yp = yk;
+        ap = ak;
+        bp = bk;
+    }
+}
+
+// K += D g g', rhs -= rho g for the gradient shape of pair p (diag / bidiagonal / prefix).
+template <int N>
+HVP_HD inline void scatter_pair(const LaneQp<N>& q, int p, double D, double rho, double* K, double* rhs, double* beta,
+                                double* rpre) {
+    if (p < 3 * N) {
+        const int j = p / 3, r = p % 3;
+        K[tri(j, j)] += D;
+        rhs[j] -= rho;
+        if (r != 0 && j >= 1) {
+            const double a = r == 1 ? q.am[j] : 1.0;
+            K[tri(j - 1, j - 1)] += D * a * a;
+            K[tri(j, j - 1)] -= D * a;
+            rhs[j - 1] += a * rho;
+        }
+    } else {
+        beta[p - 3 * N] += D;
+        rpre[p - 3 * N] += rho;
+    }
+}
+
+// rhs -= rho g only (corrector: the factorised K is reused).
+template <int N>
+HVP_HD inline void scatter_rhs(const LaneQp<N>& q, int p, double rho, double* rhs, double* rpre) {
+    if (p < 3 * N) {
+        const int j = p / 3, r = p % 3;
+        rhs[j] -= rho;
+        if (r != 0 && j >= 1) rhs[j - 1] += (r == 1 ? q.am[j] : 1.0) * rho;
+    } else {
+        rpre[p - 3 * N] += rho;
+    }
+}
+
+// prefix groups: entry (i1, i2) of K receives ts^2 beta of every step whose prefix covers
+// max(i1, i2); rhs[i] -= ts * rho of every step covering i.
+template <int N>
+HVP_HD inline void expand_prefix(const LaneQp<N>& q, const double* beta, const double* rpre, double* K, double* rhs) {
+    double sb_ = 0.0, sr = 0.0;
+    const double ts = q.ts;
+#pragma unroll
+    for (int m = N - 2; m >= 0; --m) {
+        sb_ += beta[m];
+        sr += rpre[m];
+        rhs[m] -= ts * sr;
+        if (K) {
+#pragma unroll
+            for (int i2 = 0; i2 <= m; ++i2) K[tri(m, i2)] += ts * ts * sb_;
+        }
     }
 }
 
 template <int N>
-HVP_HD inline double row_h(const LaneQp<N>& q, const Consts& C, int i) {
-    if (i < LaneQp<N>::RV) {
-        const int k = i / 6, r = i % 6;  // step k+1
-        switch (r) {
-            case VLO: return -q.vlo[k];
-            case VHI: return q.vhi[k];
-            case ULO: return -q.ulo[k];
-            case UHI: return q.uhi[k];
-            case ALO: return -C.dec[k];
-            default: return C.acc[k];
-        }
-    }
-    const int k = (i - LaneQp<N>::RV) / 6, r = (i - LaneQp<N>::RV) % 6;  // step k+2
-    switch (r) {
-        case PLO: return -q.pmin;
-        case PHI: return q.pmax;
-        case SFR: return q.hf[k];
-        case SBR: return -q.hb[k];
-        default: return 0.0;
-    }
-}
-
-// Newton direction of the reduced (y-space) system.
-//   d[i]   : row scaling lambda_i / t_i
-//   rt[i]  : r~_i = r_p,i - r_c,i / lambda_i
-//   rd[N]  : dual residual of y, rsf/rsb: dual residuals of the slacks
-// Outputs dy, dsf, dsb.  K is factorised here (Cholesky, packed).
-template <int N>
-HVP_HD inline bool reduced_solve(const LaneQp<N>& q, const double* d, const double* rt, const double* rd,
-                                 const double* rsf, const double* rsb, double* dy, double* dsf, double* dsb) {
-    constexpr int NT = LaneQp<N>::NT;
-    constexpr int RV = LaneQp<N>::RV;
-    double K[NT];
-    double rhs[N];
-#pragma unroll
-    for (int i = 0; i < NT; ++i) K[i] = q.H[i];
-#pragma unroll
-    for (int j = 0; j < N; ++j) rhs[j] = -rd[j];
-    // V / U / A rows of step k (variable j = k-1)
-#pragma unroll
-    for (int j = 0; j < N; ++j) {
-        const int b = 6 * j;
-        const double DV = d[b + VLO] + d[b + VHI];
-        const double rV = -d[b + VLO] * rt[b + VLO] + d[b + VHI] * rt[b + VHI];
-        const double DU = d[b + ULO] + d[b + UHI];
-        const double rU = -d[b + ULO] * rt[b + ULO] + d[b + UHI] * rt[b + UHI];
-        const double DA = d[b + ALO] + d[b + AHI];
-        const double rA = -d[b + ALO] * rt[b + ALO] + d[b + AHI] * rt[b + AHI];
-        K[tri(j, j)] += DV + DU + DA;
-        rhs[j] -= rV + rU + rA;
-        if (j >= 1) {
-            const double a = q.am[j];
-            K[tri(j - 1, j - 1)] += DU * a * a + DA;
-            K[tri(j, j - 1)] -= DU * a + DA;
-            rhs[j - 1] += a * rU + rA;
-        }
-    }
-    // position-type rows of step k = j+2 act on y[0..j] through ts * prefix
-    if (N >= 2) {
-        double beta[N > 1 ? N - 1 : 1], rho[N > 1 ? N - 1 : 1];
-#pragma unroll
-        for (int j = 0; j < N - 1; ++j) {
-            const int c = RV + 6 * j;
-            double B = d[c + PLO] + d[c + PHI];
-            double r = -d[c + PLO] * rt[c + PLO] + d[c + PHI] * rt[c + PHI];
-            if (q.has_sf) {
-                const double d1 = d[c + SFR], d2 = d[c + SF0], inv = 1.0 / (d1 + d2);
-                B += d1 * d2 * inv;
-                r += (d1 * d2 * (rt[c + SFR] - rt[c + SF0]) + d1 * rsf[j]) * inv;
-            }
-            if (q.has_sb) {
-                const double d1 = d[c + SBR], d2 = d[c + SB0], inv = 1.0 / (d1 + d2);
-                B += d1 * d2 * inv;
-                r -= (d1 * d2 * (rt[c + SBR] - rt[c + SB0]) + d1 * rsb[j]) * inv;
-            }
-            beta[j] = B * q.ts * q.ts;
-            rho[j] = r * q.ts;
-        }
-        // suffix sums: entry (i1, i2) receives beta of every step whose prefix covers max(i1, i2)
-        double sb_ = 0.0, sr = 0.0;
-#pragma unroll
-        for (int m = N - 2; m >= 0; --m) {
-            sb_ += beta[m];
-            sr += rho[m];
-            rhs[m] -= sr;
-#pragma unroll
-            for (int i2 = 0; i2 <= m; ++i2) K[tri(m, i2)] += sb_;
-        }
-    }
-    // Cholesky K = L L^T (in place, packed)
+HVP_HD inline bool cholesky(double* K) {
 #pragma unroll
     for (int j = 0; j < N; ++j) {
         double s = K[tri(j, j)];
 #pragma unroll
         for (int k = 0; k < j; ++k) s -= K[tri(j, k)] * K[tri(j, k)];
         if (!(s > 0.0)) return false;
-        const double l = sqrt(s), il = 1.0 / l;
-        K[tri(j, j)] = l;
+        const double il = frcp(sqrt(s));
+        K[tri(j, j)] = il;  // the inverse diagonal is stored
 #pragma unroll
         for (int i = j + 1; i < N; ++i) {
             double v = K[tri(i, j)];
@@ -239,265 +209,505 @@ HVP_HD inline bool reduced_solve(const LaneQp<N>& q, const double* d, const doub
             K[tri(i, j)] = v * il;
         }
     }
+    return true;
+}
+
+template <int N>
+HVP_HD inline void chol_solve(const double* L, const double* rhs, double* x) {
 #pragma unroll
     for (int i = 0; i < N; ++i) {
         double v = rhs[i];
 #pragma unroll
-        for (int k = 0; k < i; ++k) v -= K[tri(i, k)] * dy[k];
-        dy[i] = v / K[tri(i, i)];
+        for (int k = 0; k < i; ++k) v -= L[tri(i, k)] * x[k];
+        x[i] = v * L[tri(i, i)];
     }
 #pragma unroll
     for (int i = N - 1; i >= 0; --i) {
-        double v = dy[i];
+        double v = x[i];
 #pragma unroll
-        for (int k = i + 1; k < N; ++k) v -= K[tri(k, i)] * dy[k];
-        dy[i] = v / K[tri(i, i)];
+        for (int k = i + 1; k < N; ++k) v -= L[tri(k, i)] * x[k];
+        x[i] = v * L[tri(i, i)];
     }
-    // slack directions (eliminated 2x2 blocks)
-    double cum = 0.0;
-#pragma unroll
-    for (int j = 0; j < N - 1; ++j) {
-        cum += dy[j];
-        const int c = RV + 6 * j;
-        const double gdy = q.ts * cum;
-        if (q.has_sf) {
-            const double d1 = d[c + SFR], d2 = d[c + SF0];
-            dsf[j] = (d1 * gdy + d1 * rt[c + SFR] + d2 * rt[c + SF0] - rsf[j]) / (d1 + d2);
+}
+
+// ---------------------------------------------------------------- row algebra
+// Generic row  val(z) <= h  with slack t, multiplier l, primal residual r = val + t - h,
+// scaling d = l / t and  rt = r - rc / l :
+//   dl = d (g.dz + rt),   dt = -r - g.dz,   predictor rc = l t,   corrector rc = l t + dl_a dt_a - s mu
+//
+// Two-sided pair lo <= g.y <= hi (rows -g.y <= -lo and g.y <= hi):
+struct PairRow {
+    double rlo, rhi, dlo, dhi;
+    HVP_HD PairRow(double gy, double lo, double hi, double tlo, double thi, double llo, double lhi) {
+        rlo = -gy + tlo + lo;
+        rhi = gy + thi - hi;
+        dlo = llo * frcp(tlo);
+        dhi = lhi * frcp(thi);
+    }
+    // direction for g.dy = gd and scaled residuals rtlo / rthi
+    HVP_HD void dir(double gd, double rtlo, double rthi, double& dtlo, double& dthi, double& dllo, double& dlhi) const {
+        dtlo = -rlo + gd;
+        dthi = -rhi - gd;
+        dllo = dlo * (rtlo - gd);
+        dlhi = dhi * (rthi + gd);
+    }
+};
+
+// Safe pair: row 1  sgn * p_k - s <= h1 (t1, l1), row 2  -s <= 0 (t2 == s, l2); the slack s
+// is eliminated with its dual residual r_s = w - l1 - l2 (K gets e g g', rhs gets c g).
+struct SafeRow {
+    double r1, d1, d2, ie, rs;
+    HVP_HD SafeRow(double sgn_pk, double h1, double s, double t1, double l1, double l2, double w) {
+        r1 = sgn_pk - s + t1 - h1;
+        d1 = l1 * frcp(t1);
+        d2 = l2 * frcp(s);
+        ie = frcp(d1 + d2);
+        rs = w - l1 - l2;
+    }
+    HVP_HD double e() const { return d1 * d2 * ie; }
+    HVP_HD double c(double rt1, double rt2) const { return (d1 * d2 * (rt1 - rt2) + d1 * rs) * ie; }
+    // gd = sgn * (prefix gradient . dy)
+    HVP_HD void dir(double gd, double rt1, double rt2, double& ds, double& dt1, double& dl1, double& dl2) const {
+        ds = (d1 * (gd + rt1) + d2 * rt2 - rs) * ie;
+        dl1 = d1 * (gd - ds + rt1);
+        dl2 = d2 * (rt2 - ds);
+        dt1 = -r1 - gd + ds;
+    }
+};
+
+// Ratio test with the raw hardware reciprocal: the step is scaled by 0.99 afterwards, so a
+// relative error of ~1e-8 in the limit is harmless and saves the Newton refinement.
+HVP_HD inline double rcp_approx(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_rcp(x);
+#else
+    return 1.0 / x;
+#endif
+}
+HVP_HD inline void ratio_test(double& a, double v, double dv) {
+    const double r = -v * rcp_approx(dv);
+    a = dv < 0.0 ? fmin(a, r) : a;
+}
+
+// Accumulators of one assembly of the reduced system.
+template <int N>
+struct Assembly {
+    static constexpr int NPX = N > 1 ? N - 1 : 1;
+    double K[N * (N + 1) / 2];
+    double rhs[N];            // - sum_rows d rt g   (the -rd part is added at the end)
+    double beta[NPX], rpre[NPX];
+    double lam_pre[NPX];      // prefix part of sum lam g
+    double rd[N];             // non-prefix part of sum lam g
+    double gap, rpmax, rsmax;
+};
+
+// Row set: two-sided pairs V, U, A for every step (and P when PBOX), safe pairs for k >= 2.
+// PBOX = false drops the position-box rows 0 <= p_k <= 10000 (never active for a platoon:
+// the caller verifies the solution and re-solves the rare violator with PBOX = true, which is
+// exact: a relaxed optimum that satisfies the dropped rows is the optimum).
+template <int N, bool PBOX>
+struct Solver {
+    static constexpr int NP = N - 1;
+    static constexpr int NPX = N > 1 ? N - 1 : 1;
+    static constexpr int NT = N * (N + 1) / 2;
+    static constexpr int NPAIR_ACTIVE = 3 * N + (PBOX ? NP : 0);
+
+    // traversal over (y, a, b) skipping the P pairs when !PBOX
+    template <class FP, class FS>
+    HVP_HD static void groups(const LaneQp<N>& q, const double* y, const double* a, const double* b, FP&& fp,
+                              FS&& fs) {
+        for_groups3(
+            q, y, a, b,
+            [&](int p, double gy, double ga, double gb) {
+                if (PBOX || p < 3 * N) fp(p, gy, ga, gb);
+            },
+            fs);
+    }
+
+    // contributions of the state (tlo, thi, llo, lhi / s, t1, l1, l2) at row values gy / pk
+    HVP_HD static void assemble_pair(const LaneQp<N>& q, const Consts& C, Assembly<N>& A, int p, double gy) {
+        double lo, hi;
+        pair_bounds(q, C, p, lo, hi);
+        const double tl = q.tlo[p], th = q.thi[p], ll = q.llo[p], lh = q.lhi[p];
+        const PairRow R(gy, lo, hi, tl, th, ll, lh);
+        A.gap += ll * tl + lh * th;
+        A.rpmax = fmax(A.rpmax, fmax(fabs(R.rlo), fabs(R.rhi)));
+        // predictor rt = r - t ; rho = -dlo rtlo + dhi rthi ; dual part (lhi - llo) g
+        const double rho = -R.dlo * (R.rlo - tl) + R.dhi * (R.rhi - th);
+        double Kd[1];
+        (void)Kd;
+        if (p < 3 * N) {
+            const int j = p / 3, r = p % 3;
+            const double D = R.dlo + R.dhi, lg = lh - ll;
+            A.K[tri(j, j)] += D;
+            A.rhs[j] -= rho;
+            A.rd[j] += lg;
+            if (r != 0 && j >= 1) {
+                const double am = r == 1 ? q.am[j] : 1.0;
+                A.K[tri(j - 1, j - 1)] += D * am * am;
+                A.K[tri(j, j - 1)] -= D * am;
+                A.rhs[j - 1] += am * rho;
+                A.rd[j - 1] -= am * lg;
+            }
         } else {
-            dsf[j] = 0.0;
-        }
-        if (q.has_sb) {
-            const double d1 = d[c + SBR], d2 = d[c + SB0];
-            dsb[j] = (-d1 * gdy + d1 * rt[c + SBR] + d2 * rt[c + SB0] - rsb[j]) / (d1 + d2);
-        } else {
-            dsb[j] = 0.0;
+            const int j = p - 3 * N;
+            A.beta[j] += R.dlo + R.dhi;
+            A.rpre[j] += rho;
+            A.lam_pre[j] += lh - ll;
         }
     }
-    return true;
-}
+    HVP_HD static void assemble_safe(const LaneQp<N>& q, Assembly<N>& A, int j, double sgn, double sgnpk, double h1,
+                                     double s, double t1, double l1, double l2, double w) {
+        const SafeRow R(sgnpk, h1, s, t1, l1, l2, w);
+        A.gap += l1 * t1 + l2 * s;
+        A.rpmax = fmax(A.rpmax, fabs(R.r1));
+        A.rsmax = fmax(A.rsmax, fabs(R.rs));
+        A.beta[j] += R.e();
+        A.rpre[j] += sgn * R.c(R.r1 - t1, -s);
+        A.lam_pre[j] += sgn * l1;
+    }
 
-// Dual residuals r_d = H y + f + G_y' lam and r_s = w - lam_row - lam_nonneg.
-template <int N>
-HVP_HD inline void dual_residual(const LaneQp<N>& q, const Consts& C, const double* y, const double* lam, double* rd,
-                                 double* rsf, double* rsb) {
-    constexpr int RV = LaneQp<N>::RV;
+    HVP_HD static void assemble_begin(const LaneQp<N>& q, Assembly<N>& A) {
 #pragma unroll
-    for (int i = 0; i < N; ++i) {
-        double s = q.f[i];
+        for (int i = 0; i < NT; ++i) A.K[i] = q.H[i];
 #pragma unroll
-        for (int j = 0; j < N; ++j) s += q.H[i >= j ? tri(i, j) : tri(j, i)] * y[j];
-        rd[i] = s;
+        for (int i = 0; i < N; ++i) { A.rhs[i] = 0.0; A.rd[i] = 0.0; }
+#pragma unroll
+        for (int i = 0; i < NPX; ++i) { A.beta[i] = 0.0; A.rpre[i] = 0.0; A.lam_pre[i] = 0.0; }
+        A.gap = 0.0;
+        A.rpmax = 0.0;
+        A.rsmax = 0.0;
     }
+    // finish: rd = H y + f + G'lam ; rhs = -rd - sum d rt g ; K prefix expansion
+    HVP_HD static void assemble_end(const LaneQp<N>& q, Assembly<N>& A, const double* y) {
+        double sb_ = 0.0, sr = 0.0, sl = 0.0;
+        const double ts = q.ts;
 #pragma unroll
-    for (int j = 0; j < N; ++j) {
-        const int b = 6 * j;
-        const double lU = lam[b + UHI] - lam[b + ULO];
-        rd[j] += lam[b + VHI] - lam[b + VLO] + lU + lam[b + AHI] - lam[b + ALO];
-        if (j >= 1) rd[j - 1] -= q.am[j] * lU + (lam[b + AHI] - lam[b + ALO]);
-    }
-    double s = 0.0;
+        for (int m = N - 2; m >= 0; --m) {
+            sb_ += A.beta[m];
+            sr += A.rpre[m];
+            sl += A.lam_pre[m];
+            A.rhs[m] -= ts * sr;
+            A.rd[m] += ts * sl;
 #pragma unroll
-    for (int m = N - 2; m >= 0; --m) {
-        const int c = RV + 6 * m;
-        double g = lam[c + PHI] - lam[c + PLO];
-        if (q.has_sf) g += lam[c + SFR];
-        if (q.has_sb) g -= lam[c + SBR];
-        s += g;
-        rd[m] += q.ts * s;
-        rsf[m] = q.has_sf ? C.w - lam[c + SFR] - lam[c + SF0] : 0.0;
-        rsb[m] = q.has_sb ? C.w - lam[c + SBR] - lam[c + SB0] : 0.0;
+            for (int i2 = 0; i2 <= m; ++i2) A.K[tri(m, i2)] += ts * ts * sb_;
+        }
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            double s = q.f[i];
+#pragma unroll
+            for (int j = 0; j < N; ++j) s += q.H[i >= j ? tri(i, j) : tri(j, i)] * y[j];
+            A.rd[i] += s;
+            A.rhs[i] -= A.rd[i];
+        }
     }
-}
 
-template <int N>
-HVP_HD inline double objective(const LaneQp<N>& q, const Consts& C, const double* y) {
-    double J = q.C0;
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-        double hy = 0.0;
-#pragma unroll
-        for (int j = 0; j < N; ++j) hy += q.H[i >= j ? tri(i, j) : tri(j, i)] * y[j];
-        J += (0.5 * hy + q.f[i]) * y[i];
-    }
-    // exact penalty of the safe rows at y (= w * optimal slack)
-    double cum = 0.0;
-#pragma unroll
-    for (int j = 0; j < N - 1; ++j) {
-        cum += y[j];
-        const double pk = q.P1 + q.ts * cum;
-        if (q.has_sf) J += C.w * fmax(0.0, pk - q.hf[j]);
-        if (q.has_sb) J += C.w * fmax(0.0, q.hb[j] - pk);
-    }
-    return J;
-}
+    HVP_HD static QpOut solve(LaneQp<N>& q, const Consts& C) {
+        QpOut out{0.0, 2, 0};
+        const double w = C.w;
+        const int m = 2 * NPAIR_ACTIVE + (q.has_sf ? 2 * NP : 0) + (q.has_sb ? 2 * NP : 0);
+        const double zero[N] = {};
 
-template <int N>
-HVP_HD inline double max_step(const double* v, const double* dv, const LaneQp<N>& q) {
-    double a = 1.0;
+        // =============== initial point (CVXOPT / Mehrotra): minimise 1/2 y'Hy + f'y + w 1's
+        // + 1/2 |h - Gz|^2 (one unit-scaled reduced solve from z = t = lam = 0), then
+        // t = h - Gz, lam = -t, both shifted into the interior and centred.
+        {
+            double K[NT], rhs[N], beta[NPX], rpre[NPX];
 #pragma unroll
-    for (int i = 0; i < LaneQp<N>::R; ++i)
-        if (row_active(q, i) && dv[i] < 0.0) a = fmin(a, -v[i] / dv[i]);
-    return a;
-}
+            for (int i = 0; i < NT; ++i) K[i] = q.H[i];
+#pragma unroll
+            for (int i = 0; i < N; ++i) rhs[i] = -q.f[i];
+#pragma unroll
+            for (int i = 0; i < NPX; ++i) { beta[i] = 0.0; rpre[i] = 0.0; }
+            groups(q, zero, zero, zero,
+                   [&](int p, double gy, double, double) {
+                       double lo, hi;
+                       pair_bounds(q, C, p, lo, hi);
+                       scatter_pair(q, p, 2.0, -(-gy + lo) + (gy - hi), K, rhs, beta, rpre);
+                   },
+                   [&](int j, double pk, double, double) {
+                       if (q.has_sf) { beta[j] += 0.5; rpre[j] += 0.5 * ((pk - q.hf[j]) + w); }
+                       if (q.has_sb) { beta[j] += 0.5; rpre[j] -= 0.5 * ((-pk + q.hb[j]) + w); }
+                   });
+            expand_prefix<N>(q, beta, rpre, K, rhs);
+            if (!cholesky<N>(K)) return out;
+            chol_solve<N>(K, rhs, q.y);
+            double tmin = 1e300, tmax = -1e300;
+            groups(q, q.y, zero, zero,
+                   [&](int p, double gy, double, double) {
+                       double lo, hi;
+                       pair_bounds(q, C, p, lo, hi);
+                       q.tlo[p] = gy - lo;
+                       q.thi[p] = hi - gy;
+                       tmin = fmin(tmin, fmin(q.tlo[p], q.thi[p]));
+                       tmax = fmax(tmax, fmax(q.tlo[p], q.thi[p]));
+                   },
+                   [&](int j, double pk, double, double) {
+                       // slack of the unit solve: s = (g.y + rt1 - r_s) / 2 = (sgn p_k - h - w) / 2
+                       if (q.has_sf) {
+                           const double s = 0.5 * (pk - q.hf[j] - w);
+                           q.sf[j] = s;
+                           q.tf[j] = q.hf[j] - (pk - s);
+                           tmin = fmin(tmin, fmin(q.tf[j], s));
+                           tmax = fmax(tmax, fmax(q.tf[j], s));
+                       }
+                       if (q.has_sb) {
+                           const double s = 0.5 * (-pk + q.hb[j] - w);
+                           q.sb[j] = s;
+                           q.tb[j] = -q.hb[j] - (-pk - s);
+                           tmin = fmin(tmin, fmin(q.tb[j], s));
+                           tmax = fmax(tmax, fmax(q.tb[j], s));
+                       }
+                   });
+            const double st = fmax(-1.5 * tmin, 0.0), sl = fmax(1.5 * tmax, 0.0);  // lam = -t
+            double tl = 0.0, tsum = 0.0, lsum = 0.0;
+            auto acc = [&](double t) {
+                const double tt = t + st, ll = -t + sl;
+                tl += tt * ll;
+                tsum += tt;
+                lsum += ll;
+            };
+            groups(q, zero, zero, zero, [&](int p, double, double, double) { acc(q.tlo[p]); acc(q.thi[p]); },
+                   [&](int j, double, double, double) {
+                       if (q.has_sf) { acc(q.tf[j]); acc(q.sf[j]); }
+                       if (q.has_sb) { acc(q.tb[j]); acc(q.sb[j]); }
+                   });
+            const double dt0 = lsum > 0 ? 0.5 * tl / lsum : 1.0, dl0 = tsum > 0 ? 0.5 * tl / tsum : 1.0;
+            auto fix = [&](double& t, double& l) {
+                const double t0v = t;
+                t = t0v + st + dt0;
+                l = -t0v + sl + dl0;
+                t = t > 0.0 ? t : 1.0;
+                l = l > 0.0 ? l : 1.0;
+            };
+            groups(q, zero, zero, zero,
+                   [&](int p, double, double, double) { fix(q.tlo[p], q.llo[p]); fix(q.thi[p], q.lhi[p]); },
+                   [&](int j, double, double, double) {
+                       if (q.has_sf) { fix(q.tf[j], q.lf[j]); fix(q.sf[j], q.lf2[j]); }
+                       if (q.has_sb) { fix(q.tb[j], q.lb[j]); fix(q.sb[j], q.lb2[j]); }
+                   });
+        }
 
-// Mehrotra predictor-corrector.  Returns objective (exact penalty form) and status.
+        double sq = fmax(1.0, w);
+#pragma unroll
+        for (int i = 0; i < N; ++i) sq = fmax(sq, fabs(q.f[i]));
+        const double sh = fmax(fmax(1.0, fabs(q.pmax)), fmax(fabs(q.pmin), fmax(fabs(q.P1), 1e4)));
+
+        // =============== assembly at the initial point
+        Assembly<N> A;
+        assemble_begin(q, A);
+        groups(q, q.y, zero, zero, [&](int p, double gy, double, double) { assemble_pair(q, C, A, p, gy); },
+               [&](int j, double pk, double, double) {
+                   if (q.has_sf) assemble_safe(q, A, j, 1.0, pk, q.hf[j], q.sf[j], q.tf[j], q.lf[j], q.lf2[j], w);
+                   if (q.has_sb) assemble_safe(q, A, j, -1.0, -pk, -q.hb[j], q.sb[j], q.tb[j], q.lb[j], q.lb2[j], w);
+               });
+        assemble_end(q, A, q.y);
+
+        const int maxit = C.max_iter;
+        double dya[N], dy[N];
+        for (int it = 0; it <= maxit; ++it) {
+            // ------------------------------------------------ convergence
+            double rdmax = A.rsmax;
+#pragma unroll
+            for (int i = 0; i < N; ++i) rdmax = fmax(rdmax, fabs(A.rd[i]));
+            double J = q.C0;
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                double hy = 0.0;
+#pragma unroll
+                for (int j = 0; j < N; ++j) hy += q.H[i >= j ? tri(i, j) : tri(j, i)] * q.y[j];
+                J += (0.5 * hy + q.f[i]) * q.y[i];
+            }
+            out.iters = it;
+            if (rdmax <= C.tol * sq && A.rpmax <= C.tol * sh && A.gap <= 0.1 * C.tol * fmax(1.0, fabs(J))) {
+                out.status = 0;
+                return out;
+            }
+            if (it == maxit) {
+                // fp64 floor: accept a solution that meets a 1e3-looser tolerance
+                if (rdmax <= 1e3 * C.tol * sq && A.rpmax <= 1e3 * C.tol * sh &&
+                    A.gap <= 1e2 * C.tol * fmax(1.0, fabs(J)))
+                    out.status = 0;
+                return out;
+            }
+            if (!cholesky<N>(A.K)) break;
+            chol_solve<N>(A.K, A.rhs, dya);
+            const double mu = A.gap / m;
+
+            // ------------------------------------------------ pass X: affine step, centring and the
+            // corrector rhs split as  rhsA + sigma mu * rhsB  (linear in sigma mu)
+            double amax_a = 1.0, S1 = 0.0, S2 = 0.0;
+            double rA[N], rB[N], pA[NPX], pB[NPX];
+#pragma unroll
+            for (int i = 0; i < N; ++i) { rA[i] = 0.0; rB[i] = 0.0; }
+#pragma unroll
+            for (int i = 0; i < NPX; ++i) { pA[i] = 0.0; pB[i] = 0.0; }
+            groups(q, q.y, dya, zero,
+                   [&](int p, double gy, double ga, double) {
+                       double lo, hi;
+                       pair_bounds(q, C, p, lo, hi);
+                       const double tl = q.tlo[p], th = q.thi[p], ll = q.llo[p], lh = q.lhi[p];
+                       const PairRow R(gy, lo, hi, tl, th, ll, lh);
+                       double dtl, dth, dll, dlh;
+                       R.dir(ga, R.rlo - tl, R.rhi - th, dtl, dth, dll, dlh);
+                       ratio_test(amax_a, tl, dtl);
+                       ratio_test(amax_a, th, dth);
+                       ratio_test(amax_a, ll, dll);
+                       ratio_test(amax_a, lh, dlh);
+                       S1 += ll * dtl + tl * dll + lh * dth + th * dlh;
+                       S2 += dll * dtl + dlh * dth;
+                       // rt_c = r - t - (dl_a dt_a)/l + sigma mu / l ; d / l = 1 / t
+                       const double rtlA = R.rlo - tl - dll * dtl * frcp(ll);
+                       const double rthA = R.rhi - th - dlh * dth * frcp(lh);
+                       const double rhoA = -R.dlo * rtlA + R.dhi * rthA;
+                       const double rhoB = -frcp(tl) + frcp(th);
+                       scatter_rhs(q, p, rhoA, rA, pA);
+                       scatter_rhs(q, p, rhoB, rB, pB);
+                   },
+                   [&](int j, double pk, double ga, double) {
+                       auto safe = [&](double sgn, double h1, double s, double t1, double l1, double l2) {
+                           const SafeRow R(sgn * pk, h1, s, t1, l1, l2, w);
+                           double ds, dt1, dl1, dl2;
+                           R.dir(sgn * ga, R.r1 - t1, -s, ds, dt1, dl1, dl2);
+                           ratio_test(amax_a, s, ds);
+                           ratio_test(amax_a, t1, dt1);
+                           ratio_test(amax_a, l1, dl1);
+                           ratio_test(amax_a, l2, dl2);
+                           S1 += l1 * dt1 + t1 * dl1 + l2 * ds + s * dl2;
+                           S2 += dl1 * dt1 + dl2 * ds;
+                           const double rt1A = R.r1 - t1 - dl1 * dt1 * frcp(l1);
+                           const double rt2A = -s - dl2 * ds * frcp(l2);
+                           pA[j] += sgn * R.c(rt1A, rt2A);
+                           pB[j] += sgn * R.d1 * R.d2 * R.ie * (frcp(l1) - frcp(l2));
+                       };
+                       if (q.has_sf) safe(1.0, q.hf[j], q.sf[j], q.tf[j], q.lf[j], q.lf2[j]);
+                       if (q.has_sb) safe(-1.0, -q.hb[j], q.sb[j], q.tb[j], q.lb[j], q.lb2[j]);
+                   });
+            const double mua = (A.gap + amax_a * S1 + amax_a * amax_a * S2) / m;
+            const double sr = fmax(mua, 0.0) / mu;
+            const double smu = sr * sr * sr * mu;
+            {
+                double rhs[N];
+                double sa = 0.0, sb_ = 0.0;
+#pragma unroll
+                for (int mm = N - 2; mm >= 0; --mm) {
+                    sa += pA[mm];
+                    sb_ += pB[mm];
+                    rA[mm] -= q.ts * sa;
+                    rB[mm] -= q.ts * sb_;
+                }
+                // rA / rB hold -sum rho g (scatter_rhs subtracts)
+#pragma unroll
+                for (int i = 0; i < N; ++i) rhs[i] = -A.rd[i] + rA[i] + smu * rB[i];
+                chol_solve<N>(A.K, rhs, dy);
+            }
+
+            // ------------------------------------------------ pass Y: corrector step length
+            // corrector scaled residuals of a row from its affine direction
+            auto pair_dirs = [&](const PairRow& R, double ga, double gd, double tl, double th, double ll, double lh,
+                                 double& dtl, double& dth, double& dll, double& dlh) {
+                double atl, ath, all_, alh;
+                R.dir(ga, R.rlo - tl, R.rhi - th, atl, ath, all_, alh);
+                const double rtl = R.rlo - tl - (all_ * atl - smu) * frcp(ll);
+                const double rth = R.rhi - th - (alh * ath - smu) * frcp(lh);
+                R.dir(gd, rtl, rth, dtl, dth, dll, dlh);
+            };
+            auto safe_dirs = [&](const SafeRow& R, double ga, double gd, double s, double t1, double l1, double l2,
+                                 double& ds, double& dt1, double& dl1, double& dl2) {
+                double as, at1, al1, al2;
+                R.dir(ga, R.r1 - t1, -s, as, at1, al1, al2);
+                const double rt1 = R.r1 - t1 - (al1 * at1 - smu) * frcp(l1);
+                const double rt2 = -s - (al2 * as - smu) * frcp(l2);
+                R.dir(gd, rt1, rt2, ds, dt1, dl1, dl2);
+            };
+            double amax = 1.0;
+            groups(q, q.y, dya, dy,
+                   [&](int p, double gy, double ga, double gd) {
+                       double lo, hi;
+                       pair_bounds(q, C, p, lo, hi);
+                       const double tl = q.tlo[p], th = q.thi[p], ll = q.llo[p], lh = q.lhi[p];
+                       const PairRow R(gy, lo, hi, tl, th, ll, lh);
+                       double dtl, dth, dll, dlh;
+                       pair_dirs(R, ga, gd, tl, th, ll, lh, dtl, dth, dll, dlh);
+                       ratio_test(amax, tl, dtl);
+                       ratio_test(amax, th, dth);
+                       ratio_test(amax, ll, dll);
+                       ratio_test(amax, lh, dlh);
+                   },
+                   [&](int j, double pk, double ga, double gd) {
+                       auto safe = [&](double sgn, double h1, double s, double t1, double l1, double l2) {
+                           const SafeRow R(sgn * pk, h1, s, t1, l1, l2, w);
+                           double ds, dt1, dl1, dl2;
+                           safe_dirs(R, sgn * ga, sgn * gd, s, t1, l1, l2, ds, dt1, dl1, dl2);
+                           ratio_test(amax, s, ds);
+                           ratio_test(amax, t1, dt1);
+                           ratio_test(amax, l1, dl1);
+                           ratio_test(amax, l2, dl2);
+                       };
+                       if (q.has_sf) safe(1.0, q.hf[j], q.sf[j], q.tf[j], q.lf[j], q.lf2[j]);
+                       if (q.has_sb) safe(-1.0, -q.hb[j], q.sb[j], q.tb[j], q.lb[j], q.lb2[j]);
+                   });
+            const double alpha = fmin(1.0, 0.99 * amax);
+
+            // ------------------------------------------------ pass Z: update + next assembly
+            double ynew[N];
+#pragma unroll
+            for (int i = 0; i < N; ++i) ynew[i] = q.y[i] + alpha * dy[i];
+            assemble_begin(q, A);
+            groups(q, q.y, dya, dy,
+                   [&](int p, double gy, double ga, double gd) {
+                       double lo, hi;
+                       pair_bounds(q, C, p, lo, hi);
+                       const double tl = q.tlo[p], th = q.thi[p], ll = q.llo[p], lh = q.lhi[p];
+                       const PairRow R(gy, lo, hi, tl, th, ll, lh);
+                       double dtl, dth, dll, dlh;
+                       pair_dirs(R, ga, gd, tl, th, ll, lh, dtl, dth, dll, dlh);
+                       q.tlo[p] = tl + alpha * dtl;
+                       q.thi[p] = th + alpha * dth;
+                       q.llo[p] = ll + alpha * dll;
+                       q.lhi[p] = lh + alpha * dlh;
+                       assemble_pair(q, C, A, p, gy + alpha * gd);
+                   },
+                   [&](int j, double pk, double ga, double gd) {
+                       auto safe = [&](double sgn, double h1, double& s, double& t1, double& l1, double& l2) {
+                           const SafeRow R(sgn * pk, h1, s, t1, l1, l2, w);
+                           double ds, dt1, dl1, dl2;
+                           safe_dirs(R, sgn * ga, sgn * gd, s, t1, l1, l2, ds, dt1, dl1, dl2);
+                           s += alpha * ds;
+                           t1 += alpha * dt1;
+                           l1 += alpha * dl1;
+                           l2 += alpha * dl2;
+                           assemble_safe(q, A, j, sgn, sgn * (pk + alpha * gd), h1, s, t1, l1, l2, w);
+                       };
+                       if (q.has_sf) safe(1.0, q.hf[j], q.sf[j], q.tf[j], q.lf[j], q.lf2[j]);
+                       if (q.has_sb) safe(-1.0, -q.hb[j], q.sb[j], q.tb[j], q.lb[j], q.lb2[j]);
+                   });
+#pragma unroll
+            for (int i = 0; i < N; ++i) q.y[i] = ynew[i];
+            assemble_end(q, A, q.y);
+        }
+        out.status = 2;
+        return out;
+    }
+};
+
 template <int N>
 HVP_HD inline QpOut solve_lane(LaneQp<N>& q, const Consts& C) {
-    constexpr int R = LaneQp<N>::R;
-    constexpr int NP1 = N > 1 ? N - 1 : 1;
-    double h[R];
-    int m = 0;
-#pragma unroll
-    for (int i = 0; i < R; ++i) {
-        h[i] = row_h(q, C, i);
-        m += row_active(q, i) ? 1 : 0;
-    }
-    double val[R], rp[R], d[R], rt[R], dl[R], dt[R];
-    double rd[N], rsf[NP1], rsb[NP1], dy[N], dsf[NP1], dsb[NP1];
-    QpOut out{0.0, 2, 0};
+    return Solver<N, true>::solve(q, C);
+}
 
-    // ---- initial point: one reduced solve with unit scaling from (y, s, t, lam) = 0
-    {
-        const double zero[N > 0 ? N : 1] = {};
-        const double zs[NP1] = {};
-        for_rows(q, zero, zs, zs, true, [&](int i, double v) { val[i] = v; });
+// Position-box check of a relaxed (PBOX = false) solution: p_k in [pmin, pmax] for k = 2..N.
+template <int N>
+HVP_HD inline bool pbox_ok(const LaneQp<N>& q) {
+    double cum = 0.0;
+    const double tol = 1e-9 * (1.0 + fmax(fabs(q.pmin), fabs(q.pmax)));
 #pragma unroll
-        for (int i = 0; i < R; ++i) {
-            d[i] = row_active(q, i) ? 1.0 : 0.0;
-            rt[i] = val[i] - h[i];
-        }
-#pragma unroll
-        for (int i = 0; i < N; ++i) rd[i] = q.f[i];
-#pragma unroll
-        for (int j = 0; j < NP1; ++j) { rsf[j] = q.has_sf ? C.w : 0.0; rsb[j] = q.has_sb ? C.w : 0.0; }
-        // masked rows: d = 0 would make the slack blocks singular; give them unit weight there
-        if (!q.has_sf)
-#pragma unroll
-            for (int j = 0; j < N - 1; ++j) { d[LaneQp<N>::RV + 6 * j + SFR] = 1.0; d[LaneQp<N>::RV + 6 * j + SF0] = 1.0; }
-        if (!q.has_sb)
-#pragma unroll
-            for (int j = 0; j < N - 1; ++j) { d[LaneQp<N>::RV + 6 * j + SBR] = 1.0; d[LaneQp<N>::RV + 6 * j + SB0] = 1.0; }
-        if (!reduced_solve(q, d, rt, rd, rsf, rsb, q.y, q.sf, q.sb)) return out;
-        for_rows(q, q.y, q.sf, q.sb, true, [&](int i, double v) { val[i] = v; });
-        double tmin = 1e300, lmin = 1e300;
-#pragma unroll
-        for (int i = 0; i < R; ++i) {
-            q.t[i] = h[i] - val[i];
-            q.lam[i] = -q.t[i];
-            if (row_active(q, i)) { tmin = fmin(tmin, q.t[i]); lmin = fmin(lmin, q.lam[i]); }
-        }
-        const double st = fmax(-1.5 * tmin, 0.0), sl = fmax(-1.5 * lmin, 0.0);
-        double tl = 0.0, ssum = 0.0, lsum = 0.0;
-#pragma unroll
-        for (int i = 0; i < R; ++i) {
-            q.t[i] += st;
-            q.lam[i] += sl;
-            if (row_active(q, i)) { tl += q.t[i] * q.lam[i]; ssum += q.t[i]; lsum += q.lam[i]; }
-        }
-        const double dt0 = lsum > 0 ? 0.5 * tl / lsum : 1.0, dl0 = ssum > 0 ? 0.5 * tl / ssum : 1.0;
-#pragma unroll
-        for (int i = 0; i < R; ++i) {
-            q.t[i] += dt0;
-            q.lam[i] += dl0;
-            if (!(q.t[i] > 0.0)) q.t[i] = 1.0;
-            if (!(q.lam[i] > 0.0)) q.lam[i] = 1.0;
-            if (!row_active(q, i)) { q.t[i] = 1.0; q.lam[i] = 0.0; }
-        }
+    for (int j = 0; j < N - 1; ++j) {
+        cum += q.y[j];
+        const double pk = q.P1 + q.ts * cum;
+        if (pk < q.pmin - tol || pk > q.pmax + tol) return false;
     }
-
-    double sq = fmax(1.0, C.w);
-#pragma unroll
-    for (int i = 0; i < N; ++i) sq = fmax(sq, fabs(q.f[i]));
-    double sh = 1.0;
-#pragma unroll
-    for (int i = 0; i < R; ++i)
-        if (row_active(q, i)) sh = fmax(sh, fabs(h[i]));
-
-    const int maxit = C.max_iter;
-    for (int it = 0; it <= maxit; ++it) {
-        // ---- residuals
-        for_rows(q, q.y, q.sf, q.sb, true, [&](int i, double v) { val[i] = v; });
-        double gap = 0.0, rpmax = 0.0;
-#pragma unroll
-        for (int i = 0; i < R; ++i) {
-            rp[i] = val[i] + q.t[i] - h[i];
-            if (row_active(q, i)) {
-                gap += q.lam[i] * q.t[i];
-                rpmax = fmax(rpmax, fabs(rp[i]));
-            }
-        }
-        dual_residual(q, C, q.y, q.lam, rd, rsf, rsb);
-        double rdmax = 0.0;
-#pragma unroll
-        for (int i = 0; i < N; ++i) rdmax = fmax(rdmax, fabs(rd[i]));
-#pragma unroll
-        for (int j = 0; j < N - 1; ++j) rdmax = fmax(rdmax, fmax(fabs(rsf[j]), fabs(rsb[j])));
-        const double J = objective(q, C, q.y);
-        out.iters = it;
-        if (rdmax <= C.tol * sq && rpmax <= C.tol * sh && gap <= 0.1 * C.tol * fmax(1.0, fabs(J))) {
-            out.status = 0;
-            out.cost = J;
-            return out;
-        }
-        if (it == maxit) break;
-        const double mu = gap / m;
-#pragma unroll
-        for (int i = 0; i < R; ++i) {
-            if (row_active(q, i)) {
-                d[i] = q.lam[i] / q.t[i];
-                rt[i] = rp[i] - q.t[i];  // predictor: r_c = lam * t
-            } else {
-                d[i] = 1.0;
-                rt[i] = 0.0;
-            }
-        }
-        // ---- predictor
-        double dya[N], dsfa[NP1], dsba[NP1];
-        if (!reduced_solve(q, d, rt, rd, rsf, rsb, dya, dsfa, dsba)) break;
-        for_rows(q, dya, dsfa, dsba, false, [&](int i, double v) { val[i] = v; });
-#pragma unroll
-        for (int i = 0; i < R; ++i) {
-            dl[i] = d[i] * (val[i] + rt[i]);
-            dt[i] = -rp[i] - val[i];
-        }
-        const double aa = fmin(max_step(q.t, dt, q), max_step(q.lam, dl, q));
-        double mua = 0.0;
-#pragma unroll
-        for (int i = 0; i < R; ++i)
-            if (row_active(q, i)) mua += (q.lam[i] + aa * dl[i]) * (q.t[i] + aa * dt[i]);
-        mua /= m;
-        const double sr = mua / mu;
-        const double sig = sr * sr * sr;
-        // ---- corrector: r_c = lam t + dlam_a dt_a - sig mu
-#pragma unroll
-        for (int i = 0; i < R; ++i)
-            if (row_active(q, i)) rt[i] = rp[i] - q.t[i] - (dl[i] * dt[i] - sig * mu) / q.lam[i];
-        if (!reduced_solve(q, d, rt, rd, rsf, rsb, dy, dsf, dsb)) break;
-        for_rows(q, dy, dsf, dsb, false, [&](int i, double v) { val[i] = v; });
-#pragma unroll
-        for (int i = 0; i < R; ++i) {
-            dl[i] = d[i] * (val[i] + rt[i]);
-            dt[i] = -rp[i] - val[i];
-        }
-        const double amax = fmin(max_step(q.t, dt, q), max_step(q.lam, dl, q));
-        const double alpha = fmin(1.0, 0.99 * amax);
-#pragma unroll
-        for (int i = 0; i < N; ++i) q.y[i] += alpha * dy[i];
-#pragma unroll
-        for (int j = 0; j < N - 1; ++j) {
-            q.sf[j] += alpha * dsf[j];
-            q.sb[j] += alpha * dsb[j];
-        }
-#pragma unroll
-        for (int i = 0; i < R; ++i)
-            if (row_active(q, i)) {
-                q.lam[i] += alpha * dl[i];
-                q.t[i] += alpha * dt[i];
-            }
-    }
-    out.status = 2;
-    out.cost = objective(q, C, q.y);
-    return out;
+    return true;
 }
 
 // ------------------------------------------------------------------ problem setup

@@ -53,7 +53,8 @@ struct Workspace {
     int32_t* inst_off = nullptr;   // [max_batch] first candidate slot (-1: overflow)
     int32_t* inst_cnt = nullptr;   // [max_batch] candidates of the instance
     int32_t* inst_flag = nullptr;  // [max_batch] 0 ok, 1 infeasible constant rows
-    unsigned long long* counter = nullptr;  // [2] reserved slots, ipm iteration total
+    unsigned long long* counter = nullptr;  // [4] reserved slots, ipm iterations, redo count, pad
+    int32_t* redo = nullptr;       // [cap] candidates whose relaxed optimum left the position box
     int32_t* task_inst = nullptr;  // [cap]
     uint32_t* task_code = nullptr; // [cap]
     double* task_cost = nullptr;   // [cap]
@@ -136,15 +137,18 @@ __global__ __launch_bounds__(kBlock) void k_enum(int B, const hvp_system* __rest
 }
 
 // ------------------------------------------------------------------ K_qp
-template <int N>
+// PBOX = false: every candidate, position-box rows dropped (checked afterwards);
+// PBOX = true : the redo list only, full row set.
+template <int N, bool PBOX>
 __global__ __launch_bounds__(kBlock) void k_qp(const hvp_system* __restrict__ systems, const int32_t* __restrict__ sys,
                                                const int32_t* __restrict__ role, const double* __restrict__ params,
                                                hvp::Consts C, Workspace ws) {
-    const unsigned long long reserved = ws.counter[0];
+    const unsigned long long reserved = PBOX ? ws.counter[2] : ws.counter[0];
     const long long total = (long long)(reserved < (unsigned long long)ws.cap ? reserved : ws.cap);
     unsigned long long iter_sum = 0;
-    for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
-         t += (long long)gridDim.x * blockDim.x) {
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (long long)gridDim.x * blockDim.x) {
+        const long long t = PBOX ? (long long)ws.redo[i] : i;
         const int inst = ws.task_inst[t];
         const uint32_t code = ws.task_code[t];
         const hvp_system& S = systems[sys[inst]];
@@ -152,7 +156,13 @@ __global__ __launch_bounds__(kBlock) void k_qp(const hvp_system* __restrict__ sy
         const double* prm = params + (size_t)inst * (2 + 6 * (N + 1));
         hvp::LaneQp<N> q;
         hvp::setup_lane<N>(q, S, C, rl, prm, code);
-        hvp::QpOut o = hvp::solve_lane<N>(q, C);
+        hvp::QpOut o = hvp::Solver<N, PBOX>::solve(q, C);
+        if (!PBOX && o.status == 0 && !hvp::pbox_ok<N>(q)) {
+            // relaxed optimum leaves the position box: queue the candidate for the full QP
+            const unsigned long long r = atomicAdd(&ws.counter[2], 1ull);
+            ws.redo[r] = (int32_t)t;
+            o.status = 4;
+        }
         ws.task_cost[t] = o.status == 0 ? hvp::direct_cost<N>(q, S, C, rl, prm, code) : 1e300;
         ws.task_stat[t] = o.status | (o.iters << 8);
 #pragma unroll
@@ -236,7 +246,7 @@ int launch_all(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
                double* x_out, int8_t* region_out, int8_t* gear_out, double* cost_out, int32_t* status_out,
                int32_t* nodes_out, int32_t* iters_out, hipStream_t st) {
     Workspace ws = h->ws;
-    HIP_TRY(hipMemsetAsync(ws.counter, 0, 2 * sizeof(unsigned long long), st));
+    HIP_TRY(hipMemsetAsync(ws.counter, 0, 4 * sizeof(unsigned long long), st));
     HIP_TRY(hipEventRecord(h->ev0, st));
     hipLaunchKernelGGL(k_enum<N>, dim3(grid_for(B)), dim3(kBlock), 0, st, B, h->d_sys, sys, role, params, h->C, ws);
     HIP_TRY(hipGetLastError());
@@ -244,9 +254,13 @@ int launch_all(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
     // (≈ every CU x 8 blocks) and let the kernel grid-stride over the real count
     const long long want = std::min<long long>(grid_for(h->ws.cap), (long long)h->n_cu * 8);
     HIP_TRY(hipEventRecord(h->evq0, st));
-    hipLaunchKernelGGL(k_qp<N>, dim3((int)want), dim3(kBlock), 0, st, h->d_sys, sys, role, params, h->C, ws);
+    hipLaunchKernelGGL((k_qp<N, false>), dim3((int)want), dim3(kBlock), 0, st, h->d_sys, sys, role, params, h->C, ws);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(h->evq1, st));
+    // redo list (normally empty: the launch reads a zero count and exits)
+    hipLaunchKernelGGL((k_qp<N, true>), dim3(std::max(1, h->n_cu)), dim3(kBlock), 0, st, h->d_sys, sys, role, params,
+                       h->C, ws);
+    HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_select<N>, dim3(grid_for(B)), dim3(kBlock), 0, st, B, h->d_sys, sys, params, ws, u_out,
                        x_out, region_out, gear_out, cost_out, status_out, nodes_out, iters_out);
     HIP_TRY(hipGetLastError());
@@ -261,6 +275,7 @@ void free_ws(Workspace& w) {
     (void)hipFree(w.inst_cnt);
     (void)hipFree(w.inst_flag);
     (void)hipFree(w.counter);
+    (void)hipFree(w.redo);
     (void)hipFree(w.task_inst);
     (void)hipFree(w.task_code);
     (void)hipFree(w.task_cost);
@@ -344,7 +359,8 @@ int hvp_reserve(hvp_handle* h, int max_batch, int64_t cap) {
     bool ok = hipMalloc(&w.inst_off, sizeof(int32_t) * max_batch) == hipSuccess &&
               hipMalloc(&w.inst_cnt, sizeof(int32_t) * max_batch) == hipSuccess &&
               hipMalloc(&w.inst_flag, sizeof(int32_t) * max_batch) == hipSuccess &&
-              hipMalloc(&w.counter, sizeof(unsigned long long) * 2) == hipSuccess &&
+              hipMalloc(&w.counter, sizeof(unsigned long long) * 4) == hipSuccess &&
+              hipMalloc(&w.redo, sizeof(int32_t) * cap) == hipSuccess &&
               hipMalloc(&w.task_inst, sizeof(int32_t) * cap) == hipSuccess &&
               hipMalloc(&w.task_code, sizeof(uint32_t) * cap) == hipSuccess &&
               hipMalloc(&w.task_cost, sizeof(double) * cap) == hipSuccess &&
@@ -389,7 +405,7 @@ int hvp_sync(hvp_handle* h, void* stream) {
 int hvp_get_stats(hvp_handle* h, hvp_stats* out) {
     if (!h || !out) return fail(HVP_E_ARG, "hvp_get_stats: bad argument");
     HIP_TRY(hipStreamSynchronize(h->last_stream));
-    unsigned long long c[2] = {0, 0};
+    unsigned long long c[4] = {0, 0, 0, 0};
     if (h->ws.counter) HIP_TRY(hipMemcpy(c, h->ws.counter, sizeof(c), hipMemcpyDeviceToHost));
     float ms = 0.f, qms = 0.f;
     if (h->last_B > 0) {
@@ -400,6 +416,7 @@ int hvp_get_stats(hvp_handle* h, hvp_stats* out) {
     out->n_instances = h->last_B;
     out->n_candidates = (int64_t)c[0];
     out->ipm_iterations = (int64_t)c[1];
+    out->n_pbox_redo = (int64_t)c[2];
     out->capacity = h->ws.cap;
     out->last_ms = ms;
     return 0;

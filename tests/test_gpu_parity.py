@@ -73,3 +73,26 @@ def test_device_path_matches_host_path(gpu_available):
     assert np.array_equal(dev["region"].cpu().numpy(), host.region)
     assert np.array_equal(dev["cost"].cpu().numpy(), host.cost)
     assert np.array_equal(dev["u"].cpu().numpy(), host.u)
+
+
+def test_position_box_fallback(gpu_available):
+    """Vehicles near p_max: the relaxed fast path must hand these to the full-row solve."""
+    s = _solver([_gear_system()])
+    sysd = O.gear_pwa_system(800.0)
+    P, R = [], []
+    for p0, v0, vl in [(9870, 30, 40), (9800, 25, 45), (9900, 20, 30), (9700, 35, 45), (9890, 22, 32)]:
+        lead = np.stack([p0 + 60 + vl * np.arange(N + 1), np.full(N + 1, float(vl))])
+        xb = O.constant_velocity_prediction(p0 - 80, v0, N)
+        P.append(np.concatenate([[p0, v0], np.zeros(2 * (N + 1)), xb.ravel(), lead.ravel()]))
+        R.append(O.role_bits(0, 2))
+    params, roles = np.array(P), np.array(R, np.int32)
+    res = s.solve(np.zeros(len(R), np.int32), roles, params)
+    ref = oracle_solve(sysd, O.Cfg(), N, params, roles)
+    for i, r in enumerate(ref):
+        assert res.status[i] == r.status, (i, res.status[i], r.status)
+        if r.status == 0:
+            assert list(res.region[i]) == list(r.sigma)
+            assert abs(res.cost[i] - r.cost) <= 1e-9 * max(1.0, abs(r.cost))
+            assert np.abs(res.u[i] - r.u).max() <= 1e-6
+    ok = res.status == 0
+    assert res.x[ok, 0].max() <= 10000 + 1e-6
