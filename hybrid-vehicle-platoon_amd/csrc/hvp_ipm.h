@@ -73,7 +73,20 @@ HVP_HD inline double frcp(double x) {
 #endif
 }
 
+// Per-lane constant row data (sigma- and instance-dependent bounds).  The host build keeps it
+// in the lane's own array; the gfx950 kernel keeps it in LDS (LdsMem in hvp_kernels.hip) so the
+// register file holds only the IPM iterate.
+enum { F_AM = 0, F_VLO, F_VHI, F_ULO, F_UHI, F_HF, F_HB, F_COUNT };
+
 template <int N>
+struct ArrayMem {
+    double v[F_COUNT * N];
+    HVP_HD double get(int f, int j) const { return v[f * N + j]; }
+    HVP_HD void set(int f, int j, double x) { v[f * N + j] = x; }
+    HVP_HD void refresh() {}
+};
+
+template <int N, class M = ArrayMem<N>>
 struct LaneQp {
     static constexpr int NP = N - 1;              // position-type groups exist for k = 2..N
     static constexpr int NPX = N > 1 ? N - 1 : 1;
@@ -82,13 +95,17 @@ struct LaneQp {
 
     // ---------------- problem data
     double v0, P1, ts;
-    double am[N];             // a_{k-1} (coefficient of v_{k-1} in the U row of step k)
-    double vlo[N], vhi[N];    // bounds on v_k
-    double ulo[N], uhi[N];    // bounds on v_k - a v_{k-1}
     double pmin, pmax;
-    double hf[NPX], hb[NPX];  // pf_k - d_safe, pb_k + d_safe (k = 2..N)
     bool has_sf, has_sb;
     double H[NT], f[N], C0;
+    M mem;                    // a_{k-1}, bounds of v_k, of v_k - a v_{k-1}, pf_k - d_safe, pb_k + d_safe
+    HVP_HD double am(int j) const { return mem.get(F_AM, j); }
+    HVP_HD double vlo(int j) const { return mem.get(F_VLO, j); }
+    HVP_HD double vhi(int j) const { return mem.get(F_VHI, j); }
+    HVP_HD double ulo(int j) const { return mem.get(F_ULO, j); }
+    HVP_HD double uhi(int j) const { return mem.get(F_UHI, j); }
+    HVP_HD double hf(int j) const { return mem.get(F_HF, j); }
+    HVP_HD double hb(int j) const { return mem.get(F_HB, j); }
 
     // ---------------- iterate: slack t and multiplier l of both sides of every two-sided row;
     // for a safe row pair {sgn*p_k - s <= h, -s <= 0} the slack variable s (which is also the
@@ -100,12 +117,12 @@ struct LaneQp {
 };
 
 // bounds of pair p (V,U,A of step k = p/3 + 1; P of step k = p - 3N + 2)
-template <int N>
-HVP_HD inline void pair_bounds(const LaneQp<N>& q, const Consts& C, int p, double& lo, double& hi) {
+template <int N, class M>
+HVP_HD inline void pair_bounds(const LaneQp<N, M>& q, const Consts& C, int p, double& lo, double& hi) {
     if (p < 3 * N) {
         const int j = p / 3, r = p % 3;
-        if (r == 0) { lo = q.vlo[j]; hi = q.vhi[j]; }
-        else if (r == 1) { lo = q.ulo[j]; hi = q.uhi[j]; }
+        if (r == 0) { lo = q.vlo(j); hi = q.vhi(j); }
+        else if (r == 1) { lo = q.ulo(j); hi = q.uhi(j); }
         else { lo = C.dec[j]; hi = C.acc[j]; }
     } else {
         lo = q.pmin;
@@ -116,14 +133,14 @@ HVP_HD inline void pair_bounds(const LaneQp<N>& q, const Consts& C, int p, doubl
 // Row-group traversal over three vectors at once: y (with the constants v0 / P1), a and b
 // (directions, no constants).  emit_pair(p, g.y, g.a, g.b); emit_safe(j, p_k(y), g.a, g.b)
 // with g the prefix gradient ts * (e_0 + .. + e_j) of p_{j+2}.
-template <int N, class FP, class FS>
-HVP_HD inline void for_groups3(const LaneQp<N>& q, const double* y, const double* a, const double* b, FP&& emit_pair,
+template <int N, class M, class FP, class FS>
+HVP_HD inline void for_groups3(const LaneQp<N, M>& q, const double* y, const double* a, const double* b, FP&& emit_pair,
                                FS&& emit_safe) {
     double yp = q.v0, ap = 0.0, bp = 0.0;
     double cy = 0.0, ca = 0.0, cb = 0.0;
 #pragma unroll
     for (int k = 1; k <= N; ++k) {
-        const double yk = y[k - 1], ak = a[k - 1], bk = b[k - 1], am = q.am[k - 1];
+        const double yk = y[k - 1], ak = a[k - 1], bk = b[k - 1], am = q.am(k - 1);
         emit_pair(3 * (k - 1) + 0, yk, ak, bk);
         emit_pair(3 * (k - 1) + 1, yk - am * yp, ak - am * ap, bk - am * bp);
         emit_pair(3 * (k - 1) + 2, yk - yp, ak - ap, bk - bp);
@@ -142,15 +159,15 @@ HVP_HD inline void for_groups3(const LaneQp<N>& q, const double* y, const double
 }
 
 // K += D g g', rhs -= rho g for the gradient shape of pair p (diag / bidiagonal / prefix).
-template <int N>
-HVP_HD inline void scatter_pair(const LaneQp<N>& q, int p, double D, double rho, double* K, double* rhs, double* beta,
+template <int N, class M>
+HVP_HD inline void scatter_pair(const LaneQp<N, M>& q, int p, double D, double rho, double* K, double* rhs, double* beta,
                                 double* rpre) {
     if (p < 3 * N) {
         const int j = p / 3, r = p % 3;
         K[tri(j, j)] += D;
         rhs[j] -= rho;
         if (r != 0 && j >= 1) {
-            const double a = r == 1 ? q.am[j] : 1.0;
+            const double a = r == 1 ? q.am(j) : 1.0;
             K[tri(j - 1, j - 1)] += D * a * a;
             K[tri(j, j - 1)] -= D * a;
             rhs[j - 1] += a * rho;
@@ -162,12 +179,12 @@ HVP_HD inline void scatter_pair(const LaneQp<N>& q, int p, double D, double rho,
 }
 
 // rhs -= rho g only (corrector: the factorised K is reused).
-template <int N>
-HVP_HD inline void scatter_rhs(const LaneQp<N>& q, int p, double rho, double* rhs, double* rpre) {
+template <int N, class M>
+HVP_HD inline void scatter_rhs(const LaneQp<N, M>& q, int p, double rho, double* rhs, double* rpre) {
     if (p < 3 * N) {
         const int j = p / 3, r = p % 3;
         rhs[j] -= rho;
-        if (r != 0 && j >= 1) rhs[j - 1] += (r == 1 ? q.am[j] : 1.0) * rho;
+        if (r != 0 && j >= 1) rhs[j - 1] += (r == 1 ? q.am(j) : 1.0) * rho;
     } else {
         rpre[p - 3 * N] += rho;
     }
@@ -175,8 +192,8 @@ HVP_HD inline void scatter_rhs(const LaneQp<N>& q, int p, double rho, double* rh
 
 // prefix groups: entry (i1, i2) of K receives ts^2 beta of every step whose prefix covers
 // max(i1, i2); rhs[i] -= ts * rho of every step covering i.
-template <int N>
-HVP_HD inline void expand_prefix(const LaneQp<N>& q, const double* beta, const double* rpre, double* K, double* rhs) {
+template <int N, class M>
+HVP_HD inline void expand_prefix(const LaneQp<N, M>& q, const double* beta, const double* rpre, double* K, double* rhs) {
     double sb_ = 0.0, sr = 0.0;
     const double ts = q.ts;
 #pragma unroll
@@ -305,7 +322,7 @@ struct Assembly {
 // PBOX = false drops the position-box rows 0 <= p_k <= 10000 (never active for a platoon:
 // the caller verifies the solution and re-solves the rare violator with PBOX = true, which is
 // exact: a relaxed optimum that satisfies the dropped rows is the optimum).
-template <int N, bool PBOX>
+template <int N, bool PBOX, class M = ArrayMem<N>>
 struct Solver {
     static constexpr int NP = N - 1;
     static constexpr int NPX = N > 1 ? N - 1 : 1;
@@ -314,7 +331,7 @@ struct Solver {
 
     // traversal over (y, a, b) skipping the P pairs when !PBOX
     template <class FP, class FS>
-    HVP_HD static void groups(const LaneQp<N>& q, const double* y, const double* a, const double* b, FP&& fp,
+    HVP_HD static void groups(const LaneQp<N, M>& q, const double* y, const double* a, const double* b, FP&& fp,
                               FS&& fs) {
         for_groups3(
             q, y, a, b,
@@ -325,7 +342,7 @@ struct Solver {
     }
 
     // contributions of the state (tlo, thi, llo, lhi / s, t1, l1, l2) at row values gy / pk
-    HVP_HD static void assemble_pair(const LaneQp<N>& q, const Consts& C, Assembly<N>& A, int p, double gy) {
+    HVP_HD static void assemble_pair(const LaneQp<N, M>& q, const Consts& C, Assembly<N>& A, int p, double gy) {
         double lo, hi;
         pair_bounds(q, C, p, lo, hi);
         const double tl = q.tlo[p], th = q.thi[p], ll = q.llo[p], lh = q.lhi[p];
@@ -343,7 +360,7 @@ struct Solver {
             A.rhs[j] -= rho;
             A.rd[j] += lg;
             if (r != 0 && j >= 1) {
-                const double am = r == 1 ? q.am[j] : 1.0;
+                const double am = r == 1 ? q.am(j) : 1.0;
                 A.K[tri(j - 1, j - 1)] += D * am * am;
                 A.K[tri(j, j - 1)] -= D * am;
                 A.rhs[j - 1] += am * rho;
@@ -356,7 +373,7 @@ struct Solver {
             A.lam_pre[j] += lh - ll;
         }
     }
-    HVP_HD static void assemble_safe(const LaneQp<N>& q, Assembly<N>& A, int j, double sgn, double sgnpk, double h1,
+    HVP_HD static void assemble_safe(const LaneQp<N, M>& q, Assembly<N>& A, int j, double sgn, double sgnpk, double h1,
                                      double s, double t1, double l1, double l2, double w) {
         const SafeRow R(sgnpk, h1, s, t1, l1, l2, w);
         A.gap += l1 * t1 + l2 * s;
@@ -367,7 +384,7 @@ struct Solver {
         A.lam_pre[j] += sgn * l1;
     }
 
-    HVP_HD static void assemble_begin(const LaneQp<N>& q, Assembly<N>& A) {
+    HVP_HD static void assemble_begin(const LaneQp<N, M>& q, Assembly<N>& A) {
 #pragma unroll
         for (int i = 0; i < NT; ++i) A.K[i] = q.H[i];
 #pragma unroll
@@ -379,7 +396,7 @@ struct Solver {
         A.rsmax = 0.0;
     }
     // finish: rd = H y + f + G'lam ; rhs = -rd - sum d rt g ; K prefix expansion
-    HVP_HD static void assemble_end(const LaneQp<N>& q, Assembly<N>& A, const double* y) {
+    HVP_HD static void assemble_end(const LaneQp<N, M>& q, Assembly<N>& A, const double* y) {
         double sb_ = 0.0, sr = 0.0, sl = 0.0;
         const double ts = q.ts;
 #pragma unroll
@@ -402,7 +419,7 @@ struct Solver {
         }
     }
 
-    HVP_HD static QpOut solve(LaneQp<N>& q, const Consts& C) {
+    HVP_HD static QpOut solve(LaneQp<N, M>& q, const Consts& C) {
         QpOut out{0.0, 2, 0};
         const double w = C.w;
         const int m = 2 * NPAIR_ACTIVE + (q.has_sf ? 2 * NP : 0) + (q.has_sb ? 2 * NP : 0);
@@ -426,8 +443,8 @@ struct Solver {
                        scatter_pair(q, p, 2.0, -(-gy + lo) + (gy - hi), K, rhs, beta, rpre);
                    },
                    [&](int j, double pk, double, double) {
-                       if (q.has_sf) { beta[j] += 0.5; rpre[j] += 0.5 * ((pk - q.hf[j]) + w); }
-                       if (q.has_sb) { beta[j] += 0.5; rpre[j] -= 0.5 * ((-pk + q.hb[j]) + w); }
+                       if (q.has_sf) { beta[j] += 0.5; rpre[j] += 0.5 * ((pk - q.hf(j)) + w); }
+                       if (q.has_sb) { beta[j] += 0.5; rpre[j] -= 0.5 * ((-pk + q.hb(j)) + w); }
                    });
             expand_prefix<N>(q, beta, rpre, K, rhs);
             if (!cholesky<N>(K)) return out;
@@ -445,16 +462,16 @@ struct Solver {
                    [&](int j, double pk, double, double) {
                        // slack of the unit solve: s = (g.y + rt1 - r_s) / 2 = (sgn p_k - h - w) / 2
                        if (q.has_sf) {
-                           const double s = 0.5 * (pk - q.hf[j] - w);
+                           const double s = 0.5 * (pk - q.hf(j) - w);
                            q.sf[j] = s;
-                           q.tf[j] = q.hf[j] - (pk - s);
+                           q.tf[j] = q.hf(j) - (pk - s);
                            tmin = fmin(tmin, fmin(q.tf[j], s));
                            tmax = fmax(tmax, fmax(q.tf[j], s));
                        }
                        if (q.has_sb) {
-                           const double s = 0.5 * (-pk + q.hb[j] - w);
+                           const double s = 0.5 * (-pk + q.hb(j) - w);
                            q.sb[j] = s;
-                           q.tb[j] = -q.hb[j] - (-pk - s);
+                           q.tb[j] = -q.hb(j) - (-pk - s);
                            tmin = fmin(tmin, fmin(q.tb[j], s));
                            tmax = fmax(tmax, fmax(q.tb[j], s));
                        }
@@ -498,13 +515,14 @@ struct Solver {
         assemble_begin(q, A);
         groups(q, q.y, zero, zero, [&](int p, double gy, double, double) { assemble_pair(q, C, A, p, gy); },
                [&](int j, double pk, double, double) {
-                   if (q.has_sf) assemble_safe(q, A, j, 1.0, pk, q.hf[j], q.sf[j], q.tf[j], q.lf[j], q.lf2[j], w);
-                   if (q.has_sb) assemble_safe(q, A, j, -1.0, -pk, -q.hb[j], q.sb[j], q.tb[j], q.lb[j], q.lb2[j], w);
+                   if (q.has_sf) assemble_safe(q, A, j, 1.0, pk, q.hf(j), q.sf[j], q.tf[j], q.lf[j], q.lf2[j], w);
+                   if (q.has_sb) assemble_safe(q, A, j, -1.0, -pk, -q.hb(j), q.sb[j], q.tb[j], q.lb[j], q.lb2[j], w);
                });
         assemble_end(q, A, q.y);
 
         const int maxit = C.max_iter;
         double dya[N], dy[N];
+        double last_step = 1e300;  // max |alpha dy| of the previous iteration: u / x accuracy
         for (int it = 0; it <= maxit; ++it) {
             // ------------------------------------------------ convergence
             double rdmax = A.rsmax;
@@ -519,7 +537,8 @@ struct Solver {
                 J += (0.5 * hy + q.f[i]) * q.y[i];
             }
             out.iters = it;
-            if (rdmax <= C.tol * sq && A.rpmax <= C.tol * sh && A.gap <= 0.1 * C.tol * fmax(1.0, fabs(J))) {
+            if (rdmax <= C.tol * sq && A.rpmax <= C.tol * sh && A.gap <= 0.1 * C.tol * fmax(1.0, fabs(J)) &&
+                last_step <= 1e-9) {
                 out.status = 0;
                 return out;
             }
@@ -534,6 +553,7 @@ struct Solver {
             chol_solve<N>(A.K, A.rhs, dya);
             const double mu = A.gap / m;
 
+            q.mem.refresh();
             // ------------------------------------------------ pass X: affine step, centring and the
             // corrector rhs split as  rhsA + sigma mu * rhsB  (linear in sigma mu)
             double amax_a = 1.0, S1 = 0.0, S2 = 0.0;
@@ -580,8 +600,8 @@ struct Solver {
                            pA[j] += sgn * R.c(rt1A, rt2A);
                            pB[j] += sgn * R.d1 * R.d2 * R.ie * (frcp(l1) - frcp(l2));
                        };
-                       if (q.has_sf) safe(1.0, q.hf[j], q.sf[j], q.tf[j], q.lf[j], q.lf2[j]);
-                       if (q.has_sb) safe(-1.0, -q.hb[j], q.sb[j], q.tb[j], q.lb[j], q.lb2[j]);
+                       if (q.has_sf) safe(1.0, q.hf(j), q.sf[j], q.tf[j], q.lf[j], q.lf2[j]);
+                       if (q.has_sb) safe(-1.0, -q.hb(j), q.sb[j], q.tb[j], q.lb[j], q.lb2[j]);
                    });
             const double mua = (A.gap + amax_a * S1 + amax_a * amax_a * S2) / m;
             const double sr = fmax(mua, 0.0) / mu;
@@ -621,6 +641,7 @@ struct Solver {
                 R.dir(gd, rt1, rt2, ds, dt1, dl1, dl2);
             };
             double amax = 1.0;
+            q.mem.refresh();
             groups(q, q.y, dya, dy,
                    [&](int p, double gy, double ga, double gd) {
                        double lo, hi;
@@ -644,8 +665,8 @@ struct Solver {
                            ratio_test(amax, l1, dl1);
                            ratio_test(amax, l2, dl2);
                        };
-                       if (q.has_sf) safe(1.0, q.hf[j], q.sf[j], q.tf[j], q.lf[j], q.lf2[j]);
-                       if (q.has_sb) safe(-1.0, -q.hb[j], q.sb[j], q.tb[j], q.lb[j], q.lb2[j]);
+                       if (q.has_sf) safe(1.0, q.hf(j), q.sf[j], q.tf[j], q.lf[j], q.lf2[j]);
+                       if (q.has_sb) safe(-1.0, -q.hb(j), q.sb[j], q.tb[j], q.lb[j], q.lb2[j]);
                    });
             const double alpha = fmin(1.0, 0.99 * amax);
 
@@ -654,6 +675,7 @@ struct Solver {
 #pragma unroll
             for (int i = 0; i < N; ++i) ynew[i] = q.y[i] + alpha * dy[i];
             assemble_begin(q, A);
+            q.mem.refresh();
             groups(q, q.y, dya, dy,
                    [&](int p, double gy, double ga, double gd) {
                        double lo, hi;
@@ -679,11 +701,15 @@ struct Solver {
                            l2 += alpha * dl2;
                            assemble_safe(q, A, j, sgn, sgn * (pk + alpha * gd), h1, s, t1, l1, l2, w);
                        };
-                       if (q.has_sf) safe(1.0, q.hf[j], q.sf[j], q.tf[j], q.lf[j], q.lf2[j]);
-                       if (q.has_sb) safe(-1.0, -q.hb[j], q.sb[j], q.tb[j], q.lb[j], q.lb2[j]);
+                       if (q.has_sf) safe(1.0, q.hf(j), q.sf[j], q.tf[j], q.lf[j], q.lf2[j]);
+                       if (q.has_sb) safe(-1.0, -q.hb(j), q.sb[j], q.tb[j], q.lb[j], q.lb2[j]);
                    });
+            last_step = 0.0;
 #pragma unroll
-            for (int i = 0; i < N; ++i) q.y[i] = ynew[i];
+            for (int i = 0; i < N; ++i) {
+                last_step = fmax(last_step, fabs(ynew[i] - q.y[i]));
+                q.y[i] = ynew[i];
+            }
             assemble_end(q, A, q.y);
         }
         out.status = 2;
@@ -691,14 +717,14 @@ struct Solver {
     }
 };
 
-template <int N>
-HVP_HD inline QpOut solve_lane(LaneQp<N>& q, const Consts& C) {
-    return Solver<N, true>::solve(q, C);
+template <int N, class M>
+HVP_HD inline QpOut solve_lane(LaneQp<N, M>& q, const Consts& C) {
+    return Solver<N, true, M>::solve(q, C);
 }
 
 // Position-box check of a relaxed (PBOX = false) solution: p_k in [pmin, pmax] for k = 2..N.
-template <int N>
-HVP_HD inline bool pbox_ok(const LaneQp<N>& q) {
+template <int N, class M>
+HVP_HD inline bool pbox_ok(const LaneQp<N, M>& q) {
     double cum = 0.0;
     const double tol = 1e-9 * (1.0 + fmax(fabs(q.pmin), fabs(q.pmax)));
 #pragma unroll
@@ -713,8 +739,8 @@ HVP_HD inline bool pbox_ok(const LaneQp<N>& q) {
 // ------------------------------------------------------------------ problem setup
 // Builds the lane QP for instance params (x0, x_front, x_back, leader_x) and region code.
 // Returns false when a sigma-independent constant row (p_1 box) is violated.
-template <int N>
-HVP_HD inline bool setup_lane(LaneQp<N>& q, const hvp_system& S, const Consts& C, int role, const double* prm,
+template <int N, class M>
+HVP_HD inline bool setup_lane(LaneQp<N, M>& q, const hvp_system& S, const Consts& C, int role, const double* prm,
                               uint32_t code) {
     const double p0 = prm[0], v0 = prm[1];
     const double* xf = prm + 2;
@@ -735,29 +761,29 @@ HVP_HD inline bool setup_lane(LaneQp<N>& q, const hvp_system& S, const Consts& C
         a[k] = S.a[r];
         b[k] = S.b[r];
         c[k] = S.c[r];
-        q.am[k] = a[k];
-        q.ulo[k] = c[k] + b[k] * S.umin;
-        q.uhi[k] = c[k] + b[k] * S.umax;
+        q.mem.set(F_AM, k, a[k]);
+        q.mem.set(F_ULO, k, c[k] + b[k] * S.umin);
+        q.mem.set(F_UHI, k, c[k] + b[k] * S.umax);
         // bounds on v_{k+1}: region sigma_{k+1} (if any) intersected with the state box
         if (k + 1 < N) {
             const int r1 = (code >> (3 * (k + 1))) & 7;
-            q.vlo[k] = fmax(S.vmin, S.vlo[r1]);
-            q.vhi[k] = fmin(S.vmax, S.vhi[r1]);
+            q.mem.set(F_VLO, k, fmax(S.vmin, S.vlo[r1]));
+            q.mem.set(F_VHI, k, fmin(S.vmax, S.vhi[r1]));
         } else {
-            q.vlo[k] = S.vmin;
-            q.vhi[k] = S.vmax;
+            q.mem.set(F_VLO, k, S.vmin);
+            q.mem.set(F_VHI, k, S.vmax);
         }
     }
     // step-1 rows carry the constant v0 on the left: U: v1 - a0 v0, A: v1 - v0 (handled in for_rows)
 #pragma unroll
     for (int j = 0; j < N - 1; ++j) {
-        q.hf[j] = xf[j + 2] - C.d_safe;
-        q.hb[j] = xb[j + 2] + C.d_safe;
+        q.mem.set(F_HF, j, xf[j + 2] - C.d_safe);
+        q.mem.set(F_HB, j, xb[j + 2] + C.d_safe);
     }
 
     // ---- cost: 1/2 y'Hy + f'y + C0
 #pragma unroll
-    for (int i = 0; i < LaneQp<N>::NT; ++i) q.H[i] = 0.0;
+    for (int i = 0; i < LaneQp<N, M>::NT; ++i) q.H[i] = 0.0;
 #pragma unroll
     for (int i = 0; i < N; ++i) q.f[i] = 0.0;
     double C0 = 0.0;
@@ -863,8 +889,8 @@ HVP_HD inline bool setup_lane(LaneQp<N>& q, const hvp_system& S, const Consts& C
 // writes it (fleet_decent_mld.py:107-169): squared tracking errors, Q_u u^2, Q_du du^2 and
 // w * max(0, .) slacks.  Avoids the cancellation of C0 + 1/2 y'Hy + f'y (positions ~3e3), so
 // the costs the argmin compares carry relative error ~1e-15 instead of ~1e-9.
-template <int N>
-HVP_HD inline double direct_cost(const LaneQp<N>& q, const hvp_system& S, const Consts& C, int role,
+template <int N, class M>
+HVP_HD inline double direct_cost(const LaneQp<N, M>& q, const hvp_system& S, const Consts& C, int role,
                                  const double* prm, uint32_t code) {
     const double* xf = prm + 2;
     const double* xb = prm + 2 + 2 * (N + 1);

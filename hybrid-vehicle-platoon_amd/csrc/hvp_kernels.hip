@@ -137,6 +137,20 @@ __global__ __launch_bounds__(kBlock) void k_enum(int B, const hvp_system* __rest
 }
 
 // ------------------------------------------------------------------ K_qp
+// Per-lane constant rows in LDS: field f, step j of lane l at s_rows[(f * N + j) * kBlock + l]
+// (consecutive lanes -> consecutive 8-byte words: conflict-free ds_read_b64).  refresh() makes
+// the lane offset opaque at the start of every IPM sweep so the compiler re-reads the rows from
+// LDS instead of hoisting them into VGPRs for the whole solve.
+extern __shared__ double s_rows[];
+
+template <int N>
+struct LdsMem {
+    unsigned lane;
+    __device__ double get(int f, int j) const { return s_rows[(f * N + j) * kBlock + lane]; }
+    __device__ void set(int f, int j, double x) { s_rows[(f * N + j) * kBlock + lane] = x; }
+    __device__ void refresh() { asm volatile("" : "+v"(lane)); }
+};
+
 // PBOX = false: every candidate, position-box rows dropped (checked afterwards);
 // PBOX = true : the redo list only, full row set.
 template <int N, bool PBOX>
@@ -154,9 +168,10 @@ __global__ __launch_bounds__(kBlock) void k_qp(const hvp_system* __restrict__ sy
         const hvp_system& S = systems[sys[inst]];
         const int rl = role[inst];
         const double* prm = params + (size_t)inst * (2 + 6 * (N + 1));
-        hvp::LaneQp<N> q;
+        hvp::LaneQp<N, LdsMem<N>> q;
+        q.mem.lane = threadIdx.x;
         hvp::setup_lane<N>(q, S, C, rl, prm, code);
-        hvp::QpOut o = hvp::Solver<N, PBOX>::solve(q, C);
+        hvp::QpOut o = hvp::Solver<N, PBOX, LdsMem<N>>::solve(q, C);
         if (!PBOX && o.status == 0 && !hvp::pbox_ok<N>(q)) {
             // relaxed optimum leaves the position box: queue the candidate for the full QP
             const unsigned long long r = atomicAdd(&ws.counter[2], 1ull);
@@ -254,12 +269,13 @@ int launch_all(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
     // (≈ every CU x 8 blocks) and let the kernel grid-stride over the real count
     const long long want = std::min<long long>(grid_for(h->ws.cap), (long long)h->n_cu * 8);
     HIP_TRY(hipEventRecord(h->evq0, st));
-    hipLaunchKernelGGL((k_qp<N, false>), dim3((int)want), dim3(kBlock), 0, st, h->d_sys, sys, role, params, h->C, ws);
+    const size_t lds = sizeof(double) * hvp::F_COUNT * N * kBlock;
+    hipLaunchKernelGGL((k_qp<N, false>), dim3((int)want), dim3(kBlock), lds, st, h->d_sys, sys, role, params, h->C, ws);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(h->evq1, st));
     // redo list (normally empty: the launch reads a zero count and exits)
-    hipLaunchKernelGGL((k_qp<N, true>), dim3(std::max(1, h->n_cu)), dim3(kBlock), 0, st, h->d_sys, sys, role, params,
-                       h->C, ws);
+    hipLaunchKernelGGL((k_qp<N, true>), dim3(std::max(1, h->n_cu)), dim3(kBlock), lds, st, h->d_sys, sys, role,
+                       params, h->C, ws);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_select<N>, dim3(grid_for(B)), dim3(kBlock), 0, st, B, h->d_sys, sys, params, ws, u_out,
                        x_out, region_out, gear_out, cost_out, status_out, nodes_out, iters_out);
@@ -309,6 +325,14 @@ bool valid_system(const hvp_system& s, std::string* why) {
 extern "C" {
 
 int hvp_abi_version(void) { return HVP_ABI_VERSION; }
+
+int hvp_abi_sizes(int32_t* sizes) {
+    if (!sizes) return HVP_E_ARG;
+    sizes[0] = (int32_t)sizeof(hvp_system);
+    sizes[1] = (int32_t)sizeof(hvp_problem);
+    sizes[2] = (int32_t)sizeof(hvp_stats);
+    return 0;
+}
 
 int hvp_last_error(char* buf, size_t len) {
     if (!buf || len == 0) return HVP_E_ARG;

@@ -108,6 +108,7 @@ EXPORTS = {
     "hvp_destroy": ([_P], None),
     "hvp_last_error": ([ctypes.c_char_p, ctypes.c_size_t], ctypes.c_int),
     "hvp_abi_version": ([], ctypes.c_int),
+    "hvp_abi_sizes": ([_I32P], ctypes.c_int),
 }
 
 
@@ -132,6 +133,11 @@ def load():
         fn.restype = rest
     if lib.hvp_abi_version() != ABI_VERSION:
         raise HvpError(f"libhvpsolve ABI {lib.hvp_abi_version()} != expected {ABI_VERSION}")
+    sizes = (ctypes.c_int32 * 3)()
+    lib.hvp_abi_sizes(sizes)
+    want = (ctypes.sizeof(HvpSystem), ctypes.sizeof(HvpProblem), ctypes.sizeof(HvpStats))
+    if tuple(sizes) != want:
+        raise HvpError(f"struct layout mismatch: library {tuple(sizes)} vs binding {want}")
     _lib = lib
     return lib
 

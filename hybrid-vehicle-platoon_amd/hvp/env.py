@@ -119,7 +119,7 @@ class PlatoonEnv:
 
     def _cost(self, e: np.ndarray, Q: np.ndarray) -> float:
         if self.quadratic_cost:
-            return float(e.T @ Q @ e)
+            return (e.T @ Q @ e).item()
         return float(np.linalg.norm(Q @ e, ord=1))
 
     def get_stage_cost(self, state: np.ndarray, action: np.ndarray) -> float:

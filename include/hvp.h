@@ -147,6 +147,8 @@ int hvp_get_stats(hvp_handle* h, hvp_stats* out); /* synchronises the handle's l
 void hvp_destroy(hvp_handle* h);
 int hvp_last_error(char* buf, size_t len);
 int hvp_abi_version(void);
+/* sizes[0..2] = sizeof(hvp_system), sizeof(hvp_problem), sizeof(hvp_stats) (binding checks). */
+int hvp_abi_sizes(int32_t* sizes);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,181 @@
+#!/usr/bin/env python3
+"""Regenerate the committed golden fixtures (TEST INFRASTRUCTURE).
+
+The reference cannot run in this container (Gurobi / dmpcpwa absent; importing the reference
+was refused by the environment), so the expected outputs come from the CPU
+oracle (oracle/hvp_oracle.c: exhaustive region-sequence enumeration + certified QP solves).
+Inputs follow the reference's own generators, restated in oracle/oracle.py:
+env.reset init with the SeedSequence-derived seed (env.py:70-116), constant-velocity neighbour
+predictions (fleet_decent_mld.py:421-428), the leader trajectories of misc/leader_trajectory.py
+and the controller constants of misc/common_controller_params.py.
+
+Files (numpy .npz, no pickles):
+  decent_n10_N5.npz   configs[1]: n=10, N=5, mass 800, ConstantSpacing(50), seeds 0..9, t=0
+  decent_n2_N5.npz    configs[0]: n=2, N=5, seeds 0..9
+  decent_rollout_n4_N5.npz  mid-trajectory states: 6 steps along the MPC's own predictions
+  task2_n5_N5.npz     Sim_n_task_2 flavour: masses U(700,1000), ConstantTime(10,3), stop-and-go leader
+  variants_n4.npz     N = 3, 4, 6, 7; Q_du = 0.5; leader_index = 2; real_vehicle_as_reference
+  known_answers.json  constants derived from the reference source
+
+Run:  python tests/golden/make_golden.py
+"""
+
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import oracle as O  # noqa: E402
+from instances import decent_instances, leader_window, split_params  # noqa: E402
+
+
+def stop_and_go(N: int, t: int, p=3000.0, vh=20.0, vl=10.0, vf=30.0, c0=30, c1=50, L=200):
+    x = np.zeros((2, L))
+    x[:, 0] = (p, vh)
+    v = vh
+    for k in range(L - 1):
+        x[0, k + 1] = x[0, k] + v
+        if c0 <= k < c1:
+            v = vl
+        elif k >= c1:
+            v = vf
+        x[1, k + 1] = v if k >= c0 else x[1, k]
+    return x[:, t:t + N + 1]
+
+
+def solve_set(systems, masses_idx, cfg, N, params, roles, quadratic=True):
+    out = {k: [] for k in ("region", "u", "x", "cost", "nodes", "status", "certified")}
+    for p, r, si in zip(params, roles, masses_idx):
+        x0, xf, xb, xl = split_params(p, N)
+        res = O.solve_miqp(systems[si], cfg, N, int(r), x0, xf, xb, xl, quadratic=quadratic)
+        out["region"].append(res.sigma if res.status == 0 else np.full(N, -1))
+        out["u"].append(res.u)
+        out["x"].append(res.x)
+        out["cost"].append(res.cost)
+        out["nodes"].append(res.n_candidates)
+        out["status"].append(res.status)
+        out["certified"].append(res.best_certified)
+    return {k: np.array(v) for k, v in out.items()}
+
+
+def save(name, N, masses, cfg, params, roles, sys_idx, exp):
+    path = os.path.join(HERE, name)
+    np.savez_compressed(path, N=N, masses=np.asarray(masses, float), cfg=cfg.vector(), params=params,
+                        roles=roles.astype(np.int32), sys=np.asarray(sys_idx, np.int32),
+                        **{f"exp_{k}": v for k, v in exp.items()})
+    cert = exp["certified"][exp["status"] == 0].mean() if (exp["status"] == 0).any() else 0
+    print(f"{name}: {len(roles)} instances, optimal {int((exp['status'] == 0).sum())}, certified {cert:.3f}")
+
+
+def decent_seeds(n, N, seeds, mass=800.0, cfg=None):
+    cfg = cfg or O.Cfg()
+    P, R = [], []
+    for s in seeds:
+        p, r = decent_instances(O.env_initial_state(n, s), N, leader_window(N))
+        P.append(p)
+        R.append(r)
+    params, roles = np.concatenate(P), np.concatenate(R)
+    sys_idx = np.zeros(len(roles), np.int32)
+    return params, roles, sys_idx, solve_set([O.gear_pwa_system(mass)], sys_idx, cfg, N, params, roles)
+
+
+def rollout(n, N, seeds, steps):
+    """States along the platoon's own predicted trajectories (x_1 of every local solution)."""
+    cfg = O.Cfg()
+    sysd = O.gear_pwa_system(800.0)
+    P, R = [], []
+    for s in seeds:
+        state = O.env_initial_state(n, s).astype(float)
+        for t in range(steps):
+            p, r = decent_instances(state, N, leader_window(N, t))
+            P.append(p)
+            R.append(r)
+            exp = solve_set([sysd], np.zeros(n, int), cfg, N, p, r)
+            state = np.stack([exp["x"][i][:, 1] if exp["status"][i] == 0 else state[2 * i:2 * i + 2]
+                              for i in range(n)]).reshape(-1)
+    params, roles = np.concatenate(P), np.concatenate(R)
+    sys_idx = np.zeros(len(roles), np.int32)
+    return params, roles, sys_idx, solve_set([sysd], sys_idx, cfg, N, params, roles)
+
+
+def task2(n, N, seeds, t_list):
+    cfg = O.Cfg(d0=10.0, t0=3.0)
+    P, R, S, masses = [], [], [], []
+    for s in seeds:
+        rs = np.random.RandomState(s)
+        m = rs.uniform(700, 1000, n)
+        base = len(masses)
+        masses.extend(m.tolist())
+        state = O.env_initial_state(n, s).astype(float)
+        for t in t_list:
+            p, r = decent_instances(state, N, stop_and_go(N, t))
+            P.append(p)
+            R.append(r)
+            S.append(base + np.arange(n))
+    params, roles, sys_idx = np.concatenate(P), np.concatenate(R), np.concatenate(S)
+    systems = [O.gear_pwa_system(m) for m in masses]
+    return params, roles, sys_idx, masses, cfg, solve_set(systems, sys_idx, cfg, N, params, roles)
+
+
+def main():
+    N = 5
+    params, roles, si, exp = decent_seeds(10, N, range(10))
+    save("decent_n10_N5.npz", N, [800.0], O.Cfg(), params, roles, si, exp)
+    params, roles, si, exp = decent_seeds(2, N, range(10))
+    save("decent_n2_N5.npz", N, [800.0], O.Cfg(), params, roles, si, exp)
+    params, roles, si, exp = rollout(4, N, range(3), 6)
+    save("decent_rollout_n4_N5.npz", N, [800.0], O.Cfg(), params, roles, si, exp)
+    params, roles, si, masses, cfg, exp = task2(5, N, range(3), [0, 29, 31, 49, 52])
+    save("task2_n5_N5.npz", N, masses, cfg, params, roles, si, exp)
+    # variants: horizon, Q_du, leader index, real_vehicle_as_reference
+    for NN in (3, 4, 6, 7):
+        params, roles, si, exp = decent_seeds(4, NN, range(4))
+        save(f"variant_n4_N{NN}.npz", NN, [800.0], O.Cfg(), params, roles, si, exp)
+    cfg = O.Cfg(Qdu=0.5)
+    params, roles, si, exp = decent_seeds(4, N, range(4), cfg=cfg)
+    save("variant_n4_N5_qdu.npz", N, [800.0], cfg, params, roles, si, exp)
+    P, R = [], []
+    for s in range(4):
+        p, r = decent_instances(O.env_initial_state(5, s), N, leader_window(N), leader_index=2)
+        P.append(p)
+        R.append(r)
+        p, r = decent_instances(O.env_initial_state(5, s + 10), N, leader_window(N, 0, 3100.0),
+                                real_vehicle_as_reference=True)
+        P.append(p)
+        R.append(r)
+    params, roles = np.concatenate(P), np.concatenate(R)
+    si = np.zeros(len(roles), np.int32)
+    exp = solve_set([O.gear_pwa_system(800.0)], si, O.Cfg(), N, params, roles)
+    save("variant_n5_N5_roles.npz", N, [800.0], O.Cfg(), params, roles, si, exp)
+
+    # known answers derived from the reference's constants
+    g = O.gear_pwa_system(800.0)
+    ka = {
+        "seed0_env_seed": O.env_seed(0),
+        "env_init_n10_seed0": O.env_initial_state(10, 0).tolist(),
+        "Ad22_m800": [float(a[1, 1]) for a in g["A"]],
+        "Bd2_m800": [float(b[1]) for b in g["B"]],
+        "cd2_m800": [float(c[1]) for c in g["c"]],
+        "v_gear_lim": [9.235, 12.855, 16.93, 23.315, 32.47],
+        "alpha": 22.92,
+        "region_gear": [1, 2, 3, 4, 4, 5, 6],
+        "survey_values": {"Ad22": [0.989256, 0.953444], "Bd2": [5.07125, 3.68125, 2.645, 2.00875, 2.00875, 1.4575,
+                                                                 1.0475], "cd2": [-0.098, 0.722823],
+                          "env_init_n10_seed0": [3000, 21, 2931, 22, 2808, 10, 2728, 16, 2603, 26, 2517, 22, 2454,
+                                                 22, 2353, 28, 2235, 32, 2127, 31]},
+    }
+    with open(os.path.join(HERE, "known_answers.json"), "w") as f:
+        json.dump(ka, f, indent=1)
+    print("known_answers.json written")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,47 @@
+"""Loading of the committed golden fixtures for the product-side tests."""
+
+from __future__ import annotations
+
+import glob
+import os
+
+import numpy as np
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def fixture_names() -> list[str]:
+    return sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLDEN, "*.npz")))
+
+
+def load(name: str) -> dict:
+    with np.load(os.path.join(GOLDEN, name), allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+class CfgParams:
+    """A Params-like class (misc/common_controller_params.py:14-23) built from an oracle cfg vector."""
+
+    def __init__(self, v) -> None:
+        v = np.asarray(v, dtype=float)
+        self.Q_x = v[0:4].reshape(2, 2)
+        self.Q_u = np.array([[v[4]]])
+        self.Q_du = np.array([[v[5]]])
+        self.w = v[6]
+        self.a_acc, self.a_dec, self.ts, self.d_safe = v[7], v[8], v[9], v[10]
+        self.tight, self.d0, self.t0 = v[11], v[12], v[13]
+
+
+def product_problem(fx: dict):
+    """hvp_problem + system tables of a fixture, through the product's own table builders."""
+    from hvp import tables
+    from hvp.models import PwaGearVehicle
+    from hvp.params import ConstantTimePolicy
+
+    cp = CfgParams(fx["cfg"])
+    prob = tables.problem(int(fx["N"]), ConstantTimePolicy(cp.d0, cp.t0), accel_cnstr_tightening=cp.tight, params=cp)
+    systems = []
+    for m in fx["masses"]:
+        veh = PwaGearVehicle(float(m))
+        systems.append(tables.system_from_dict(veh.get_discrete_system(float(cp.ts)), tables.gears_of(veh)))
+    return prob, systems

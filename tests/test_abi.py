@@ -1,0 +1,57 @@
+"""The C ABI library: builds for gfx950, loads without a GPU and exports every symbol of
+include/hvp.h with the struct layouts the ctypes binding assumes (no compute call)."""
+
+from __future__ import annotations
+
+import os
+import re
+import subprocess
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "hybrid-vehicle-platoon_amd")
+
+
+def header_functions() -> set[str]:
+    src = open(os.path.join(ROOT, "include", "hvp.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return set(re.findall(r"^\s*(?:int|void|const char\s*\*)\s+(hvp_\w+)\s*\(", src, flags=re.M)) - {
+        "hvp_params_stride"}
+
+
+def test_library_builds_and_exports_the_header():
+    from hvp import _abi
+
+    subprocess.run(["make", "-s", "-C", PKG, "lib/libhvpsolve.so"], check=True)  # no-op when up to date
+    lib = _abi.load()  # checks ABI version and struct sizes
+    funcs = header_functions()
+    assert funcs == set(_abi.EXPORTS), funcs ^ set(_abi.EXPORTS)
+    for f in funcs:
+        assert hasattr(lib, f), f
+    nm = subprocess.run(["nm", "-D", "--defined-only", _abi.LIB_PATH], capture_output=True, text=True).stdout
+    for f in funcs:
+        assert re.search(rf"\bT {f}\b", nm), f
+
+
+def test_code_object_targets_gfx950():
+    from hvp import _abi
+
+    # the fat binary embeds the amdgcn code object; its target id names the architecture
+    assert b"amdgcn-amd-amdhsa--gfx950" in open(_abi.LIB_PATH, "rb").read()
+
+
+def test_invalid_arguments_fail_loudly_without_touching_the_gpu():
+    import ctypes
+
+    from hvp import _abi, tables
+    from hvp.models import PwaGearVehicle
+
+    lib = _abi.load()
+    h = ctypes.c_void_p()
+    veh = PwaGearVehicle(800)
+    sysv = (_abi.HvpSystem * 1)(tables.system_from_dict(veh.get_discrete_system(1), tables.gears_of(veh)))
+    bad = tables.problem(12)  # beyond HVP_MAX_N
+    assert lib.hvp_create(ctypes.byref(h), ctypes.byref(bad), sysv, 1, 0) == -3
+    assert "horizon" in _abi.last_error()
+    l1 = tables.problem(5)
+    l1.quadratic_cost = 0
+    assert lib.hvp_create(ctypes.byref(h), ctypes.byref(l1), sysv, 1, 0) == -3

@@ -1,0 +1,73 @@
+"""The reference-shaped API on the GPU: LocalMpcMld.solve_mpc, MldAgent, the batched
+TrackingDecentMldCoordinator and a short closed-loop simulate()."""
+
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import oracle as O
+from instances import split_params
+
+pytestmark = pytest.mark.gpu
+
+
+def test_local_mpc_solve_mpc_matches_oracle(gpu_available):
+    from hvp.models import PwaGearVehicle
+    from hvp.mpc import LocalMpcMld
+
+    N = 5
+    veh = PwaGearVehicle(800)
+    m = LocalMpcMld(N, veh.get_discrete_system(1), is_front=False, is_trailer=False, gears=veh.REGION_GEAR)
+    x = O.env_initial_state(3, 0).astype(float)
+    xf = O.constant_velocity_prediction(x[0], x[1], N)
+    xb = O.constant_velocity_prediction(x[4], x[5], N)
+    m.set_x_front(xf)
+    m.set_x_back(xb)
+    u0, info = m.solve_mpc(x[2:4].reshape(2, 1))
+    ref = O.solve_miqp(O.gear_pwa_system(800.0), O.Cfg(), N, O.role_bits(1, 3), x[2:4], xf, xb, np.zeros((2, N + 1)))
+    assert u0.shape == (1, 1) and info["u"].shape == (1, N) and info["x"].shape == (2, N + 1)
+    assert np.abs(info["u"][0] - ref.u).max() <= 1e-6
+    assert abs(info["cost"] - ref.cost) <= 1e-9 * abs(ref.cost)
+    assert info["bin_vars"] == 7 * N and info["nodes"] == ref.n_candidates and info["run_time"] > 0
+    assert list(m.gears_pred[0].astype(int)) == [PwaGearVehicle.REGION_GEAR[r] for r in ref.sigma]
+
+
+def test_infeasible_raises_or_returns_zeros(gpu_available):
+    from hvp.models import PwaGearVehicle
+    from hvp.mpc import LocalMpcMld
+
+    N = 5
+    veh = PwaGearVehicle(800)
+    m = LocalMpcMld(N, veh.get_discrete_system(1), is_front=True, is_leader=True, is_trailer=False)
+    lead = np.stack([9950 + 40 * np.arange(N + 1), np.full(N + 1, 40.0)])
+    m.set_leader_x(lead)
+    m.set_x_back(O.constant_velocity_prediction(9790, 30, N))
+    with pytest.raises(RuntimeError):
+        m.solve_mpc(np.array([[9870.0], [30.0]]))  # the position box cannot be respected
+    u0, info = m.solve_mpc(np.array([[9870.0], [30.0]]), raises=False)
+    assert np.all(u0 == 0) and info["cost"] == float("inf")
+
+
+def test_closed_loop_simulate(gpu_available):
+    from hvp.decent import simulate
+    from hvp.params import Sim
+
+    class Short(Sim):
+        n = 4
+        N = 5
+        ep_len = 12
+
+    X, U, R, agent, env = simulate(Short(), seed=1)
+    assert X.shape == (13, 8) and U.shape == (12, 4) and R.shape == (12,)
+    assert np.all(np.abs(U) <= 1 + 1e-9)
+    assert (agent.solve_times[:12] > 0).all() and (agent.node_counts[:12] >= 1).all()
+    # the first action is the batched solution of the t = 0 problems, identical to the oracle
+    x0 = X[0]
+    lead = np.stack([3000 + 20.0 * np.arange(6), np.full(6, 20.0)])
+    for i in range(4):
+        xf = O.constant_velocity_prediction(x0[2 * i - 2], x0[2 * i - 1], 5) if i else np.zeros((2, 6))
+        xb = O.constant_velocity_prediction(x0[2 * i + 2], x0[2 * i + 3], 5) if i < 3 else np.zeros((2, 6))
+        ref = O.solve_miqp(O.gear_pwa_system(800.0), O.Cfg(), 5, O.role_bits(i, 4), x0[2 * i:2 * i + 2], xf, xb,
+                           lead if i == 0 else np.zeros((2, 6)))
+        assert abs(U[0][i] - ref.u[0]) <= 1e-6

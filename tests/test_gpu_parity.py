@@ -96,3 +96,71 @@ def test_position_box_fallback(gpu_available):
             assert np.abs(res.u[i] - r.u).max() <= 1e-6
     ok = res.status == 0
     assert res.x[ok, 0].max() <= 10000 + 1e-6
+
+
+# ---------------------------------------------------------------- golden fixtures through the C ABI
+from golden_io import fixture_names, load, product_problem  # noqa: E402
+
+
+@pytest.mark.parametrize("name", fixture_names())
+def test_golden_fixture_on_gpu(gpu_available, name):
+    from hvp.solver import BatchSolver
+
+    fx = load(name)
+    prob, systems = product_problem(fx)
+    s = BatchSolver(prob, systems)
+    res = s.solve(fx["sys"], fx["roles"], fx["params"])
+    ok = fx["exp_status"] == 0
+    assert np.array_equal(res.status, fx["exp_status"])
+    assert np.array_equal(res.nodes, fx["exp_nodes"])
+    assert np.array_equal(res.region[ok], fx["exp_region"][ok])
+    gear_of = np.array([1, 2, 3, 4, 4, 5, 6])
+    assert np.array_equal(res.gear[ok], gear_of[fx["exp_region"][ok]])
+    ce = fx["exp_cost"][ok]
+    assert np.all(np.abs(res.cost[ok] - ce) <= 1e-9 * np.maximum(1, np.abs(ce)))
+    assert np.abs(res.u[ok] - fx["exp_u"][ok]).max() <= 1e-6
+    assert np.abs(res.x[ok] - fx["exp_x"][ok]).max() <= 1e-4
+
+
+def test_full_size_batch_properties(gpu_available):
+    """configs[1] at bench size: every solution feasible for the MLD constraints, deterministic,
+    and a random sample bit-exact in regions against the oracle."""
+    import torch
+
+    import bench
+
+    n, N, S = 10, 5, 16384
+    s = _solver([_gear_system()])
+    params, roles = bench.make_inputs(range(S), n, N)
+    dev = torch.device("cuda", 0)
+    tp, tr = torch.from_numpy(params).to(dev), torch.from_numpy(roles).to(dev)
+    ts = torch.zeros(len(roles), dtype=torch.int32, device=dev)
+    a = s.solve_device(ts, tr, tp)
+    b = s.solve_device(ts, tr, tp)
+    torch.cuda.synchronize()
+    for k in a:
+        assert torch.equal(a[k], b[k]), k  # deterministic
+    st = a["status"].cpu().numpy()
+    assert (st == 0).all()
+    u, x, reg = a["u"].cpu().numpy(), a["x"].cpu().numpy(), a["region"].cpu().numpy()
+    assert np.abs(u).max() <= 1 + 1e-9
+    v = x[:, 1, :]
+    assert v[:, 1:].min() >= 3.94 - 1e-9 and v[:, 1:].max() <= 45.84 + 1e-9
+    dv = np.diff(v, axis=1)
+    assert dv.min() >= -2 - 1e-9 and dv.max() <= 2.5 + 1e-9
+    # velocity inside the chosen region at every step k < N (closed intervals)
+    lim = np.array([-np.inf, 9.235, 12.855, 16.93, 22.92, 23.315, 32.47, np.inf])
+    vk = v[:, :N]
+    assert np.all(vk >= lim[reg] - 1e-7) and np.all(vk <= lim[reg + 1] + 1e-7)
+    # dynamics of the chosen region reproduce x from u
+    g = O.gear_pwa_system(800.0)
+    pred = g["A"][reg, 1, 1] * vk + g["B"][reg, 1] * u + g["c"][reg, 1]
+    assert np.abs(pred - v[:, 1:]).max() <= 1e-9
+    # random sample against the oracle
+    rng = np.random.default_rng(0)
+    idx = rng.choice(len(roles), 200, replace=False)
+    ref = oracle_solve(O.gear_pwa_system(800.0), O.Cfg(), N, params[idx], roles[idx])
+    for j, r in zip(idx, ref):
+        assert list(reg[j]) == list(r.sigma)
+        assert abs(float(a["cost"][j]) - r.cost) <= 1e-9 * max(1.0, abs(r.cost))
+        assert np.abs(u[j] - r.u).max() <= 1e-6
