@@ -114,6 +114,27 @@ struct LaneQp {
     double tlo[NPAIR], thi[NPAIR], llo[NPAIR], lhi[NPAIR];
     double sf[NPX], tf[NPX], lf[NPX], lf2[NPX];
     double sb[NPX], tb[NPX], lb[NPX], lb2[NPX];
+
+    // Start of a sweep: make the iterate opaque to the compiler.  Every sweep recomputes its
+    // per-row quantities (scalings, residuals, directions) from the iterate instead of storing
+    // them; without this fence GVN merges the identical expressions of different sweeps and
+    // keeps them live across the whole iteration, which spills the register file.
+    HVP_HD void fence() {
+        mem.refresh();
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+        for (int i = 0; i < N; ++i) asm volatile("" : "+v"(y[i]));
+#pragma unroll
+        for (int i = 0; i < NPAIR; ++i) {
+            asm volatile("" : "+v"(tlo[i]), "+v"(thi[i]), "+v"(llo[i]), "+v"(lhi[i]));
+        }
+#pragma unroll
+        for (int i = 0; i < NPX; ++i) {
+            asm volatile("" : "+v"(sf[i]), "+v"(tf[i]), "+v"(lf[i]), "+v"(lf2[i]));
+            asm volatile("" : "+v"(sb[i]), "+v"(tb[i]), "+v"(lb[i]), "+v"(lb2[i]));
+        }
+#endif
+    }
 };
 
 // bounds of pair p (V,U,A of step k = p/3 + 1; P of step k = p - 3N + 2)
@@ -422,7 +443,7 @@ struct Solver {
     HVP_HD static QpOut solve(LaneQp<N, M>& q, const Consts& C) {
         QpOut out{0.0, 2, 0};
         const double w = C.w;
-        const int m = 2 * NPAIR_ACTIVE + (q.has_sf ? 2 * NP : 0) + (q.has_sb ? 2 * NP : 0);
+        const int m = 2 * NPAIR_ACTIVE + (true ? 2 * NP : 0) + (true ? 2 * NP : 0);
         const double zero[N] = {};
 
         // =============== initial point (CVXOPT / Mehrotra): minimise 1/2 y'Hy + f'y + w 1's
@@ -443,8 +464,8 @@ struct Solver {
                        scatter_pair(q, p, 2.0, -(-gy + lo) + (gy - hi), K, rhs, beta, rpre);
                    },
                    [&](int j, double pk, double, double) {
-                       if (q.has_sf) { beta[j] += 0.5; rpre[j] += 0.5 * ((pk - q.hf(j)) + w); }
-                       if (q.has_sb) { beta[j] += 0.5; rpre[j] -= 0.5 * ((-pk + q.hb(j)) + w); }
+                       if (true) { beta[j] += 0.5; rpre[j] += 0.5 * ((pk - q.hf(j)) + w); }
+                       if (true) { beta[j] += 0.5; rpre[j] -= 0.5 * ((-pk + q.hb(j)) + w); }
                    });
             expand_prefix<N>(q, beta, rpre, K, rhs);
             if (!cholesky<N>(K)) return out;
@@ -461,14 +482,14 @@ struct Solver {
                    },
                    [&](int j, double pk, double, double) {
                        // slack of the unit solve: s = (g.y + rt1 - r_s) / 2 = (sgn p_k - h - w) / 2
-                       if (q.has_sf) {
+                       if (true) {
                            const double s = 0.5 * (pk - q.hf(j) - w);
                            q.sf[j] = s;
                            q.tf[j] = q.hf(j) - (pk - s);
                            tmin = fmin(tmin, fmin(q.tf[j], s));
                            tmax = fmax(tmax, fmax(q.tf[j], s));
                        }
-                       if (q.has_sb) {
+                       if (true) {
                            const double s = 0.5 * (-pk + q.hb(j) - w);
                            q.sb[j] = s;
                            q.tb[j] = -q.hb(j) - (-pk - s);
@@ -486,8 +507,8 @@ struct Solver {
             };
             groups(q, zero, zero, zero, [&](int p, double, double, double) { acc(q.tlo[p]); acc(q.thi[p]); },
                    [&](int j, double, double, double) {
-                       if (q.has_sf) { acc(q.tf[j]); acc(q.sf[j]); }
-                       if (q.has_sb) { acc(q.tb[j]); acc(q.sb[j]); }
+                       if (true) { acc(q.tf[j]); acc(q.sf[j]); }
+                       if (true) { acc(q.tb[j]); acc(q.sb[j]); }
                    });
             const double dt0 = lsum > 0 ? 0.5 * tl / lsum : 1.0, dl0 = tsum > 0 ? 0.5 * tl / tsum : 1.0;
             auto fix = [&](double& t, double& l) {
@@ -500,8 +521,8 @@ struct Solver {
             groups(q, zero, zero, zero,
                    [&](int p, double, double, double) { fix(q.tlo[p], q.llo[p]); fix(q.thi[p], q.lhi[p]); },
                    [&](int j, double, double, double) {
-                       if (q.has_sf) { fix(q.tf[j], q.lf[j]); fix(q.sf[j], q.lf2[j]); }
-                       if (q.has_sb) { fix(q.tb[j], q.lb[j]); fix(q.sb[j], q.lb2[j]); }
+                       if (true) { fix(q.tf[j], q.lf[j]); fix(q.sf[j], q.lf2[j]); }
+                       if (true) { fix(q.tb[j], q.lb[j]); fix(q.sb[j], q.lb2[j]); }
                    });
         }
 
@@ -515,8 +536,8 @@ struct Solver {
         assemble_begin(q, A);
         groups(q, q.y, zero, zero, [&](int p, double gy, double, double) { assemble_pair(q, C, A, p, gy); },
                [&](int j, double pk, double, double) {
-                   if (q.has_sf) assemble_safe(q, A, j, 1.0, pk, q.hf(j), q.sf[j], q.tf[j], q.lf[j], q.lf2[j], w);
-                   if (q.has_sb) assemble_safe(q, A, j, -1.0, -pk, -q.hb(j), q.sb[j], q.tb[j], q.lb[j], q.lb2[j], w);
+                   if (true) assemble_safe(q, A, j, 1.0, pk, q.hf(j), q.sf[j], q.tf[j], q.lf[j], q.lf2[j], w);
+                   if (true) assemble_safe(q, A, j, -1.0, -pk, -q.hb(j), q.sb[j], q.tb[j], q.lb[j], q.lb2[j], w);
                });
         assemble_end(q, A, q.y);
 
@@ -553,7 +574,7 @@ struct Solver {
             chol_solve<N>(A.K, A.rhs, dya);
             const double mu = A.gap / m;
 
-            q.mem.refresh();
+            q.fence();
             // ------------------------------------------------ pass X: affine step, centring and the
             // corrector rhs split as  rhsA + sigma mu * rhsB  (linear in sigma mu)
             double amax_a = 1.0, S1 = 0.0, S2 = 0.0;
@@ -600,8 +621,8 @@ struct Solver {
                            pA[j] += sgn * R.c(rt1A, rt2A);
                            pB[j] += sgn * R.d1 * R.d2 * R.ie * (frcp(l1) - frcp(l2));
                        };
-                       if (q.has_sf) safe(1.0, q.hf(j), q.sf[j], q.tf[j], q.lf[j], q.lf2[j]);
-                       if (q.has_sb) safe(-1.0, -q.hb(j), q.sb[j], q.tb[j], q.lb[j], q.lb2[j]);
+                       if (true) safe(1.0, q.hf(j), q.sf[j], q.tf[j], q.lf[j], q.lf2[j]);
+                       if (true) safe(-1.0, -q.hb(j), q.sb[j], q.tb[j], q.lb[j], q.lb2[j]);
                    });
             const double mua = (A.gap + amax_a * S1 + amax_a * amax_a * S2) / m;
             const double sr = fmax(mua, 0.0) / mu;
@@ -641,7 +662,7 @@ struct Solver {
                 R.dir(gd, rt1, rt2, ds, dt1, dl1, dl2);
             };
             double amax = 1.0;
-            q.mem.refresh();
+            q.fence();
             groups(q, q.y, dya, dy,
                    [&](int p, double gy, double ga, double gd) {
                        double lo, hi;
@@ -665,8 +686,8 @@ struct Solver {
                            ratio_test(amax, l1, dl1);
                            ratio_test(amax, l2, dl2);
                        };
-                       if (q.has_sf) safe(1.0, q.hf(j), q.sf[j], q.tf[j], q.lf[j], q.lf2[j]);
-                       if (q.has_sb) safe(-1.0, -q.hb(j), q.sb[j], q.tb[j], q.lb[j], q.lb2[j]);
+                       if (true) safe(1.0, q.hf(j), q.sf[j], q.tf[j], q.lf[j], q.lf2[j]);
+                       if (true) safe(-1.0, -q.hb(j), q.sb[j], q.tb[j], q.lb[j], q.lb2[j]);
                    });
             const double alpha = fmin(1.0, 0.99 * amax);
 
@@ -675,7 +696,7 @@ struct Solver {
 #pragma unroll
             for (int i = 0; i < N; ++i) ynew[i] = q.y[i] + alpha * dy[i];
             assemble_begin(q, A);
-            q.mem.refresh();
+            q.fence();
             groups(q, q.y, dya, dy,
                    [&](int p, double gy, double ga, double gd) {
                        double lo, hi;
@@ -701,8 +722,8 @@ struct Solver {
                            l2 += alpha * dl2;
                            assemble_safe(q, A, j, sgn, sgn * (pk + alpha * gd), h1, s, t1, l1, l2, w);
                        };
-                       if (q.has_sf) safe(1.0, q.hf(j), q.sf[j], q.tf[j], q.lf[j], q.lf2[j]);
-                       if (q.has_sb) safe(-1.0, -q.hb(j), q.sb[j], q.tb[j], q.lb[j], q.lb2[j]);
+                       if (true) safe(1.0, q.hf(j), q.sf[j], q.tf[j], q.lf[j], q.lf2[j]);
+                       if (true) safe(-1.0, -q.hb(j), q.sb[j], q.tb[j], q.lb[j], q.lb2[j]);
                    });
             last_step = 0.0;
 #pragma unroll
@@ -775,10 +796,14 @@ HVP_HD inline bool setup_lane(LaneQp<N, M>& q, const hvp_system& S, const Consts
         }
     }
     // step-1 rows carry the constant v0 on the left: U: v1 - a0 v0, A: v1 - v0 (handled in for_rows)
+    // An absent neighbour (front / trailer vehicle) gets an INERT safe row instead of none: its
+    // bound lies beyond any position reachable under the velocity box, so the row can never be
+    // active and the optimum is unchanged, while every lane runs the same branch-free code.
 #pragma unroll
     for (int j = 0; j < N - 1; ++j) {
-        q.mem.set(F_HF, j, xf[j + 2] - C.d_safe);
-        q.mem.set(F_HB, j, xb[j + 2] + C.d_safe);
+        const double reach = ts * (j + 1);
+        q.mem.set(F_HF, j, q.has_sf ? xf[j + 2] - C.d_safe : q.P1 + reach * S.vmax + 100.0);
+        q.mem.set(F_HB, j, q.has_sb ? xb[j + 2] + C.d_safe : q.P1 + reach * S.vmin - 100.0);
     }
 
     // ---- cost: 1/2 y'Hy + f'y + C0
@@ -889,9 +914,21 @@ HVP_HD inline bool setup_lane(LaneQp<N, M>& q, const hvp_system& S, const Consts
 // writes it (fleet_decent_mld.py:107-169): squared tracking errors, Q_u u^2, Q_du du^2 and
 // w * max(0, .) slacks.  Avoids the cancellation of C0 + 1/2 y'Hy + f'y (positions ~3e3), so
 // the costs the argmin compares carry relative error ~1e-15 instead of ~1e-9.
+// Launders a pointer on the device so that loads through it are not merged with loads made
+// before a solve (which would keep those values live in registers across the whole IPM).
+template <class T>
+HVP_HD inline T* opaque_ptr(T* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+v"(p));
+#endif
+    return p;
+}
+
 template <int N, class M>
-HVP_HD inline double direct_cost(const LaneQp<N, M>& q, const hvp_system& S, const Consts& C, int role,
-                                 const double* prm, uint32_t code) {
+HVP_HD inline double direct_cost(const LaneQp<N, M>& q, const hvp_system& S_in, const Consts& C, int role,
+                                 const double* prm_in, uint32_t code) {
+    const double* prm = opaque_ptr(prm_in);
+    const hvp_system& S = *opaque_ptr(&S_in);
     const double* xf = prm + 2;
     const double* xb = prm + 2 + 2 * (N + 1);
     const double* xl = prm + 2 + 4 * (N + 1);

@@ -178,7 +178,6 @@ __global__ __launch_bounds__(kBlock) void k_qp(const hvp_system* __restrict__ sy
             ws.redo[r] = (int32_t)t;
             o.status = 4;
         }
-        ws.task_cost[t] = o.status == 0 ? hvp::direct_cost<N>(q, S, C, rl, prm, code) : 1e300;
         ws.task_stat[t] = o.status | (o.iters << 8);
 #pragma unroll
         for (int k = 0; k < N; ++k) ws.task_y[t * N + k] = q.y[k];
@@ -188,6 +187,34 @@ __global__ __launch_bounds__(kBlock) void k_qp(const hvp_system* __restrict__ sy
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) iter_sum += __shfl_down(iter_sum, off, 64);
     if ((threadIdx.x & 63) == 0 && iter_sum) atomicAdd(&ws.counter[1], iter_sum);
+}
+
+// ------------------------------------------------------------------ K_cost
+// Objective of every converged candidate, evaluated term by term on its trajectory (separate
+// launch: fused into K_qp its reference loads stay live across the IPM and spill).
+template <int N>
+__global__ __launch_bounds__(kBlock) void k_cost(const hvp_system* __restrict__ systems,
+                                                 const int32_t* __restrict__ sys, const int32_t* __restrict__ role,
+                                                 const double* __restrict__ params, hvp::Consts C, Workspace ws) {
+    const unsigned long long reserved = ws.counter[0];
+    const long long total = (long long)(reserved < (unsigned long long)ws.cap ? reserved : ws.cap);
+    for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (long long)gridDim.x * blockDim.x) {
+        const int inst = ws.task_inst[t];
+        double cost = 1e300;
+        if ((ws.task_stat[t] & 0xff) == 0) {
+            const hvp_system& S = systems[sys[inst]];
+            const double* prm = params + (size_t)inst * (2 + 6 * (N + 1));
+            hvp::LaneQp<N> q;
+            const int rl = role[inst];
+            q.has_sf = (rl & HVP_ROLE_SAFE_FRONT) != 0;
+            q.has_sb = (rl & HVP_ROLE_SAFE_BACK) != 0;
+#pragma unroll
+            for (int k = 0; k < N; ++k) q.y[k] = ws.task_y[t * N + k];
+            cost = hvp::direct_cost<N>(q, S, C, rl, prm, ws.task_code[t]);
+        }
+        ws.task_cost[t] = cost;
+    }
 }
 
 // ------------------------------------------------------------------ K_select
@@ -276,6 +303,8 @@ int launch_all(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
     // redo list (normally empty: the launch reads a zero count and exits)
     hipLaunchKernelGGL((k_qp<N, true>), dim3(std::max(1, h->n_cu)), dim3(kBlock), lds, st, h->d_sys, sys, role,
                        params, h->C, ws);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_cost<N>, dim3((int)want), dim3(kBlock), 0, st, h->d_sys, sys, role, params, h->C, ws);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_select<N>, dim3(grid_for(B)), dim3(kBlock), 0, st, B, h->d_sys, sys, params, ws, u_out,
                        x_out, region_out, gear_out, cost_out, status_out, nodes_out, iters_out);
