@@ -152,7 +152,7 @@ def main() -> None:
     torch.cuda.synchronize()
     st0 = solver.stats()
 
-    qp_ms, cand, iters = [], 0, 0
+    qp_ms, cand, iters, fallback = [], 0, 0, 0
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -163,6 +163,7 @@ def main() -> None:
         qp_ms.append(s.qp_ms)
         cand += s.n_candidates
         iters += s.ipm_iterations
+        fallback += s.n_fallback
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -198,11 +199,12 @@ def main() -> None:
                    "platoons_per_gpu": S, "local_miqps_per_step": B * world, "parallelism": f"seeds-sharded x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "k_qp", "kernel_avg_ms": qp_avg_ms,
+                     "kernel": "k_qp_gi", "kernel_avg_ms": qp_avg_ms,
                      "note": "achieved = SURVEY 8(d) dense-QP bytes of the sequences solved per launch / K_qp time; "
                              "the kernel builds its QPs in registers (FP64-VALU bound), see DESIGN.md"},
         "candidates_per_step": cand_per_launch,
-        "ipm_iters_per_candidate": iters / max(cand, 1),
+        "qp_iters_per_candidate": iters / max(cand, 1),
+        "ipm_fallbacks_per_step": fallback / args.steps,
         "all_optimal": ok,
     }
     if rank == 0 and not args.no_cpu and args.cpu_budget > 0 and world == 1:

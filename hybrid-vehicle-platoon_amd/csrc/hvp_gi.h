@@ -1,0 +1,399 @@
+// hvp_gi.h -- Goldfarb-Idnani dual active-set solver of the fixed-sequence QP (fast path).
+//
+// Same QP as hvp_ipm.h, written as an exact-penalty problem in velocity space:
+//     min  1/2 y'Hy + f'y + w sum_soft max(0, c_i.y - d_i)   s.t.  c_i.y <= d_i  (hard rows)
+// The soft rows are the safe-distance rows (fleet_decent_mld.py:190-208) with their slack
+// variables eliminated: a slack s >= 0 with cost w s is exactly the penalty w max(0, .), i.e.
+// a constraint whose multiplier is bounded above by w.
+//
+// Goldfarb & Idnani (1983): start from the unconstrained minimiser, repeatedly add the most
+// violated row, keep the current point optimal for the active rows (J = L^-T Q, R from the QR
+// of L^-1 N_A), drop rows whose multipliers would turn negative.  Extension for the soft rows:
+// when a soft row's multiplier reaches w during a step it is SATURATED -- removed from the
+// active set and moved into the objective as the linear term w c_i (stationarity is preserved
+// exactly, since its multiplier equals w at that point).
+//
+// State per lane: y, J (N x N), R (N x N upper), the active multipliers and ids -- a few dozen
+// doubles instead of the IPM's per-row slacks and multipliers.  All loops run over the static
+// bound N with predication so every array stays in registers.
+//
+// The result is verified (primal feasibility, multiplier signs and bounds, consistency of the
+// saturated rows); a lane that fails verification or the iteration cap reports GI_FAIL and is
+// re-solved by the interior-point path (hvp_ipm.h).
+#pragma once
+
+#include "hvp_ipm.h"
+
+namespace hvp {
+
+enum { GI_OK = 0, GI_FAIL = 5 };
+
+template <int N>
+struct GiConstraintSet {
+    static constexpr int NV = 6 * N;            // V/U/A rows, 6 per step
+    static constexpr int NPRE = 4 * (N - 1);    // P_lo, P_hi, SF (soft), SB (soft) per step >= 2
+    static constexpr int NC = NV + NPRE;
+};
+
+// Normal (in <= form, c.y <= d) of row id, densely in c[], its bound d and whether it is soft.
+template <int N, class M>
+HVP_HD inline void gi_row(const LaneQp<N, M>& q, const Consts& C, int id, double* c, double& d, bool& soft) {
+    soft = false;
+#pragma unroll
+    for (int i = 0; i < N; ++i) c[i] = 0.0;
+    if (id < 6 * N) {
+        const int j = id / 6, r = id % 6;
+        const int pair = r / 2;               // 0 V, 1 U, 2 A
+        const double sgn = (r & 1) ? 1.0 : -1.0;  // lo rows are negated
+        const double a = pair == 1 ? q.am(j) : (pair == 2 ? 1.0 : 0.0);
+        double lo, hi;
+        if (pair == 0) { lo = q.vlo(j); hi = q.vhi(j); }
+        else if (pair == 1) { lo = q.ulo(j); hi = q.uhi(j); }
+        else { lo = C.dec[j]; hi = C.acc[j]; }
+        // row value g.y (+ const for j = 0): V: y_j ; U: y_j - a y_{j-1} ; A: y_j - y_{j-1}
+        const double cst = j == 0 ? -a * q.v0 : 0.0;
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            c[i] = (i == j ? sgn : 0.0) + (i + 1 == j ? -sgn * a : 0.0);
+        }
+        d = (r & 1) ? hi - cst : -(lo - cst);
+    } else {
+        const int m = (id - 6 * N) / 4, r = (id - 6 * N) % 4;
+        const double sgn = (r == 1 || r == 2) ? 1.0 : -1.0;  // P_hi, SF: +prefix ; P_lo, SB: -prefix
+#pragma unroll
+        for (int i = 0; i < N; ++i) c[i] = i <= m ? sgn * q.ts : 0.0;
+        if (r == 0) d = q.P1 - q.pmin;
+        else if (r == 1) d = q.pmax - q.P1;
+        else if (r == 2) d = q.hf(m) - q.P1;
+        else d = q.P1 - q.hb(m);
+        soft = r >= 2;
+    }
+}
+
+// Slack d - c.y of every row (structured: O(1) per row) and the most violated one
+// (largest violation relative to |c|), skipping the active and saturated rows.
+template <int N, class M>
+HVP_HD inline int gi_most_violated(const LaneQp<N, M>& q, const Consts& C, const double* y, uint64_t skip0,
+                                   uint64_t skip1, double tol, double& s_out) {
+    int best = -1;
+    double best_v2 = 0.0, best_nn = 1.0, best_s = 0.0;
+    auto consider = [&](int id, double slack, double nn, double scale) {
+        const bool skipped = id < 64 ? ((skip0 >> id) & 1ull) : ((skip1 >> (id - 64)) & 1ull);
+        if (skipped || !(slack < -tol * scale)) return;
+        // maximise slack^2 / |c|^2 among violated rows
+        const double v2 = slack * slack;
+        if (best < 0 || v2 * best_nn > best_v2 * nn) {
+            best = id;
+            best_v2 = v2;
+            best_nn = nn;
+            best_s = slack;
+        }
+    };
+    double yprev = q.v0, cum = 0.0;
+#pragma unroll
+    for (int k = 1; k <= N; ++k) {
+        const int j = k - 1;
+        const double yk = y[j];
+        const double a = q.am(j);
+        const double gv = yk, gu = yk - a * yprev, ga = yk - yprev;
+        const double nu = j ? 1.0 + a * a : 1.0, na = j ? 2.0 : 1.0;
+        const double vl = q.vlo(j), vh = q.vhi(j), ul = q.ulo(j), uh = q.uhi(j), al = C.dec[j], ah = C.acc[j];
+        consider(6 * j + 0, gv - vl, 1.0, 1.0 + fabs(vl));
+        consider(6 * j + 1, vh - gv, 1.0, 1.0 + fabs(vh));
+        consider(6 * j + 2, gu - ul, nu, 1.0 + fabs(ul) + fabs(a * yprev));
+        consider(6 * j + 3, uh - gu, nu, 1.0 + fabs(uh) + fabs(a * yprev));
+        consider(6 * j + 4, ga - al, na, 1.0 + fabs(yprev));
+        consider(6 * j + 5, ah - ga, na, 1.0 + fabs(yprev));
+        if (k >= 2) {
+            const int m = k - 2;
+            cum += y[m];
+            const double p = q.P1 + q.ts * cum, nn = q.ts * q.ts * (m + 1);
+            const double sc = 1.0 + fabs(p);
+            const int b = 6 * N + 4 * m;
+            consider(b + 0, p - q.pmin, nn, sc);
+            consider(b + 1, q.pmax - p, nn, sc);
+            consider(b + 2, q.hf(m) - p, nn, sc);
+            consider(b + 3, p - q.hb(m), nn, sc);
+        }
+        yprev = yk;
+    }
+    s_out = best_s;
+    return best;
+}
+
+HVP_HD inline void givens(double a, double b, double& c, double& s) {
+    // rotation [c s; -s c] with  c a + s b = r,  -s a + c b = 0
+    const double h = sqrt(a * a + b * b);
+    if (h == 0.0) { c = 1.0; s = 0.0; return; }
+    const double ih = frcp(h);
+    c = a * ih;
+    s = b * ih;
+}
+
+template <int N, class M>
+HVP_HD inline int solve_gi(LaneQp<N, M>& q, const Consts& C, int max_iter, int& iters) {
+    iters = 0;
+    // ---- unconstrained minimiser and J = L^-T
+    double L[N * (N + 1) / 2];
+#pragma unroll
+    for (int i = 0; i < N * (N + 1) / 2; ++i) L[i] = q.H[i];
+    if (!cholesky<N>(L)) return GI_FAIL;  // stores the inverse diagonal
+    double negf[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) negf[i] = -q.f[i];
+    chol_solve<N>(L, negf, q.y);
+    double J[N][N];  // J[row][col]
+    // L^-1 (lower) by forward substitution of the identity; J = (L^-1)^T
+#pragma unroll
+    for (int col = 0; col < N; ++col) {
+        double x[N];
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            double v = i == col ? 1.0 : 0.0;
+#pragma unroll
+            for (int k = 0; k < i; ++k) v -= L[tri(i, k)] * x[k];
+            x[i] = v * L[tri(i, i)];
+        }
+        // x = column col of L^-1 ; J = L^-T  ->  J[col][i] = x[i]
+#pragma unroll
+        for (int i = 0; i < N; ++i) J[col][i] = x[i];
+    }
+    double R[N][N];
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+#pragma unroll
+        for (int j = 0; j < N; ++j) R[i][j] = 0.0;
+    double u[N];
+    int ids[N];
+    bool usoft[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) { u[i] = 0.0; ids[i] = -1; usoft[i] = false; }
+    int nact = 0;
+    uint64_t act0 = 0, act1 = 0, sat0 = 0, sat1 = 0;  // active / saturated row masks
+    const double w = C.w;
+    const double tol = 1e-11;
+    auto setbit = [](uint64_t& m0, uint64_t& m1, int id, bool on) {
+        if (id < 64) { if (on) m0 |= 1ull << id; else m0 &= ~(1ull << id); }
+        else { if (on) m1 |= 1ull << (id - 64); else m1 &= ~(1ull << (id - 64)); }
+    };
+
+    int iter = 0;
+    for (;;) {
+        // ---------------- step 1: most violated row
+        q.mem.refresh();
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            asm volatile("" : "+v"(q.y[i]), "+v"(u[i]));
+#pragma unroll
+            for (int j = 0; j < N; ++j) asm volatile("" : "+v"(J[i][j]), "+v"(R[i][j]));
+        }
+#endif
+        double sp;
+        const int p = gi_most_violated(q, C, q.y, act0 | sat0, act1 | sat1, tol, sp);
+        if (p < 0) break;
+        double np[N], dp;
+        bool psoft;
+        gi_row(q, C, p, np, dp, psoft);
+#pragma unroll
+        for (int i = 0; i < N; ++i) np[i] = -np[i];  // >= form: n = -c, b = -d ; slack s = n.y - b
+        double unew = 0.0;
+        bool added = false;
+        for (;;) {
+            if (++iter > max_iter) { iters = iter; return GI_FAIL; }
+            // ---------------- step 2: directions
+            double dv[N];
+#pragma unroll
+            for (int col = 0; col < N; ++col) {
+                double s = 0.0;
+#pragma unroll
+                for (int i = 0; i < N; ++i) s += J[i][col] * np[i];
+                dv[col] = s;
+            }
+            double z[N];
+            double d2n = 0.0, dn = 0.0;
+#pragma unroll
+            for (int col = 0; col < N; ++col) {
+                dn += dv[col] * dv[col];
+                if (col >= nact) d2n += dv[col] * dv[col];
+            }
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                double s = 0.0;
+#pragma unroll
+                for (int col = 0; col < N; ++col) s += col >= nact ? J[i][col] * dv[col] : 0.0;
+                z[i] = s;
+            }
+            double r[N];
+#pragma unroll
+            for (int i = N - 1; i >= 0; --i) {
+                double v = dv[i];
+#pragma unroll
+                for (int j = i + 1; j < N; ++j) v -= (j < nact) ? R[i][j] * r[j] : 0.0;
+                r[i] = (i < nact) ? v / R[i][i] : 0.0;
+            }
+            // partial step: an active multiplier reaches zero
+            double t1 = 1e300;
+            int k1 = -1;
+#pragma unroll
+            for (int j = 0; j < N; ++j) {
+                if (j < nact && r[j] > 0.0) {
+                    const double tj = u[j] / r[j];
+                    if (tj < t1) { t1 = tj; k1 = j; }
+                }
+            }
+            // soft bound: a multiplier reaches w (active soft rows with r < 0, or the new row)
+            double t3 = psoft ? w - unew : 1e300;
+            int k3 = psoft ? N : -1;  // N denotes the new row p
+#pragma unroll
+            for (int j = 0; j < N; ++j) {
+                if (j < nact && usoft[j] && r[j] < 0.0) {
+                    const double tj = (w - u[j]) / (-r[j]);
+                    if (tj < t3) { t3 = tj; k3 = j; }
+                }
+            }
+            // full step: the new row becomes active
+            const bool zstep = d2n > 1e-14 * dn;
+            double zn = 0.0;
+#pragma unroll
+            for (int i = 0; i < N; ++i) zn += z[i] * np[i];
+            double sp_now = dp;
+#pragma unroll
+            for (int i = 0; i < N; ++i) sp_now += np[i] * q.y[i];  // current slack n.y - b
+            const double t2 = zstep && zn > 0.0 ? fmax(-sp_now, 0.0) / zn : 1e300;
+            const double t = fmin(t1, fmin(t2, t3));
+            if (!(t < 1e299)) { iters = iter; return GI_FAIL; }  // infeasible (cannot happen for enumerated sequences)
+            // apply the step
+            if (zstep && t2 < 1e299) {
+#pragma unroll
+                for (int i = 0; i < N; ++i) q.y[i] += t * z[i];
+            }
+#pragma unroll
+            for (int j = 0; j < N; ++j)
+                if (j < nact) u[j] -= t * r[j];
+            unew += t;
+            if (t == t2 && t2 <= t1 && t2 <= t3) {
+                // ---- add p: Givens rotations zero dv[nact+1..N-1], rotating J's columns
+#pragma unroll
+                for (int i = N - 1; i >= 1; --i) {
+                    if (i > nact) {
+                        double gc, gs;
+                        givens(dv[i - 1], dv[i], gc, gs);
+                        dv[i - 1] = gc * dv[i - 1] + gs * dv[i];
+                        dv[i] = 0.0;
+#pragma unroll
+                        for (int row = 0; row < N; ++row) {
+                            const double a0 = J[row][i - 1], a1 = J[row][i];
+                            J[row][i - 1] = gc * a0 + gs * a1;
+                            J[row][i] = -gs * a0 + gc * a1;
+                        }
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < N; ++i)
+#pragma unroll
+                    for (int col = 0; col < N; ++col)
+                        if (col == nact && i <= nact) R[i][col] = dv[i];
+#pragma unroll
+                for (int j = 0; j < N; ++j)
+                    if (j == nact) { u[j] = unew; ids[j] = p; usoft[j] = psoft; }
+                setbit(act0, act1, p, true);
+                ++nact;
+                added = true;
+                break;
+            }
+            // ---- a row leaves the active set: the zero-multiplier one (t1) or a saturating soft one (t3)
+            int drop = -1;
+            if (t3 <= t1) {
+                if (k3 == N) {
+                    // the new soft row saturates: it joins the objective as w c_p, no constraint added
+                    setbit(sat0, sat1, p, true);
+                    added = true;
+                    break;
+                }
+                drop = k3;
+                setbit(sat0, sat1, ids[k3 < N ? k3 : 0], true);
+            } else {
+                drop = k1;
+            }
+            // remove active row at position `drop`: shift columns of R, u, ids; re-triangularise
+            int dropped_id = -1;
+#pragma unroll
+            for (int j = 0; j < N; ++j)
+                if (j == drop) dropped_id = ids[j];
+            setbit(act0, act1, dropped_id, false);
+#pragma unroll
+            for (int j = 0; j < N - 1; ++j) {
+                if (j >= drop && j < nact - 1) {
+                    u[j] = u[j + 1];
+                    ids[j] = ids[j + 1];
+                    usoft[j] = usoft[j + 1];
+#pragma unroll
+                    for (int i = 0; i < N; ++i) R[i][j] = R[i][j + 1];
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < N; ++i)
+#pragma unroll
+                for (int j = 0; j < N; ++j)
+                    if (j == nact - 1) R[i][j] = 0.0;
+            // R is now upper Hessenberg in columns drop..nact-2: rotate rows (i, i+1)
+#pragma unroll
+            for (int i = 0; i < N - 1; ++i) {
+                if (i >= drop && i < nact - 1) {
+                    double gc, gs;
+                    givens(R[i][i], R[i + 1][i], gc, gs);
+#pragma unroll
+                    for (int col = 0; col < N; ++col) {
+                        if (col >= i && col < nact - 1) {
+                            const double a0 = R[i][col], a1 = R[i + 1][col];
+                            R[i][col] = gc * a0 + gs * a1;
+                            R[i + 1][col] = -gs * a0 + gc * a1;
+                        }
+                    }
+#pragma unroll
+                    for (int row = 0; row < N; ++row) {
+                        const double a0 = J[row][i], a1 = J[row][i + 1];
+                        J[row][i] = gc * a0 + gs * a1;
+                        J[row][i + 1] = -gs * a0 + gc * a1;
+                    }
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < N; ++j)
+                if (j == nact - 1) { u[j] = 0.0; ids[j] = -1; usoft[j] = false; }
+            --nact;
+            // continue with the same p (step 2)
+        }
+        (void)added;
+    }
+
+    // ---------------- verification (KKT of the exact-penalty problem)
+    // saturated rows must still be on their violated side
+    double yprev = q.v0, cum = 0.0;
+    bool ok = true;
+#pragma unroll
+    for (int k = 2; k <= N; ++k) {
+        const int m = k - 2;
+        cum += q.y[m];
+        const double pk = q.P1 + q.ts * cum;
+        const int b = 6 * N + 4 * m;
+        const bool satf = ((b + 2) < 64 ? (sat0 >> (b + 2)) & 1ull : (sat1 >> (b + 2 - 64)) & 1ull) != 0;
+        const bool satb = ((b + 3) < 64 ? (sat0 >> (b + 3)) & 1ull : (sat1 >> (b + 3 - 64)) & 1ull) != 0;
+        if (satf && pk < q.hf(m) - 1e-9 * (1.0 + fabs(pk))) ok = false;
+        if (satb && pk > q.hb(m) + 1e-9 * (1.0 + fabs(pk))) ok = false;
+    }
+    (void)yprev;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        if (j < nact) {
+            if (u[j] < -1e-9 * w) ok = false;
+            if (usoft[j] && u[j] > w * (1.0 + 1e-9)) ok = false;
+        }
+    }
+    // no violated rows left (the loop exits only then) -- stationarity holds by construction
+    iters = iter;
+    return ok ? GI_OK : GI_FAIL;
+}
+
+}  // namespace hvp

@@ -8,9 +8,14 @@
 
 #include <vector>
 
+#include "hvp_gi.h"
 #include "hvp_ipm.h"
 
 namespace {
+
+// 0: interior point only; 1: Goldfarb-Idnani active set, interior point on failure
+int g_solver = 1;
+long long g_gi_fail = 0, g_gi_iters = 0, g_gi_runs = 0;
 
 hvp::Consts make_consts(const hvp_problem& p) {
     hvp::Consts C;
@@ -52,8 +57,28 @@ void solve_one(const hvp_system& S, const hvp::Consts& C, int role, const double
         n = hvp::enumerate_sequences(S, C, prm[1], [&](uint32_t code, int) {
             hvp::LaneQp<N> q;
             hvp::setup_lane<N>(q, S, C, role, prm, code);
-            hvp::QpOut o = hvp::Solver<N, false>::solve(q, C);
-            if (o.status == 0 && !hvp::pbox_ok<N>(q)) {
+            hvp::QpOut o;
+            bool gi_done = false;
+            if (g_solver == 1) {
+                int it = 0;
+                const int r = hvp::solve_gi<N>(q, C, 8 * hvp::GiConstraintSet<N>::NC, it);
+#pragma omp atomic
+                g_gi_runs += 1;
+#pragma omp atomic
+                g_gi_iters += it;
+                if (r == hvp::GI_OK) {
+                    o.status = 0;
+                    o.iters = it;
+                    o.cost = 0.0;
+                    gi_done = true;
+                } else {
+#pragma omp atomic
+                    g_gi_fail += 1;
+                    hvp::setup_lane<N>(q, S, C, role, prm, code);
+                }
+            }
+            if (!gi_done) o = hvp::Solver<N, false>::solve(q, C);
+            if (!gi_done && o.status == 0 && !hvp::pbox_ok<N>(q)) {
                 // relaxed optimum leaves the position box: solve the full QP (exact fallback)
                 hvp::setup_lane<N>(q, S, C, role, prm, code);
                 const int it0 = o.iters;
@@ -127,6 +152,14 @@ void solve_range(const hvp_problem& P, const hvp_system* systems, int B, const i
 }  // namespace
 
 extern "C" {
+
+void hvp_hostref_set_solver(int s) { g_solver = s; }
+void hvp_hostref_gi_stats(long long* out) {
+    out[0] = g_gi_runs;
+    out[1] = g_gi_fail;
+    out[2] = g_gi_iters;
+    g_gi_runs = g_gi_fail = g_gi_iters = 0;
+}
 
 // Same outputs as hvp_solve_batch (host pointers); test / baseline use only.
 int hvp_hostref_solve_batch(const hvp_problem* P, const hvp_system* systems, int B, const int32_t* sys,

@@ -28,6 +28,7 @@
 
 #define HVP_HD __host__ __device__
 #include "hvp.h"
+#include "hvp_gi.h"
 #include "hvp_ipm.h"
 
 namespace {
@@ -46,6 +47,9 @@ int fail(int code, const std::string& msg) {
     } while (0)
 
 constexpr int kBlock = 256;
+// active-set iteration cap (then the interior-point fallback takes the candidate)
+template <int N>
+constexpr int kGiMaxIter = 8 * hvp::GiConstraintSet<N>::NC;
 
 struct Workspace {
     int max_batch = 0;
@@ -53,8 +57,8 @@ struct Workspace {
     int32_t* inst_off = nullptr;   // [max_batch] first candidate slot (-1: overflow)
     int32_t* inst_cnt = nullptr;   // [max_batch] candidates of the instance
     int32_t* inst_flag = nullptr;  // [max_batch] 0 ok, 1 infeasible constant rows
-    unsigned long long* counter = nullptr;  // [4] reserved slots, ipm iterations, redo count, pad
-    int32_t* redo = nullptr;       // [cap] candidates whose relaxed optimum left the position box
+    unsigned long long* counter = nullptr;  // [4] reserved slots, qp iterations, fallback count, pad
+    int32_t* redo = nullptr;       // [cap] candidates the active-set method hands to the IPM
     int32_t* task_inst = nullptr;  // [cap]
     uint32_t* task_code = nullptr; // [cap]
     double* task_cost = nullptr;   // [cap]
@@ -151,18 +155,17 @@ struct LdsMem {
     __device__ void refresh() { asm volatile("" : "+v"(lane)); }
 };
 
-// PBOX = false: every candidate, position-box rows dropped (checked afterwards);
-// PBOX = true : the redo list only, full row set.
-template <int N, bool PBOX>
-__global__ __launch_bounds__(kBlock) void k_qp(const hvp_system* __restrict__ systems, const int32_t* __restrict__ sys,
-                                               const int32_t* __restrict__ role, const double* __restrict__ params,
-                                               hvp::Consts C, Workspace ws) {
-    const unsigned long long reserved = PBOX ? ws.counter[2] : ws.counter[0];
+// K_qp: every candidate by the Goldfarb-Idnani active-set method (hvp_gi.h).  A lane whose
+// result fails the KKT verification (or hits the iteration cap) is queued on the fallback list.
+template <int N>
+__global__ __launch_bounds__(kBlock) void k_qp_gi(const hvp_system* __restrict__ systems,
+                                                  const int32_t* __restrict__ sys, const int32_t* __restrict__ role,
+                                                  const double* __restrict__ params, hvp::Consts C, Workspace ws) {
+    const unsigned long long reserved = ws.counter[0];
     const long long total = (long long)(reserved < (unsigned long long)ws.cap ? reserved : ws.cap);
     unsigned long long iter_sum = 0;
-    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-         i += (long long)gridDim.x * blockDim.x) {
-        const long long t = PBOX ? (long long)ws.redo[i] : i;
+    for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (long long)gridDim.x * blockDim.x) {
         const int inst = ws.task_inst[t];
         const uint32_t code = ws.task_code[t];
         const hvp_system& S = systems[sys[inst]];
@@ -171,19 +174,50 @@ __global__ __launch_bounds__(kBlock) void k_qp(const hvp_system* __restrict__ sy
         hvp::LaneQp<N, LdsMem<N>> q;
         q.mem.lane = threadIdx.x;
         hvp::setup_lane<N>(q, S, C, rl, prm, code);
-        hvp::QpOut o = hvp::Solver<N, PBOX, LdsMem<N>>::solve(q, C);
-        if (!PBOX && o.status == 0 && !hvp::pbox_ok<N>(q)) {
-            // relaxed optimum leaves the position box: queue the candidate for the full QP
+        int iters = 0;
+        int status = hvp::solve_gi<N>(q, C, kGiMaxIter<N>, iters);
+        if (status != hvp::GI_OK) {
             const unsigned long long r = atomicAdd(&ws.counter[2], 1ull);
             ws.redo[r] = (int32_t)t;
-            o.status = 4;
+            status = 4;  // pending: the fallback kernel overwrites it
         }
-        ws.task_stat[t] = o.status | (o.iters << 8);
+        ws.task_stat[t] = status | (iters << 8);
+#pragma unroll
+        for (int k = 0; k < N; ++k) ws.task_y[t * N + k] = q.y[k];
+        iter_sum += (unsigned long long)iters;
+    }
+    // one atomic per wave for the iteration statistics
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) iter_sum += __shfl_down(iter_sum, off, 64);
+    if ((threadIdx.x & 63) == 0 && iter_sum) atomicAdd(&ws.counter[1], iter_sum);
+}
+
+// K_qp_ipm: the fallback list only (normally empty: the launch reads a zero count and exits),
+// full row set by the Mehrotra interior-point method (hvp_ipm.h).
+template <int N>
+__global__ __launch_bounds__(kBlock) void k_qp_ipm(const hvp_system* __restrict__ systems,
+                                                   const int32_t* __restrict__ sys, const int32_t* __restrict__ role,
+                                                   const double* __restrict__ params, hvp::Consts C, Workspace ws) {
+    const unsigned long long reserved = ws.counter[2];
+    const long long total = (long long)(reserved < (unsigned long long)ws.cap ? reserved : ws.cap);
+    unsigned long long iter_sum = 0;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (long long)gridDim.x * blockDim.x) {
+        const long long t = (long long)ws.redo[i];
+        const int inst = ws.task_inst[t];
+        const uint32_t code = ws.task_code[t];
+        const hvp_system& S = systems[sys[inst]];
+        const int rl = role[inst];
+        const double* prm = params + (size_t)inst * (2 + 6 * (N + 1));
+        hvp::LaneQp<N, LdsMem<N>> q;
+        q.mem.lane = threadIdx.x;
+        hvp::setup_lane<N>(q, S, C, rl, prm, code);
+        const hvp::QpOut o = hvp::Solver<N, true, LdsMem<N>>::solve(q, C);
+        ws.task_stat[t] = o.status | ((o.iters + (ws.task_stat[t] >> 8)) << 8);
 #pragma unroll
         for (int k = 0; k < N; ++k) ws.task_y[t * N + k] = q.y[k];
         iter_sum += (unsigned long long)o.iters;
     }
-    // one atomic per wave for the iteration statistics
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) iter_sum += __shfl_down(iter_sum, off, 64);
     if ((threadIdx.x & 63) == 0 && iter_sum) atomicAdd(&ws.counter[1], iter_sum);
@@ -297,11 +331,11 @@ int launch_all(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
     const long long want = std::min<long long>(grid_for(h->ws.cap), (long long)h->n_cu * 8);
     HIP_TRY(hipEventRecord(h->evq0, st));
     const size_t lds = sizeof(double) * hvp::F_COUNT * N * kBlock;
-    hipLaunchKernelGGL((k_qp<N, false>), dim3((int)want), dim3(kBlock), lds, st, h->d_sys, sys, role, params, h->C, ws);
+    hipLaunchKernelGGL(k_qp_gi<N>, dim3((int)want), dim3(kBlock), lds, st, h->d_sys, sys, role, params, h->C, ws);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(h->evq1, st));
-    // redo list (normally empty: the launch reads a zero count and exits)
-    hipLaunchKernelGGL((k_qp<N, true>), dim3(std::max(1, h->n_cu)), dim3(kBlock), lds, st, h->d_sys, sys, role,
+    // fallback list (normally empty: the launch reads a zero count and exits)
+    hipLaunchKernelGGL(k_qp_ipm<N>, dim3(std::max(1, h->n_cu)), dim3(kBlock), lds, st, h->d_sys, sys, role,
                        params, h->C, ws);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_cost<N>, dim3((int)want), dim3(kBlock), 0, st, h->d_sys, sys, role, params, h->C, ws);
@@ -469,7 +503,7 @@ int hvp_get_stats(hvp_handle* h, hvp_stats* out) {
     out->n_instances = h->last_B;
     out->n_candidates = (int64_t)c[0];
     out->ipm_iterations = (int64_t)c[1];
-    out->n_pbox_redo = (int64_t)c[2];
+    out->n_fallback = (int64_t)c[2];
     out->capacity = h->ws.cap;
     out->last_ms = ms;
     return 0;

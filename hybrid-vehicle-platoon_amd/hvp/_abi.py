@@ -75,7 +75,7 @@ class HvpStats(ctypes.Structure):
         ("capacity", ctypes.c_int64),
         ("last_ms", ctypes.c_double),
         ("qp_ms", ctypes.c_double),
-        ("n_pbox_redo", ctypes.c_int64),
+        ("n_fallback", ctypes.c_int64),
     ]
 
 

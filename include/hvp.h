@@ -126,7 +126,7 @@ typedef struct hvp_stats {
     int64_t capacity;       /* candidate workspace                                     */
     double last_ms;         /* device time of the last solve (event-timed), ms         */
     double qp_ms;           /* device time of its QP kernel (K_qp), ms                 */
-    int64_t n_pbox_redo;    /* candidates re-solved with the position-box rows         */
+    int64_t n_fallback;     /* candidates re-solved by the interior-point fallback    */
 } hvp_stats;
 
 int hvp_create(hvp_handle** out, const hvp_problem* problem, const hvp_system* systems,

@@ -46,11 +46,18 @@ def run(L, prob, systems, fx):
     return out
 
 
+@pytest.mark.parametrize("solver", ["active_set", "ipm"])
 @pytest.mark.parametrize("name", fixture_names())
-def test_lane_algorithm_matches_golden(hostref, name):
+def test_lane_algorithm_matches_golden(hostref, name, solver):
+    """Both QP methods of the lane: the active-set fast path (hvp_gi.h, the product's K_qp_gi
+    with its interior-point fallback) and the interior-point method alone (hvp_ipm.h)."""
     fx = load(name)
     prob, systems = product_problem(fx)
-    out = run(hostref, prob, systems, fx)
+    hostref.hvp_hostref_set_solver(1 if solver == "active_set" else 0)
+    try:
+        out = run(hostref, prob, systems, fx)
+    finally:
+        hostref.hvp_hostref_set_solver(1)
     ok = fx["exp_status"] == 0
     assert np.array_equal(out["status"], fx["exp_status"])
     assert np.array_equal(out["nodes"], fx["exp_nodes"])
@@ -59,3 +66,23 @@ def test_lane_algorithm_matches_golden(hostref, name):
     assert np.all(np.abs(c - ce) <= 1e-9 * np.maximum(1, np.abs(ce)))
     assert np.abs(out["u"][ok] - fx["exp_u"][ok]).max() <= 1e-6
     assert np.abs(out["x"][ok] - fx["exp_x"][ok]).max() <= 1e-4
+
+
+def test_active_set_rarely_falls_back(hostref):
+    """The active-set method must carry (almost) every candidate QP of the golden sets itself;
+    the interior-point fallback is a safety net, not a second hot path."""
+    import ctypes
+
+    st = (ctypes.c_longlong * 3)()
+    hostref.hvp_hostref_set_solver(1)
+    hostref.hvp_hostref_gi_stats(st)  # reset
+    runs = fails = 0
+    for name in fixture_names():
+        fx = load(name)
+        prob, systems = product_problem(fx)
+        run(hostref, prob, systems, fx)
+        hostref.hvp_hostref_gi_stats(st)
+        runs += st[0]
+        fails += st[1]
+    assert runs > 10000
+    assert fails <= 1e-3 * runs
