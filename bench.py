@@ -42,6 +42,19 @@ def instance_io_bytes(N: int) -> int:
     return 8 * (2 + 6 * (N + 1) + N + 2 * (N + 1) + 1) + N
 
 
+def profiled(kernel: str):
+    """Per-launch PMC figures of `kernel` from the newest committed profiles/r*_summary.json
+    (profiles/run_profiles.sh runs this bench at its default workload under rocprofv3)."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_summary.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)["kernels"].get(kernel)
+    return (d, os.path.relpath(files[-1], ROOT)) if d else (None, None)
+
+
 def make_inputs(seeds, n: int, N: int):
     """(params, roles, sys) for n-vehicle platoons at t = 0 (vectorised over seeds)."""
     from hvp.batched import decent_params_from_states
@@ -150,20 +163,13 @@ def main() -> None:
     for _ in range(args.warmup):
         solver.solve_device(t_sys, t_roles, t_params, out)
     torch.cuda.synchronize()
-    st0 = solver.stats()
 
-    qp_ms, cand, iters, fallback = [], 0, 0, 0
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         solver.solve_device(t_sys, t_roles, t_params, out)
-        s = solver.stats()  # event times of this step (syncs the stream: per-step host sync)
-        qp_ms.append(s.qp_ms)
-        cand += s.n_candidates
-        iters += s.ipm_iterations
-        fallback += s.n_fallback
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -173,6 +179,18 @@ def main() -> None:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
 
+    # per-launch kernel time (HIP events recorded by the library on the solve stream around
+    # K_qp_gi) and work counters: a second pass of the same steps, outside the timed region,
+    # since reading them synchronises the stream after every step
+    qp_ms, cand, iters, fallback = [], 0, 0, 0
+    for _ in range(args.steps):
+        solver.solve_device(t_sys, t_roles, t_params, out)
+        s = solver.stats()
+        qp_ms.append(s.qp_ms)
+        cand += s.n_candidates
+        iters += s.qp_iterations
+        fallback += s.n_fallback
+
     ok = bool((out["status"] == 0).all().item())
     steps_total = S * world * args.steps
     value = steps_total / dt
@@ -180,6 +198,13 @@ def main() -> None:
     cand_per_launch = cand / args.steps
     alg_bytes = cand_per_launch * dense_qp_bytes(N) + B * instance_io_bytes(N)
     achieved = alg_bytes / (qp_avg_ms * 1e-3) / 1e9
+    prof, prof_src = profiled("k_qp_gi")
+    traffic = prof.get("hbm_bytes") if prof else None
+    fp64 = None
+    if prof and prof.get("f64_flop"):
+        tf = prof["f64_flop"] / (qp_avg_ms * 1e-3) / 1e12
+        fp64 = {"achieved": tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tf / FP64_PEAK_TFLOPS,
+                "flop_per_launch": prof["f64_flop"], "source": prof_src}
 
     result = {
         "metric": "MPC timesteps/sec (whole platoon) at n=10 N=5 decent_mld",
@@ -198,10 +223,15 @@ def main() -> None:
         "config": {"workload": "fleet_decent_mld n=10 N=5 pwa_gear (configs[1])", "n_vehicles": n, "horizon": N,
                    "platoons_per_gpu": S, "local_miqps_per_step": B * world, "parallelism": f"seeds-sharded x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "k_qp_gi", "kernel_avg_ms": qp_avg_ms,
-                     "note": "achieved = SURVEY 8(d) dense-QP bytes of the sequences solved per launch / K_qp time; "
-                             "the kernel builds its QPs in registers (FP64-VALU bound), see DESIGN.md"},
+                     "algorithmic_bytes_per_launch": alg_bytes, "traffic_source": prof_src,
+                     "note": "achieved = SURVEY 8(d) notional dense-QP bytes (13104 B per sequence at N=5) + "
+                             "instance I/O, per K_qp_gi launch / its HIP-event time. The kernel never "
+                             "materialises those matrices (QPs are built in registers from a 38-double "
+                             "instance block), so frac can exceed 1; traffic = measured HBM bytes "
+                             "(2*FETCH_SIZE + WRITE_SIZE). See DESIGN.md 'Roofline'."},
+        "fp64": fp64,
         "candidates_per_step": cand_per_launch,
         "qp_iters_per_candidate": iters / max(cand, 1),
         "ipm_fallbacks_per_step": fallback / args.steps,

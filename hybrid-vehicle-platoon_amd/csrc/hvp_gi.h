@@ -26,7 +26,8 @@
 
 namespace hvp {
 
-enum { GI_OK = 0, GI_FAIL = 5 };
+// GI_OK, or why the lane is handed to the interior-point fallback
+enum { GI_OK = 0, GI_FAIL_CHOL = 5, GI_FAIL_ITER = 6, GI_FAIL_DUAL = 7, GI_FAIL_VERIFY = 8 };
 
 template <int N>
 struct GiConstraintSet {
@@ -35,15 +36,23 @@ struct GiConstraintSet {
     static constexpr int NC = NV + NPRE;
 };
 
-// Normal (in <= form, c.y <= d) of row id, densely in c[], its bound d and whether it is soft.
+// Row ids: V/U/A rows 6j + {0 V_lo, 1 V_hi, 2 U_lo, 3 U_hi, 4 A_lo, 5 A_hi} (step k = j + 1),
+// prefix rows 6N + 4m + {0 P_lo, 1 P_hi, 2 SF, 3 SB} (step k = m + 2).  GI_REV marks the
+// reversed copy of a saturated soft row (see solve_gi).
+constexpr int GI_REV = 128;
+
+template <int N>
+HVP_HD constexpr bool gi_soft(int id) {
+    return (id & (GI_REV - 1)) >= 6 * N && (((id & (GI_REV - 1)) - 6 * N) & 2) != 0;
+}
+
+// Normal (in <= form, c.y <= d) of row id, densely in c[], and its bound d.
 template <int N, class M>
-HVP_HD inline void gi_row(const LaneQp<N, M>& q, const Consts& C, int id, double* c, double& d, bool& soft) {
-    soft = false;
-#pragma unroll
-    for (int i = 0; i < N; ++i) c[i] = 0.0;
+HVP_HD inline void gi_row(const LaneQp<N, M>& q, const Consts& C, int id_in, double* c, double& d) {
+    const int id = id_in & (GI_REV - 1);
     if (id < 6 * N) {
         const int j = id / 6, r = id % 6;
-        const int pair = r / 2;               // 0 V, 1 U, 2 A
+        const int pair = r / 2;                   // 0 V, 1 U, 2 A
         const double sgn = (r & 1) ? 1.0 : -1.0;  // lo rows are negated
         const double a = pair == 1 ? q.am(j) : (pair == 2 ? 1.0 : 0.0);
         double lo, hi;
@@ -53,9 +62,7 @@ HVP_HD inline void gi_row(const LaneQp<N, M>& q, const Consts& C, int id, double
         // row value g.y (+ const for j = 0): V: y_j ; U: y_j - a y_{j-1} ; A: y_j - y_{j-1}
         const double cst = j == 0 ? -a * q.v0 : 0.0;
 #pragma unroll
-        for (int i = 0; i < N; ++i) {
-            c[i] = (i == j ? sgn : 0.0) + (i + 1 == j ? -sgn * a : 0.0);
-        }
+        for (int i = 0; i < N; ++i) c[i] = (i == j ? sgn : 0.0) + (i + 1 == j ? -sgn * a : 0.0);
         d = (r & 1) ? hi - cst : -(lo - cst);
     } else {
         const int m = (id - 6 * N) / 4, r = (id - 6 * N) % 4;
@@ -66,20 +73,34 @@ HVP_HD inline void gi_row(const LaneQp<N, M>& q, const Consts& C, int id, double
         else if (r == 1) d = q.pmax - q.P1;
         else if (r == 2) d = q.hf(m) - q.P1;
         else d = q.P1 - q.hb(m);
-        soft = r >= 2;
+    }
+    if (id_in & GI_REV) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) c[i] = -c[i];
+        d = -d;
     }
 }
 
-// Slack d - c.y of every row (structured: O(1) per row) and the most violated one
-// (largest violation relative to |c|), skipping the active and saturated rows.
+// 128-bit row mask (N <= 8 gives at most 76 rows)
+struct GiMask {
+    uint64_t lo = 0, hi = 0;
+    HVP_HD bool get(int id) const { return id < 64 ? ((lo >> id) & 1ull) != 0 : ((hi >> (id - 64)) & 1ull) != 0; }
+    HVP_HD void set(int id, bool on) {
+        if (id < 64) lo = on ? (lo | (1ull << id)) : (lo & ~(1ull << id));
+        else hi = on ? (hi | (1ull << (id - 64))) : (hi & ~(1ull << (id - 64)));
+    }
+};
+
+// Slack d - c.y of every row (structured: O(1) per row) and the most violated one (largest
+// violation relative to |c|).  Active rows are skipped; a saturated soft row is represented by
+// its reversed copy (violated when the row is satisfied strictly).
 template <int N, class M>
-HVP_HD inline int gi_most_violated(const LaneQp<N, M>& q, const Consts& C, const double* y, uint64_t skip0,
-                                   uint64_t skip1, double tol, double& s_out) {
+HVP_HD inline int gi_most_violated(const LaneQp<N, M>& q, const Consts& C, const double* y, const GiMask& act,
+                                   uint32_t sat, double tol, double& s_out) {
     int best = -1;
     double best_v2 = 0.0, best_nn = 1.0, best_s = 0.0;
     auto consider = [&](int id, double slack, double nn, double scale) {
-        const bool skipped = id < 64 ? ((skip0 >> id) & 1ull) : ((skip1 >> (id - 64)) & 1ull);
-        if (skipped || !(slack < -tol * scale)) return;
+        if (act.get(id & (GI_REV - 1)) || !(slack < -tol * scale)) return;
         // maximise slack^2 / |c|^2 among violated rows
         const double v2 = slack * slack;
         if (best < 0 || v2 * best_nn > best_v2 * nn) {
@@ -112,8 +133,10 @@ HVP_HD inline int gi_most_violated(const LaneQp<N, M>& q, const Consts& C, const
             const int b = 6 * N + 4 * m;
             consider(b + 0, p - q.pmin, nn, sc);
             consider(b + 1, q.pmax - p, nn, sc);
-            consider(b + 2, q.hf(m) - p, nn, sc);
-            consider(b + 3, p - q.hb(m), nn, sc);
+            const double sfw = q.hf(m) - p, sbw = p - q.hb(m);
+            const bool satf = (sat >> (2 * m)) & 1u, satb = (sat >> (2 * m + 1)) & 1u;
+            consider(satf ? (b + 2) | GI_REV : b + 2, satf ? -sfw : sfw, nn, sc);
+            consider(satb ? (b + 3) | GI_REV : b + 3, satb ? -sbw : sbw, nn, sc);
         }
         yprev = yk;
     }
@@ -130,6 +153,12 @@ HVP_HD inline void givens(double a, double b, double& c, double& s) {
     s = b * ih;
 }
 
+// Goldfarb-Idnani with soft rows.  Invariant: y minimises
+//     1/2 y'Hy + f'y + w sum_{i in S} (c_i.y - d_i)   subject to the active rows at equality,
+// where S is the saturated set (soft rows whose multiplier reached w).  A saturated row whose
+// penalty term turns inactive again (c_i.y < d_i) shows up as a violated REVERSED soft row
+// -c_i.y <= -d_i; saturating that reversed row (multiplier w) cancels the linear term, i.e. the
+// row leaves S.  Returns GI_OK with the optimum in q.y, or a GI_FAIL_* reason.
 template <int N, class M>
 HVP_HD inline int solve_gi(LaneQp<N, M>& q, const Consts& C, int max_iter, int& iters) {
     iters = 0;
@@ -137,7 +166,7 @@ HVP_HD inline int solve_gi(LaneQp<N, M>& q, const Consts& C, int max_iter, int& 
     double L[N * (N + 1) / 2];
 #pragma unroll
     for (int i = 0; i < N * (N + 1) / 2; ++i) L[i] = q.H[i];
-    if (!cholesky<N>(L)) return GI_FAIL;  // stores the inverse diagonal
+    if (!cholesky<N>(L)) return GI_FAIL_CHOL;  // stores the inverse diagonal
     double negf[N];
 #pragma unroll
     for (int i = 0; i < N; ++i) negf[i] = -q.f[i];
@@ -154,7 +183,6 @@ HVP_HD inline int solve_gi(LaneQp<N, M>& q, const Consts& C, int max_iter, int& 
             for (int k = 0; k < i; ++k) v -= L[tri(i, k)] * x[k];
             x[i] = v * L[tri(i, i)];
         }
-        // x = column col of L^-1 ; J = L^-T  ->  J[col][i] = x[i]
 #pragma unroll
         for (int i = 0; i < N; ++i) J[col][i] = x[i];
     }
@@ -165,16 +193,19 @@ HVP_HD inline int solve_gi(LaneQp<N, M>& q, const Consts& C, int max_iter, int& 
         for (int j = 0; j < N; ++j) R[i][j] = 0.0;
     double u[N];
     int ids[N];
-    bool usoft[N];
 #pragma unroll
-    for (int i = 0; i < N; ++i) { u[i] = 0.0; ids[i] = -1; usoft[i] = false; }
+    for (int i = 0; i < N; ++i) { u[i] = 0.0; ids[i] = -1; }
     int nact = 0;
-    uint64_t act0 = 0, act1 = 0, sat0 = 0, sat1 = 0;  // active / saturated row masks
+    GiMask act;
+    uint32_t sat = 0;  // bit 2m: SF of step m + 2 saturated, bit 2m + 1: SB
     const double w = C.w;
     const double tol = 1e-11;
-    auto setbit = [](uint64_t& m0, uint64_t& m1, int id, bool on) {
-        if (id < 64) { if (on) m0 |= 1ull << id; else m0 &= ~(1ull << id); }
-        else { if (on) m1 |= 1ull << (id - 64); else m1 &= ~(1ull << (id - 64)); }
+    // saturate (on) / unsaturate soft row id; a reversed row flips the meaning
+    auto saturate = [&](int id) {
+        const int base = id & (GI_REV - 1);
+        const uint32_t bit = 1u << (base - 6 * N - 2 - 2 * ((base - 6 * N) / 4));
+        if (id & GI_REV) sat &= ~bit;
+        else sat |= bit;
     };
 
     int iter = 0;
@@ -190,17 +221,16 @@ HVP_HD inline int solve_gi(LaneQp<N, M>& q, const Consts& C, int max_iter, int& 
         }
 #endif
         double sp;
-        const int p = gi_most_violated(q, C, q.y, act0 | sat0, act1 | sat1, tol, sp);
+        const int p = gi_most_violated(q, C, q.y, act, sat, tol, sp);
         if (p < 0) break;
         double np[N], dp;
-        bool psoft;
-        gi_row(q, C, p, np, dp, psoft);
+        gi_row(q, C, p, np, dp);
+        const bool psoft = gi_soft<N>(p);
 #pragma unroll
         for (int i = 0; i < N; ++i) np[i] = -np[i];  // >= form: n = -c, b = -d ; slack s = n.y - b
         double unew = 0.0;
-        bool added = false;
         for (;;) {
-            if (++iter > max_iter) { iters = iter; return GI_FAIL; }
+            if (++iter > max_iter) { iters = iter; return GI_FAIL_ITER; }
             // ---------------- step 2: directions
             double dv[N];
 #pragma unroll
@@ -247,7 +277,7 @@ HVP_HD inline int solve_gi(LaneQp<N, M>& q, const Consts& C, int max_iter, int& 
             int k3 = psoft ? N : -1;  // N denotes the new row p
 #pragma unroll
             for (int j = 0; j < N; ++j) {
-                if (j < nact && usoft[j] && r[j] < 0.0) {
+                if (j < nact && gi_soft<N>(ids[j]) && r[j] < 0.0) {
                     const double tj = (w - u[j]) / (-r[j]);
                     if (tj < t3) { t3 = tj; k3 = j; }
                 }
@@ -262,9 +292,8 @@ HVP_HD inline int solve_gi(LaneQp<N, M>& q, const Consts& C, int max_iter, int& 
             for (int i = 0; i < N; ++i) sp_now += np[i] * q.y[i];  // current slack n.y - b
             const double t2 = zstep && zn > 0.0 ? fmax(-sp_now, 0.0) / zn : 1e300;
             const double t = fmin(t1, fmin(t2, t3));
-            if (!(t < 1e299)) { iters = iter; return GI_FAIL; }  // infeasible (cannot happen for enumerated sequences)
-            // apply the step
-            if (zstep && t2 < 1e299) {
+            if (!(t < 1e299)) { iters = iter; return GI_FAIL_DUAL; }  // dual unbounded: infeasible QP
+            if (t2 < 1e299) {
 #pragma unroll
                 for (int i = 0; i < N; ++i) q.y[i] += t * z[i];
             }
@@ -272,7 +301,7 @@ HVP_HD inline int solve_gi(LaneQp<N, M>& q, const Consts& C, int max_iter, int& 
             for (int j = 0; j < N; ++j)
                 if (j < nact) u[j] -= t * r[j];
             unew += t;
-            if (t == t2 && t2 <= t1 && t2 <= t3) {
+            if (t2 <= t1 && t2 <= t3) {
                 // ---- add p: Givens rotations zero dv[nact+1..N-1], rotating J's columns
 #pragma unroll
                 for (int i = N - 1; i >= 1; --i) {
@@ -296,38 +325,35 @@ HVP_HD inline int solve_gi(LaneQp<N, M>& q, const Consts& C, int max_iter, int& 
                         if (col == nact && i <= nact) R[i][col] = dv[i];
 #pragma unroll
                 for (int j = 0; j < N; ++j)
-                    if (j == nact) { u[j] = unew; ids[j] = p; usoft[j] = psoft; }
-                setbit(act0, act1, p, true);
+                    if (j == nact) { u[j] = unew; ids[j] = p; }
+                act.set(p & (GI_REV - 1), true);
                 ++nact;
-                added = true;
                 break;
             }
             // ---- a row leaves the active set: the zero-multiplier one (t1) or a saturating soft one (t3)
-            int drop = -1;
+            int drop;
             if (t3 <= t1) {
                 if (k3 == N) {
-                    // the new soft row saturates: it joins the objective as w c_p, no constraint added
-                    setbit(sat0, sat1, p, true);
-                    added = true;
+                    // the new soft row saturates: it joins the objective, no constraint is added
+                    saturate(p);
                     break;
                 }
                 drop = k3;
-                setbit(sat0, sat1, ids[k3 < N ? k3 : 0], true);
             } else {
                 drop = k1;
             }
-            // remove active row at position `drop`: shift columns of R, u, ids; re-triangularise
             int dropped_id = -1;
 #pragma unroll
             for (int j = 0; j < N; ++j)
                 if (j == drop) dropped_id = ids[j];
-            setbit(act0, act1, dropped_id, false);
+            if (t3 <= t1) saturate(dropped_id);
+            act.set(dropped_id & (GI_REV - 1), false);
+            // remove the active row at position `drop`: shift columns of R, u, ids; re-triangularise
 #pragma unroll
             for (int j = 0; j < N - 1; ++j) {
                 if (j >= drop && j < nact - 1) {
                     u[j] = u[j + 1];
                     ids[j] = ids[j + 1];
-                    usoft[j] = usoft[j + 1];
 #pragma unroll
                     for (int i = 0; i < N; ++i) R[i][j] = R[i][j + 1];
                 }
@@ -361,39 +387,24 @@ HVP_HD inline int solve_gi(LaneQp<N, M>& q, const Consts& C, int max_iter, int& 
             }
 #pragma unroll
             for (int j = 0; j < N; ++j)
-                if (j == nact - 1) { u[j] = 0.0; ids[j] = -1; usoft[j] = false; }
+                if (j == nact - 1) { u[j] = 0.0; ids[j] = -1; }
             --nact;
             // continue with the same p (step 2)
         }
-        (void)added;
     }
+    iters = iter;
 
-    // ---------------- verification (KKT of the exact-penalty problem)
-    // saturated rows must still be on their violated side
-    double yprev = q.v0, cum = 0.0;
+    // ---------------- verification: multipliers of the active rows within [0, w] (soft) or >= 0
     bool ok = true;
-#pragma unroll
-    for (int k = 2; k <= N; ++k) {
-        const int m = k - 2;
-        cum += q.y[m];
-        const double pk = q.P1 + q.ts * cum;
-        const int b = 6 * N + 4 * m;
-        const bool satf = ((b + 2) < 64 ? (sat0 >> (b + 2)) & 1ull : (sat1 >> (b + 2 - 64)) & 1ull) != 0;
-        const bool satb = ((b + 3) < 64 ? (sat0 >> (b + 3)) & 1ull : (sat1 >> (b + 3 - 64)) & 1ull) != 0;
-        if (satf && pk < q.hf(m) - 1e-9 * (1.0 + fabs(pk))) ok = false;
-        if (satb && pk > q.hb(m) + 1e-9 * (1.0 + fabs(pk))) ok = false;
-    }
-    (void)yprev;
 #pragma unroll
     for (int j = 0; j < N; ++j) {
         if (j < nact) {
             if (u[j] < -1e-9 * w) ok = false;
-            if (usoft[j] && u[j] > w * (1.0 + 1e-9)) ok = false;
+            if (gi_soft<N>(ids[j]) && u[j] > w * (1.0 + 1e-9)) ok = false;
         }
     }
-    // no violated rows left (the loop exits only then) -- stationarity holds by construction
-    iters = iter;
-    return ok ? GI_OK : GI_FAIL;
+    // primal feasibility and the saturated rows' sides hold by the exit condition of step 1
+    return ok ? GI_OK : GI_FAIL_VERIFY;
 }
 
 }  // namespace hvp

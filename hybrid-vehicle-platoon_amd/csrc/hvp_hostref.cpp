@@ -15,7 +15,7 @@ namespace {
 
 // 0: interior point only; 1: Goldfarb-Idnani active set, interior point on failure
 int g_solver = 1;
-long long g_gi_fail = 0, g_gi_iters = 0, g_gi_runs = 0;
+long long g_gi_fail = 0, g_gi_iters = 0, g_gi_runs = 0, g_gi_code[4] = {0, 0, 0, 0};
 
 hvp::Consts make_consts(const hvp_problem& p) {
     hvp::Consts C;
@@ -74,6 +74,8 @@ void solve_one(const hvp_system& S, const hvp::Consts& C, int role, const double
                 } else {
 #pragma omp atomic
                     g_gi_fail += 1;
+#pragma omp atomic
+                    g_gi_code[r - hvp::GI_FAIL_CHOL] += 1;
                     hvp::setup_lane<N>(q, S, C, role, prm, code);
                 }
             }
@@ -158,6 +160,7 @@ void hvp_hostref_gi_stats(long long* out) {
     out[0] = g_gi_runs;
     out[1] = g_gi_fail;
     out[2] = g_gi_iters;
+    for (int i = 0; i < 4; ++i) out[3 + i] = g_gi_code[i], g_gi_code[i] = 0;
     g_gi_runs = g_gi_fail = g_gi_iters = 0;
 }
 

@@ -502,7 +502,7 @@ int hvp_get_stats(hvp_handle* h, hvp_stats* out) {
     out->qp_ms = qms;
     out->n_instances = h->last_B;
     out->n_candidates = (int64_t)c[0];
-    out->ipm_iterations = (int64_t)c[1];
+    out->qp_iterations = (int64_t)c[1];
     out->n_fallback = (int64_t)c[2];
     out->capacity = h->ws.cap;
     out->last_ms = ms;

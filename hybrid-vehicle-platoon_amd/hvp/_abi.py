@@ -71,7 +71,7 @@ class HvpStats(ctypes.Structure):
     _fields_ = [
         ("n_instances", ctypes.c_int64),
         ("n_candidates", ctypes.c_int64),
-        ("ipm_iterations", ctypes.c_int64),
+        ("qp_iterations", ctypes.c_int64),
         ("capacity", ctypes.c_int64),
         ("last_ms", ctypes.c_double),
         ("qp_ms", ctypes.c_double),

@@ -122,7 +122,7 @@ typedef struct hvp_handle hvp_handle;
 typedef struct hvp_stats {
     int64_t n_instances;    /* instances in the last solve                            */
     int64_t n_candidates;   /* region sequences (QPs) solved in the last solve         */
-    int64_t ipm_iterations; /* sum of IPM iterations over those QPs                    */
+    int64_t qp_iterations;  /* sum of QP iterations (active-set + fallback IPM)      */
     int64_t capacity;       /* candidate workspace                                     */
     double last_ms;         /* device time of the last solve (event-timed), ms         */
     double qp_ms;           /* device time of its QP kernel (K_qp), ms                 */

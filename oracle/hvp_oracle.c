@@ -429,39 +429,121 @@ static void residuals(const or_qp* qp, const or_work* w, double* rd, double* re,
     }
 }
 
-/* Active-set polish: solve the equality QP on {rows with lam > t} and accept it when it is
- * primal and dual feasible -- then it satisfies the KKT conditions exactly (certificate). */
+/* Active-set polish: solve the equality QP on a guessed active set (rows with lam > t), then
+ * correct the guess -- drop the row with the most negative multiplier, or add the most
+ * violated inactive row -- until the solution is primal and dual feasible.  It then satisfies
+ * the KKT conditions exactly (certificate of global optimality for the convex QP).  Degenerate
+ * vertices (dependent active rows, weakly active rows) are what the correction steps are for. */
 static int polish(const or_qp* qp, or_work* w) {
     const int nz = qp->nz, ne = qp->neq, m = qp->m;
-    int act[OR_MAX_M], na = 0;
-    for (int i = 0; i < m; ++i)
-        if (w->lam[i] > w->t[i]) act[na++] = i;
-    const int n = nz + ne + na, ld = n;
-    if (n > OR_MAX_KKT) return 0;
-    double* K = w->K;
-    memset(K, 0, sizeof(double) * (size_t)n * (size_t)n);
-    for (int i = 0; i < nz; ++i)
-        for (int j = 0; j < nz; ++j) K[i * ld + j] = qp->P[i][j];
-    for (int e = 0; e < ne; ++e)
-        for (int j = 0; j < nz; ++j) { K[(nz + e) * ld + j] = qp->Aeq[e][j]; K[j * ld + nz + e] = qp->Aeq[e][j]; }
-    for (int a = 0; a < na; ++a)
-        for (int j = 0; j < nz; ++j) { K[(nz + ne + a) * ld + j] = qp->G[act[a]][j]; K[j * ld + nz + ne + a] = qp->G[act[a]][j]; }
-    double* x = w->rhs;
-    for (int j = 0; j < nz; ++j) x[j] = -qp->q[j];
-    for (int e = 0; e < ne; ++e) x[nz + e] = qp->beq[e];
-    for (int a = 0; a < na; ++a) x[nz + ne + a] = qp->h[act[a]];
-    if (lu_factor(n, K, ld, w->piv) != 0) return 0;
-    lu_solve(n, K, ld, w->piv, x);
-    double scale_h = 1.0 + vmaxabs(qp->h, m), scale_l = 1.0 + vmaxabs(w->lam, m);
-    for (int a = 0; a < na; ++a)
-        if (x[nz + ne + a] < -1e-9 * scale_l) return 0;
-    for (int i = 0; i < m; ++i) {
-        double g = 0.0;
-        for (int j = 0; j < nz; ++j) g += qp->G[i][j] * x[j];
-        if (g > qp->h[i] + 1e-9 * scale_h) return 0;
+    int inA[OR_MAX_M];
+    for (int i = 0; i < m; ++i) inA[i] = w->lam[i] > w->t[i];
+    const double scale_h = 1.0 + vmaxabs(qp->h, m), scale_l = 1.0 + vmaxabs(w->lam, m);
+    for (int round = 0; round < 3 * OR_MAX_N + 10; ++round) {
+        int act[OR_MAX_M], na = 0;
+        for (int i = 0; i < m; ++i)
+            if (inA[i]) act[na++] = i;
+        const int n = nz + ne + na, ld = n;
+        if (n > OR_MAX_KKT) return 0;
+        /* quasi-definite regularisation (+delta on the primal block, -delta on the multiplier
+         * rows) keeps the factorisation defined for dependent active rows; iterative refinement
+         * against the unregularised system then converges to an exact solution when the system
+         * is consistent (degenerate vertex) */
+        const double delta = 1e-10;
+        double* K = w->K;
+        memset(K, 0, sizeof(double) * (size_t)n * (size_t)n);
+        for (int i = 0; i < nz; ++i)
+            for (int j = 0; j < nz; ++j) K[i * ld + j] = qp->P[i][j] + (i == j ? delta : 0.0);
+        for (int e = 0; e < ne; ++e)
+            for (int j = 0; j < nz; ++j) { K[(nz + e) * ld + j] = qp->Aeq[e][j]; K[j * ld + nz + e] = qp->Aeq[e][j]; }
+        for (int a = 0; a < na; ++a)
+            for (int j = 0; j < nz; ++j) {
+                K[(nz + ne + a) * ld + j] = qp->G[act[a]][j];
+                K[j * ld + nz + ne + a] = qp->G[act[a]][j];
+            }
+        for (int i = nz; i < n; ++i) K[i * ld + i] = -delta;
+        if (lu_factor(n, K, ld, w->piv) != 0) return 0;
+        double x[OR_MAX_KKT], r[OR_MAX_KKT];
+        for (int i = 0; i < n; ++i) x[i] = 0.0;
+        for (int ref = 0; ref < 60; ++ref) {
+            /* r = rhs - K0 x with K0 the unregularised KKT matrix */
+            double rn = 0.0;
+            for (int j = 0; j < nz; ++j) {
+                double s = -qp->q[j];
+                for (int k = 0; k < nz; ++k) s -= qp->P[j][k] * x[k];
+                for (int e = 0; e < ne; ++e) s -= qp->Aeq[e][j] * x[nz + e];
+                for (int a = 0; a < na; ++a) s -= qp->G[act[a]][j] * x[nz + ne + a];
+                r[j] = s;
+                rn = fmax(rn, fabs(s));
+            }
+            for (int e = 0; e < ne; ++e) {
+                double s = qp->beq[e];
+                for (int j = 0; j < nz; ++j) s -= qp->Aeq[e][j] * x[j];
+                r[nz + e] = s;
+                rn = fmax(rn, fabs(s));
+            }
+            for (int a = 0; a < na; ++a) {
+                double s = qp->h[act[a]];
+                for (int j = 0; j < nz; ++j) s -= qp->G[act[a]][j] * x[j];
+                r[nz + ne + a] = s;
+                rn = fmax(rn, fabs(s));
+            }
+            if (rn <= 1e-15 * scale_h) break;
+            lu_solve(n, K, ld, w->piv, r);
+            for (int i = 0; i < n; ++i) x[i] += r[i];
+        }
+        /* the certificate checks the computed KKT residuals, not the solve: stationarity,
+         * equality rows and active rows at equality (a near-singular system fails here) */
+        double kkt = 0.0, sq = 1.0 + vmaxabs(qp->q, nz);
+        for (int j = 0; j < nz; ++j) {
+            double s = qp->q[j];
+            for (int k = 0; k < nz; ++k) s += qp->P[j][k] * x[k];
+            for (int e = 0; e < ne; ++e) s += qp->Aeq[e][j] * x[nz + e];
+            for (int a = 0; a < na; ++a) s += qp->G[act[a]][j] * x[nz + ne + a];
+            kkt = fmax(kkt, fabs(s) / sq);
+        }
+        for (int e = 0; e < ne; ++e) {
+            double s = -qp->beq[e];
+            for (int j = 0; j < nz; ++j) s += qp->Aeq[e][j] * x[j];
+            kkt = fmax(kkt, fabs(s) / scale_h);
+        }
+        for (int a = 0; a < na; ++a) {
+            double s = -qp->h[act[a]];
+            for (int j = 0; j < nz; ++j) s += qp->G[act[a]][j] * x[j];
+            kkt = fmax(kkt, fabs(s) / scale_h);
+        }
+        if (!(kkt <= 1e-9)) {
+            int worst = -1;
+            for (int a = 0; a < na; ++a)
+                if (worst < 0 || w->lam[act[a]] < w->lam[act[worst]]) worst = a;
+            if (worst < 0) return 0;
+            inA[act[worst]] = 0;
+            continue;
+        }
+        int neg = -1;
+        double negv = -1e-9 * scale_l;
+        for (int a = 0; a < na; ++a)
+            if (x[nz + ne + a] < negv) { negv = x[nz + ne + a]; neg = a; }
+        if (neg >= 0) {
+            inA[act[neg]] = 0;
+            continue;
+        }
+        int vio = -1;
+        double viov = 1e-9 * scale_h;
+        for (int i = 0; i < m; ++i) {
+            if (inA[i]) continue;
+            double g = -qp->h[i];
+            for (int j = 0; j < nz; ++j) g += qp->G[i][j] * x[j];
+            if (g > viov) { viov = g; vio = i; }
+        }
+        if (vio >= 0) {
+            inA[vio] = 1;
+            continue;
+        }
+        for (int j = 0; j < nz; ++j) w->z[j] = x[j];
+        return 1;
     }
-    for (int j = 0; j < nz; ++j) w->z[j] = x[j];
-    return 1;
+    return 0;
 }
 
 static or_result ipm_solve(const or_qp* qp, or_work* w, int maxit) {
@@ -512,10 +594,25 @@ static or_result ipm_solve(const or_qp* qp, or_work* w, int maxit) {
         mu /= (m > 0 ? m : 1);
         double obj = objective(qp, w->z);
         res.iters = it;
-        if (vmaxabs(rd, nz) <= 1e-10 * sq && vmaxabs(re, ne) <= 1e-10 * sb && vmaxabs(rp, m) <= 1e-10 * sh &&
-            gap <= 1e-11 * fmax(1.0, fabs(obj))) {
+        const double rdn = vmaxabs(rd, nz), ren = vmaxabs(re, ne), rpn = vmaxabs(rp, m);
+        if (rdn <= 1e-10 * sq && ren <= 1e-10 * sb && rpn <= 1e-10 * sh && gap <= 1e-11 * fmax(1.0, fabs(obj))) {
             res.converged = 1;
             break;
+        }
+        /* Degenerate vertices (a row with t -> 0 and lam -> 0 together) make P + G'DG singular as
+         * mu -> 0 and the residuals blow up again.  Near the optimum, try the active-set polish:
+         * when it certifies the KKT conditions the solution is exact, whatever the IPM does next. */
+        if (rdn <= 1e-7 * sq && ren <= 1e-7 * sb && rpn <= 1e-7 * sh && gap <= 1e-5 * fmax(1.0, fabs(obj))) {
+            double zs[OR_MAX_NZ];
+            memcpy(zs, w->z, sizeof(double) * nz);
+            if (polish(qp, w)) {
+                res.converged = 1;
+                res.certified = 1;
+                res.iters = it;
+                res.obj = objective(qp, w->z);
+                return res;
+            }
+            memcpy(w->z, zs, sizeof(double) * nz);
         }
         for (int i = 0; i < m; ++i) d[i] = w->lam[i] / w->t[i];
         if (ipm_factor(qp, w, d) != 0) break;
@@ -539,7 +636,12 @@ static or_result ipm_solve(const or_qp* qp, or_work* w, int maxit) {
         for (int i = 0; i < m; ++i) { w->lam[i] += alpha * dl[i]; w->t[i] += alpha * dt[i]; }
         res.iters = it + 1;
     }
-    if (res.converged) res.certified = polish(qp, w);
+    if (res.converged) {
+        res.certified = polish(qp, w);
+    } else if (polish(qp, w)) {
+        res.converged = 1;  /* certified by the KKT check even though the IPM stalled */
+        res.certified = 1;
+    }
     res.obj = objective(qp, w->z);
     return res;
 }

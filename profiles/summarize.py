@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""Condense a profiles/run_profiles.sh output directory into a committed per-round summary.
+
+    python profiles/summarize.py gpurun_out/prof r01
+
+writes profiles/<round>_kernel_stats.csv (rocprofv3 --kernel-trace --stats, as produced) and
+profiles/<round>_summary.json with, per kernel:
+  avg_ms                 average duration from the kernel-trace pass
+  fetch_kb, write_kb     FETCH_SIZE / WRITE_SIZE per launch (separate PMC passes)
+  hbm_bytes              2 * FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md, HBM section: on gfx950
+                         FETCH_SIZE tallies half the bytes of wide reads; WRITE_SIZE is exact)
+  f64_wave_instrs        SQ_INSTS_VALU_{FMA,MUL,ADD,TRANS}_F64 per launch (wave instructions)
+  f64_flop               64 lanes * (2 FMA + MUL + ADD + TRANS): an upper bound (masked lanes count)
+bench.py reads hbm_bytes of its dominant kernel from here as roofline.traffic.
+"""
+
+from __future__ import annotations
+
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+
+def per_kernel(path: str) -> dict:
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            acc[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return acc
+
+
+def short(name: str) -> str:
+    for k in ("k_qp_gi", "k_qp_ipm", "k_enum", "k_cost", "k_select"):
+        if k in name:
+            return k
+    return name[:48]
+
+
+def main() -> None:
+    src, rnd = sys.argv[1], sys.argv[2]
+    here = os.path.dirname(os.path.abspath(__file__))
+    out = {}
+    with open(os.path.join(src, "trace", "run_kernel_stats.csv")) as f:
+        for r in csv.DictReader(f):
+            k = short(r["Name"])
+            out.setdefault(k, {})["avg_ms"] = float(r["AverageNs"]) / 1e6
+            out[k]["calls"] = int(r["Calls"])
+    shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(here, f"{rnd}_kernel_stats.csv"))
+    for sub in ("fetch", "write", "f64"):
+        p = os.path.join(src, sub, "run_counter_collection.csv")
+        if not os.path.exists(p):
+            continue
+        for name, ctr in per_kernel(p).items():
+            k = short(name)
+            d = out.setdefault(k, {})
+            for c, vals in ctr.items():
+                d[c] = sum(vals) / len(vals)
+    for k, d in out.items():
+        if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
+            d["fetch_kb"] = d.pop("FETCH_SIZE")
+            d["write_kb"] = d.pop("WRITE_SIZE")
+            d["hbm_bytes"] = (2.0 * d["fetch_kb"] + d["write_kb"]) * 1024.0
+        f64 = [d.get(f"SQ_INSTS_VALU_{t}_F64") for t in ("FMA", "MUL", "ADD", "TRANS")]
+        if all(v is not None for v in f64):
+            d["f64_wave_instrs"] = sum(f64)
+            d["f64_flop"] = 64.0 * (2 * f64[0] + f64[1] + f64[2] + f64[3])
+            if d.get("avg_ms"):
+                d["f64_tflops"] = d["f64_flop"] / (d["avg_ms"] * 1e-3) / 1e12
+    meta = {"round": rnd, "source": "profiles/run_profiles.sh (rocprofv3 kernel trace + separate PMC passes)",
+            "kernels": out}
+    with open(os.path.join(here, f"{rnd}_summary.json"), "w") as f:
+        json.dump(meta, f, indent=1, sort_keys=True)
+    print(json.dumps(meta, indent=1, sort_keys=True))
+
+
+if __name__ == "__main__":
+    main()

@@ -15,6 +15,10 @@ Files (numpy .npz, no pickles):
   decent_rollout_n4_N5.npz  mid-trajectory states: 6 steps along the MPC's own predictions
   task2_n5_N5.npz     Sim_n_task_2 flavour: masses U(700,1000), ConstantTime(10,3), stop-and-go leader
   variants_n4.npz     N = 3, 4, 6, 7; Q_du = 0.5; leader_index = 2; real_vehicle_as_reference
+  hard_n10_N5.npz     configs[1] instances (seed, vehicle) at degenerate QP vertices: weakly active /
+                      linearly dependent rows, where an interior-point solve stalls.  Found by
+                      scanning bench seeds 0..5999 for disagreements between the two QP methods of
+                      the lane (active set vs interior point); expected values from the oracle.
   known_answers.json  constants derived from the reference source
 
 Run:  python tests/golden/make_golden.py
@@ -125,8 +129,30 @@ def task2(n, N, seeds, t_list):
     return params, roles, sys_idx, masses, cfg, solve_set(systems, sys_idx, cfg, N, params, roles)
 
 
+# (seed, vehicle) pairs of hard_n10_N5.npz (see the module docstring)
+HARD = [(250, 3), (257, 1), (354, 7), (428, 3), (574, 8), (774, 2), (1048, 6), (1259, 2), (1322, 4), (1509, 1),
+        (1700, 6), (1717, 2), (1726, 4), (1740, 3), (1873, 7), (2089, 6), (2120, 7), (2366, 0), (2660, 6),
+        (2758, 8), (2998, 9), (3194, 1), (3307, 8), (3333, 1), (3377, 6), (3444, 1), (3451, 8), (3454, 3),
+        (3651, 7), (3660, 7), (3757, 5), (4250, 9), (4273, 9), (4320, 6), (4346, 3), (4526, 6), (4818, 9),
+        (4911, 5), (4980, 2), (4992, 7), (5021, 8), (5104, 2), (5169, 3), (5336, 7), (5380, 4), (5419, 4),
+        (5561, 4), (5744, 6), (5890, 5)]
+
+
+def hard_cases(N=5, n=10):
+    P, R = [], []
+    for s, v in HARD:
+        p, r = decent_instances(O.env_initial_state(n, s), N, leader_window(N))
+        P.append(p[v:v + 1])
+        R.append(r[v:v + 1])
+    params, roles = np.concatenate(P), np.concatenate(R)
+    sys_idx = np.zeros(len(roles), np.int32)
+    return params, roles, sys_idx, solve_set([O.gear_pwa_system(800.0)], sys_idx, O.Cfg(), N, params, roles)
+
+
 def main():
     N = 5
+    params, roles, si, exp = hard_cases(N)
+    save("hard_n10_N5.npz", N, [800.0], O.Cfg(), params, roles, si, exp)
     params, roles, si, exp = decent_seeds(10, N, range(10))
     save("decent_n10_N5.npz", N, [800.0], O.Cfg(), params, roles, si, exp)
     params, roles, si, exp = decent_seeds(2, N, range(10))
