@@ -77,9 +77,9 @@ typedef struct hvp_problem {
     double accel_tightening;
     double spacing_d0;      /* spacing(x) = [-d0 - t0 * v, 0]                          */
     double spacing_t0;
-    int32_t max_iter;       /* IPM iteration cap per candidate (<=0: default 60)       */
+    int32_t max_iter;       /* fallback IPM iteration cap per candidate (<=0: 60)      */
     int32_t pad_;
-    double tol;             /* relative IPM tolerance (<=0: default 1e-10)             */
+    double tol;             /* fallback IPM relative tolerance (<=0: 1e-12)            */
 } hvp_problem;
 
 /* Role of one local MPC (is_front / is_trailer / is_leader / real_vehicle_as_reference). */
