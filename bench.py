@@ -73,6 +73,7 @@ def cpu_baseline(n: int, N: int, budget_s: float, threads: int):
     import oracle as O
 
     sysd = O.gear_pwa_system(800.0)
+    O.set_method(O.METHOD_BNB if N > 8 else O.METHOD_ENUMERATE)  # exhaustive past N = 8 is ~1e4+ QPs/vehicle
     done = 0
     t0 = time.perf_counter()
     chunk = max(threads, 1) * 2
@@ -87,7 +88,7 @@ def cpu_baseline(n: int, N: int, budget_s: float, threads: int):
             "sample": f"{done} platoons x {n} local MIQPs (N={N}) by oracle/hvp_oracle.c, {dt:.1f} s"}
 
 
-def hostref_baseline(n: int, N: int, budget_s: float, threads: int):
+def hostref_baseline(n: int, N: int, budget_s: float, threads: int, method: int = 0):
     """The product's lane algorithm compiled for the host cores (extra, fairer CPU number)."""
     import ctypes
 
@@ -99,7 +100,7 @@ def hostref_baseline(n: int, N: int, budget_s: float, threads: int):
     L = ctypes.CDLL(_abi.HOSTREF_PATH)
     veh = PwaGearVehicle(800)
     S = (_abi.HvpSystem * 1)(tables.system_from_dict(veh.get_discrete_system(1), tables.gears_of(veh)))
-    prob = tables.problem(N)
+    prob = tables.problem(N, method=method)
     done, seed = 0, 20_000_000
     chunk = max(threads, 1) * 16
     t0 = time.perf_counter()
@@ -128,6 +129,8 @@ def main() -> None:
     ap.add_argument("--N", type=int, default=5)
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-oracle baseline (0 = skip)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--method", choices=["auto", "enum", "bnb"], default="auto",
+                    help="region-sequence search (include/hvp.h HVP_METHOD_*)")
     args = ap.parse_args()
 
     import torch
@@ -149,7 +152,8 @@ def main() -> None:
     n, N, S = args.n, args.N, args.platoons
     veh = PwaGearVehicle(800)
     system = tables.system_from_dict(veh.get_discrete_system(1), tables.gears_of(veh))
-    solver = BatchSolver(tables.problem(N), [system], device=local)
+    method = {"auto": 0, "enum": 1, "bnb": 2}[args.method]
+    solver = BatchSolver(tables.problem(N, method=method), [system], device=local)
     # each rank owns a disjoint seed range: platoons are independent (weak scaling)
     params, roles = make_inputs(range(rank * S, (rank + 1) * S), n, N)
     B = len(roles)
@@ -240,7 +244,7 @@ def main() -> None:
     if rank == 0 and not args.no_cpu and args.cpu_budget > 0 and world == 1:
         threads = min(len(os.sched_getaffinity(0)), 16)
         result["cpu_baseline"] = cpu_baseline(n, N, args.cpu_budget, threads)
-        hr = hostref_baseline(n, N, min(args.cpu_budget, 10.0), threads)
+        hr = hostref_baseline(n, N, min(args.cpu_budget, 10.0), threads, method)
         if hr:
             result["cpu_same_algorithm"] = hr
     if rank == 0:

@@ -39,7 +39,7 @@ struct GiConstraintSet {
 // Row ids: V/U/A rows 6j + {0 V_lo, 1 V_hi, 2 U_lo, 3 U_hi, 4 A_lo, 5 A_hi} (step k = j + 1),
 // prefix rows 6N + 4m + {0 P_lo, 1 P_hi, 2 SF, 3 SB} (step k = m + 2).  GI_REV marks the
 // reversed copy of a saturated soft row (see solve_gi).
-constexpr int GI_REV = 128;
+constexpr int GI_REV = 256;
 
 template <int N>
 HVP_HD constexpr bool gi_soft(int id) {
@@ -81,7 +81,8 @@ HVP_HD inline void gi_row(const LaneQp<N, M>& q, const Consts& C, int id_in, dou
     }
 }
 
-// 128-bit row mask (N <= 8 gives at most 76 rows)
+// Row mask: 128 bits cover N <= 8 (at most 76 rows); longer horizons use the generic form.
+template <int N, bool WIDE = (GiConstraintSet<N>::NC > 128)>
 struct GiMask {
     uint64_t lo = 0, hi = 0;
     HVP_HD bool get(int id) const { return id < 64 ? ((lo >> id) & 1ull) != 0 : ((hi >> (id - 64)) & 1ull) != 0; }
@@ -90,12 +91,22 @@ struct GiMask {
         else hi = on ? (hi | (1ull << (id - 64))) : (hi & ~(1ull << (id - 64)));
     }
 };
+template <int N>
+struct GiMask<N, true> {
+    static constexpr int W = (GiConstraintSet<N>::NC + 63) / 64;
+    uint64_t w[W] = {};
+    HVP_HD bool get(int id) const { return ((w[id >> 6] >> (id & 63)) & 1ull) != 0; }
+    HVP_HD void set(int id, bool on) {
+        if (on) w[id >> 6] |= 1ull << (id & 63);
+        else w[id >> 6] &= ~(1ull << (id & 63));
+    }
+};
 
 // Slack d - c.y of every row (structured: O(1) per row) and the most violated one (largest
 // violation relative to |c|).  Active rows are skipped; a saturated soft row is represented by
 // its reversed copy (violated when the row is satisfied strictly).
 template <int N, class M>
-HVP_HD inline int gi_most_violated(const LaneQp<N, M>& q, const Consts& C, const double* y, const GiMask& act,
+HVP_HD inline int gi_most_violated(const LaneQp<N, M>& q, const Consts& C, const double* y, const GiMask<N>& act,
                                    uint32_t sat, double tol, double& s_out) {
     int best = -1;
     double best_v2 = 0.0, best_nn = 1.0, best_s = 0.0;
@@ -196,7 +207,7 @@ HVP_HD inline int solve_gi(LaneQp<N, M>& q, const Consts& C, int max_iter, int& 
 #pragma unroll
     for (int i = 0; i < N; ++i) { u[i] = 0.0; ids[i] = -1; }
     int nact = 0;
-    GiMask act;
+    GiMask<N> act;
     uint32_t sat = 0;  // bit 2m: SF of step m + 2 saturated, bit 2m + 1: SB
     const double w = C.w;
     const double tol = 1e-11;

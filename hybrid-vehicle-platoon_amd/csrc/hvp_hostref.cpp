@@ -8,10 +8,13 @@
 
 #include <vector>
 
+#include "hvp_bnb.h"
 #include "hvp_gi.h"
 #include "hvp_ipm.h"
 
 namespace {
+
+constexpr int kAutoEnumMaxN = 0;  // same crossover as hvp_kernels.hip (HVP_METHOD_AUTO)
 
 // 0: interior point only; 1: Goldfarb-Idnani active set, interior point on failure
 int g_solver = 1;
@@ -138,6 +141,105 @@ void solve_one(const hvp_system& S, const hvp::Consts& C, int role, const double
     }
 }
 
+// Branch and bound (hvp_bnb.h) with the same level-synchronous order as the gfx950 kernels:
+// root bound + greedy dive, then per depth the children of the unpruned nodes, then the argmin
+// and tie rule over the leaves.
+template <int N>
+void solve_one_bnb(const hvp_system& S, const hvp::Consts& C, int role, const double* prm, double* u, double* x,
+                   int8_t* region, double* cost, int32_t* status, int32_t* nodes, int32_t* iters) {
+    struct Node {
+        uint64_t code;
+        double lo, hi, lb;
+        int stat;
+        double y[N];
+    };
+    int nq = 0, nit = 0;
+    auto qp = [&](uint64_t code, int K, double& c, double* y) {
+        hvp::LaneQp<N> q;
+        hvp::setup_lane<N>(q, S, C, role, prm, code, K);
+        int it = 0;
+        const int r = hvp::solve_gi<N>(q, C, 8 * hvp::GiConstraintSet<N>::NC, it);
+        ++nq;
+        nit += it;
+        if (r != hvp::GI_OK) return false;
+        c = hvp::direct_cost<N>(q, S, C, role, prm, code, K);
+        if (y)
+            for (int i = 0; i < N; ++i) y[i] = q.y[i];
+        return true;
+    };
+    const double v0 = prm[1], P1 = prm[0] + S.ts * v0;
+    const bool ok = P1 >= S.pmin - 1e-9 * (1.0 + fabs(S.pmin)) && P1 <= S.pmax + 1e-9 * (1.0 + fabs(S.pmax));
+    std::vector<Node> lvl, nxt;
+    double inc = HUGE_VAL;
+    if (ok) {
+        Node root;
+        root.code = 0;
+        root.lo = root.hi = v0;
+        root.lb = -1e300;
+        double c0;
+        if (qp(0, 0, c0, root.y)) {
+            root.lb = c0;
+            uint64_t code;
+            double c1;
+            if (hvp::bnb_dive<N>(S, C, v0, root.y, &code) && qp(code, N, c1, nullptr)) inc = c1;
+        }
+        lvl.push_back(root);
+    }
+    for (int k = 1; k <= N && !lvl.empty(); ++k) {
+        nxt.clear();
+        for (const Node& p : lvl) {
+            if (hvp::bnb_pruned(p.lb, inc)) continue;
+            for (int r = 0; r < S.n_regions; ++r) {
+                Node c;
+                if (!hvp::bnb_child(S, C, k - 1, p.lo, p.hi, r, &c.lo, &c.hi)) continue;
+                c.code = p.code | ((uint64_t)r << (3 * (k - 1)));
+                nxt.push_back(c);
+            }
+        }
+        for (Node& c : nxt) {
+            double lb;
+            const bool good = qp(c.code, k, lb, c.y);
+            c.stat = good ? 0 : HVP_MAXITER;
+            c.lb = good ? lb : (k < N ? -1e300 : 1e300);
+            if (k == N && good) inc = fmin(inc, lb);
+        }
+        lvl.swap(nxt);
+    }
+    *nodes = nq;
+    *iters = nit;
+    int win = -1;
+    uint64_t wkey = ~0ull;
+    if (ok && inc < HUGE_VAL) {
+        for (int i = 0; i < (int)lvl.size(); ++i) {
+            const Node& c = lvl[i];
+            if (c.stat != 0 || c.lb > inc + 1e-9 * fmax(1.0, fabs(inc))) continue;
+            const uint64_t key = hvp::bnb_lexkey(c.code, N);
+            if (key < wkey) { wkey = key; win = i; }
+        }
+    }
+    if (win < 0) {
+        *status = !ok ? HVP_INFEASIBLE : (nq > 1 && inc < HUGE_VAL ? HVP_MAXITER : HVP_INFEASIBLE);
+        *cost = 1e300;
+        return;
+    }
+    const Node& c = lvl[win];
+    *status = HVP_OPTIMAL;
+    *cost = c.lb;
+    x[0] = prm[0];
+    x[N + 1] = v0;
+    double p = prm[0], v = v0;
+    for (int k = 0; k < N; ++k) {
+        const int r = (c.code >> (3 * k)) & 7;
+        region[k] = (int8_t)r;
+        const double vn = c.y[k];
+        u[k] = (vn - S.a[r] * v - S.c[r]) / S.b[r];
+        p = p + S.ts * v;
+        v = vn;
+        x[k + 1] = p;
+        x[N + 1 + k + 1] = v;
+    }
+}
+
 template <int N>
 void solve_range(const hvp_problem& P, const hvp_system* systems, int B, const int32_t* sys, const int32_t* role,
                  const double* params, double* u, double* x, int8_t* region, double* cost, int32_t* status,
@@ -145,10 +247,19 @@ void solve_range(const hvp_problem& P, const hvp_system* systems, int B, const i
     const hvp::Consts C = make_consts(P);
     const int stride = hvp_params_stride(N);
 #pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1)
-    for (int i = 0; i < B; ++i)
-        solve_one<N>(systems[sys[i]], C, role[i], params + (size_t)i * stride, u + (size_t)i * N,
+    for (int i = 0; i < B; ++i) {
+        const bool bnb = P.method == HVP_METHOD_BNB || (P.method == HVP_METHOD_AUTO && N > kAutoEnumMaxN);
+        if (bnb || N > HVP_MAX_N_ENUM) {
+            solve_one_bnb<N>(systems[sys[i]], C, role[i], params + (size_t)i * stride, u + (size_t)i * N,
+                             x + (size_t)i * 2 * (N + 1), region + (size_t)i * N, cost + i, status + i, nodes + i,
+                             iters + i);
+            continue;
+        }
+        if constexpr (N <= HVP_MAX_N_ENUM)
+            solve_one<N>(systems[sys[i]], C, role[i], params + (size_t)i * stride, u + (size_t)i * N,
                      x + (size_t)i * 2 * (N + 1), region + (size_t)i * N, cost + i, status + i, nodes + i, iters + i,
                      nullptr, nullptr, 0);
+    }
 }
 
 }  // namespace
@@ -172,6 +283,7 @@ int hvp_hostref_solve_batch(const hvp_problem* P, const hvp_system* systems, int
 #define HVP_CASE(n) \
     case n: solve_range<n>(*P, systems, B, sys, role, params, u, x, region, cost, status, nodes, iters, nthreads); return 0;
         HVP_CASE(2) HVP_CASE(3) HVP_CASE(4) HVP_CASE(5) HVP_CASE(6) HVP_CASE(7) HVP_CASE(8)
+        HVP_CASE(9) HVP_CASE(10) HVP_CASE(11) HVP_CASE(12) HVP_CASE(13) HVP_CASE(14) HVP_CASE(15) HVP_CASE(16)
 #undef HVP_CASE
         default: return HVP_E_UNSUPPORTED;
     }

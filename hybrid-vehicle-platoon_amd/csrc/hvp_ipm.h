@@ -762,7 +762,7 @@ HVP_HD inline bool pbox_ok(const LaneQp<N, M>& q) {
 // Returns false when a sigma-independent constant row (p_1 box) is violated.
 template <int N, class M>
 HVP_HD inline bool setup_lane(LaneQp<N, M>& q, const hvp_system& S, const Consts& C, int role, const double* prm,
-                              uint32_t code) {
+                              uint64_t code, int K = N) {
     const double p0 = prm[0], v0 = prm[1];
     const double* xf = prm + 2;
     const double* xb = prm + 2 + 2 * (N + 1);
@@ -778,15 +778,19 @@ HVP_HD inline bool setup_lane(LaneQp<N, M>& q, const hvp_system& S, const Consts
     double a[N], b[N], c[N];
 #pragma unroll
     for (int k = 0; k < N; ++k) {
+        // steps k >= K are RELAXED (branch-and-bound bound problem): their region is free, so
+        // the input rows are dropped (inert bounds) and so is their input cost (>= 0) below;
+        // what remains is a valid lower bound of every completion of the fixed prefix.
         const int r = (code >> (3 * k)) & 7;
-        a[k] = S.a[r];
-        b[k] = S.b[r];
-        c[k] = S.c[r];
+        const bool fixed = k < K;
+        a[k] = fixed ? S.a[r] : 1.0;
+        b[k] = fixed ? S.b[r] : 1.0;
+        c[k] = fixed ? S.c[r] : 0.0;
         q.mem.set(F_AM, k, a[k]);
-        q.mem.set(F_ULO, k, c[k] + b[k] * S.umin);
-        q.mem.set(F_UHI, k, c[k] + b[k] * S.umax);
-        // bounds on v_{k+1}: region sigma_{k+1} (if any) intersected with the state box
-        if (k + 1 < N) {
+        q.mem.set(F_ULO, k, fixed ? c[k] + b[k] * S.umin : -1e30);
+        q.mem.set(F_UHI, k, fixed ? c[k] + b[k] * S.umax : 1e30);
+        // bounds on v_{k+1}: region sigma_{k+1} (if fixed) intersected with the state box
+        if (k + 1 < K) {
             const int r1 = (code >> (3 * (k + 1))) & 7;
             q.mem.set(F_VLO, k, fmax(S.vmin, S.vlo[r1]));
             q.mem.set(F_VHI, k, fmin(S.vmax, S.vhi[r1]));
@@ -872,7 +876,7 @@ HVP_HD inline bool setup_lane(LaneQp<N, M>& q, const hvp_system& S, const Consts
         ubar[k] = k == 0 ? -(a[0] * v0 + c[0]) * ib : -c[k] * ib;
         gk[k] = ib;
         gkm[k] = k == 0 ? 0.0 : -a[k] * ib;
-        const double w2 = 2.0 * C.Qu;
+        const double w2 = k < K ? 2.0 * C.Qu : 0.0;
         q.H[tri(k, k)] += w2 * gk[k] * gk[k];
         q.f[k] += w2 * ubar[k] * gk[k];
         if (k >= 1) {
@@ -880,7 +884,7 @@ HVP_HD inline bool setup_lane(LaneQp<N, M>& q, const hvp_system& S, const Consts
             q.H[tri(k, k - 1)] += w2 * gk[k] * gkm[k];
             q.f[k - 1] += w2 * ubar[k] * gkm[k];
         }
-        C0 += C.Qu * ubar[k] * ubar[k];
+        C0 += k < K ? C.Qu * ubar[k] * ubar[k] : 0.0;
     }
     if (C.Qdu != 0.0) {
 #pragma unroll
@@ -893,14 +897,14 @@ HVP_HD inline bool setup_lane(LaneQp<N, M>& q, const hvp_system& S, const Consts
             g[k] += gkm[k + 1] - gk[k];
             if (k >= 1) g[k - 1] -= gkm[k];
             const double eb = ubar[k + 1] - ubar[k];
-            const double w2 = 2.0 * C.Qdu;
+            const double w2 = k + 1 < K ? 2.0 * C.Qdu : 0.0;
 #pragma unroll
             for (int i = 0; i < N; ++i) {
                 q.f[i] += w2 * eb * g[i];
 #pragma unroll
                 for (int i2 = 0; i2 <= i; ++i2) q.H[tri(i, i2)] += w2 * g[i] * g[i2];
             }
-            C0 += C.Qdu * eb * eb;
+            C0 += k + 1 < K ? C.Qdu * eb * eb : 0.0;
         }
     }
     // constant slacks of k = 0, 1 (p_0, p_1 fixed)
@@ -926,7 +930,7 @@ HVP_HD inline T* opaque_ptr(T* p) {
 
 template <int N, class M>
 HVP_HD inline double direct_cost(const LaneQp<N, M>& q, const hvp_system& S_in, const Consts& C, int role,
-                                 const double* prm_in, uint32_t code) {
+                                 const double* prm_in, uint64_t code, int K = N) {
     const double* prm = opaque_ptr(prm_in);
     const hvp_system& S = *opaque_ptr(&S_in);
     const double* xf = prm + 2;
@@ -948,8 +952,8 @@ HVP_HD inline double direct_cost(const LaneQp<N, M>& q, const hvp_system& S_in, 
             const int r = (code >> (3 * k)) & 7;
             const double vn = q.y[k];
             const double u = (vn - S.a[r] * v - S.c[r]) / S.b[r];
-            J += C.Qu * u * u;
-            if (k >= 1) J += C.Qdu * (u - uprev) * (u - uprev);
+            if (k < K) J += C.Qu * u * u;  // relaxed steps carry no input cost
+            if (k >= 1 && k < K) J += C.Qdu * (u - uprev) * (u - uprev);
             uprev = u;
             p = p + S.ts * v;
             v = vn;

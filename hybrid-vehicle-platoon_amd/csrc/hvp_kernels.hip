@@ -28,6 +28,7 @@
 
 #define HVP_HD __host__ __device__
 #include "hvp.h"
+#include "hvp_bnb.h"
 #include "hvp_gi.h"
 #include "hvp_ipm.h"
 
@@ -47,6 +48,8 @@ int fail(int code, const std::string& msg) {
     } while (0)
 
 constexpr int kBlock = 256;
+// HVP_METHOD_AUTO: exhaustive enumeration up to this horizon, branch and bound beyond
+constexpr int kAutoEnumMaxN = 0;  // measured: B&B beats enumeration already at N = 5 (profiles/)
 // active-set iteration cap (then the interior-point fallback takes the candidate)
 template <int N>
 constexpr int kGiMaxIter = 8 * hvp::GiConstraintSet<N>::NC;
@@ -64,6 +67,19 @@ struct Workspace {
     double* task_cost = nullptr;   // [cap]
     int32_t* task_stat = nullptr;  // [cap] status | iters << 8
     double* task_y = nullptr;      // [cap * N]
+    // branch and bound (hvp_bnb.h): two node lists (parents / children of a level, ping-pong),
+    // per-instance incumbent and winner key
+    int32_t* nd_inst[2] = {nullptr, nullptr};    // [cap] owning instance (-1: dead)
+    uint64_t* nd_code[2] = {nullptr, nullptr};   // [cap] region prefix, 3 bits per step
+    double* nd_lo[2] = {nullptr, nullptr};       // [cap] reachable interval of v_depth
+    double* nd_hi[2] = {nullptr, nullptr};
+    double* nd_lb[2] = {nullptr, nullptr};       // [cap] bound (relaxed QP) or leaf cost
+    int32_t* leaf_stat = nullptr;                // [cap] 0 ok, else the QP failed
+    unsigned long long* inc = nullptr;           // [max_batch] incumbent cost (bits of a double >= 0)
+    unsigned long long* key = nullptr;           // [max_batch] lexicographic key of the winner
+    int32_t* nodes = nullptr;                    // [max_batch] QPs solved for the instance
+    int32_t* iters = nullptr;                    // [max_batch] active-set iterations
+    unsigned long long* lvl = nullptr;           // [HVP_MAX_N + 1] nodes per level
 };
 
 }  // namespace
@@ -77,8 +93,11 @@ struct hvp_handle {
     Workspace ws;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;  // around the whole solve
     hipEvent_t evq0 = nullptr, evq1 = nullptr; // around K_qp (the dominant kernel)
+    hipEvent_t evb[2 * (HVP_MAX_N + 1)] = {};    // B&B: around K_bnb_root and every K_bnb_bound
     hipStream_t last_stream = nullptr;
     int last_B = 0;
+    bool bnb = false;       // search method resolved at hvp_create (HVP_METHOD_*)
+    bool last_bnb = false;
     int n_cu = 256;
     // host-pointer entry point staging (grown on demand)
     size_t stage_bytes = 0;
@@ -147,11 +166,11 @@ __global__ __launch_bounds__(kBlock) void k_enum(int B, const hvp_system* __rest
 // LDS instead of hoisting them into VGPRs for the whole solve.
 extern __shared__ double s_rows[];
 
-template <int N>
+template <int N, int BS = kBlock>
 struct LdsMem {
     unsigned lane;
-    __device__ double get(int f, int j) const { return s_rows[(f * N + j) * kBlock + lane]; }
-    __device__ void set(int f, int j, double x) { s_rows[(f * N + j) * kBlock + lane] = x; }
+    __device__ double get(int f, int j) const { return s_rows[(f * N + j) * BS + lane]; }
+    __device__ void set(int f, int j, double x) { s_rows[(f * N + j) * BS + lane] = x; }
     __device__ void refresh() { asm volatile("" : "+v"(lane)); }
 };
 
@@ -315,7 +334,319 @@ __global__ __launch_bounds__(kBlock) void k_select(int B, const hvp_system* __re
     }
 }
 
+// ================================================================== branch and bound
+// Level-synchronous over the whole batch (hvp_bnb.h): K_root (relaxed root QP + greedy dive ->
+// incumbent), then for every depth k = 1..N  K_expand (children of the unpruned parents, one
+// atomicAdd per parent) and K_bound (one lane per child: QP with the tail relaxed after k steps;
+// exact QP at k = N), then K_key / K_write / K_finish (argmin + tie rule over the leaves).
+// Every kernel grid-strides over a count that lives on the device: no host round trip.
+template <int N>
+constexpr int kBnbBlock = N <= 8 ? 256 : 64;  // LDS rows: 7 N doubles per lane
+
+__device__ inline double inc_of(const Workspace& ws, int inst) { return __longlong_as_double((long long)ws.inc[inst]); }
+
+template <int N, int BS>
+__device__ inline int bnb_qp(hvp::LaneQp<N, LdsMem<N, BS>>& q, const hvp_system& S, const hvp::Consts& C, int rl,
+                             const double* prm, uint64_t code, int K, double& cost) {
+    hvp::setup_lane<N>(q, S, C, rl, prm, code, K);
+    int it = 0;
+    const int st = hvp::solve_gi<N>(q, C, kGiMaxIter<N>, it);
+    cost = st == hvp::GI_OK ? hvp::direct_cost<N>(q, S, C, rl, prm, code, K) : 0.0;
+    return st == hvp::GI_OK ? it : -1 - it;
+}
+
+template <int N>
+__global__ __launch_bounds__(kBnbBlock<N>) void k_bnb_root(int B, const hvp_system* __restrict__ systems,
+                                                           const int32_t* __restrict__ sys,
+                                                           const int32_t* __restrict__ role,
+                                                           const double* __restrict__ params, hvp::Consts C,
+                                                           Workspace ws) {
+    constexpr int BS = kBnbBlock<N>;
+    const int i = blockIdx.x * BS + threadIdx.x;
+    if (i == 0) ws.lvl[0] = (unsigned long long)B;
+    if (i >= B) return;
+    const hvp_system& S = systems[sys[i]];
+    const int rl = role[i];
+    const double* prm = params + (size_t)i * (2 + 6 * (N + 1));
+    const double v0 = prm[1], P1 = prm[0] + S.ts * v0;
+    const bool ok = P1 >= S.pmin - 1e-9 * (1.0 + fabs(S.pmin)) && P1 <= S.pmax + 1e-9 * (1.0 + fabs(S.pmax));
+    ws.key[i] = ~0ull;
+    ws.inst_flag[i] = ok ? 0 : 1;
+    ws.nd_inst[0][i] = ok ? i : -1;
+    ws.nd_code[0][i] = 0;
+    ws.nd_lo[0][i] = v0;
+    ws.nd_hi[0][i] = v0;
+    double inc = __longlong_as_double(0x7ff0000000000000ll);  // +inf: no incumbent
+    double lb = -1e300;
+    int nodes = 0, iters = 0;
+    if (ok) {
+        hvp::LaneQp<N, LdsMem<N, BS>> q;
+        q.mem.lane = threadIdx.x;
+        double c0;
+        int it = bnb_qp<N, BS>(q, S, C, rl, prm, 0, 0, c0);
+        ++nodes;
+        iters += it >= 0 ? it : -1 - it;
+        if (it >= 0) {
+            lb = c0;
+            double ystar[N];
+#pragma unroll
+            for (int k = 0; k < N; ++k) ystar[k] = q.y[k];
+            uint64_t code;
+            if (hvp::bnb_dive<N>(S, C, v0, ystar, &code)) {
+                double c1;
+                it = bnb_qp<N, BS>(q, S, C, rl, prm, code, N, c1);
+                ++nodes;
+                iters += it >= 0 ? it : -1 - it;
+                if (it >= 0) inc = c1;
+            }
+        }
+    }
+    ws.nd_lb[0][i] = lb;
+    ws.inc[i] = (unsigned long long)__double_as_longlong(inc);
+    ws.nodes[i] = nodes;
+    ws.iters[i] = iters;
+    atomicAdd(&ws.counter[3], (unsigned long long)nodes);
+    atomicAdd(&ws.counter[1], (unsigned long long)iters);
+}
+
+// children of the level-(k-1) nodes that survive the incumbent test
+template <int N>
+__global__ __launch_bounds__(kBlock) void k_bnb_expand(int k, const hvp_system* __restrict__ systems,
+                                                       const int32_t* __restrict__ sys, hvp::Consts C, Workspace ws) {
+    const int src = (k - 1) & 1, dst = k & 1;
+    const unsigned long long np = ws.lvl[k - 1];
+    const long long total = (long long)(np < (unsigned long long)ws.cap ? np : ws.cap);
+    for (long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x; p < total;
+         p += (long long)gridDim.x * blockDim.x) {
+        const int inst = ws.nd_inst[src][p];
+        if (inst < 0) continue;
+        const double plb = ws.nd_lb[src][p];
+        if (hvp::bnb_pruned(plb, inc_of(ws, inst))) continue;
+        const hvp_system& S = systems[sys[inst]];
+        const double lo = ws.nd_lo[src][p], hi = ws.nd_hi[src][p];
+        const uint64_t code = ws.nd_code[src][p];
+        unsigned mask = 0;
+        for (int r = 0; r < S.n_regions; ++r) {
+            double a, b;
+            if (hvp::bnb_child(S, C, k - 1, lo, hi, r, &a, &b)) mask |= 1u << r;
+        }
+        const int nc = __popc(mask);
+        if (!nc) continue;
+        const unsigned long long off = atomicAdd(&ws.lvl[k], (unsigned long long)nc);
+        if (off + nc > (unsigned long long)ws.cap) {
+            atomicOr(&ws.inst_flag[inst], 2);  // overflow: reported, never truncated silently
+            continue;
+        }
+        int j = 0;
+        for (int r = 0; r < S.n_regions; ++r) {
+            if (!((mask >> r) & 1u)) continue;
+            double a, b;
+            hvp::bnb_child(S, C, k - 1, lo, hi, r, &a, &b);
+            ws.nd_inst[dst][off + j] = inst;
+            ws.nd_code[dst][off + j] = code | ((uint64_t)r << (3 * (k - 1)));
+            ws.nd_lo[dst][off + j] = a;
+            ws.nd_hi[dst][off + j] = b;
+            ws.nd_lb[dst][off + j] = plb;  // inherited: kept by a leaf whose QP fails
+            ++j;
+        }
+    }
+}
+
+// one lane per level-k node: bound (k < N) or exact leaf QP (k = N)
+template <int N>
+__global__ __launch_bounds__(kBnbBlock<N>) void k_bnb_bound(int k, const hvp_system* __restrict__ systems,
+                                                            const int32_t* __restrict__ sys,
+                                                            const int32_t* __restrict__ role,
+                                                            const double* __restrict__ params, hvp::Consts C,
+                                                            Workspace ws) {
+    constexpr int BS = kBnbBlock<N>;
+    const int dst = k & 1;
+    const unsigned long long nn = ws.lvl[k];
+    const long long total = (long long)(nn < (unsigned long long)ws.cap ? nn : ws.cap);
+    unsigned long long iter_sum = 0, fails = 0;
+    for (long long t = (long long)blockIdx.x * BS + threadIdx.x; t < total; t += (long long)gridDim.x * BS) {
+        const int inst = ws.nd_inst[dst][t];
+        const uint64_t code = ws.nd_code[dst][t];
+        const hvp_system& S = systems[sys[inst]];
+        const int rl = role[inst];
+        const double* prm = params + (size_t)inst * (2 + 6 * (N + 1));
+        hvp::LaneQp<N, LdsMem<N, BS>> q;
+        q.mem.lane = threadIdx.x;
+        double c;
+        const int it = bnb_qp<N, BS>(q, S, C, rl, prm, code, k, c);
+        const bool ok = it >= 0;
+        const int its = ok ? it : -1 - it;
+        iter_sum += (unsigned long long)its;
+        atomicAdd(&ws.nodes[inst], 1);
+        atomicAdd(&ws.iters[inst], its);
+        if (k < N) {
+            // a failed bound QP prunes nothing
+            ws.nd_lb[dst][t] = ok ? c : -1e300;
+        } else {
+            // a failed leaf keeps its parent's bound: K_key flags the instance MAXITER if that
+            // bound leaves the leaf in contention (never a silent wrong answer)
+            if (ok) ws.nd_lb[dst][t] = c;
+            ws.leaf_stat[t] = ok ? 0 : HVP_MAXITER;
+#pragma unroll
+            for (int j = 0; j < N; ++j) ws.task_y[t * N + j] = q.y[j];
+            if (ok) atomicMin(&ws.inc[inst], (unsigned long long)__double_as_longlong(c));
+            else ++fails;
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        iter_sum += __shfl_down(iter_sum, off, 64);
+        fails += __shfl_down(fails, off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (iter_sum) atomicAdd(&ws.counter[1], iter_sum);
+        if (fails) atomicAdd(&ws.counter[2], fails);
+    }
+}
+
+// tie rule: the lexicographically first leaf within 1e-9 relative of the minimum
+template <int N>
+__global__ __launch_bounds__(kBlock) void k_bnb_key(Workspace ws) {
+    const int src = N & 1;
+    const unsigned long long nn = ws.lvl[N];
+    const long long total = (long long)(nn < (unsigned long long)ws.cap ? nn : ws.cap);
+    for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (long long)gridDim.x * blockDim.x) {
+        const int inst = ws.nd_inst[src][t];
+        const double best = inc_of(ws, inst);
+        if (ws.leaf_stat[t] != 0) {
+            if (!hvp::bnb_pruned(ws.nd_lb[src][t], best)) atomicOr(&ws.inst_flag[inst], 4);
+            continue;
+        }
+        if (ws.nd_lb[src][t] <= best + 1e-9 * fmax(1.0, fabs(best)))
+            atomicMin(&ws.key[inst], (unsigned long long)hvp::bnb_lexkey(ws.nd_code[src][t], N));
+    }
+}
+
+template <int N>
+__device__ inline void write_solution(int i, const hvp_system& S, const double* prm, bool win, uint64_t code,
+                                      const double* y, double* u_out, double* x_out, int8_t* region_out,
+                                      int8_t* gear_out) {
+    double p = prm[0], v = prm[1];
+    if (x_out) {
+        x_out[(size_t)i * 2 * (N + 1)] = p;
+        x_out[(size_t)i * 2 * (N + 1) + N + 1] = v;
+    }
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        const int r = (code >> (3 * k)) & 7;
+        const double vn = win ? y[k] : v;
+        const double u = win ? (vn - S.a[r] * v - S.c[r]) / S.b[r] : 0.0;
+        p = p + S.ts * v;
+        v = vn;
+        if (u_out) u_out[(size_t)i * N + k] = u;
+        if (x_out) {
+            x_out[(size_t)i * 2 * (N + 1) + k + 1] = p;
+            x_out[(size_t)i * 2 * (N + 1) + N + 1 + k + 1] = v;
+        }
+        if (region_out) region_out[(size_t)i * N + k] = (int8_t)(win ? r : -1);
+        if (gear_out) gear_out[(size_t)i * N + k] = (int8_t)(win ? S.gear[r] : 0);
+    }
+}
+
+template <int N>
+__global__ __launch_bounds__(kBlock) void k_bnb_write(const hvp_system* __restrict__ systems,
+                                                      const int32_t* __restrict__ sys,
+                                                      const double* __restrict__ params, Workspace ws,
+                                                      double* __restrict__ u_out, double* __restrict__ x_out,
+                                                      int8_t* __restrict__ region_out, int8_t* __restrict__ gear_out,
+                                                      double* __restrict__ cost_out) {
+    const int src = N & 1;
+    const unsigned long long nn = ws.lvl[N];
+    const long long total = (long long)(nn < (unsigned long long)ws.cap ? nn : ws.cap);
+    for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (long long)gridDim.x * blockDim.x) {
+        if (ws.leaf_stat[t] != 0) continue;
+        const int inst = ws.nd_inst[src][t];
+        const uint64_t code = ws.nd_code[src][t];
+        if (hvp::bnb_lexkey(code, N) != ws.key[inst]) continue;
+        const hvp_system& S = systems[sys[inst]];
+        double y[N];
+#pragma unroll
+        for (int j = 0; j < N; ++j) y[j] = ws.task_y[t * N + j];
+        write_solution<N>(inst, S, params + (size_t)inst * (2 + 6 * (N + 1)), true, code, y, u_out, x_out,
+                          region_out, gear_out);
+        if (cost_out) cost_out[inst] = ws.nd_lb[src][t];
+    }
+}
+
+template <int N>
+__global__ __launch_bounds__(kBlock) void k_bnb_finish(int B, const hvp_system* __restrict__ systems,
+                                                       const int32_t* __restrict__ sys,
+                                                       const double* __restrict__ params, Workspace ws,
+                                                       double* __restrict__ u_out, double* __restrict__ x_out,
+                                                       int8_t* __restrict__ region_out, int8_t* __restrict__ gear_out,
+                                                       double* __restrict__ cost_out, int32_t* __restrict__ status_out,
+                                                       int32_t* __restrict__ nodes_out,
+                                                       int32_t* __restrict__ iters_out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B) return;
+    const int flag = ws.inst_flag[i];
+    const bool win = ws.key[i] != ~0ull;
+    int status;
+    if (flag & 1) status = HVP_INFEASIBLE;
+    else if (flag & 2) status = HVP_OVERFLOW;
+    else if (flag & 4) status = HVP_MAXITER;  // a leaf in contention whose QP did not converge
+    else if (win) status = HVP_OPTIMAL;
+    else status = ws.nodes[i] > 1 && __longlong_as_double((long long)ws.inc[i]) < 1e300 ? HVP_MAXITER : HVP_INFEASIBLE;
+    if (status_out) status_out[i] = status;
+    if (nodes_out) nodes_out[i] = ws.nodes[i];
+    if (iters_out) iters_out[i] = ws.iters[i];
+    if (!win || status != HVP_OPTIMAL) {
+        if (cost_out) cost_out[i] = 1e300;
+        write_solution<N>(i, systems[sys[i]], params + (size_t)i * (2 + 6 * (N + 1)), false, 0, nullptr, u_out, x_out,
+                          region_out, gear_out);
+    }
+}
+
 int grid_for(long long n) { return (int)std::max<long long>(1, (n + kBlock - 1) / kBlock); }
+
+template <int N>
+int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, const double* params, double* u_out,
+               double* x_out, int8_t* region_out, int8_t* gear_out, double* cost_out, int32_t* status_out,
+               int32_t* nodes_out, int32_t* iters_out, hipStream_t st) {
+    Workspace ws = h->ws;
+    constexpr int BS = kBnbBlock<N>;
+    HIP_TRY(hipMemsetAsync(ws.counter, 0, 4 * sizeof(unsigned long long), st));
+    HIP_TRY(hipMemsetAsync(ws.lvl, 0, (HVP_MAX_N + 1) * sizeof(unsigned long long), st));
+    HIP_TRY(hipEventRecord(h->ev0, st));
+    HIP_TRY(hipEventRecord(h->evq0, st));
+    const size_t lds = sizeof(double) * hvp::F_COUNT * N * BS;
+    HIP_TRY(hipEventRecord(h->evb[0], st));
+    hipLaunchKernelGGL(k_bnb_root<N>, dim3((B + BS - 1) / BS), dim3(BS), lds, st, B, h->d_sys, sys, role, params,
+                       h->C, ws);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(h->evb[1], st));
+    const int g_small = (int)std::min<long long>(grid_for(h->ws.cap), (long long)h->n_cu * 8);
+    const int g_qp = (int)std::min<long long>((h->ws.cap + BS - 1) / BS, (long long)h->n_cu * 8 * (kBlock / BS));
+    for (int k = 1; k <= N; ++k) {
+        hipLaunchKernelGGL(k_bnb_expand<N>, dim3(g_small), dim3(kBlock), 0, st, k, h->d_sys, sys, h->C, ws);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(h->evb[2 * k], st));
+        hipLaunchKernelGGL(k_bnb_bound<N>, dim3(g_qp), dim3(BS), lds, st, k, h->d_sys, sys, role, params, h->C, ws);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(h->evb[2 * k + 1], st));
+    }
+    HIP_TRY(hipEventRecord(h->evq1, st));
+    hipLaunchKernelGGL(k_bnb_key<N>, dim3(g_small), dim3(kBlock), 0, st, ws);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_bnb_write<N>, dim3(g_small), dim3(kBlock), 0, st, h->d_sys, sys, params, ws, u_out, x_out,
+                       region_out, gear_out, cost_out);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_bnb_finish<N>, dim3(grid_for(B)), dim3(kBlock), 0, st, B, h->d_sys, sys, params, ws, u_out,
+                       x_out, region_out, gear_out, cost_out, status_out, nodes_out, iters_out);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(h->ev1, st));
+    h->last_stream = st;
+    h->last_B = B;
+    h->last_bnb = true;
+    return 0;
+}
 
 template <int N>
 int launch_all(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, const double* params, double* u_out,
@@ -346,6 +677,7 @@ int launch_all(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
     HIP_TRY(hipEventRecord(h->ev1, st));
     h->last_stream = st;
     h->last_B = B;
+    h->last_bnb = false;
     return 0;
 }
 
@@ -360,15 +692,40 @@ void free_ws(Workspace& w) {
     (void)hipFree(w.task_cost);
     (void)hipFree(w.task_stat);
     (void)hipFree(w.task_y);
+    for (int b = 0; b < 2; ++b) {
+        (void)hipFree(w.nd_inst[b]);
+        (void)hipFree(w.nd_code[b]);
+        (void)hipFree(w.nd_lo[b]);
+        (void)hipFree(w.nd_hi[b]);
+        (void)hipFree(w.nd_lb[b]);
+    }
+    (void)hipFree(w.leaf_stat);
+    (void)hipFree(w.inc);
+    (void)hipFree(w.key);
+    (void)hipFree(w.nodes);
+    (void)hipFree(w.iters);
+    (void)hipFree(w.lvl);
     w = Workspace{};
 }
 
-int64_t default_capacity(int N, int B) {
+int64_t default_capacity(int N, int B, bool bnb) {
+    if (bnb) {
+        // nodes of ONE tree level, pooled over the batch (C2..C5 means: 3 leaves at N = 5, 4 at
+        // N = 10, 30 at N = 15; the widest level a few times that)
+        const int64_t per = N <= 8 ? 64 : (N <= 12 ? 256 : 1024);
+        return per * (int64_t)std::max(B, 1);
+    }
     // per-instance average budget: 7^N capped (N = 5: mean ~30, max ~85 region sequences)
     int64_t per = 1;
     for (int k = 0; k < N; ++k) per = std::min<int64_t>(per * 7, 1 << 20);
     per = std::min<int64_t>(per, N <= 5 ? 256 : (N <= 6 ? 1024 : 4096));
     return per * (int64_t)std::max(B, 1);
+}
+
+bool create_events(hipEvent_t* ev, int n) {
+    for (int i = 0; i < n; ++i)
+        if (hipEventCreate(&ev[i]) != hipSuccess) return false;
+    return true;
 }
 
 bool valid_system(const hvp_system& s, std::string* why) {
@@ -408,6 +765,11 @@ int hvp_create(hvp_handle** out, const hvp_problem* problem, const hvp_system* s
     *out = nullptr;
     if (problem->N < 2 || problem->N > HVP_MAX_N)
         return fail(HVP_E_UNSUPPORTED, "hvp_create: horizon N must be in [2, " + std::to_string(HVP_MAX_N) + "]");
+    if (problem->method < HVP_METHOD_AUTO || problem->method > HVP_METHOD_BNB)
+        return fail(HVP_E_ARG, "hvp_create: unknown method");
+    if (problem->method == HVP_METHOD_ENUMERATE && problem->N > HVP_MAX_N_ENUM)
+        return fail(HVP_E_UNSUPPORTED, "hvp_create: enumeration supports N <= " + std::to_string(HVP_MAX_N_ENUM) +
+                                           " (use HVP_METHOD_BNB)");
     if (problem->quadratic_cost != 1)
         return fail(HVP_E_UNSUPPORTED, "hvp_create: only the quadratic cost (min_2_norm) runs on the GPU");
     for (int i = 0; i < n_systems; ++i) {
@@ -419,12 +781,14 @@ int hvp_create(hvp_handle** out, const hvp_problem* problem, const hvp_system* s
     h->device = device;
     h->prob = *problem;
     h->C = make_consts(*problem);
+    h->bnb = problem->method == HVP_METHOD_BNB || (problem->method == HVP_METHOD_AUTO && problem->N > kAutoEnumMaxN);
     h->n_systems = n_systems;
     (void)hipDeviceGetAttribute(&h->n_cu, hipDeviceAttributeMultiprocessorCount, device);
     if (hipMalloc(&h->d_sys, sizeof(hvp_system) * n_systems) != hipSuccess ||
         hipMemcpy(h->d_sys, systems, sizeof(hvp_system) * n_systems, hipMemcpyHostToDevice) != hipSuccess ||
         hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess ||
-        hipEventCreate(&h->evq0) != hipSuccess || hipEventCreate(&h->evq1) != hipSuccess) {
+        hipEventCreate(&h->evq0) != hipSuccess || hipEventCreate(&h->evq1) != hipSuccess ||
+        !create_events(h->evb, 2 * (HVP_MAX_N + 1))) {
         hvp_destroy(h);
         return fail(HVP_E_HIP, "hvp_create: device allocation failed");
     }
@@ -434,7 +798,7 @@ int hvp_create(hvp_handle** out, const hvp_problem* problem, const hvp_system* s
 
 int hvp_reserve(hvp_handle* h, int max_batch, int64_t cap) {
     if (!h || max_batch <= 0) return fail(HVP_E_ARG, "hvp_reserve: bad argument");
-    if (cap <= 0) cap = default_capacity(h->prob.N, max_batch);
+    if (cap <= 0) cap = default_capacity(h->prob.N, max_batch, h->bnb);
     if (max_batch <= h->ws.max_batch && cap <= h->ws.cap) return 0;
     HIP_TRY(hipSetDevice(h->device));
     HIP_TRY(hipDeviceSynchronize());
@@ -453,6 +817,20 @@ int hvp_reserve(hvp_handle* h, int max_batch, int64_t cap) {
               hipMalloc(&w.task_cost, sizeof(double) * cap) == hipSuccess &&
               hipMalloc(&w.task_stat, sizeof(int32_t) * cap) == hipSuccess &&
               hipMalloc(&w.task_y, sizeof(double) * cap * N) == hipSuccess;
+    if (ok && h->bnb) {
+        for (int b = 0; b < 2 && ok; ++b)
+            ok = hipMalloc(&w.nd_inst[b], sizeof(int32_t) * cap) == hipSuccess &&
+                 hipMalloc(&w.nd_code[b], sizeof(uint64_t) * cap) == hipSuccess &&
+                 hipMalloc(&w.nd_lo[b], sizeof(double) * cap) == hipSuccess &&
+                 hipMalloc(&w.nd_hi[b], sizeof(double) * cap) == hipSuccess &&
+                 hipMalloc(&w.nd_lb[b], sizeof(double) * cap) == hipSuccess;
+        ok = ok && hipMalloc(&w.leaf_stat, sizeof(int32_t) * cap) == hipSuccess &&
+             hipMalloc(&w.inc, sizeof(unsigned long long) * max_batch) == hipSuccess &&
+             hipMalloc(&w.key, sizeof(unsigned long long) * max_batch) == hipSuccess &&
+             hipMalloc(&w.nodes, sizeof(int32_t) * max_batch) == hipSuccess &&
+             hipMalloc(&w.iters, sizeof(int32_t) * max_batch) == hipSuccess &&
+             hipMalloc(&w.lvl, sizeof(unsigned long long) * (HVP_MAX_N + 1)) == hipSuccess;
+    }
     if (!ok) {
         free_ws(w);
         return fail(HVP_E_NOMEM, "hvp_reserve: device allocation failed");
@@ -469,11 +847,21 @@ int hvp_solve_batch(hvp_handle* h, int B, const int32_t* sys, const int32_t* rol
         return fail(HVP_E_ARG, "hvp_solve_batch: bad argument");
     if (B == 0) return 0;
     if (B > h->ws.max_batch) {
-        int rc = hvp_reserve(h, B, default_capacity(h->prob.N, B));
+        int rc = hvp_reserve(h, B, default_capacity(h->prob.N, B, h->bnb));
         if (rc) return rc;
     }
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t st = (hipStream_t)stream;
+    if (h->bnb) {
+        switch (h->prob.N) {
+#define HVP_CASE(n) \
+    case n: return launch_bnb<n>(h, B, sys, role, params, u_out, x_out, region_out, gear_out, cost_out, status_out, nodes_out, iters_out, st);
+            HVP_CASE(2) HVP_CASE(3) HVP_CASE(4) HVP_CASE(5) HVP_CASE(6) HVP_CASE(7) HVP_CASE(8)
+            HVP_CASE(9) HVP_CASE(10) HVP_CASE(11) HVP_CASE(12) HVP_CASE(13) HVP_CASE(14) HVP_CASE(15) HVP_CASE(16)
+#undef HVP_CASE
+            default: return fail(HVP_E_UNSUPPORTED, "hvp_solve_batch: unsupported N");
+        }
+    }
     switch (h->prob.N) {
 #define HVP_CASE(n) \
     case n: return launch_all<n>(h, B, sys, role, params, u_out, x_out, region_out, gear_out, cost_out, status_out, nodes_out, iters_out, st);
@@ -502,6 +890,22 @@ int hvp_get_stats(hvp_handle* h, hvp_stats* out) {
     out->qp_ms = qms;
     out->n_instances = h->last_B;
     out->n_candidates = (int64_t)c[0];
+    if (h->last_bnb) {
+        // tree nodes solved: root + dive QPs (counter[3]) and every level's nodes
+        unsigned long long lv[HVP_MAX_N + 1];
+        HIP_TRY(hipMemcpy(lv, h->ws.lvl, sizeof(lv), hipMemcpyDeviceToHost));
+        int64_t n = (int64_t)c[3];
+        for (int k = 1; k <= h->prob.N; ++k) n += (int64_t)std::min<unsigned long long>(lv[k], (unsigned long long)h->ws.cap);
+        out->n_candidates = n;
+        // QP time = K_bnb_root + every K_bnb_bound launch (the expand / select kernels excluded)
+        float sum = 0.f;
+        for (int k = 0; k <= h->prob.N; ++k) {
+            float t = 0.f;
+            HIP_TRY(hipEventElapsedTime(&t, h->evb[2 * k], h->evb[2 * k + 1]));
+            sum += t;
+        }
+        out->qp_ms = sum;
+    }
     out->qp_iterations = (int64_t)c[1];
     out->n_fallback = (int64_t)c[2];
     out->capacity = h->ws.cap;
@@ -573,6 +977,8 @@ void hvp_destroy(hvp_handle* h) {
     if (h->ev1) (void)hipEventDestroy(h->ev1);
     if (h->evq0) (void)hipEventDestroy(h->evq0);
     if (h->evq1) (void)hipEventDestroy(h->evq1);
+    for (hipEvent_t& e : h->evb)
+        if (e) (void)hipEventDestroy(e);
     delete h;
 }
 

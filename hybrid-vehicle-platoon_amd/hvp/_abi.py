@@ -10,8 +10,11 @@ import ctypes
 import os
 
 MAX_REGIONS = 8
-MAX_N = 8
-ABI_VERSION = 1
+MAX_N = 16
+MAX_N_ENUM = 8
+ABI_VERSION = 2
+
+METHOD_AUTO, METHOD_ENUMERATE, METHOD_BNB = 0, 1, 2
 
 ROLE_SAFE_FRONT = 1
 ROLE_SAFE_BACK = 2
@@ -62,7 +65,7 @@ class HvpProblem(ctypes.Structure):
         ("spacing_d0", ctypes.c_double),
         ("spacing_t0", ctypes.c_double),
         ("max_iter", ctypes.c_int32),
-        ("pad_", ctypes.c_int32),
+        ("method", ctypes.c_int32),
         ("tol", ctypes.c_double),
     ]
 

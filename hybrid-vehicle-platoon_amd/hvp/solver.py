@@ -90,13 +90,29 @@ class BatchSolver:
         )
         if B == 0:
             return out
+        self._solve_host(sys_idx, roles, params, out)
+        # the search workspace is pooled over the batch: instances that did not fit (HVP_OVERFLOW,
+        # reported, never truncated) are re-solved with a larger reservation
+        for _ in range(4):
+            over = np.flatnonzero(out.status == _abi.OVERFLOW)
+            if not len(over):
+                break
+            cap = self.stats().capacity
+            self.reserve(max(B, 1), 4 * cap)
+            sub = BatchResult(**{k: v[over].copy() for k, v in out.__dict__.items()})
+            self._solve_host(sys_idx[over], roles[over], np.ascontiguousarray(params[over]), sub)
+            for k, v in sub.__dict__.items():
+                getattr(out, k)[over] = v
+        return out
+
+    def _solve_host(self, sys_idx, roles, params, out: BatchResult) -> None:
         P = lambda a, t: a.ctypes.data_as(ctypes.POINTER(t))  # noqa: E731
         d, i32, i8 = ctypes.c_double, ctypes.c_int32, ctypes.c_int8
         rc = self._lib.hvp_solve_batch_host(
-            self._h, B, P(sys_idx, i32), P(roles, i32), P(params, d), P(out.u, d), P(out.x, d), P(out.region, i8),
-            P(out.gear, i8), P(out.cost, d), P(out.status, i32), P(out.nodes, i32), P(out.iters, i32))
+            self._h, len(roles), P(sys_idx, i32), P(roles, i32), P(params, d), P(out.u, d), P(out.x, d),
+            P(out.region, i8), P(out.gear, i8), P(out.cost, d), P(out.status, i32), P(out.nodes, i32),
+            P(out.iters, i32))
         _abi.check(rc, "hvp_solve_batch_host")
-        return out
 
     # -------------------------------------------------------------- device path
     def alloc_outputs(self, B: int, device=None) -> dict:
@@ -116,7 +132,10 @@ class BatchSolver:
         }
 
     def solve_device(self, sys_idx, roles, params, out: dict | None = None, stream=None) -> dict:
-        """Asynchronous solve of device-resident tensors; returns (and fills) the output dict."""
+        """Asynchronous solve of device-resident tensors; returns (and fills) the output dict.
+
+        Instances whose search did not fit the workspace come back as HVP_OVERFLOW (reserve a
+        larger ``candidate_capacity``, or use :meth:`solve`, which retries them)."""
         import torch
 
         B = int(roles.shape[0])

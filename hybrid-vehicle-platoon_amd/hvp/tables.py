@@ -91,8 +91,8 @@ def spacing_params(policy: SpacingPolicy) -> tuple[float, float]:
 
 
 def problem(N: int, spacing_policy: SpacingPolicy | None = None, quadratic_cost: bool = True,
-            accel_cnstr_tightening: float = 0.0, params=Params, max_iter: int = 0, tol: float = 0.0
-            ) -> _abi.HvpProblem:
+            accel_cnstr_tightening: float = 0.0, params=Params, max_iter: int = 0, tol: float = 0.0,
+            method: int = _abi.METHOD_AUTO) -> _abi.HvpProblem:
     """hvp_problem for LocalMpcMld's cost / constraints (fleet_decent_mld.py:24-31, 61-208)."""
     d0, t0 = spacing_params(spacing_policy or ConstantSpacingPolicy(50))
     p = _abi.HvpProblem()
@@ -108,6 +108,7 @@ def problem(N: int, spacing_policy: SpacingPolicy | None = None, quadratic_cost:
     p.accel_tightening = float(accel_cnstr_tightening)
     p.spacing_d0, p.spacing_t0 = d0, t0
     p.max_iter = max_iter
+    p.method = method
     p.tol = tol
     return p
 

@@ -38,9 +38,10 @@
 extern "C" {
 #endif
 
-#define HVP_ABI_VERSION 1
+#define HVP_ABI_VERSION 2
 #define HVP_MAX_REGIONS 8
-#define HVP_MAX_N 8 /* horizon supported by the enumeration path */
+#define HVP_MAX_N 16     /* longest horizon (branch-and-bound path)            */
+#define HVP_MAX_N_ENUM 8 /* longest horizon of the exhaustive-enumeration path */
 
 /* Discrete-time PWA model of one vehicle, velocity-partitioned (the form every system dict of
  * models.py:370-492 has): region r holds for vlo[r] <= v <= vhi[r] (closed; overlapping
@@ -78,9 +79,17 @@ typedef struct hvp_problem {
     double spacing_d0;      /* spacing(x) = [-d0 - t0 * v, 0]                          */
     double spacing_t0;
     int32_t max_iter;       /* fallback IPM iteration cap per candidate (<=0: 60)      */
-    int32_t pad_;
+    int32_t method;         /* HVP_METHOD_*: how the region sequences are searched     */
     double tol;             /* fallback IPM relative tolerance (<=0: 1e-12)            */
 } hvp_problem;
+
+/* Search over the region sequences (hvp_problem.method).  Both give the same sequence: the
+ * exact argmin with ties to the lexicographically first sequence (DESIGN.md "Algorithm"). */
+enum {
+    HVP_METHOD_AUTO = 0,      /* branch and bound (measured faster from N = 5 on)          */
+    HVP_METHOD_ENUMERATE = 1, /* every velocity-feasible sequence (N <= HVP_MAX_N_ENUM)     */
+    HVP_METHOD_BNB = 2        /* branch and bound with horizon-relaxed QP bounds             */
+};
 
 /* Role of one local MPC (is_front / is_trailer / is_leader / real_vehicle_as_reference). */
 enum {

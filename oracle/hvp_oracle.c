@@ -167,9 +167,21 @@ static void add_norm(or_qp* qp, or_layout* L, const or_cfg* cf, const lin e[2], 
     }
 }
 
-/* Builds the fixed-sigma QP. Returns number of variables (0 on layout overflow). */
+/* Builds the fixed-sigma QP. Returns number of variables (0 on layout overflow).
+ * K < N builds the branch-and-bound RELAXATION of the prefix sigma_0..sigma_{K-1}: for steps
+ * k >= K the region is free, so the region-dependent rows are dropped -- the velocity row of the
+ * dynamics, the region rows S x_k + R u_k <= T and the input cost -- while the position row of
+ * the dynamics (identical in every region, checked by oracle_bnb_ok), the state box, the
+ * acceleration rows and all tracking / slack terms stay.  Its optimum bounds every completion of
+ * the prefix from below. */
+static int build_qp_k(or_qp* qp, const or_model* md, const or_cfg* cf, const int* sigma, int K, const double* x0,
+                      const double* xf, const double* xb, const double* xl);
 static int build_qp(or_qp* qp, const or_model* md, const or_cfg* cf, const int* sigma, const double* x0,
                     const double* xf, const double* xb, const double* xl) {
+    return build_qp_k(qp, md, cf, sigma, cf->N, x0, xf, xb, xl);
+}
+static int build_qp_k(or_qp* qp, const or_model* md, const or_cfg* cf, const int* sigma, int K, const double* x0,
+                      const double* xf, const double* xb, const double* xl) {
     const int N = cf->N;
     or_layout L;
     L.N = N; L.x0 = x0; L.xf = xf; L.xb = xb; L.xl = xl;
@@ -190,8 +202,8 @@ static int build_qp(or_qp* qp, const or_model* md, const or_cfg* cf, const int* 
 
     /* dynamics of the selected region (MLD with delta fixed) */
     for (int k = 0; k < N; ++k) {
-        int r = sigma[k];
-        for (int i = 0; i < 2; ++i) {
+        int r = k < K ? sigma[k] : 0;
+        for (int i = 0; i < (k < K ? 2 : 1); ++i) {
             lin e = X(&L, k + 1, i);
             for (int j = 0; j < 2; ++j) { lin xj = X(&L, k, j); e = lin_axpy(-md->A[r][i][j], &xj, &e); }
             lin uk = U(&L, k);
@@ -200,7 +212,7 @@ static int build_qp(or_qp* qp, const or_model* md, const or_cfg* cf, const int* 
         }
     }
     /* region rows S x_k + R u_k <= T (k = 0..N-1) */
-    for (int k = 0; k < N; ++k) {
+    for (int k = 0; k < K; ++k) {
         int r = sigma[k];
         for (int row = 0; row < md->nsr; ++row) {
             lin e = lin_const(0.0);
@@ -281,11 +293,11 @@ static int build_qp(or_qp* qp, const or_model* md, const or_cfg* cf, const int* 
     }
     /* control effort and variation */
     double Qu[2][2] = {{cf->Qu, 0}, {0, 0}}, Qdu[2][2] = {{cf->Qdu, 0}, {0, 0}};
-    for (int k = 0; k < N; ++k) {
+    for (int k = 0; k < K; ++k) {
         lin e[2]; e[0] = U(&L, k); e[1] = lin_const(0.0);
         add_norm(qp, &L, cf, e, Qu, 1);
     }
-    for (int k = 0; k + 1 < N; ++k) {
+    for (int k = 0; k + 1 < K; ++k) {
         lin e[2];
         lin a = U(&L, k + 1), b = U(&L, k);
         e[0] = lin_axpy(-1.0, &b, &a); e[1] = lin_const(0.0);
@@ -649,8 +661,15 @@ static or_result ipm_solve(const or_qp* qp, or_work* w, int maxit) {
 /* Objective evaluated term by term on the trajectory (the form of fleet_decent_mld.py:107-169):
  * sums of squared tracking errors, control terms and w * slack with the slacks at their optimal
  * value max(0, .).  Avoids the cancellation of 1/2 z'Pz + q'z + r0 (positions ~3e3). */
+static double direct_objective_k(const or_cfg* cf, const double* x0, const double* xf, const double* xb,
+                                 const double* xl, const double* z, int K);
 static double direct_objective(const or_cfg* cf, const double* x0, const double* xf, const double* xb,
                                const double* xl, const double* z) {
+    return direct_objective_k(cf, x0, xf, xb, xl, z, cf->N);
+}
+/* K < N: objective of the relaxation built by build_qp_k (no input terms for k >= K) */
+static double direct_objective_k(const or_cfg* cf, const double* x0, const double* xf, const double* xb,
+                                 const double* xl, const double* z, int K) {
     const int N = cf->N;
     double J = 0.0;
     for (int k = 0; k <= N; ++k) {
@@ -676,10 +695,10 @@ static double direct_objective(const or_cfg* cf, const double* x0, const double*
         if (cf->role & R_SF) J += cf->w * fmax(0.0, p - par(xf, N, 0, k) + cf->d_safe);
         if (cf->role & R_SB) J += cf->w * fmax(0.0, par(xb, N, 0, k) + cf->d_safe - p);
     }
-    for (int k = 0; k < N; ++k) {
+    for (int k = 0; k < K; ++k) {
         double u = z[2 * N + k];
         J += cf->quadratic ? cf->Qu * u * u : fabs(cf->Qu * u);
-        if (k + 1 < N) {
+        if (k + 1 < K) {
             double du = z[2 * N + k + 1] - u;
             J += cf->quadratic ? cf->Qdu * du * du : fabs(cf->Qdu * du);
         }
@@ -789,7 +808,7 @@ typedef struct {
     or_qp* qp;
     or_work* w;
     int maxit;
-    int n_conv, n_cert, iters;
+    int n_conv, n_cert, iters, n_qp;
     /* every candidate in DFS (= lexicographic) order */
     int ncand, cap;
     double* obj;
@@ -821,6 +840,99 @@ static void visit_qp(const int* sigma, void* vctx) {
     C->cert[C->ncand] = (unsigned char)cert;
     memcpy(C->sig + (size_t)C->ncand * N, sigma, sizeof(int) * N);
     C->ncand++;
+}
+
+/* ------------------------------------------------------------------ branch and bound
+ * Depth-first branch and bound over the region sequences (the search Gurobi performs over the
+ * MLD binaries, restated): children of a prefix are the regions reachable at the next step;
+ * each child gets the optimum of its relaxation (build_qp_k) as lower bound, children are
+ * visited in increasing bound order, and a child whose bound exceeds the best leaf so far by
+ * more than 1e-7 relative is pruned (100x the 1e-9 tie window, so every sequence tied with the
+ * optimum is still evaluated and the tie rule below sees it).  Leaves are exact fixed-sequence
+ * QPs and go through visit-style bookkeeping. */
+static int g_method = 0; /* 0 exhaustive enumeration, 1 branch and bound */
+
+static void bnb_record(or_ctx* C, const int* sigma, double obj, int cert) {
+    const int N = C->cf->N;
+    if (C->ncand == C->cap) {
+        int nc = C->cap ? 2 * C->cap : 64;
+        C->obj = (double*)realloc(C->obj, sizeof(double) * nc);
+        C->sig = (int*)realloc(C->sig, sizeof(int) * (size_t)nc * N);
+        C->cert = (unsigned char*)realloc(C->cert, (size_t)nc);
+        C->cap = nc;
+    }
+    C->obj[C->ncand] = obj;
+    C->cert[C->ncand] = (unsigned char)cert;
+    memcpy(C->sig + (size_t)C->ncand * N, sigma, sizeof(int) * N);
+    C->ncand++;
+}
+
+/* relaxed (K < N) or exact (K = N) QP of prefix sigma[0..K-1]: objective or +inf */
+static double bnb_qp(or_ctx* C, const int* sigma, int K, int* cert) {
+    *cert = 0;
+    C->n_qp++;
+    if (build_qp_k(C->qp, C->md, C->cf, sigma, K, C->x0, C->xf, C->xb, C->xl) <= 0 || C->qp->infeasible_const)
+        return INFINITY;
+    or_result r = ipm_solve(C->qp, C->w, C->maxit);
+    C->iters += r.iters;
+    if (!r.converged) return K < C->cf->N ? -INFINITY : INFINITY; /* an unsolved bound prunes nothing */
+    *cert = r.certified;
+    return direct_objective_k(C->cf, C->x0, C->xf, C->xb, C->xl, C->w->z, K);
+}
+
+static void bnb_dfs(or_ctx* C, const or_vmodel* vm, int nreg, int k, double lo, double hi, int* sigma, double* inc,
+                    int* count) {
+    const int N = C->cf->N;
+    const or_cfg* cf = C->cf;
+    double dec = cf->a_dec * cf->ts + k * cf->tight, acc = cf->a_acc * cf->ts - k * cf->tight;
+    int child[OR_MAX_REG], nch = 0;
+    double clo[OR_MAX_REG], chi[OR_MAX_REG], lb[OR_MAX_REG];
+    for (int r = 0; r < nreg; ++r) {
+        if (!vm->rok[r]) continue;
+        double ilo = fmax(lo, vm->rlo[r]), ihi = fmin(hi, vm->rhi[r]);
+        if (ilo > ihi + 1e-9 * (1.0 + fabs(ihi))) continue;
+        if (ilo > ihi) ilo = ihi = 0.5 * (ilo + ihi);
+        double nlo, nhi;
+        if (!next_interval(ilo, ihi, vm->a[r], vm->b[r], vm->c[r], vm->ul, vm->uh, dec, acc, vm->blo, vm->bhi,
+                           &nlo, &nhi))
+            continue;
+        sigma[k] = r;
+        int cert;
+        double b = bnb_qp(C, sigma, k + 1, &cert);
+        if (k + 1 == N) {
+            (*count)++;
+            if (isfinite(b)) { C->n_conv++; C->n_cert += cert; }
+            bnb_record(C, sigma, b, cert);
+            if (b < *inc) *inc = b;
+            continue;
+        }
+        child[nch] = r; clo[nch] = nlo; chi[nch] = nhi; lb[nch] = b; nch++;
+    }
+    /* visit in increasing bound order (insertion sort, stable) */
+    for (int i = 1; i < nch; ++i)
+        for (int j = i; j > 0 && lb[j] < lb[j - 1]; --j) {
+            double t = lb[j]; lb[j] = lb[j - 1]; lb[j - 1] = t;
+            t = clo[j]; clo[j] = clo[j - 1]; clo[j - 1] = t;
+            t = chi[j]; chi[j] = chi[j - 1]; chi[j - 1] = t;
+            int ti = child[j]; child[j] = child[j - 1]; child[j - 1] = ti;
+        }
+    for (int i = 0; i < nch; ++i) {
+        if (lb[i] > *inc + 1e-7 * (1.0 + fabs(*inc))) continue;
+        sigma[k] = child[i];
+        bnb_dfs(C, vm, nreg, k + 1, clo[i], chi[i], sigma, inc, count);
+    }
+}
+
+void oracle_set_method(int m) { g_method = m; }
+
+/* The relaxation drops only velocity rows: the position row of the dynamics must be the same
+ * in every region (true for the reference's PWA models, models.py:370-387). */
+static int oracle_bnb_ok(const or_model* md) {
+    for (int r = 1; r < md->nreg; ++r)
+        if (md->A[r][0][0] != md->A[0][0][0] || md->A[r][0][1] != md->A[0][0][1] || md->B[r][0] != md->B[0][0] ||
+            md->c[r][0] != md->c[0][0])
+            return 0;
+    return 1;
 }
 
 /* Winner: the minimum objective; among candidates within 1e-9 relative of it the first in
@@ -910,8 +1022,32 @@ int oracle_solve_miqp(int N, int nreg, int nsr, const double* S, const double* R
     C.md = &md; C.cf = &cf; C.x0 = x0; C.xf = xf; C.xb = xb; C.xl = xl; C.qp = qp; C.w = w;
     C.maxit = maxit > 0 ? maxit : 200;
     int sigma[OR_MAX_N], count = 0;
-    dfs(&vm, md.nreg, &cf, 0, x0[1], x0[1], sigma, visit_qp, &C, &count);
-    int win = select_winner(C.obj, C.ncand);
+    int win;
+    if (g_method == 1) {
+        if (!oracle_bnb_ok(&md)) { free(qp); free(w); return -4; }
+        double inc = INFINITY;
+        bnb_dfs(&C, &vm, md.nreg, 0, x0[1], x0[1], sigma, &inc, &count);
+        /* exploration order is by bound: the tie rule compares sequences lexicographically */
+        win = -1;
+        if (isfinite(inc)) {
+            double tol = 1e-9 * fmax(1.0, fabs(inc));
+            for (int i = 0; i < C.ncand; ++i) {
+                if (!(C.obj[i] <= inc + tol)) continue;
+                int less = win < 0;
+                for (int k = 0; k < N && !less; ++k) {
+                    int a = C.sig[(size_t)i * N + k], b = C.sig[(size_t)win * N + k];
+                    if (a != b) { less = a < b; break; }
+                }
+                if (less) win = i;
+            }
+        }
+        /* nodes = QPs of the search (the reference's Gurobi NodeCount analogue); no leaf at all
+         * means no feasible sequence */
+        count = count ? C.n_qp : 0;
+    } else {
+        dfs(&vm, md.nreg, &cf, 0, x0[1], x0[1], sigma, visit_qp, &C, &count);
+        win = select_winner(C.obj, C.ncand);
+    }
     int status = win >= 0 ? 0 : (count == 0 ? 1 : 2);
     int best_cert = 0;
     double best_obj = INFINITY;

@@ -202,6 +202,8 @@ def lib():
         L.oracle_solve_batch.argtypes = [c_int, c_int, c_int, c_int, c_int, dp, dp, dp, dp, dp, dp, c_int, dp, dp,
                                          c_int, dp, dp, dp, c_int, ip, ip, dp, c_int, dp, dp, ip, dp, c_int]
         L.oracle_solve_batch.restype = c_int
+        L.oracle_set_method.argtypes = [c_int]
+        L.oracle_set_method.restype = None
         _lib = L
     return _lib
 
@@ -243,6 +245,15 @@ class MiqpResult:
     iters: int
     cand_obj: np.ndarray | None = None
     cand_sigma: np.ndarray | None = None
+
+
+METHOD_ENUMERATE, METHOD_BNB = 0, 1
+
+
+def set_method(method: int) -> None:
+    """0: exhaustive enumeration of the region sequences (default); 1: depth-first branch and
+    bound with relaxed-prefix bounds (hvp_oracle.c bnb_dfs), needed for N >= 10."""
+    lib().oracle_set_method(int(method))
 
 
 def solve_miqp(sysd: dict, cfg: Cfg, N: int, role: int, x0, xf, xb, xl, quadratic: bool = True,

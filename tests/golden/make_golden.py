@@ -19,9 +19,13 @@ Files (numpy .npz, no pickles):
                       linearly dependent rows, where an interior-point solve stalls.  Found by
                       scanning bench seeds 0..5999 for disagreements between the two QP methods of
                       the lane (active set vs interior point); expected values from the oracle.
+  sweep_n*_N{10,15}.npz  configs[4] (C5 sweep) horizons beyond exhaustive enumeration: t=0 states and
+                      mid-rollout states; expected values from the oracle's branch and bound
+                      (oracle_set_method(1), cross-checked against its enumeration at N <= 10 by
+                      tests/test_oracle.py); "method" = 1 marks them (node counts not comparable)
   known_answers.json  constants derived from the reference source
 
-Run:  python tests/golden/make_golden.py
+Run:  python tests/golden/make_golden.py [sweep]
 """
 
 from __future__ import annotations
@@ -70,10 +74,10 @@ def solve_set(systems, masses_idx, cfg, N, params, roles, quadratic=True):
     return {k: np.array(v) for k, v in out.items()}
 
 
-def save(name, N, masses, cfg, params, roles, sys_idx, exp):
+def save(name, N, masses, cfg, params, roles, sys_idx, exp, method=0):
     path = os.path.join(HERE, name)
     np.savez_compressed(path, N=N, masses=np.asarray(masses, float), cfg=cfg.vector(), params=params,
-                        roles=roles.astype(np.int32), sys=np.asarray(sys_idx, np.int32),
+                        roles=roles.astype(np.int32), sys=np.asarray(sys_idx, np.int32), method=method,
                         **{f"exp_{k}": v for k, v in exp.items()})
     cert = exp["certified"][exp["status"] == 0].mean() if (exp["status"] == 0).any() else 0
     print(f"{name}: {len(roles)} instances, optimal {int((exp['status'] == 0).sum())}, certified {cert:.3f}")
@@ -149,7 +153,24 @@ def hard_cases(N=5, n=10):
     return params, roles, sys_idx, solve_set([O.gear_pwa_system(800.0)], sys_idx, O.Cfg(), N, params, roles)
 
 
+def sweep():
+    """C5 sweep points with N = 10, 15 (oracle branch and bound)."""
+    O.set_method(O.METHOD_BNB)
+    try:
+        for n, N, seeds in ((5, 10, range(4)), (10, 10, range(3)), (20, 10, range(1)), (5, 15, range(3)),
+                            (10, 15, range(2)), (15, 15, range(1)), (20, 15, range(1))):
+            params, roles, si, exp = decent_seeds(n, N, seeds)
+            save(f"sweep_n{n}_N{N}.npz", N, [800.0], O.Cfg(), params, roles, si, exp, method=1)
+        params, roles, si, exp = rollout(5, 10, range(2), 5)
+        save("sweep_rollout_n5_N10.npz", 10, [800.0], O.Cfg(), params, roles, si, exp, method=1)
+    finally:
+        O.set_method(O.METHOD_ENUMERATE)
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "sweep":
+        sweep()
+        return
     N = 5
     params, roles, si, exp = hard_cases(N)
     save("hard_n10_N5.npz", N, [800.0], O.Cfg(), params, roles, si, exp)

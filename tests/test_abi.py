@@ -49,9 +49,14 @@ def test_invalid_arguments_fail_loudly_without_touching_the_gpu():
     h = ctypes.c_void_p()
     veh = PwaGearVehicle(800)
     sysv = (_abi.HvpSystem * 1)(tables.system_from_dict(veh.get_discrete_system(1), tables.gears_of(veh)))
-    bad = tables.problem(12)  # beyond HVP_MAX_N
+    bad = tables.problem(17)  # beyond HVP_MAX_N
     assert lib.hvp_create(ctypes.byref(h), ctypes.byref(bad), sysv, 1, 0) == -3
     assert "horizon" in _abi.last_error()
+    enum12 = tables.problem(12, method=_abi.METHOD_ENUMERATE)  # enumeration stops at HVP_MAX_N_ENUM
+    assert lib.hvp_create(ctypes.byref(h), ctypes.byref(enum12), sysv, 1, 0) == -3
+    assert "enumeration" in _abi.last_error()
+    badm = tables.problem(5, method=7)
+    assert lib.hvp_create(ctypes.byref(h), ctypes.byref(badm), sysv, 1, 0) == -1
     l1 = tables.problem(5)
     l1.quadratic_cost = 0
     assert lib.hvp_create(ctypes.byref(h), ctypes.byref(l1), sysv, 1, 0) == -3

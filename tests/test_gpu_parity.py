@@ -32,27 +32,29 @@ def _gear_system(mass=800.0):
     return tables.system_from_dict(veh.get_discrete_system(1), tables.gears_of(veh))
 
 
-def _compare(res, ref, params, tol_c=1e-9, tol_u=1e-6):
+def _compare(res, ref, params, tol_c=1e-9, tol_u=1e-6, nodes=True):
     gear_of = np.array([1, 2, 3, 4, 4, 5, 6])
     for i, r in enumerate(ref):
         assert res.status[i] == 0, (i, res.status[i])
         assert list(res.region[i]) == list(r.sigma), (i, res.region[i], r.sigma, res.cost[i], r.cost)
         assert list(res.gear[i]) == list(gear_of[r.sigma]), i
-        assert res.nodes[i] == r.n_candidates, (i, res.nodes[i], r.n_candidates)
+        if nodes:
+            assert res.nodes[i] == r.n_candidates, (i, res.nodes[i], r.n_candidates)
         assert abs(res.cost[i] - r.cost) <= tol_c * max(1.0, abs(r.cost)), (i, res.cost[i], r.cost)
         assert np.abs(res.u[i] - r.u).max() <= tol_u, (i, res.u[i], r.u)
         assert np.abs(res.x[i] - r.x).max() <= tol_u * 100, i  # positions ~3e3: 1e-4 absolute
 
 
+@pytest.mark.parametrize("method", [1, 2])  # HVP_METHOD_ENUMERATE, HVP_METHOD_BNB
 @pytest.mark.parametrize("n", [2, 10])
-def test_decent_seeds_match_oracle(gpu_available, n):
-    s = _solver([_gear_system()])
+def test_decent_seeds_match_oracle(gpu_available, n, method):
+    s = _solver([_gear_system()], method=method)
     sysd = O.gear_pwa_system(800.0)
     lead = leader_window(N)
     for seed in range(10):
         params, roles = decent_instances(O.env_initial_state(n, seed), N, lead)
         res = s.solve(np.zeros(n, np.int32), roles, params)
-        _compare(res, oracle_solve(sysd, O.Cfg(), N, params, roles), params)
+        _compare(res, oracle_solve(sysd, O.Cfg(), N, params, roles), params, nodes=method == 1)
 
 
 def test_device_path_matches_host_path(gpu_available):
@@ -102,17 +104,22 @@ def test_position_box_fallback(gpu_available):
 from golden_io import fixture_names, load, product_problem  # noqa: E402
 
 
+@pytest.mark.parametrize("method", [1, 2])  # HVP_METHOD_ENUMERATE, HVP_METHOD_BNB
 @pytest.mark.parametrize("name", fixture_names())
-def test_golden_fixture_on_gpu(gpu_available, name):
+def test_golden_fixture_on_gpu(gpu_available, name, method):
     from hvp.solver import BatchSolver
 
     fx = load(name)
+    if method == 1 and int(fx["N"]) > 8:
+        pytest.skip("beyond exhaustive enumeration: branch and bound only")
     prob, systems = product_problem(fx)
+    prob.method = method
     s = BatchSolver(prob, systems)
     res = s.solve(fx["sys"], fx["roles"], fx["params"])
     ok = fx["exp_status"] == 0
     assert np.array_equal(res.status, fx["exp_status"])
-    assert np.array_equal(res.nodes, fx["exp_nodes"])
+    if method == 1:
+        assert np.array_equal(res.nodes, fx["exp_nodes"])
     assert np.array_equal(res.region[ok], fx["exp_region"][ok])
     gear_of = np.array([1, 2, 3, 4, 4, 5, 6])
     assert np.array_equal(res.gear[ok], gear_of[fx["exp_region"][ok]])
@@ -160,6 +167,75 @@ def test_full_size_batch_properties(gpu_available):
     rng = np.random.default_rng(0)
     idx = rng.choice(len(roles), 200, replace=False)
     ref = oracle_solve(O.gear_pwa_system(800.0), O.Cfg(), N, params[idx], roles[idx])
+    for j, r in zip(idx, ref):
+        assert list(reg[j]) == list(r.sigma)
+        assert abs(float(a["cost"][j]) - r.cost) <= 1e-9 * max(1.0, abs(r.cost))
+        assert np.abs(u[j] - r.u).max() <= 1e-6
+
+
+def test_branch_and_bound_equals_enumeration_at_bench_size(gpu_available):
+    """configs[1] at bench size through both searches: the same sequence for every one of the
+    163,840 local MIQPs, costs and trajectories equal to rounding."""
+    import torch
+
+    import bench
+
+    n, S = 10, 16384
+    params, roles = bench.make_inputs(range(S), n, N)
+    dev = torch.device("cuda", 0)
+    tp, tr = torch.from_numpy(params).to(dev), torch.from_numpy(roles).to(dev)
+    ts = torch.zeros(len(roles), dtype=torch.int32, device=dev)
+    a = _solver([_gear_system()], method=1).solve_device(ts, tr, tp)
+    b = _solver([_gear_system()], method=2).solve_device(ts, tr, tp)
+    torch.cuda.synchronize()
+    assert (a["status"] == 0).all() and (b["status"] == 0).all()
+    assert torch.equal(a["region"], b["region"])
+    assert torch.equal(a["gear"], b["gear"])
+    rel = ((a["cost"] - b["cost"]).abs() / a["cost"].abs().clamp(min=1.0)).max().item()
+    assert rel <= 1e-12
+    assert (a["u"] - b["u"]).abs().max().item() <= 1e-9
+    # branch and bound must solve far fewer QPs than there are sequences
+    assert b["nodes"].double().mean().item() < 0.6 * a["nodes"].double().mean().item()
+
+
+@pytest.mark.parametrize("n,NN", [(10, 10), (5, 15)])
+def test_sweep_horizons_full_batch(gpu_available, n, NN):
+    """C5 sweep horizons at a throughput-size batch: deterministic, every instance optimal and
+    feasible for the MLD constraints, and a sample equal to the oracle's branch and bound."""
+    import torch
+
+    import bench
+
+    S = 2048
+    s = _solver([_gear_system()], N=NN)
+    params, roles = bench.make_inputs(range(S), n, NN)
+    dev = torch.device("cuda", 0)
+    tp, tr = torch.from_numpy(params).to(dev), torch.from_numpy(roles).to(dev)
+    ts = torch.zeros(len(roles), dtype=torch.int32, device=dev)
+    a = s.solve_device(ts, tr, tp)
+    b = s.solve_device(ts, tr, tp)
+    torch.cuda.synchronize()
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
+    assert (a["status"] == 0).all()
+    u, x, reg = a["u"].cpu().numpy(), a["x"].cpu().numpy(), a["region"].cpu().numpy()
+    assert np.abs(u).max() <= 1 + 1e-9
+    v = x[:, 1, :]
+    dv = np.diff(v, axis=1)
+    assert dv.min() >= -2 - 1e-9 and dv.max() <= 2.5 + 1e-9
+    lim = np.array([-np.inf, 9.235, 12.855, 16.93, 22.92, 23.315, 32.47, np.inf])
+    vk = v[:, :NN]
+    assert np.all(vk >= lim[reg] - 1e-7) and np.all(vk <= lim[reg + 1] + 1e-7)
+    g = O.gear_pwa_system(800.0)
+    pred = g["A"][reg, 1, 1] * vk + g["B"][reg, 1] * u + g["c"][reg, 1]
+    assert np.abs(pred - v[:, 1:]).max() <= 1e-9
+    rng = np.random.default_rng(1)
+    idx = rng.choice(len(roles), 40, replace=False)
+    O.set_method(O.METHOD_BNB)
+    try:
+        ref = oracle_solve(O.gear_pwa_system(800.0), O.Cfg(), NN, params[idx], roles[idx])
+    finally:
+        O.set_method(O.METHOD_ENUMERATE)
     for j, r in zip(idx, ref):
         assert list(reg[j]) == list(r.sigma)
         assert abs(float(a["cost"][j]) - r.cost) <= 1e-9 * max(1.0, abs(r.cost))

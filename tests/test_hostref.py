@@ -55,7 +55,10 @@ def test_lane_algorithm_matches_golden(hostref, name, solver):
         pytest.xfail("interior point alone stalls at degenerate vertices (the fixture's purpose); "
                      "it is only the fallback of the active-set method")
     fx = load(name)
+    if int(fx["N"]) > 8:
+        pytest.skip("beyond exhaustive enumeration (HVP_MAX_N_ENUM): branch and bound only")
     prob, systems = product_problem(fx)
+    prob.method = 1  # HVP_METHOD_ENUMERATE
     hostref.hvp_hostref_set_solver(1 if solver == "active_set" else 0)
     try:
         out = run(hostref, prob, systems, fx)
@@ -63,12 +66,34 @@ def test_lane_algorithm_matches_golden(hostref, name, solver):
         hostref.hvp_hostref_set_solver(1)
     ok = fx["exp_status"] == 0
     assert np.array_equal(out["status"], fx["exp_status"])
-    assert np.array_equal(out["nodes"], fx["exp_nodes"])
+    if int(fx.get("method", 0)) == 0:
+        assert np.array_equal(out["nodes"], fx["exp_nodes"])
     assert np.array_equal(out["region"][ok], fx["exp_region"][ok])
     c, ce = out["cost"][ok], fx["exp_cost"][ok]
     assert np.all(np.abs(c - ce) <= 1e-9 * np.maximum(1, np.abs(ce)))
     assert np.abs(out["u"][ok] - fx["exp_u"][ok]).max() <= 1e-6
     assert np.abs(out["x"][ok] - fx["exp_x"][ok]).max() <= 1e-4
+
+
+@pytest.mark.parametrize("name", fixture_names())
+def test_branch_and_bound_matches_golden(hostref, name):
+    """Branch and bound over the region sequences (hvp_bnb.h, the product's K_bnb_* launches)
+    returns the same sequence, cost and trajectory as the oracle -- at N = 5 against exhaustive
+    enumeration, at N = 10 / 15 (C5 sweep) against the oracle's own branch and bound."""
+    fx = load(name)
+    prob, systems = product_problem(fx)
+    prob.method = 2  # HVP_METHOD_BNB
+    out = run(hostref, prob, systems, fx)
+    ok = fx["exp_status"] == 0
+    assert np.array_equal(out["status"], fx["exp_status"])
+    assert np.array_equal(out["region"][ok], fx["exp_region"][ok])
+    c, ce = out["cost"][ok], fx["exp_cost"][ok]
+    assert np.all(np.abs(c - ce) <= 1e-9 * np.maximum(1, np.abs(ce)))
+    assert np.abs(out["u"][ok] - fx["exp_u"][ok]).max() <= 1e-6
+    assert np.abs(out["x"][ok] - fx["exp_x"][ok]).max() <= 1e-4
+    # the search must prune: far fewer QPs than the sequences it decides between
+    if int(fx["N"]) <= 8 and int(fx.get("method", 0)) == 0:
+        assert out["nodes"][ok].mean() < fx["exp_nodes"][ok].mean() or int(fx["N"]) <= 4
 
 
 def test_active_set_rarely_falls_back(hostref):
@@ -82,7 +107,10 @@ def test_active_set_rarely_falls_back(hostref):
     runs = fails = 0
     for name in fixture_names():
         fx = load(name)
+        if int(fx["N"]) > 8:
+            continue
         prob, systems = product_problem(fx)
+        prob.method = 1  # every sequence through the lane QP (the statistic this test bounds)
         run(hostref, prob, systems, fx)
         hostref.hvp_hostref_gi_stats(st)
         runs += st[0]

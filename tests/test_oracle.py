@@ -239,3 +239,26 @@ def test_miqp_l1_vs_highs_milp(seed, veh):
     ref = _milp_l1(sysd, O.Cfg(), N, role, x0, xf, xb, xl)
     assert ora.status == 0 and ref.status == 0
     assert abs(ora.cost - ref.fun) <= 1e-6 * max(1.0, abs(ref.fun)), (ora.cost, ref.fun)
+
+
+@pytest.mark.parametrize("n,N,seed", [(4, 5, 0), (4, 6, 1), (3, 7, 2), (10, 5, 3)])
+def test_oracle_branch_and_bound_equals_enumeration(n, N, seed):
+    """The oracle's branch and bound (used for the N = 10 / 15 sweep fixtures, where exhaustive
+    enumeration needs ~1e4 .. 1e6 QPs per vehicle) returns exactly what its exhaustive
+    enumeration returns: same sequence (tie rule included), same cost, same trajectory."""
+    sysd = O.gear_pwa_system(800.0)
+    params, roles = decent_instances(O.env_initial_state(n, seed), N, leader_window(N))
+    for p, r in zip(params, roles):
+        x0, xf, xb, xl = split_params(p, N)
+        O.set_method(O.METHOD_ENUMERATE)
+        a = O.solve_miqp(sysd, O.Cfg(), N, int(r), x0, xf, xb, xl)
+        O.set_method(O.METHOD_BNB)
+        try:
+            b = O.solve_miqp(sysd, O.Cfg(), N, int(r), x0, xf, xb, xl)
+        finally:
+            O.set_method(O.METHOD_ENUMERATE)
+        assert a.status == b.status == 0
+        assert list(a.sigma) == list(b.sigma)
+        assert abs(a.cost - b.cost) <= 1e-10 * max(1.0, abs(a.cost))
+        assert np.abs(a.u - b.u).max() <= 1e-7
+        assert b.n_candidates < a.n_candidates or N <= 5
