@@ -47,12 +47,12 @@ def profiled(kernel: str):
     (profiles/run_profiles.sh runs this bench at its default workload under rocprofv3)."""
     import glob
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_summary.json")))
-    if not files:
-        return None, None
-    with open(files[-1]) as f:
-        d = json.load(f)["kernels"].get(kernel)
-    return (d, os.path.relpath(files[-1], ROOT)) if d else (None, None)
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_summary.json")), reverse=True):
+        with open(path) as f:
+            d = json.load(f)["kernels"].get(kernel)
+        if d:
+            return d, os.path.relpath(path, ROOT)
+    return None, None
 
 
 def make_inputs(seeds, n: int, N: int):
@@ -198,20 +198,35 @@ def main() -> None:
     ok = bool((out["status"] == 0).all().item())
     steps_total = S * world * args.steps
     value = steps_total / dt
-    qp_avg_ms = float(np.mean(qp_ms))
-    cand_per_launch = cand / args.steps
-    alg_bytes = cand_per_launch * dense_qp_bytes(N) + B * instance_io_bytes(N)
-    achieved = alg_bytes / (qp_avg_ms * 1e-3) / 1e9
-    prof, prof_src = profiled("k_qp_gi")
-    traffic = prof.get("hbm_bytes") if prof else None
-    fp64 = None
-    if prof and prof.get("f64_flop"):
-        tf = prof["f64_flop"] / (qp_avg_ms * 1e-3) / 1e12
+    bnb = method != 1
+    # QP time per step: K_qp_gi (enumeration) or K_bnb_root + the N K_bnb_bound launches (B&B),
+    # each bracketed by HIP events the library records on the solve stream
+    qp_step_ms = float(np.mean(qp_ms))
+    launches = (N + 1) if bnb else 1
+    qp_avg_ms = qp_step_ms / launches
+    cand_per_step = cand / args.steps
+    alg_bytes = cand_per_step * dense_qp_bytes(N) + B * instance_io_bytes(N)
+    achieved = alg_bytes / (qp_step_ms * 1e-3) / 1e9
+    traffic, flop, fp64, prof_src = None, None, None, None
+    if (n, N) == (10, 5):  # the committed PMC summary (profiles/) is of the default workload
+        if bnb:
+            pb, prof_src = profiled("k_bnb_bound")
+            pr, _ = profiled("k_bnb_root")
+            if pb and pr and "hbm_bytes" in pb and "hbm_bytes" in pr:
+                traffic = pb["hbm_bytes"] * N + pr["hbm_bytes"]
+                if pb.get("f64_flop") and pr.get("f64_flop"):
+                    flop = pb["f64_flop"] * N + pr["f64_flop"]
+        else:
+            prof, prof_src = profiled("k_qp_gi")
+            if prof:
+                traffic, flop = prof.get("hbm_bytes"), prof.get("f64_flop")
+    if traffic is not None and flop:
+        tf = flop / (qp_step_ms * 1e-3) / 1e12
         fp64 = {"achieved": tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tf / FP64_PEAK_TFLOPS,
-                "flop_per_launch": prof["f64_flop"], "source": prof_src}
+                "flop_per_step": flop, "source": prof_src}
 
     result = {
-        "metric": "MPC timesteps/sec (whole platoon) at n=10 N=5 decent_mld",
+        "metric": f"MPC timesteps/sec (whole platoon) at n={n} N={N} decent_mld",
         "value": value,
         "unit": "platoon-timesteps/s",
         "n_gpus": world,
@@ -224,19 +239,23 @@ def main() -> None:
         "dtype": "f64",
         "data": "synthetic: env.reset random-init platoon states (seeded), constant-velocity neighbour "
                 "predictions, constant-velocity leader",
-        "config": {"workload": "fleet_decent_mld n=10 N=5 pwa_gear (configs[1])", "n_vehicles": n, "horizon": N,
+        "config": {"workload": (f"fleet_decent_mld n={n} N={N} pwa_gear"
+                                + (" (configs[1])" if (n, N) == (10, 5) else " (configs[4] sweep point)")),
+                   "n_vehicles": n, "horizon": N, "search": "branch-and-bound" if bnb else "enumeration",
                    "platoons_per_gpu": S, "local_miqps_per_step": B * world, "parallelism": f"seeds-sharded x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "k_qp_gi", "kernel_avg_ms": qp_avg_ms,
-                     "algorithmic_bytes_per_launch": alg_bytes, "traffic_source": prof_src,
-                     "note": "achieved = SURVEY 8(d) notional dense-QP bytes (13104 B per sequence at N=5) + "
-                             "instance I/O, per K_qp_gi launch / its HIP-event time. The kernel never "
-                             "materialises those matrices (QPs are built in registers from a 38-double "
-                             "instance block), so frac can exceed 1; traffic = measured HBM bytes "
-                             "(2*FETCH_SIZE + WRITE_SIZE). See DESIGN.md 'Roofline'."},
+                     "kernel": "k_bnb_root+k_bnb_bound" if bnb else "k_qp_gi", "kernel_avg_ms": qp_avg_ms,
+                     "launches_per_step": launches, "qp_ms_per_step": qp_step_ms,
+                     "algorithmic_bytes_per_step": alg_bytes, "traffic_source": prof_src,
+                     "note": "achieved = SURVEY 8(d) notional dense-QP bytes (8(n_w^2+m n_w+m+n_w) per QP solved) "
+                             "+ instance I/O, per step / the HIP-event time of the QP launches of the step "
+                             "(per-launch average = kernel_avg_ms). The kernels never materialise those "
+                             "matrices (QPs are built in registers from the instance block), so frac can "
+                             "exceed 1; traffic = measured HBM bytes of the same launches per step "
+                             "(2*FETCH_SIZE + WRITE_SIZE, profiles/). See DESIGN.md 'Roofline'."},
         "fp64": fp64,
-        "candidates_per_step": cand_per_launch,
+        "qps_per_step": cand_per_step,
         "qp_iters_per_candidate": iters / max(cand, 1),
         "ipm_fallbacks_per_step": fallback / args.steps,
         "all_optimal": ok,

@@ -33,7 +33,8 @@ def per_kernel(path: str) -> dict:
 
 
 def short(name: str) -> str:
-    for k in ("k_qp_gi", "k_qp_ipm", "k_enum", "k_cost", "k_select"):
+    for k in ("k_qp_gi", "k_qp_ipm", "k_enum", "k_cost", "k_select", "k_bnb_root", "k_bnb_expand", "k_bnb_bound",
+              "k_bnb_key", "k_bnb_write", "k_bnb_finish"):
         if k in name:
             return k
     return name[:48]

@@ -29,7 +29,9 @@ def test_local_mpc_solve_mpc_matches_oracle(gpu_available):
     assert u0.shape == (1, 1) and info["u"].shape == (1, N) and info["x"].shape == (2, N + 1)
     assert np.abs(info["u"][0] - ref.u).max() <= 1e-6
     assert abs(info["cost"] - ref.cost) <= 1e-9 * abs(ref.cost)
-    assert info["bin_vars"] == 7 * N and info["nodes"] == ref.n_candidates and info["run_time"] > 0
+    # nodes: QPs of the branch-and-bound search (Gurobi NodeCount analogue), far below the
+    # number of sequences an exhaustive search would solve
+    assert info["bin_vars"] == 7 * N and 0 < info["nodes"] < ref.n_candidates and info["run_time"] > 0
     assert list(m.gears_pred[0].astype(int)) == [PwaGearVehicle.REGION_GEAR[r] for r in ref.sigma]
 
 
