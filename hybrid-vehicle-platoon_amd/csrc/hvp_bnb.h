@@ -7,7 +7,7 @@
 // and ~1e6 at N = 15 (C5 sweep).  This header holds the tree logic shared by the gfx950 kernels
 // (hvp_kernels.hip) and the test-only host build (hvp_hostref.cpp):
 //
-//   node      a region prefix sigma_0..sigma_{k-1} (3 bits per step, step j at bits 3j) with the
+//   node      a region prefix sigma_0..sigma_{k-1} (4 bits per step, step j at bits 4j) with the
 //             exact interval [lo, hi] of v_k reachable under that prefix (reach_step).
 //   bound     the QP of the prefix with the tail RELAXED (setup_lane(.., K = k)): steps >= k
 //             keep the state box, acceleration rows, tracking and safe-distance terms, but
@@ -40,7 +40,7 @@ HVP_HD inline bool bnb_pruned(double lb, double inc) { return lb > inc + kPruneR
 // the enumeration order of enumerate_sequences.
 HVP_HD inline uint64_t bnb_lexkey(uint64_t code, int N) {
     uint64_t key = 0;
-    for (int k = 0; k < N; ++k) key = (key << 3) | ((code >> (3 * k)) & 7u);
+    for (int k = 0; k < N; ++k) key = (key << kCodeBits) | (uint64_t)code_region(code, k);
     return key;
 }
 
@@ -75,7 +75,7 @@ HVP_HD inline bool bnb_dive(const hvp_system& S, const Consts& C, double v0, con
             if (d < bd) { bd = d; best = r; blo = nlo; bhi = nhi; }
         }
         if (best < 0) return false;
-        code |= (uint64_t)best << (3 * k);
+        code = code_with(code, k, best);
         lo = blo;
         hi = bhi;
     }

@@ -130,7 +130,7 @@ void solve_one(const hvp_system& S, const hvp::Consts& C, int role, const double
     x[N + 1] = v0;
     double p = p0, v = v0;
     for (int k = 0; k < N; ++k) {
-        const int r = (c.code >> (3 * k)) & 7;
+        const int r = hvp::code_region(c.code, k);
         region[k] = (int8_t)r;
         const double vn = c.y[k];
         u[k] = (vn - S.a[r] * v - S.c[r]) / S.b[r];
@@ -192,7 +192,7 @@ void solve_one_bnb(const hvp_system& S, const hvp::Consts& C, int role, const do
             for (int r = 0; r < S.n_regions; ++r) {
                 Node c;
                 if (!hvp::bnb_child(S, C, k - 1, p.lo, p.hi, r, &c.lo, &c.hi)) continue;
-                c.code = p.code | ((uint64_t)r << (3 * (k - 1)));
+                c.code = hvp::code_with(p.code, k - 1, r);
                 nxt.push_back(c);
             }
         }
@@ -229,7 +229,7 @@ void solve_one_bnb(const hvp_system& S, const hvp::Consts& C, int role, const do
     x[N + 1] = v0;
     double p = prm[0], v = v0;
     for (int k = 0; k < N; ++k) {
-        const int r = (c.code >> (3 * k)) & 7;
+        const int r = hvp::code_region(c.code, k);
         region[k] = (int8_t)r;
         const double vn = c.y[k];
         u[k] = (vn - S.a[r] * v - S.c[r]) / S.b[r];

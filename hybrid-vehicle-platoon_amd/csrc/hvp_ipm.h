@@ -60,6 +60,14 @@ struct QpOut {
 // packed lower-triangular index
 HVP_HD constexpr int tri(int i, int j) { return i * (i + 1) / 2 + j; }
 
+// Region sequence codes: 4 bits per step (HVP_MAX_REGIONS = 16 modes), step k at bits 4k.
+constexpr int kCodeBits = 4;
+constexpr uint32_t kCodeMask = (1u << kCodeBits) - 1u;
+HVP_HD constexpr int code_region(uint64_t code, int k) { return (int)((code >> (kCodeBits * k)) & kCodeMask); }
+HVP_HD constexpr uint64_t code_with(uint64_t code, int k, int r) {
+    return (code & ~((uint64_t)kCodeMask << (kCodeBits * k))) | ((uint64_t)r << (kCodeBits * k));
+}
+
 // Refined hardware reciprocal: v_rcp_f64 estimate + two Newton steps (full double accuracy
 // in 1 + 4 FMA instead of the ~12-instruction IEEE division sequence).
 HVP_HD inline double frcp(double x) {
@@ -781,7 +789,7 @@ HVP_HD inline bool setup_lane(LaneQp<N, M>& q, const hvp_system& S, const Consts
         // steps k >= K are RELAXED (branch-and-bound bound problem): their region is free, so
         // the input rows are dropped (inert bounds) and so is their input cost (>= 0) below;
         // what remains is a valid lower bound of every completion of the fixed prefix.
-        const int r = (code >> (3 * k)) & 7;
+        const int r = code_region(code, k);
         const bool fixed = k < K;
         a[k] = fixed ? S.a[r] : 1.0;
         b[k] = fixed ? S.b[r] : 1.0;
@@ -791,7 +799,7 @@ HVP_HD inline bool setup_lane(LaneQp<N, M>& q, const hvp_system& S, const Consts
         q.mem.set(F_UHI, k, fixed ? c[k] + b[k] * S.umax : 1e30);
         // bounds on v_{k+1}: region sigma_{k+1} (if fixed) intersected with the state box
         if (k + 1 < K) {
-            const int r1 = (code >> (3 * (k + 1))) & 7;
+            const int r1 = code_region(code, k + 1);
             q.mem.set(F_VLO, k, fmax(S.vmin, S.vlo[r1]));
             q.mem.set(F_VHI, k, fmin(S.vmax, S.vhi[r1]));
         } else {
@@ -949,7 +957,7 @@ HVP_HD inline double direct_cost(const LaneQp<N, M>& q, const hvp_system& S_in, 
         if (q.has_sf) J += C.w * fmax(0.0, p - xf[k] + C.d_safe);
         if (q.has_sb) J += C.w * fmax(0.0, xb[k] + C.d_safe - p);
         if (k < N) {
-            const int r = (code >> (3 * k)) & 7;
+            const int r = code_region(code, k);
             const double vn = q.y[k];
             const double u = (vn - S.a[r] * v - S.c[r]) / S.b[r];
             if (k < K) J += C.Qu * u * u;  // relaxed steps carry no input cost
@@ -1023,7 +1031,7 @@ HVP_HD inline int enumerate_sequences(const hvp_system& S, const Consts& C, doub
                             &nlo, &nhi))
                 continue;
             reg[k] = r;
-            code = (code & ~(7u << (3 * k))) | ((uint32_t)r << (3 * k));
+            code = (uint32_t)code_with(code, k, r);
             lo[k + 1] = nlo;
             hi[k + 1] = nhi;
             advanced = true;

@@ -7,7 +7,7 @@
 //   K_enum   one thread per instance: depth-first enumeration of the velocity-feasible region
 //            sequences (exact interval reachability), reservation of a contiguous slice of the
 //            global candidate list with ONE atomicAdd per instance, and the candidate codes
-//            (3 bits per step) written in lexicographic order.
+//            (4 bits per step) written in lexicographic order.
 //   K_qp     one LANE per candidate (instance, sigma): the condensed velocity-space QP is built
 //            and solved by a Mehrotra IPM entirely in registers (hvp_ipm.h); writes cost, status,
 //            iteration count and v_1..v_N.  Grid-stride over the candidate count read on the
@@ -70,7 +70,7 @@ struct Workspace {
     // branch and bound (hvp_bnb.h): two node lists (parents / children of a level, ping-pong),
     // per-instance incumbent and winner key
     int32_t* nd_inst[2] = {nullptr, nullptr};    // [cap] owning instance (-1: dead)
-    uint64_t* nd_code[2] = {nullptr, nullptr};   // [cap] region prefix, 3 bits per step
+    uint64_t* nd_code[2] = {nullptr, nullptr};   // [cap] region prefix, 4 bits per step
     double* nd_lo[2] = {nullptr, nullptr};       // [cap] reachable interval of v_depth
     double* nd_hi[2] = {nullptr, nullptr};
     double* nd_lb[2] = {nullptr, nullptr};       // [cap] bound (relaxed QP) or leaf cost
@@ -319,7 +319,7 @@ __global__ __launch_bounds__(kBlock) void k_select(int B, const hvp_system* __re
     }
 #pragma unroll
     for (int k = 0; k < N; ++k) {
-        const int r = (code >> (3 * k)) & 7;
+        const int r = hvp::code_region(code, k);
         const double vn = win >= 0 ? ws.task_y[(size_t)win * N + k] : v;
         const double u = win >= 0 ? (vn - S.a[r] * v - S.c[r]) / S.b[r] : 0.0;
         p = p + S.ts * v;
@@ -443,7 +443,7 @@ __global__ __launch_bounds__(kBlock) void k_bnb_expand(int k, const hvp_system* 
             double a, b;
             hvp::bnb_child(S, C, k - 1, lo, hi, r, &a, &b);
             ws.nd_inst[dst][off + j] = inst;
-            ws.nd_code[dst][off + j] = code | ((uint64_t)r << (3 * (k - 1)));
+            ws.nd_code[dst][off + j] = hvp::code_with(code, k - 1, r);
             ws.nd_lo[dst][off + j] = a;
             ws.nd_hi[dst][off + j] = b;
             ws.nd_lb[dst][off + j] = plb;  // inherited: kept by a leaf whose QP fails
@@ -534,7 +534,7 @@ __device__ inline void write_solution(int i, const hvp_system& S, const double* 
     }
 #pragma unroll
     for (int k = 0; k < N; ++k) {
-        const int r = (code >> (3 * k)) & 7;
+        const int r = hvp::code_region(code, k);
         const double vn = win ? y[k] : v;
         const double u = win ? (vn - S.a[r] * v - S.c[r]) / S.b[r] : 0.0;
         p = p + S.ts * v;
@@ -602,6 +602,64 @@ __global__ __launch_bounds__(kBlock) void k_bnb_finish(int B, const hvp_system* 
         write_solution<N>(i, systems[sys[i]], params + (size_t)i * (2 + 6 * (N + 1)), false, 0, nullptr, u_out, x_out,
                           region_out, gear_out);
     }
+}
+
+// ================================================================== fixed-control evaluation
+// MpcGear.evaluate_cost (mpcs/mpc_gear.py:137-170): with u (u_g for the gear model) and the
+// gear of every step fixed, the MIQP has no free decision left but the slacks: the trajectory
+// follows from the dynamics of the mode (gear label, region band containing v_k -- at a shared
+// band edge the PWA dynamics coincide), the slacks take max(0, .), and the objective is the
+// direct cost of that trajectory.  Status HVP_INFEASIBLE when a row of the MLD model fails.
+template <int N>
+__global__ __launch_bounds__(kBlock) void k_evaluate(int B, const hvp_system* __restrict__ systems,
+                                                     const int32_t* __restrict__ sys, const int32_t* __restrict__ role,
+                                                     const double* __restrict__ params, hvp::Consts C,
+                                                     const int8_t* __restrict__ gear_in, const double* __restrict__ u_in,
+                                                     double* __restrict__ cost_out, int32_t* __restrict__ status_out,
+                                                     double* __restrict__ x_out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B) return;
+    const hvp_system& S = systems[sys[i]];
+    const int rl = role[i];
+    const double* prm = params + (size_t)i * (2 + 6 * (N + 1));
+    hvp::LaneQp<N> q;
+    q.has_sf = (rl & HVP_ROLE_SAFE_FRONT) != 0;
+    q.has_sb = (rl & HVP_ROLE_SAFE_BACK) != 0;
+    double p = prm[0], v = prm[1];
+    uint64_t code = 0;
+    bool ok = true;
+    if (x_out) {
+        x_out[(size_t)i * 2 * (N + 1)] = p;
+        x_out[(size_t)i * 2 * (N + 1) + N + 1] = v;
+    }
+    for (int k = 0; k < N; ++k) {
+        const int g = gear_in[(size_t)i * N + k];
+        const double u = u_in[(size_t)i * N + k];
+        int r = -1;
+        for (int m = 0; m < S.n_regions && r < 0; ++m) {
+            const double tol = 1e-9 * (1.0 + fabs(v));
+            if (S.gear[m] == g && v >= S.vlo[m] - tol && v <= S.vhi[m] + tol) r = m;
+        }
+        if (r < 0) { ok = false; r = 0; }
+        const double vn = S.a[r] * v + S.b[r] * u + S.c[r];
+        const double tolu = 1e-9 * (1.0 + fabs(u));
+        if (u < S.umin - tolu || u > S.umax + tolu) ok = false;
+        const double dv = vn - v, tola = 1e-9 * (1.0 + fabs(dv));
+        if (dv < C.dec[k] - tola || dv > C.acc[k] + tola) ok = false;
+        p = p + S.ts * v;
+        v = vn;
+        const double tolv = 1e-9 * (1.0 + fabs(v)), tolp = 1e-9 * (1.0 + fabs(p));
+        if (v < S.vmin - tolv || v > S.vmax + tolv || p < S.pmin - tolp || p > S.pmax + tolp) ok = false;
+        q.y[k] = v;
+        code = hvp::code_with(code, k, r);
+        if (x_out) {
+            x_out[(size_t)i * 2 * (N + 1) + k + 1] = p;
+            x_out[(size_t)i * 2 * (N + 1) + N + 1 + k + 1] = v;
+        }
+    }
+    const double cost = hvp::direct_cost<N>(q, S, C, rl, prm, code);
+    cost_out[i] = ok ? cost : 1e300;
+    status_out[i] = ok ? HVP_OPTIMAL : HVP_INFEASIBLE;
 }
 
 int grid_for(long long n) { return (int)std::max<long long>(1, (n + kBlock - 1) / kBlock); }
@@ -869,6 +927,29 @@ int hvp_solve_batch(hvp_handle* h, int B, const int32_t* sys, const int32_t* rol
 #undef HVP_CASE
         default: return fail(HVP_E_UNSUPPORTED, "hvp_solve_batch: unsupported N");
     }
+}
+
+int hvp_evaluate_batch(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, const double* params,
+                       const int8_t* gear_in, const double* u_in, double* cost_out, int32_t* status_out, double* x_out,
+                       void* stream) {
+    if (!h || B < 0 || (B > 0 && (!sys || !role || !params || !gear_in || !u_in || !cost_out || !status_out)))
+        return fail(HVP_E_ARG, "hvp_evaluate_batch: bad argument");
+    if (B == 0) return 0;
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t st = (hipStream_t)stream;
+    switch (h->prob.N) {
+#define HVP_CASE(n)                                                                                              \
+    case n:                                                                                                      \
+        hipLaunchKernelGGL(k_evaluate<n>, dim3(grid_for(B)), dim3(kBlock), 0, st, B, h->d_sys, sys, role, params, \
+                           h->C, gear_in, u_in, cost_out, status_out, x_out);                                    \
+        break;
+        HVP_CASE(2) HVP_CASE(3) HVP_CASE(4) HVP_CASE(5) HVP_CASE(6) HVP_CASE(7) HVP_CASE(8)
+        HVP_CASE(9) HVP_CASE(10) HVP_CASE(11) HVP_CASE(12) HVP_CASE(13) HVP_CASE(14) HVP_CASE(15) HVP_CASE(16)
+#undef HVP_CASE
+        default: return fail(HVP_E_UNSUPPORTED, "hvp_evaluate_batch: unsupported N");
+    }
+    HIP_TRY(hipGetLastError());
+    return 0;
 }
 
 int hvp_sync(hvp_handle* h, void* stream) {

@@ -9,7 +9,7 @@ from __future__ import annotations
 import ctypes
 import os
 
-MAX_REGIONS = 8
+MAX_REGIONS = 16
 MAX_N = 16
 MAX_N_ENUM = 8
 ABI_VERSION = 2
@@ -106,6 +106,7 @@ EXPORTS = {
     "hvp_solve_batch": ([_P, ctypes.c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
     "hvp_solve_batch_host": ([_P, ctypes.c_int, _I32P, _I32P, _DP, _DP, _DP, _I8P, _I8P, _DP, _I32P, _I32P,
                               _I32P], ctypes.c_int),
+    "hvp_evaluate_batch": ([_P, ctypes.c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
     "hvp_sync": ([_P, _P], ctypes.c_int),
     "hvp_get_stats": ([_P, ctypes.POINTER(HvpStats)], ctypes.c_int),
     "hvp_destroy": ([_P], None),

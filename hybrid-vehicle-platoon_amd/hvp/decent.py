@@ -22,7 +22,7 @@ from .agent import MldAgent
 from .batched import extrapolate
 from .env import EpisodeMonitor, PlatoonEnv
 from .models import Platoon, Vehicle
-from .mpc import LocalMpcMld
+from .mpc import LocalMpcGear, LocalMpcMld
 from .params import Params, Sim
 from .solver import BatchSolver
 from .tables import gears_of
@@ -65,6 +65,8 @@ class TrackingDecentMldCoordinator(MldAgent):
             ui, info = a.mpc.absorb(res, i, dt, raises, x[i])
             a.record(info)
             u.append(ui)
+        if u[0].shape[0] > self.nu_l:  # gear MPCs: continuous controls first, then the gears (:318-324)
+            return np.vstack((np.vstack([ui[: self.nu_l] for ui in u]), np.vstack([ui[self.nu_l:] for ui in u]))), {}
         return np.vstack(u), {}
 
     # ------------------------------------------------------------ hooks
@@ -112,8 +114,9 @@ def simulate(sim: Sim, save: bool = False, plot: bool = False, seed: int = 2, th
     n, N, ep_len, ts = sim.n, sim.N, sim.ep_len, Params.ts
     leader_x = sim.leader_trajectory.get_leader_trajectory()
     platoon = Platoon(n, vehicle_type=sim.vehicle_model_type, masses=sim.masses)
-    if sim.vehicle_model_type != "pwa_gear":
-        raise NotImplementedError("the decentralised GPU path implements the pwa_gear model (LocalMpcMld)")
+    if sim.vehicle_model_type not in ("pwa_gear", "pwa_friction"):
+        raise NotImplementedError("the GPU path implements the pwa_gear (LocalMpcMld) and pwa_friction "
+                                  "(LocalMpcGear) models; the nonlinear model is out of scope (DESIGN.md)")
     systems = platoon.get_vehicle_system_dicts(ts)
     env = EpisodeMonitor(
         PlatoonEnv(n=n, platoon=platoon, leader_trajectory=sim.leader_trajectory, spacing_policy=sim.spacing_policy,
@@ -122,12 +125,14 @@ def simulate(sim: Sim, save: bool = False, plot: bool = False, seed: int = 2, th
         max_episode_steps=ep_len,
     )
     vehicles = platoon.get_vehicles()
-    mpcs = [
-        LocalMpcMld(N, systems[i], sim.spacing_policy, is_front=i == 0, is_leader=i == leader_index,
-                    is_trailer=i == n - 1, thread_limit=thread_limit,
-                    real_vehicle_as_reference=sim.real_vehicle_as_reference, gears=gears_of(vehicles[i]))
-        for i in range(n)
-    ]
+    def local(i):
+        kw = dict(is_front=i == 0, is_leader=i == leader_index, is_trailer=i == n - 1, thread_limit=thread_limit,
+                  real_vehicle_as_reference=sim.real_vehicle_as_reference)
+        if sim.vehicle_model_type == "pwa_friction":  # fleet_decent_mld.py:532-533
+            return LocalMpcGear(N, systems[i], sim.spacing_policy, **kw)
+        return LocalMpcMld(N, systems[i], sim.spacing_policy, gears=gears_of(vehicles[i]), **kw)
+
+    mpcs = [local(i) for i in range(n)]
     agent = TrackingDecentMldCoordinator(mpcs, ep_len=ep_len, N=N, leader_x=leader_x, ts=ts,
                                          velocity_estimator=velocity_estimator, leader_index=leader_index)
     agent.evaluate(env=env, episodes=1, seed=seed)

@@ -4,6 +4,9 @@
                            ``__init__(system, N, thread_limit, constrain_first_state)``,
                            ``solve_mpc(state, raises) -> (u0, info)`` (called via
                            ``MldAgent.get_control``, fleet_decent_mld.py:316).
+* :class:`MpcGear`      <- mpcs/mpc_gear.py:8-170: MLD MPC with discrete gears scaling the
+                           throttle (``setup_gears``, ``solve_mpc -> [u_g0; gear0]``,
+                           ``evaluate_cost``); :class:`LocalMpcGear` <- fleet_decent_mld.py:226-253.
 * :class:`LocalMpcMld`  <- fleet_decent_mld.py:21-223: the decentralised local MPC with its
                            cost / constraints (``setup_cost_and_constraints`` :61-208) and the
                            parameter setters ``set_leader_x / set_x_front / set_x_back``
@@ -165,3 +168,104 @@ class LocalMpcMld(MpcMld):
 
     def set_x_back(self, x_back) -> None:
         self._set(1, x_back)
+
+
+class MpcGear(MpcMld):
+    """MLD MPC whose input is a throttle u_g scaled by a discrete gear (mpcs/mpc_gear.py:8-170).
+
+    The reference adds gear binaries sigma (6 per step) with u = sum_j sigma_j b_j u_g and the
+    gear's velocity window to the PWA model's region binaries; the GPU table enumerates the
+    (gear, region) modes instead (:func:`hvp.tables.gear_system_from_dict`), so one mode choice
+    per step carries both binary families and the same search / tie rule applies."""
+
+    def __init__(self, system: dict, N: int, thread_limit: int | None = None,
+                 constrain_first_state: bool = False) -> None:
+        MpcMld.__init__(self, system, N, thread_limit=thread_limit, constrain_first_state=constrain_first_state)
+        from .models import Vehicle
+
+        self.table = tables.gear_system_from_dict(system)
+        # delta (PWA regions) + sigma (gears) per step, as built by MpcMld + setup_gears
+        self.num_bin_vars = (len(system["S"]) + len(Vehicle.b)) * N
+        self.gears_ready = False
+
+    def setup_gears(self, N: int, F, G) -> None:
+        """mpcs/mpc_gear.py:30-114.  The control box F u_g <= G replaces F u <= G (:57-76)."""
+        F = np.asarray(F, dtype=float).reshape(-1)
+        G = np.asarray(G, dtype=float).reshape(-1)
+        lo, hi = -np.inf, np.inf
+        for f, g in zip(F, G):
+            if f > 0:
+                hi = min(hi, g / f)
+            elif f < 0:
+                lo = max(lo, g / f)
+        self.table.umin, self.table.umax = lo, hi
+        self.gears_ready = True
+
+    def solve_mpc(self, state, raises: bool = True):
+        """[u_g0; gear0] and info with info["u"] = vstack(u_g, gears) (mpc_gear.py:116-135)."""
+        if not self.gears_ready:
+            raise RuntimeError("setup_gears not called")
+        t0 = time.perf_counter()
+        res = self._solver().solve(np.zeros(1, np.int32), np.array([self.role], np.int32), self.params_for(state)[None])
+        return self.absorb(res, 0, time.perf_counter() - t0, raises, state)
+
+    def absorb(self, res, i: int, run_time: float, raises: bool, state=None):
+        """Solution i of a batch result as MpcGear.solve_mpc returns it."""
+        ok = int(res.status[i]) == _abi.OPTIMAL
+        if not ok and raises:
+            raise RuntimeWarning(f"gear mpc for state {state} is infeasible.")
+        _, info = MpcMld.absorb(self, res, i, run_time, False, state)
+        if ok:
+            u_g = res.u[i].reshape(1, -1).copy()
+            gears = res.gear[i].reshape(1, -1).astype(float)
+        else:
+            u_g = np.zeros((1, self.N))
+            gears = 6 * np.ones((1, self.N))  # default: all gears 6 (:129-131)
+        info["u"] = np.vstack((u_g, gears))
+        self.gears_pred = gears
+        return np.vstack((u_g[:, [0]], gears[:, [0]])), info
+
+    def evaluate_cost(self, x0, u, j=None):
+        """Cost of the fixed throttle u (1, N) and gears j (1, N) from x0 (mpc_gear.py:137-170);
+        the string 'inf' when infeasible, as the reference returns.  j=None: the gears of the
+        last solution (the reference leaves them free; its only use fixes them)."""
+        u = np.asarray(u, dtype=float)
+        if u.shape != (1, self.N):
+            raise ValueError(f"Expected u shape {(1, self.N)}. Got {u.shape}.")
+        if j is None:
+            if self.gears_pred is None:
+                raise ValueError("no gears given and no previous solution")
+            j = self.gears_pred
+        j = np.asarray(j).reshape(1, self.N).astype(np.int8)
+        out = self._solver().evaluate(np.zeros(1, np.int32), np.array([self.role], np.int32),
+                                      self.params_for(x0)[None], j, u)
+        return float(out["cost"][0]) if int(out["status"][0]) == _abi.OPTIMAL else "inf"
+
+
+class LocalMpcGear(LocalMpcMld, MpcGear):
+    """fleet_decent_mld.py:226-253: LocalMpcMld's cost / constraints on the gear MPC, with the
+    input cost on u_g."""
+
+    def __init__(
+        self,
+        N: int,
+        pwa_system: dict,
+        spacing_policy: SpacingPolicy = ConstantSpacingPolicy(50),
+        quadratic_cost: bool = True,
+        is_front: bool = False,
+        is_leader: bool = False,
+        is_trailer: bool = False,
+        thread_limit: int | None = None,
+        accel_cnstr_tightening: float = 0.0,
+        real_vehicle_as_reference: bool = False,
+    ) -> None:
+        MpcGear.__init__(self, pwa_system, N, thread_limit=thread_limit)
+        self.setup_gears(N, pwa_system["F"], pwa_system["G"])
+        self.setup_cost_and_constraints(None, spacing_policy, quadratic_cost, is_front, is_leader, is_trailer,
+                                        accel_cnstr_tightening, real_vehicle_as_reference)
+
+    def solve_mpc(self, state, raises: bool = True):
+        return MpcGear.solve_mpc(self, state, raises)
+
+    def absorb(self, res, i: int, run_time: float, raises: bool, state=None):
+        return MpcGear.absorb(self, res, i, run_time, raises, state)

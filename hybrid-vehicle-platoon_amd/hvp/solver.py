@@ -155,3 +155,39 @@ class BatchSolver:
             ctypes.c_void_p(stream.cuda_stream))
         _abi.check(rc, "hvp_solve_batch")
         return out
+
+    # -------------------------------------------------------------- fixed-control evaluation
+    def evaluate_device(self, sys_idx, roles, params, gears, u, stream=None) -> dict:
+        """Cost of fixed controls u (B, N) and gear labels (B, N) on the device (hvp_evaluate_batch:
+        MpcGear.evaluate_cost, mpcs/mpc_gear.py:137-170).  Returns cost, status, x."""
+        import torch
+
+        B = int(roles.shape[0])
+        dev = params.device
+        for name, t, dt in (("gears", gears, torch.int8), ("u", u, torch.float64)):
+            if not t.is_cuda or t.dtype != dt or not t.is_contiguous() or t.numel() != B * self.N:
+                raise ValueError(f"{name} must be a contiguous CUDA ({B}, {self.N}) tensor of dtype {dt}")
+        out = {"cost": torch.empty(B, dtype=torch.float64, device=dev),
+               "status": torch.empty(B, dtype=torch.int32, device=dev),
+               "x": torch.empty((B, 2, self.N + 1), dtype=torch.float64, device=dev)}
+        if stream is None:
+            stream = torch.cuda.current_stream(dev)
+        ptr = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        rc = self._lib.hvp_evaluate_batch(self._h, B, ptr(sys_idx), ptr(roles), ptr(params), ptr(gears), ptr(u),
+                                          ptr(out["cost"]), ptr(out["status"]), ptr(out["x"]),
+                                          ctypes.c_void_p(stream.cuda_stream))
+        _abi.check(rc, "hvp_evaluate_batch")
+        return out
+
+    def evaluate(self, sys_idx, roles, params, gears, u) -> dict:
+        """Host-array form of :meth:`evaluate_device` (synchronous)."""
+        import torch
+
+        dev = torch.device("cuda", self.device)
+        t = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a), dtype=dt).reshape(-1).to(dev)  # noqa: E731
+        B = len(np.asarray(roles).reshape(-1))
+        out = self.evaluate_device(t(sys_idx, torch.int32), t(roles, torch.int32),
+                                   t(params, torch.float64).reshape(B, -1), t(gears, torch.int8).reshape(B, self.N),
+                                   t(u, torch.float64).reshape(B, self.N))
+        torch.cuda.synchronize(dev)
+        return {k: v.cpu().numpy() for k, v in out.items()}

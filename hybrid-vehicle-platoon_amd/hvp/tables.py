@@ -76,6 +76,48 @@ def system_from_dict(sysd: dict, gears=None) -> _abi.HvpSystem:
     return out
 
 
+def gear_system_from_dict(sysd: dict, b=None, vl=None, vh=None) -> _abi.HvpSystem:
+    """Solver table of ``MpcGear.setup_gears`` (mpcs/mpc_gear.py:30-114) on a PWA system dict
+    (``pwa_friction``: fleet_decent_mld.py:226-253 ``LocalMpcGear``).
+
+    The MIQP has the PWA region binaries delta (2 friction regions) and the gear binaries sigma
+    (6 gears) per step; with both fixed it is the convex QP of one *mode* (region r, gear j):
+
+    * u = b_j * u_g (the four big-M rows of :75-96 with sigma_j = 1), so
+      v+ = a_r v + (B_r b_j) u_g + c_r;
+    * the control box F u <= G is moved onto u_g (:57-76), and the cost penalises u_g
+      (setup_cost_and_constraints(self.u_g, ...), fleet_decent_mld.py:241);
+    * gear j requires vl_j <= v_k <= vh_j (:98-110), region r its own velocity band.
+
+    So the table holds one entry per non-empty (gear, region) mode, band = gear band ∩ region
+    band, input gain B_r b_j and gear label j + 1 -- the search over modes is the search over
+    (delta, sigma).  Modes are ordered gear-major (gear 1 first), then by region.
+    """
+    from .models import Vehicle
+
+    b = list(Vehicle.b if b is None else b)
+    vl = list(Vehicle.vl if vl is None else vl)
+    vh = list(Vehicle.vh if vh is None else vh)
+    base = system_from_dict(sysd)
+    modes = []
+    for j in range(len(b)):
+        for r in range(base.n_regions):
+            lo, hi = max(vl[j], base.vlo[r]), min(vh[j], base.vhi[r])
+            if lo <= hi:
+                modes.append((j, r, lo, hi))
+    if len(modes) > _abi.MAX_REGIONS:
+        raise ValueError(f"{len(modes)} (gear, region) modes exceed {_abi.MAX_REGIONS}")
+    out = _abi.HvpSystem()
+    for f in ("ts", "pmin", "pmax", "vmin", "vmax", "umin", "umax"):
+        setattr(out, f, getattr(base, f))
+    out.n_regions = len(modes)
+    for m, (j, r, lo, hi) in enumerate(modes):
+        out.a[m], out.b[m], out.c[m] = base.a[r], base.b[r] * b[j], base.c[r]
+        out.vlo[m], out.vhi[m] = lo, hi
+        out.gear[m] = j + 1
+    return out
+
+
 def gears_of(vehicle) -> list[int]:
     """Gear label per region (PwaGearVehicle: the gear implied by each region)."""
     g = getattr(vehicle, "REGION_GEAR", None)

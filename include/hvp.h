@@ -39,7 +39,7 @@ extern "C" {
 #endif
 
 #define HVP_ABI_VERSION 2
-#define HVP_MAX_REGIONS 8
+#define HVP_MAX_REGIONS 16
 #define HVP_MAX_N 16     /* longest horizon (branch-and-bound path)            */
 #define HVP_MAX_N_ENUM 8 /* longest horizon of the exhaustive-enumeration path */
 
@@ -151,6 +151,15 @@ int hvp_solve_batch_host(hvp_handle* h, int B, const int32_t* sys, const int32_t
                          const double* params, double* u_out, double* x_out,
                          int8_t* region_out, int8_t* gear_out, double* cost_out,
                          int32_t* status_out, int32_t* nodes_out, int32_t* iters_out);
+/* Cost of FIXED controls (device pointers, async on stream): replaces MpcGear.evaluate_cost
+ * (mpcs/mpc_gear.py:137-170).  gear_in[B][N] = gear label per step (for the 7-region gear model
+ * the label of the region the velocity lies in), u_in[B][N] = the control (u_g for the gear
+ * model).  cost_out = objective of the resulting trajectory with optimal slacks, status_out =
+ * HVP_OPTIMAL or HVP_INFEASIBLE (a constraint of the MLD model is violated; the reference returns
+ * the string 'inf').  x_out[B][2][N+1] (may be NULL) receives the trajectory. */
+int hvp_evaluate_batch(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, const double* params,
+                       const int8_t* gear_in, const double* u_in, double* cost_out, int32_t* status_out,
+                       double* x_out, void* stream);
 int hvp_sync(hvp_handle* h, void* stream);
 int hvp_get_stats(hvp_handle* h, hvp_stats* out); /* synchronises the handle's last stream */
 void hvp_destroy(hvp_handle* h);

@@ -35,7 +35,7 @@
 #include <string.h>
 
 #define OR_MAX_N 16
-#define OR_MAX_REG 8
+#define OR_MAX_REG 16
 #define OR_MAX_NZ 200
 #define OR_MAX_EQ 40
 #define OR_MAX_M 420

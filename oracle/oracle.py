@@ -100,6 +100,43 @@ def friction_pwa_system(mass: float, ts: float = 1.0) -> dict:
     return dict(S=S, R=np.zeros((2, 2)), T=T, A=A, B=B, c=c, D=D, E=E, F=F, G=G, gear=np.array([1, 2]))
 
 
+def gear_friction_mld_system(mass: float, ts: float = 1.0) -> dict:
+    """MpcGear's MIQP (mpcs/mpc_gear.py:30-114) on the pwa_friction model, restated as one PWA
+    mode per (gear j, friction region r) with both binary families fixed:
+
+    * u = sum_j b_j with b_j = sigma_j * Vehicle.b[j] * u_g (big-M rows :75-96) -> with
+      sigma_j = 1 the velocity row reads v+ = A_r v + B_r Vehicle.b[j] u_g + c_r;
+    * the control box F u <= G is replaced by F u_g <= G (:57-76), and the cost is on u_g
+      (fleet_decent_mld.py:241 passes self.u_g to setup_cost_and_constraints);
+    * sigma_j = 1 only if vl_j <= v_k <= vh_j (:98-110): two more region rows.
+
+    Region rows per mode = the friction region's 2 rows + the gear's 2 rows.  Modes whose rows
+    are jointly infeasible are dropped; order: gear-major, then friction region.  ``gear`` gives
+    the gear label of each mode, ``friction`` its friction region."""
+    fr = friction_pwa_system(mass, ts)
+    S, T, A, B, c, gear, fric = [], [], [], [], [], [], []
+    for j in range(6):
+        for r in range(2):
+            lo, hi = _VL[j], _VH[j]
+            if r == 0:
+                hi = min(hi, fr["T"][0][0])
+            else:
+                lo = max(lo, -fr["T"][1][1])
+            if lo > hi:
+                continue
+            S.append(np.vstack([fr["S"][r], [[0, 1], [0, -1]]]))
+            T.append(np.concatenate([fr["T"][r], [_VH[j], -_VL[j]]]))
+            A.append(fr["A"][r])
+            B.append(fr["B"][r] * _B_GEAR[j])
+            c.append(fr["c"][r])
+            gear.append(j + 1)
+            fric.append(r)
+    D, E, F, G = _box()
+    nm = len(S)
+    return dict(S=np.array(S), R=np.zeros((nm, 4)), T=np.array(T), A=np.array(A), B=np.array(B), c=np.array(c),
+                D=D, E=E, F=F, G=G, gear=np.array(gear), friction=np.array(fric))
+
+
 def env_seed(seed: int) -> int:
     return int(np.random.SeedSequence(seed).generate_state(1)[0])
 

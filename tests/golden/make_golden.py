@@ -25,7 +25,9 @@ Files (numpy .npz, no pickles):
                       tests/test_oracle.py); "method" = 1 marks them (node counts not comparable)
   known_answers.json  constants derived from the reference source
 
-Run:  python tests/golden/make_golden.py [sweep]
+  gear_n4_N5.npz, gear_n5_N8.npz  LocalMpcGear on the pwa_friction model ("model" = 1):
+                      (gear, friction region) modes, oracle gear_friction_mld_system
+Run:  python tests/golden/make_golden.py [sweep | gear]
 """
 
 from __future__ import annotations
@@ -74,16 +76,16 @@ def solve_set(systems, masses_idx, cfg, N, params, roles, quadratic=True):
     return {k: np.array(v) for k, v in out.items()}
 
 
-def save(name, N, masses, cfg, params, roles, sys_idx, exp, method=0):
+def save(name, N, masses, cfg, params, roles, sys_idx, exp, method=0, model=0):
     path = os.path.join(HERE, name)
     np.savez_compressed(path, N=N, masses=np.asarray(masses, float), cfg=cfg.vector(), params=params,
-                        roles=roles.astype(np.int32), sys=np.asarray(sys_idx, np.int32), method=method,
+                        roles=roles.astype(np.int32), sys=np.asarray(sys_idx, np.int32), method=method, model=model,
                         **{f"exp_{k}": v for k, v in exp.items()})
     cert = exp["certified"][exp["status"] == 0].mean() if (exp["status"] == 0).any() else 0
     print(f"{name}: {len(roles)} instances, optimal {int((exp['status'] == 0).sum())}, certified {cert:.3f}")
 
 
-def decent_seeds(n, N, seeds, mass=800.0, cfg=None):
+def decent_seeds(n, N, seeds, mass=800.0, cfg=None, system=None):
     cfg = cfg or O.Cfg()
     P, R = [], []
     for s in seeds:
@@ -92,7 +94,25 @@ def decent_seeds(n, N, seeds, mass=800.0, cfg=None):
         R.append(r)
     params, roles = np.concatenate(P), np.concatenate(R)
     sys_idx = np.zeros(len(roles), np.int32)
-    return params, roles, sys_idx, solve_set([O.gear_pwa_system(mass)], sys_idx, cfg, N, params, roles)
+    system = system or O.gear_pwa_system(mass)
+    return params, roles, sys_idx, solve_set([system], sys_idx, cfg, N, params, roles)
+
+
+def gear_model():
+    """LocalMpcGear on pwa_friction (mpcs/mpc_gear.py, fleet_decent_mld.py:226-253): model = 1.
+    N = 5 by exhaustive enumeration (~1e3 mode sequences per vehicle), N = 8 by the oracle's
+    branch and bound."""
+    g = O.gear_friction_mld_system(800.0)
+    params, roles, si, exp = decent_seeds(4, 5, range(4), system=g)
+    exp["gear"] = g["gear"][exp["region"]]
+    save("gear_n4_N5.npz", 5, [800.0], O.Cfg(), params, roles, si, exp, model=1)
+    O.set_method(O.METHOD_BNB)
+    try:
+        params, roles, si, exp = decent_seeds(5, 8, range(2), system=g)
+        exp["gear"] = g["gear"][exp["region"]]
+        save("gear_n5_N8.npz", 8, [800.0], O.Cfg(), params, roles, si, exp, method=1, model=1)
+    finally:
+        O.set_method(O.METHOD_ENUMERATE)
 
 
 def rollout(n, N, seeds, steps):
@@ -170,6 +190,9 @@ def sweep():
 def main():
     if len(sys.argv) > 1 and sys.argv[1] == "sweep":
         sweep()
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == "gear":
+        gear_model()
         return
     N = 5
     params, roles, si, exp = hard_cases(N)

@@ -38,10 +38,23 @@ def product_problem(fx: dict):
     from hvp.models import PwaGearVehicle
     from hvp.params import ConstantTimePolicy
 
+    from hvp.models import PwaFrictionVehicle
+
     cp = CfgParams(fx["cfg"])
     prob = tables.problem(int(fx["N"]), ConstantTimePolicy(cp.d0, cp.t0), accel_cnstr_tightening=cp.tight, params=cp)
     systems = []
     for m in fx["masses"]:
-        veh = PwaGearVehicle(float(m))
-        systems.append(tables.system_from_dict(veh.get_discrete_system(float(cp.ts)), tables.gears_of(veh)))
+        if int(fx.get("model", 0)) == 1:  # LocalMpcGear on pwa_friction
+            veh = PwaFrictionVehicle(float(m))
+            systems.append(tables.gear_system_from_dict(veh.get_discrete_system(float(cp.ts))))
+        else:
+            veh = PwaGearVehicle(float(m))
+            systems.append(tables.system_from_dict(veh.get_discrete_system(float(cp.ts)), tables.gears_of(veh)))
     return prob, systems
+
+
+def expected_gears(fx: dict):
+    """Gear label per step of the expected solutions."""
+    if "exp_gear" in fx:
+        return fx["exp_gear"]
+    return np.array([1, 2, 3, 4, 4, 5, 6])[fx["exp_region"]]

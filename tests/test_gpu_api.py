@@ -73,3 +73,50 @@ def test_closed_loop_simulate(gpu_available):
         ref = O.solve_miqp(O.gear_pwa_system(800.0), O.Cfg(), 5, O.role_bits(i, 4), x0[2 * i:2 * i + 2], xf, xb,
                            lead if i == 0 else np.zeros((2, 6)))
         assert abs(U[0][i] - ref.u[0]) <= 1e-6
+
+
+def test_local_mpc_gear_matches_oracle_and_evaluates(gpu_available):
+    """LocalMpcGear on pwa_friction (fleet_decent_mld.py:226-253, mpcs/mpc_gear.py): returns
+    [u_g0; gear0], info["u"] = vstack(u_g, gears), gears_pred; evaluate_cost of the optimal
+    (u_g, gears) reproduces the optimal cost, and an infeasible throttle gives 'inf'."""
+    from hvp.models import PwaFrictionVehicle
+    from hvp.mpc import LocalMpcGear
+
+    N = 5
+    veh = PwaFrictionVehicle(800)
+    g = O.gear_friction_mld_system(800.0)
+    x = O.env_initial_state(3, 2).astype(float)
+    xf = O.constant_velocity_prediction(x[0], x[1], N)
+    xb = O.constant_velocity_prediction(x[4], x[5], N)
+    m = LocalMpcGear(N, veh.get_discrete_system(1))
+    m.set_x_front(xf)
+    m.set_x_back(xb)
+    u0, info = m.solve_mpc(x[2:4].reshape(2, 1))
+    ref = O.solve_miqp(g, O.Cfg(), N, O.role_bits(1, 3), x[2:4], xf, xb, np.zeros((2, N + 1)))
+    assert ref.status == 0
+    assert u0.shape == (2, 1) and info["u"].shape == (2, N)
+    assert np.abs(info["u"][0] - ref.u).max() <= 1e-6
+    assert list(info["u"][1].astype(int)) == list(g["gear"][ref.sigma])
+    assert abs(info["cost"] - ref.cost) <= 1e-9 * abs(ref.cost)
+    assert info["bin_vars"] == 8 * N
+    assert np.array_equal(m.gears_pred, info["u"][[1]])
+    c = m.evaluate_cost(x[2:4].reshape(2, 1), info["u"][[0]], info["u"][[1]])
+    assert abs(c - ref.cost) <= 1e-9 * abs(ref.cost)
+    # full throttle in first gear at ~20 m/s is outside gear 1's window -> infeasible
+    assert m.evaluate_cost(x[2:4].reshape(2, 1), np.ones((1, N)), np.ones((1, N))) == "inf"
+
+
+def test_closed_loop_simulate_gear_model(gpu_available):
+    from hvp.decent import simulate
+    from hvp.params import Sim
+
+    class ShortGear(Sim):
+        n = 3
+        N = 5
+        ep_len = 8
+        vehicle_model_type = "pwa_friction"
+
+    X, U, R, agent, env = simulate(ShortGear(), seed=3)
+    assert X.shape == (9, 6) and U.shape == (8, 6)
+    assert np.all(np.abs(U[:, :3]) <= 1 + 1e-9)
+    assert set(np.unique(U[:, 3:]).astype(int)) <= set(range(1, 7))

@@ -101,7 +101,7 @@ def test_position_box_fallback(gpu_available):
 
 
 # ---------------------------------------------------------------- golden fixtures through the C ABI
-from golden_io import fixture_names, load, product_problem  # noqa: E402
+from golden_io import expected_gears, fixture_names, load, product_problem  # noqa: E402
 
 
 @pytest.mark.parametrize("method", [1, 2])  # HVP_METHOD_ENUMERATE, HVP_METHOD_BNB
@@ -121,8 +121,7 @@ def test_golden_fixture_on_gpu(gpu_available, name, method):
     if method == 1:
         assert np.array_equal(res.nodes, fx["exp_nodes"])
     assert np.array_equal(res.region[ok], fx["exp_region"][ok])
-    gear_of = np.array([1, 2, 3, 4, 4, 5, 6])
-    assert np.array_equal(res.gear[ok], gear_of[fx["exp_region"][ok]])
+    assert np.array_equal(res.gear[ok], expected_gears(fx)[ok])
     ce = fx["exp_cost"][ok]
     assert np.all(np.abs(res.cost[ok] - ce) <= 1e-9 * np.maximum(1, np.abs(ce)))
     assert np.abs(res.u[ok] - fx["exp_u"][ok]).max() <= 1e-6

@@ -262,3 +262,32 @@ def test_oracle_branch_and_bound_equals_enumeration(n, N, seed):
         assert abs(a.cost - b.cost) <= 1e-10 * max(1.0, abs(a.cost))
         assert np.abs(a.u - b.u).max() <= 1e-7
         assert b.n_candidates < a.n_candidates or N <= 5
+
+
+def test_gear_model_restatement():
+    """MpcGear on pwa_friction (mpcs/mpc_gear.py:30-114): one mode per (gear, friction region),
+    band = gear window ∩ region, input gain B_r * Vehicle.b[j] on u_g.  Branch and bound and
+    enumeration agree on it, and every optimal mode respects its gear's velocity window."""
+    g = O.gear_friction_mld_system(800.0)
+    assert list(g["gear"]) == [1, 2, 3, 4, 4, 5, 5, 6, 6]
+    assert list(g["friction"]) == [0, 0, 0, 0, 1, 0, 1, 0, 1]
+    assert np.allclose(g["B"][:, 1] * 800.0, [4057, 2945, 2116, 1607, 1607, 1166, 1166, 838, 838])
+    N = 4
+    params, roles = decent_instances(O.env_initial_state(3, 5), N, leader_window(N))
+    vl = np.array([3.94, 5.43, 7.56, 9.96, 13.70, 19.10])
+    vh = np.array([9.46, 13.04, 18.15, 23.90, 32.93, 45.84])
+    for p, r in zip(params, roles):
+        x0, xf, xb, xl = split_params(p, N)
+        a = O.solve_miqp(g, O.Cfg(), N, int(r), x0, xf, xb, xl)
+        O.set_method(O.METHOD_BNB)
+        try:
+            b = O.solve_miqp(g, O.Cfg(), N, int(r), x0, xf, xb, xl)
+        finally:
+            O.set_method(O.METHOD_ENUMERATE)
+        assert a.status == b.status == 0
+        assert list(a.sigma) == list(b.sigma)
+        assert abs(a.cost - b.cost) <= 1e-10 * max(1.0, abs(a.cost))
+        gears = g["gear"][a.sigma] - 1
+        v = a.x[1, :N]
+        assert np.all(v >= vl[gears] - 1e-7) and np.all(v <= vh[gears] + 1e-7)
+        assert np.abs(a.u).max() <= 1 + 1e-9
