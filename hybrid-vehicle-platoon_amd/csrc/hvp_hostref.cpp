@@ -161,7 +161,14 @@ void solve_one_bnb(const hvp_system& S, const hvp::Consts& C, int role, const do
         const int r = hvp::solve_gi<N>(q, C, 8 * hvp::GiConstraintSet<N>::NC, it);
         ++nq;
         nit += it;
-        if (r != hvp::GI_OK) return false;
+        if (r != hvp::GI_OK) {
+            // leaves get the interior-point fallback (K_bnb_ipm on the device)
+            if (K < N || N > HVP_MAX_N_ENUM) return false;
+            hvp::setup_lane<N>(q, S, C, role, prm, code, K);
+            const hvp::QpOut o = hvp::Solver<N, true>::solve(q, C);
+            nit += o.iters;
+            if (o.status != 0) return false;
+        }
         c = hvp::direct_cost<N>(q, S, C, role, prm, code, K);
         if (y)
             for (int i = 0; i < N; ++i) y[i] = q.y[i];
@@ -171,6 +178,7 @@ void solve_one_bnb(const hvp_system& S, const hvp::Consts& C, int role, const do
     const bool ok = P1 >= S.pmin - 1e-9 * (1.0 + fabs(S.pmin)) && P1 <= S.pmax + 1e-9 * (1.0 + fabs(S.pmax));
     std::vector<Node> lvl, nxt;
     double inc = HUGE_VAL;
+    int nleaves = 0;
     if (ok) {
         Node root;
         root.code = 0;
@@ -196,6 +204,7 @@ void solve_one_bnb(const hvp_system& S, const hvp::Consts& C, int role, const do
                 nxt.push_back(c);
             }
         }
+        if (k == N) nleaves += (int)nxt.size();
         for (Node& c : nxt) {
             double lb;
             const bool good = qp(c.code, k, lb, c.y);
@@ -218,7 +227,7 @@ void solve_one_bnb(const hvp_system& S, const hvp::Consts& C, int role, const do
         }
     }
     if (win < 0) {
-        *status = !ok ? HVP_INFEASIBLE : (nq > 1 && inc < HUGE_VAL ? HVP_MAXITER : HVP_INFEASIBLE);
+        *status = (ok && !lvl.empty() && lvl.size() > 0 && nleaves > 0) ? HVP_MAXITER : HVP_INFEASIBLE;
         *cost = 1e300;
         return;
     }

@@ -148,7 +148,13 @@ __global__ __launch_bounds__(kBlock) void k_enum(int B, const hvp_system* __rest
     int off = -1;
     if (cnt > 0) {
         const unsigned long long o = atomicAdd(&ws.counter[0], (unsigned long long)cnt);
-        if ((long long)o + cnt <= ws.cap) off = (int)o;
+        if ((long long)o + cnt <= ws.cap) {
+            off = (int)o;
+        } else {
+            // overflow: the part of the reserved range below the capacity is still swept by
+            // K_qp / K_cost (they run over min(reserved, cap)): mark those slots dead
+            for (long long t = (long long)o; t < ws.cap && t < (long long)o + cnt; ++t) ws.task_inst[t] = -1;
+        }
     }
     ws.inst_off[i] = off;
     if (off < 0) return;
@@ -186,6 +192,7 @@ __global__ __launch_bounds__(kBlock) void k_qp_gi(const hvp_system* __restrict__
     for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
          t += (long long)gridDim.x * blockDim.x) {
         const int inst = ws.task_inst[t];
+        if (inst < 0) continue;  // dead slot of an overflowed instance
         const uint32_t code = ws.task_code[t];
         const hvp_system& S = systems[sys[inst]];
         const int rl = role[inst];
@@ -255,7 +262,7 @@ __global__ __launch_bounds__(kBlock) void k_cost(const hvp_system* __restrict__ 
          t += (long long)gridDim.x * blockDim.x) {
         const int inst = ws.task_inst[t];
         double cost = 1e300;
-        if ((ws.task_stat[t] & 0xff) == 0) {
+        if (inst >= 0 && (ws.task_stat[t] & 0xff) == 0) {
             const hvp_system& S = systems[sys[inst]];
             const double* prm = params + (size_t)inst * (2 + 6 * (N + 1));
             hvp::LaneQp<N> q;
@@ -435,6 +442,9 @@ __global__ __launch_bounds__(kBlock) void k_bnb_expand(int k, const hvp_system* 
         const unsigned long long off = atomicAdd(&ws.lvl[k], (unsigned long long)nc);
         if (off + nc > (unsigned long long)ws.cap) {
             atomicOr(&ws.inst_flag[inst], 2);  // overflow: reported, never truncated silently
+            // the slots of this reservation below the capacity are swept by the next kernels
+            for (unsigned long long t = off; t < (unsigned long long)ws.cap && t < off + nc; ++t)
+                ws.nd_inst[dst][t] = -1;
             continue;
         }
         int j = 0;
@@ -466,6 +476,11 @@ __global__ __launch_bounds__(kBnbBlock<N>) void k_bnb_bound(int k, const hvp_sys
     unsigned long long iter_sum = 0, fails = 0;
     for (long long t = (long long)blockIdx.x * BS + threadIdx.x; t < total; t += (long long)gridDim.x * BS) {
         const int inst = ws.nd_inst[dst][t];
+        if (inst < 0) {  // dead slot of an overflowed reservation
+            if (k == N) ws.leaf_stat[t] = HVP_OVERFLOW;
+            else ws.nd_lb[dst][t] = 1e300;
+            continue;
+        }
         const uint64_t code = ws.nd_code[dst][t];
         const hvp_system& S = systems[sys[inst]];
         const int rl = role[inst];
@@ -483,24 +498,62 @@ __global__ __launch_bounds__(kBnbBlock<N>) void k_bnb_bound(int k, const hvp_sys
             // a failed bound QP prunes nothing
             ws.nd_lb[dst][t] = ok ? c : -1e300;
         } else {
-            // a failed leaf keeps its parent's bound: K_key flags the instance MAXITER if that
-            // bound leaves the leaf in contention (never a silent wrong answer)
+            // a failed leaf keeps its parent's bound (K_key: MAXITER if it stays in contention
+            // and no fallback exists)
             if (ok) ws.nd_lb[dst][t] = c;
             ws.leaf_stat[t] = ok ? 0 : HVP_MAXITER;
 #pragma unroll
             for (int j = 0; j < N; ++j) ws.task_y[t * N + j] = q.y[j];
-            if (ok) atomicMin(&ws.inc[inst], (unsigned long long)__double_as_longlong(c));
-            else ++fails;
+            if (ok) {
+                atomicMin(&ws.inc[inst], (unsigned long long)__double_as_longlong(c));
+            } else {
+                ++fails;
+                atomicOr(&ws.inst_flag[inst], 8);  // a velocity-feasible sequence exists
+                if (N <= HVP_MAX_N_ENUM) {  // the interior-point fallback (K_bnb_ipm) re-solves it
+                    const unsigned long long r = atomicAdd(&ws.counter[2], 1ull);
+                    if (r < (unsigned long long)ws.cap) ws.redo[r] = (int32_t)t;
+                }
+            }
         }
     }
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        iter_sum += __shfl_down(iter_sum, off, 64);
-        fails += __shfl_down(fails, off, 64);
-    }
-    if ((threadIdx.x & 63) == 0) {
-        if (iter_sum) atomicAdd(&ws.counter[1], iter_sum);
-        if (fails) atomicAdd(&ws.counter[2], fails);
+    for (int off = 32; off > 0; off >>= 1) iter_sum += __shfl_down(iter_sum, off, 64);
+    if ((threadIdx.x & 63) == 0 && iter_sum) atomicAdd(&ws.counter[1], iter_sum);
+    (void)fails;
+}
+
+// Leaves whose active-set solve failed its verification (degenerate vertices, e.g. the
+// position box at p_max): re-solved by the interior-point method on the full row set
+// (hvp_ipm.h), as K_qp_ipm does for the enumeration path.  Normally an empty list.
+template <int N>
+__global__ __launch_bounds__(kBnbBlock<N>) void k_bnb_ipm(const hvp_system* __restrict__ systems,
+                                                          const int32_t* __restrict__ sys,
+                                                          const int32_t* __restrict__ role,
+                                                          const double* __restrict__ params, hvp::Consts C,
+                                                          Workspace ws) {
+    constexpr int BS = kBnbBlock<N>;
+    const int src = N & 1;
+    const unsigned long long nr = ws.counter[2];
+    const long long total = (long long)(nr < (unsigned long long)ws.cap ? nr : ws.cap);
+    for (long long i = (long long)blockIdx.x * BS + threadIdx.x; i < total; i += (long long)gridDim.x * BS) {
+        const long long t = ws.redo[i];
+        const int inst = ws.nd_inst[src][t];
+        const uint64_t code = ws.nd_code[src][t];
+        const hvp_system& S = systems[sys[inst]];
+        const int rl = role[inst];
+        const double* prm = params + (size_t)inst * (2 + 6 * (N + 1));
+        hvp::LaneQp<N, LdsMem<N, BS>> q;
+        q.mem.lane = threadIdx.x;
+        hvp::setup_lane<N>(q, S, C, rl, prm, code);
+        const hvp::QpOut o = hvp::Solver<N, true, LdsMem<N, BS>>::solve(q, C);
+        atomicAdd(&ws.iters[inst], o.iters);
+        if (o.status != 0) continue;  // stays HVP_MAXITER with its parent's bound (K_key flags it)
+        const double c = hvp::direct_cost<N>(q, S, C, rl, prm, code);
+#pragma unroll
+        for (int j = 0; j < N; ++j) ws.task_y[t * N + j] = q.y[j];
+        ws.nd_lb[src][t] = c;
+        ws.leaf_stat[t] = 0;
+        atomicMin(&ws.inc[inst], (unsigned long long)__double_as_longlong(c));
     }
 }
 
@@ -513,9 +566,14 @@ __global__ __launch_bounds__(kBlock) void k_bnb_key(Workspace ws) {
     for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
          t += (long long)gridDim.x * blockDim.x) {
         const int inst = ws.nd_inst[src][t];
+        if (inst < 0) continue;
         const double best = inc_of(ws, inst);
         if (ws.leaf_stat[t] != 0) {
-            if (!hvp::bnb_pruned(ws.nd_lb[src][t], best)) atomicOr(&ws.inst_flag[inst], 4);
+            // Up to HVP_MAX_N_ENUM a leaf that fails the active-set method AND the interior-point
+            // fallback is an infeasible QP (position box), excluded exactly as the enumeration
+            // path and the oracle exclude it.  Beyond, there is no fallback: a failed leaf still
+            // in contention makes the instance MAXITER rather than a possibly wrong answer.
+            if (N > HVP_MAX_N_ENUM && !hvp::bnb_pruned(ws.nd_lb[src][t], best)) atomicOr(&ws.inst_flag[inst], 4);
             continue;
         }
         if (ws.nd_lb[src][t] <= best + 1e-9 * fmax(1.0, fabs(best)))
@@ -563,6 +621,7 @@ __global__ __launch_bounds__(kBlock) void k_bnb_write(const hvp_system* __restri
          t += (long long)gridDim.x * blockDim.x) {
         if (ws.leaf_stat[t] != 0) continue;
         const int inst = ws.nd_inst[src][t];
+        if (inst < 0) continue;
         const uint64_t code = ws.nd_code[src][t];
         if (hvp::bnb_lexkey(code, N) != ws.key[inst]) continue;
         const hvp_system& S = systems[sys[inst]];
@@ -593,7 +652,7 @@ __global__ __launch_bounds__(kBlock) void k_bnb_finish(int B, const hvp_system* 
     else if (flag & 2) status = HVP_OVERFLOW;
     else if (flag & 4) status = HVP_MAXITER;  // a leaf in contention whose QP did not converge
     else if (win) status = HVP_OPTIMAL;
-    else status = ws.nodes[i] > 1 && __longlong_as_double((long long)ws.inc[i]) < 1e300 ? HVP_MAXITER : HVP_INFEASIBLE;
+    else status = (flag & 8) ? HVP_MAXITER : HVP_INFEASIBLE;  // sequences exist but no QP converged
     if (status_out) status_out[i] = status;
     if (nodes_out) nodes_out[i] = ws.nodes[i];
     if (iters_out) iters_out[i] = ws.iters[i];
@@ -691,6 +750,11 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
         HIP_TRY(hipEventRecord(h->evb[2 * k + 1], st));
     }
     HIP_TRY(hipEventRecord(h->evq1, st));
+    if constexpr (N <= HVP_MAX_N_ENUM) {
+        hipLaunchKernelGGL(k_bnb_ipm<N>, dim3(std::max(1, h->n_cu)), dim3(BS), lds, st, h->d_sys, sys, role, params,
+                           h->C, ws);
+        HIP_TRY(hipGetLastError());
+    }
     hipLaunchKernelGGL(k_bnb_key<N>, dim3(g_small), dim3(kBlock), 0, st, ws);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_bnb_write<N>, dim3(g_small), dim3(kBlock), 0, st, h->d_sys, sys, params, ws, u_out, x_out,
