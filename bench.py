@@ -164,8 +164,11 @@ def main() -> None:
     t_sys = torch.zeros(B, dtype=torch.int32, device=dev)
     out = solver.alloc_outputs(B, dev)
 
+    # long horizons: a heavy-tailed search can outgrow an instance's workspace share; those
+    # instances are re-solved inside the step (one synchronisation), so every step is complete
+    retry = N > 8
     for _ in range(args.warmup):
-        solver.solve_device(t_sys, t_roles, t_params, out)
+        solver.solve_device(t_sys, t_roles, t_params, out, retry_overflow=retry)
     torch.cuda.synchronize()
 
     if dist:
@@ -173,7 +176,7 @@ def main() -> None:
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        solver.solve_device(t_sys, t_roles, t_params, out)
+        solver.solve_device(t_sys, t_roles, t_params, out, retry_overflow=retry)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()

@@ -60,7 +60,7 @@ struct Workspace {
     int32_t* inst_off = nullptr;   // [max_batch] first candidate slot (-1: overflow)
     int32_t* inst_cnt = nullptr;   // [max_batch] candidates of the instance
     int32_t* inst_flag = nullptr;  // [max_batch] 0 ok, 1 infeasible constant rows
-    unsigned long long* counter = nullptr;  // [4] reserved slots, qp iterations, fallback count, pad
+    unsigned long long* counter = nullptr;  // [8] reserved slots, qp iterations, fallback count, root QPs, failed bounds
     int32_t* redo = nullptr;       // [cap] candidates the active-set method hands to the IPM
     int32_t* task_inst = nullptr;  // [cap]
     uint32_t* task_code = nullptr; // [cap]
@@ -80,6 +80,7 @@ struct Workspace {
     int32_t* nodes = nullptr;                    // [max_batch] QPs solved for the instance
     int32_t* iters = nullptr;                    // [max_batch] active-set iterations
     unsigned long long* lvl = nullptr;           // [HVP_MAX_N + 1] nodes per level
+    int32_t* inst_lvl = nullptr;                 // [max_batch] children of the instance at this level
 };
 
 }  // namespace
@@ -417,8 +418,12 @@ __global__ __launch_bounds__(kBnbBlock<N>) void k_bnb_root(int B, const hvp_syst
 }
 
 // children of the level-(k-1) nodes that survive the incumbent test
+// Every instance may hold at most `quota` = capacity / B nodes per level: an instance whose
+// tree outgrows its share (the heavy tail at long horizons, e.g. trajectories riding a region
+// boundary) is cut off deterministically and reported HVP_OVERFLOW, so it can never crowd the
+// other instances out of the pooled list.  The host path re-solves it alone (quota = capacity).
 template <int N>
-__global__ __launch_bounds__(kBlock) void k_bnb_expand(int k, const hvp_system* __restrict__ systems,
+__global__ __launch_bounds__(kBlock) void k_bnb_expand(int k, int quota, const hvp_system* __restrict__ systems,
                                                        const int32_t* __restrict__ sys, hvp::Consts C, Workspace ws) {
     const int src = (k - 1) & 1, dst = k & 1;
     const unsigned long long np = ws.lvl[k - 1];
@@ -426,7 +431,7 @@ __global__ __launch_bounds__(kBlock) void k_bnb_expand(int k, const hvp_system* 
     for (long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x; p < total;
          p += (long long)gridDim.x * blockDim.x) {
         const int inst = ws.nd_inst[src][p];
-        if (inst < 0) continue;
+        if (inst < 0 || (ws.inst_flag[inst] & 2)) continue;
         const double plb = ws.nd_lb[src][p];
         if (hvp::bnb_pruned(plb, inc_of(ws, inst))) continue;
         const hvp_system& S = systems[sys[inst]];
@@ -439,6 +444,10 @@ __global__ __launch_bounds__(kBlock) void k_bnb_expand(int k, const hvp_system* 
         }
         const int nc = __popc(mask);
         if (!nc) continue;
+        if (atomicAdd(&ws.inst_lvl[inst], nc) + nc > quota) {
+            atomicOr(&ws.inst_flag[inst], 2);
+            continue;
+        }
         const unsigned long long off = atomicAdd(&ws.lvl[k], (unsigned long long)nc);
         if (off + nc > (unsigned long long)ws.cap) {
             atomicOr(&ws.inst_flag[inst], 2);  // overflow: reported, never truncated silently
@@ -497,6 +506,7 @@ __global__ __launch_bounds__(kBnbBlock<N>) void k_bnb_bound(int k, const hvp_sys
         if (k < N) {
             // a failed bound QP prunes nothing
             ws.nd_lb[dst][t] = ok ? c : -1e300;
+            if (!ok) atomicAdd(&ws.counter[4], 1ull);
         } else {
             // a failed leaf keeps its parent's bound (K_key: MAXITER if it stays in contention
             // and no fallback exists)
@@ -729,7 +739,7 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
                int32_t* nodes_out, int32_t* iters_out, hipStream_t st) {
     Workspace ws = h->ws;
     constexpr int BS = kBnbBlock<N>;
-    HIP_TRY(hipMemsetAsync(ws.counter, 0, 4 * sizeof(unsigned long long), st));
+    HIP_TRY(hipMemsetAsync(ws.counter, 0, 8 * sizeof(unsigned long long), st));
     HIP_TRY(hipMemsetAsync(ws.lvl, 0, (HVP_MAX_N + 1) * sizeof(unsigned long long), st));
     HIP_TRY(hipEventRecord(h->ev0, st));
     HIP_TRY(hipEventRecord(h->evq0, st));
@@ -741,8 +751,10 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
     HIP_TRY(hipEventRecord(h->evb[1], st));
     const int g_small = (int)std::min<long long>(grid_for(h->ws.cap), (long long)h->n_cu * 8);
     const int g_qp = (int)std::min<long long>((h->ws.cap + BS - 1) / BS, (long long)h->n_cu * 8 * (kBlock / BS));
+    const int quota = (int)std::min<int64_t>(h->ws.cap / B, 1 << 30);
     for (int k = 1; k <= N; ++k) {
-        hipLaunchKernelGGL(k_bnb_expand<N>, dim3(g_small), dim3(kBlock), 0, st, k, h->d_sys, sys, h->C, ws);
+        HIP_TRY(hipMemsetAsync(ws.inst_lvl, 0, sizeof(int32_t) * B, st));
+        hipLaunchKernelGGL(k_bnb_expand<N>, dim3(g_small), dim3(kBlock), 0, st, k, quota, h->d_sys, sys, h->C, ws);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(h->evb[2 * k], st));
         hipLaunchKernelGGL(k_bnb_bound<N>, dim3(g_qp), dim3(BS), lds, st, k, h->d_sys, sys, role, params, h->C, ws);
@@ -775,7 +787,7 @@ int launch_all(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
                double* x_out, int8_t* region_out, int8_t* gear_out, double* cost_out, int32_t* status_out,
                int32_t* nodes_out, int32_t* iters_out, hipStream_t st) {
     Workspace ws = h->ws;
-    HIP_TRY(hipMemsetAsync(ws.counter, 0, 4 * sizeof(unsigned long long), st));
+    HIP_TRY(hipMemsetAsync(ws.counter, 0, 8 * sizeof(unsigned long long), st));
     HIP_TRY(hipEventRecord(h->ev0, st));
     hipLaunchKernelGGL(k_enum<N>, dim3(grid_for(B)), dim3(kBlock), 0, st, B, h->d_sys, sys, role, params, h->C, ws);
     HIP_TRY(hipGetLastError());
@@ -827,6 +839,7 @@ void free_ws(Workspace& w) {
     (void)hipFree(w.nodes);
     (void)hipFree(w.iters);
     (void)hipFree(w.lvl);
+    (void)hipFree(w.inst_lvl);
     w = Workspace{};
 }
 
@@ -932,7 +945,7 @@ int hvp_reserve(hvp_handle* h, int max_batch, int64_t cap) {
     bool ok = hipMalloc(&w.inst_off, sizeof(int32_t) * max_batch) == hipSuccess &&
               hipMalloc(&w.inst_cnt, sizeof(int32_t) * max_batch) == hipSuccess &&
               hipMalloc(&w.inst_flag, sizeof(int32_t) * max_batch) == hipSuccess &&
-              hipMalloc(&w.counter, sizeof(unsigned long long) * 4) == hipSuccess &&
+              hipMalloc(&w.counter, sizeof(unsigned long long) * 8) == hipSuccess &&
               hipMalloc(&w.redo, sizeof(int32_t) * cap) == hipSuccess &&
               hipMalloc(&w.task_inst, sizeof(int32_t) * cap) == hipSuccess &&
               hipMalloc(&w.task_code, sizeof(uint32_t) * cap) == hipSuccess &&
@@ -951,7 +964,8 @@ int hvp_reserve(hvp_handle* h, int max_batch, int64_t cap) {
              hipMalloc(&w.key, sizeof(unsigned long long) * max_batch) == hipSuccess &&
              hipMalloc(&w.nodes, sizeof(int32_t) * max_batch) == hipSuccess &&
              hipMalloc(&w.iters, sizeof(int32_t) * max_batch) == hipSuccess &&
-             hipMalloc(&w.lvl, sizeof(unsigned long long) * (HVP_MAX_N + 1)) == hipSuccess;
+             hipMalloc(&w.lvl, sizeof(unsigned long long) * (HVP_MAX_N + 1)) == hipSuccess &&
+             hipMalloc(&w.inst_lvl, sizeof(int32_t) * max_batch) == hipSuccess;
     }
     if (!ok) {
         free_ws(w);
@@ -1025,7 +1039,7 @@ int hvp_sync(hvp_handle* h, void* stream) {
 int hvp_get_stats(hvp_handle* h, hvp_stats* out) {
     if (!h || !out) return fail(HVP_E_ARG, "hvp_get_stats: bad argument");
     HIP_TRY(hipStreamSynchronize(h->last_stream));
-    unsigned long long c[4] = {0, 0, 0, 0};
+    unsigned long long c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (h->ws.counter) HIP_TRY(hipMemcpy(c, h->ws.counter, sizeof(c), hipMemcpyDeviceToHost));
     float ms = 0.f, qms = 0.f;
     if (h->last_B > 0) {
@@ -1035,6 +1049,7 @@ int hvp_get_stats(hvp_handle* h, hvp_stats* out) {
     out->qp_ms = qms;
     out->n_instances = h->last_B;
     out->n_candidates = (int64_t)c[0];
+    out->n_failed_bounds = (int64_t)c[4];
     if (h->last_bnb) {
         // tree nodes solved: root + dive QPs (counter[3]) and every level's nodes
         unsigned long long lv[HVP_MAX_N + 1];

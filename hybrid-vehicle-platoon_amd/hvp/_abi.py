@@ -79,6 +79,7 @@ class HvpStats(ctypes.Structure):
         ("last_ms", ctypes.c_double),
         ("qp_ms", ctypes.c_double),
         ("n_fallback", ctypes.c_int64),
+        ("n_failed_bounds", ctypes.c_int64),
     ]
 
 

@@ -91,14 +91,15 @@ class BatchSolver:
         if B == 0:
             return out
         self._solve_host(sys_idx, roles, params, out)
-        # the search workspace is pooled over the batch: instances that did not fit (HVP_OVERFLOW,
-        # reported, never truncated) are re-solved with a larger reservation
-        for _ in range(4):
+        # the search workspace is pooled over the batch with a per-instance share: instances whose
+        # search outgrew it (HVP_OVERFLOW, reported, never truncated) are re-solved on their own,
+        # where the share is the whole workspace, growing it if needed
+        for attempt in range(4):
             over = np.flatnonzero(out.status == _abi.OVERFLOW)
             if not len(over):
                 break
-            cap = self.stats().capacity
-            self.reserve(max(B, 1), 4 * cap)
+            if attempt:
+                self.reserve(max(B, 1), 4 * self.stats().capacity)
             sub = BatchResult(**{k: v[over].copy() for k, v in out.__dict__.items()})
             self._solve_host(sys_idx[over], roles[over], np.ascontiguousarray(params[over]), sub)
             for k, v in sub.__dict__.items():
@@ -131,11 +132,29 @@ class BatchSolver:
             "iters": torch.empty((B,), dtype=torch.int32, device=dev),
         }
 
-    def solve_device(self, sys_idx, roles, params, out: dict | None = None, stream=None) -> dict:
-        """Asynchronous solve of device-resident tensors; returns (and fills) the output dict.
+    def solve_device(self, sys_idx, roles, params, out: dict | None = None, stream=None,
+                     retry_overflow: bool = False) -> dict:
+        """Solve of device-resident tensors; returns (and fills) the output dict.
 
-        Instances whose search did not fit the workspace come back as HVP_OVERFLOW (reserve a
-        larger ``candidate_capacity``, or use :meth:`solve`, which retries them)."""
+        Asynchronous unless ``retry_overflow``: instances whose search outgrew their share of the
+        workspace come back as HVP_OVERFLOW; with ``retry_overflow`` they are gathered on the
+        device and re-solved on their own (synchronising once per retry round)."""
+        import torch
+
+        out = self._launch(sys_idx, roles, params, out, stream)
+        for attempt in range(4 if retry_overflow else 0):
+            over = torch.nonzero(out["status"] == _abi.OVERFLOW).reshape(-1)
+            if over.numel() == 0:
+                break
+            if attempt:
+                self.reserve(int(roles.shape[0]), 4 * self.stats().capacity)
+            sub = self._launch(sys_idx[over].contiguous(), roles[over].contiguous(), params[over].contiguous(),
+                               None, stream)
+            for k, v in sub.items():
+                out[k][over] = v
+        return out
+
+    def _launch(self, sys_idx, roles, params, out, stream) -> dict:
         import torch
 
         B = int(roles.shape[0])

@@ -136,6 +136,7 @@ typedef struct hvp_stats {
     double last_ms;         /* device time of the last solve (event-timed), ms         */
     double qp_ms;           /* device time of its QP kernel (K_qp), ms                 */
     int64_t n_fallback;     /* candidates re-solved by the interior-point fallback    */
+    int64_t n_failed_bounds;/* B&B bound QPs that did not converge (they prune nothing) */
 } hvp_stats;
 
 int hvp_create(hvp_handle** out, const hvp_problem* problem, const hvp_system* systems,

@@ -118,7 +118,7 @@ def test_golden_fixture_on_gpu(gpu_available, name, method):
     res = s.solve(fx["sys"], fx["roles"], fx["params"])
     ok = fx["exp_status"] == 0
     assert np.array_equal(res.status, fx["exp_status"])
-    if method == 1:
+    if method == 1 and int(fx.get("method", 0)) == 0:  # both enumerate: same sequence counts
         assert np.array_equal(res.nodes, fx["exp_nodes"])
     assert np.array_equal(res.region[ok], fx["exp_region"][ok])
     assert np.array_equal(res.gear[ok], expected_gears(fx)[ok])
@@ -211,8 +211,8 @@ def test_sweep_horizons_full_batch(gpu_available, n, NN):
     dev = torch.device("cuda", 0)
     tp, tr = torch.from_numpy(params).to(dev), torch.from_numpy(roles).to(dev)
     ts = torch.zeros(len(roles), dtype=torch.int32, device=dev)
-    a = s.solve_device(ts, tr, tp)
-    b = s.solve_device(ts, tr, tp)
+    a = s.solve_device(ts, tr, tp, retry_overflow=True)
+    b = s.solve_device(ts, tr, tp, retry_overflow=True)
     torch.cuda.synchronize()
     for k in a:
         assert torch.equal(a[k], b[k]), k
