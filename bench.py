@@ -119,6 +119,114 @@ def hostref_baseline(n: int, N: int, budget_s: float, threads: int, method: int 
             "sample": f"{done} platoons, same lane algorithm built with g++ -O2 -fopenmp"}
 
 
+def bench_admm(args, world: int, rank: int, local: int, dist) -> None:
+    """configs[2]: fleet_naive_admm, one step = admm_iters x (n local MIQPs per platoon + the
+    z/y update) for every platoon of the rank's seed range, all on the device."""
+    import torch
+
+    from hvp import tables
+    from hvp.admm import AdmmEngine, admm_problem
+    from hvp.env import derive_env_seed, initial_platoon_state
+    from hvp.models import PwaGearVehicle
+
+    n, N, S, iters = args.n, args.N, args.platoons, args.admm_iters
+    veh = PwaGearVehicle(800)
+    system = tables.system_from_dict(veh.get_discrete_system(1), tables.gears_of(veh))
+    seeds = range(rank * S, (rank + 1) * S)
+    states = np.stack([initial_platoon_state(n, derive_env_seed(int(s))).reshape(-1).astype(np.float64)
+                       for s in seeds])
+    roles = [tables.role_bits(i == 0, i == n - 1, i == 0) for i in range(n)] * S
+    eng = AdmmEngine(admm_problem(N, 0.5), [system], np.zeros(n * S, np.int32), roles, n, S, device=local)
+    eng.set_leader(np.stack([3000.0 + 20.0 * np.arange(N + 1), np.full(N + 1, 20.0)]))
+    t_states = torch.from_numpy(states).to(eng.dev)
+
+    def fresh():  # every timed step starts from the same coordinator state (y = z = 0, no warm start)
+        eng.params.zero_()
+        eng.y_front.zero_()
+        eng.y_back.zero_()
+        eng.x_prev = None
+        eng.set_leader(np.stack([3000.0 + 20.0 * np.arange(N + 1), np.full(N + 1, 20.0)]))
+
+    for _ in range(args.warmup):
+        fresh()
+        eng.step(t_states, iters)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        fresh()
+        eng.step(t_states, iters)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist:
+        tt = torch.tensor([dt], device=eng.dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    # QP-launch timing and work counters of one more step (stats synchronise per iteration)
+    acc = {"qp_ms": 0.0, "qps": 0, "it": 0}
+
+    def on_solve(solver):
+        st = solver.stats()
+        acc["qp_ms"] += st.qp_ms
+        acc["qps"] += st.n_candidates
+        acc["it"] += st.qp_iterations
+
+    fresh()
+    o = eng.step(t_states, iters, on_solve=on_solve)
+    ok = bool((o["status"] == 0).all().item())
+    value = S * world * args.steps / dt
+    alg_bytes = acc["qps"] * dense_qp_bytes(N) + iters * n * S * instance_io_bytes(N)
+    achieved = alg_bytes / (acc["qp_ms"] * 1e-3) / 1e9
+    result = {
+        "metric": f"MPC timesteps/sec (whole platoon) at n={n} N={N} naive_admm ({iters} ADMM iterations)",
+        "value": value, "unit": "platoon-timesteps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic: env.reset random-init platoon states (seeded), constant-velocity leader, "
+                "coordinator state reset each step (first-time-step ADMM: y = z = 0)",
+        "config": {"workload": f"fleet_naive_admm n={n} N={N} pwa_gear (configs[2])", "n_vehicles": n, "horizon": N,
+                   "admm_iters": iters, "rho": 0.5, "platoons_per_gpu": S,
+                   "local_miqps_per_step": iters * n * S * world, "parallelism": f"seeds-sharded x{world}"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "k_bnb_root+k_bnb_bound", "qp_ms_per_step": acc["qp_ms"],
+                     "kernel_avg_ms": acc["qp_ms"] / (iters * (N + 1)),
+                     "algorithmic_bytes_per_step": alg_bytes,
+                     "note": "SURVEY 8(d) dense-QP bytes per local QP solved / HIP-event time of the QP launches"},
+        "qps_per_step": acc["qps"], "qp_iters_per_qp": acc["it"] / max(acc["qps"], 1), "all_optimal": ok,
+    }
+    if rank == 0 and not args.no_cpu and args.cpu_budget > 0 and world == 1:
+        result["cpu_baseline"] = cpu_baseline_admm(n, N, iters, min(args.cpu_budget, 20.0))
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+def cpu_baseline_admm(n: int, N: int, iters: int, budget_s: float):
+    """The oracle coordinator (oracle.AdmmCoordinator: restated fleet_naive_admm get_control on
+    oracle local MIQPs), one platoon step at a time on one core."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    sysd = O.gear_pwa_system(800.0)
+    lead = np.stack([3000.0 + 20.0 * np.arange(N + 1), np.full(N + 1, 20.0)])
+    done, seed, t0 = 0, 30_000_000, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        c = O.AdmmCoordinator(sysd, O.Cfg(), N, n)
+        c.set_leader_x(lead)
+        c.step(O.env_initial_state(n, seed).astype(float), iters)
+        seed += 1
+        done += 1
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "platoon-timesteps/s", "cores": 1, "kind": "port",
+            "sample": f"{done} platoon steps x {iters} ADMM iterations x {n} local MIQPs (N={N}), oracle, {dt:.1f} s"}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -131,6 +239,9 @@ def main() -> None:
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--method", choices=["auto", "enum", "bnb"], default="auto",
                     help="region-sequence search (include/hvp.h HVP_METHOD_*)")
+    ap.add_argument("--controller", choices=["decent", "admm"], default="decent",
+                    help="decent: fleet_decent_mld (configs[1]); admm: fleet_naive_admm (configs[2])")
+    ap.add_argument("--admm-iters", type=int, default=20)
     args = ap.parse_args()
 
     import torch
@@ -149,6 +260,8 @@ def main() -> None:
     from hvp.models import PwaGearVehicle
     from hvp.solver import BatchSolver
 
+    if args.controller == "admm":
+        return bench_admm(args, world, rank, local, dist)
     n, N, S = args.n, args.N, args.platoons
     veh = PwaGearVehicle(800)
     system = tables.system_from_dict(veh.get_discrete_system(1), tables.gears_of(veh))

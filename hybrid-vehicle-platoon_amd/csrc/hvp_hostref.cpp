@@ -8,6 +8,7 @@
 
 #include <vector>
 
+#include "hvp_admm.h"
 #include "hvp_bnb.h"
 #include "hvp_gi.h"
 #include "hvp_ipm.h"
@@ -39,6 +40,9 @@ hvp::Consts make_consts(const hvp_problem& p) {
     C.tol = p.tol > 0 ? p.tol : 1e-12;
     C.max_iter = p.max_iter > 0 ? p.max_iter : 60;
     C.N = p.N;
+    C.form = p.formulation;
+    C.stride = p.formulation == HVP_FORM_ADMM ? hvp_params_stride_admm(p.N) : hvp_params_stride(p.N);
+    C.rho = p.rho;
     return C;
 }
 
@@ -146,7 +150,8 @@ void solve_one(const hvp_system& S, const hvp::Consts& C, int role, const double
 // and tie rule over the leaves.
 template <int N>
 void solve_one_bnb(const hvp_system& S, const hvp::Consts& C, int role, const double* prm, double* u, double* x,
-                   int8_t* region, double* cost, int32_t* status, int32_t* nodes, int32_t* iters) {
+                   int8_t* region, double* cost, int32_t* status, int32_t* nodes, int32_t* iters,
+                   double* xf = nullptr, double* xb = nullptr) {
     struct Node {
         uint64_t code;
         double lo, hi, lb;
@@ -156,8 +161,18 @@ void solve_one_bnb(const hvp_system& S, const hvp::Consts& C, int role, const do
     int nq = 0, nit = 0;
     auto qp = [&](uint64_t code, int K, double& c, double* y) {
         hvp::LaneQp<N> q;
-        hvp::setup_lane<N>(q, S, C, role, prm, code, K);
         int it = 0;
+        if (C.form == HVP_FORM_ADMM) {
+            const int r = hvp::solve_admm_lane<N>(q, S, C, role, prm, code, K, 8 * hvp::GiConstraintSet<N>::NC, it);
+            ++nq;
+            nit += it;
+            if (r != hvp::GI_OK) return false;
+            c = hvp::admm_direct_cost<N>(q, S, C, role, prm, code, K);
+            if (y)
+                for (int i = 0; i < N; ++i) y[i] = q.y[i];
+            return true;
+        }
+        hvp::setup_lane<N>(q, S, C, role, prm, code, K);
         const int r = hvp::solve_gi<N>(q, C, 8 * hvp::GiConstraintSet<N>::NC, it);
         ++nq;
         nit += it;
@@ -229,6 +244,8 @@ void solve_one_bnb(const hvp_system& S, const hvp::Consts& C, int role, const do
     if (win < 0) {
         *status = (ok && !lvl.empty() && lvl.size() > 0 && nleaves > 0) ? HVP_MAXITER : HVP_INFEASIBLE;
         *cost = 1e300;
+        if (xf) memset(xf, 0, sizeof(double) * 2 * (N + 1));
+        if (xb) memset(xb, 0, sizeof(double) * 2 * (N + 1));
         return;
     }
     const Node& c = lvl[win];
@@ -247,21 +264,39 @@ void solve_one_bnb(const hvp_system& S, const hvp::Consts& C, int role, const do
         x[k + 1] = p;
         x[N + 1 + k + 1] = v;
     }
+    if (C.form == HVP_FORM_ADMM) {
+        const bool on[2] = {(role & HVP_ROLE_SAFE_FRONT) != 0, (role & HVP_ROLE_SAFE_BACK) != 0};
+        const bool tr[2] = {(role & HVP_ROLE_TRACK_FRONT) != 0, (role & HVP_ROLE_TRACK_BACK) != 0};
+        double* outs[2] = {xf, xb};
+        for (int side = 0; side < 2; ++side) {
+            if (!outs[side]) continue;
+            for (int k = 0; k <= N; ++k) {
+                double e = 0.0, g = 0.0;
+                if (on[side])
+                    hvp::admm_copy_value(C, tr[side], side, hvp::admm_y(prm, side, N)[k],
+                                         hvp::admm_y(prm, side, N)[N + 1 + k], hvp::admm_z(prm, side, N)[k],
+                                         hvp::admm_z(prm, side, N)[N + 1 + k], x[k], x[N + 1 + k], &e, &g);
+                outs[side][k] = e;
+                outs[side][N + 1 + k] = g;
+            }
+        }
+    }
 }
 
 template <int N>
 void solve_range(const hvp_problem& P, const hvp_system* systems, int B, const int32_t* sys, const int32_t* role,
                  const double* params, double* u, double* x, int8_t* region, double* cost, int32_t* status,
-                 int32_t* nodes, int32_t* iters, int nthreads) {
+                 int32_t* nodes, int32_t* iters, int nthreads, double* xf = nullptr, double* xb = nullptr) {
     const hvp::Consts C = make_consts(P);
-    const int stride = hvp_params_stride(N);
+    const int stride = C.stride;
 #pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1)
     for (int i = 0; i < B; ++i) {
         const bool bnb = P.method == HVP_METHOD_BNB || (P.method == HVP_METHOD_AUTO && N > kAutoEnumMaxN);
-        if (bnb || N > HVP_MAX_N_ENUM) {
+        if (bnb || N > HVP_MAX_N_ENUM || C.form == HVP_FORM_ADMM) {
             solve_one_bnb<N>(systems[sys[i]], C, role[i], params + (size_t)i * stride, u + (size_t)i * N,
                              x + (size_t)i * 2 * (N + 1), region + (size_t)i * N, cost + i, status + i, nodes + i,
-                             iters + i);
+                             iters + i, xf ? xf + (size_t)i * 2 * (N + 1) : nullptr,
+                             xb ? xb + (size_t)i * 2 * (N + 1) : nullptr);
             continue;
         }
         if constexpr (N <= HVP_MAX_N_ENUM)
@@ -291,6 +326,22 @@ int hvp_hostref_solve_batch(const hvp_problem* P, const hvp_system* systems, int
     switch (P->N) {
 #define HVP_CASE(n) \
     case n: solve_range<n>(*P, systems, B, sys, role, params, u, x, region, cost, status, nodes, iters, nthreads); return 0;
+        HVP_CASE(2) HVP_CASE(3) HVP_CASE(4) HVP_CASE(5) HVP_CASE(6) HVP_CASE(7) HVP_CASE(8)
+        HVP_CASE(9) HVP_CASE(10) HVP_CASE(11) HVP_CASE(12) HVP_CASE(13) HVP_CASE(14) HVP_CASE(15) HVP_CASE(16)
+#undef HVP_CASE
+        default: return HVP_E_UNSUPPORTED;
+    }
+}
+
+// HVP_FORM_ADMM problems with the optimal neighbour copies (test / baseline use only).
+int hvp_hostref_solve_admm_batch(const hvp_problem* P, const hvp_system* systems, int B, const int32_t* sys,
+                                 const int32_t* role, const double* params, double* u, double* x, int8_t* region,
+                                 double* cost, int32_t* status, int32_t* nodes, int32_t* iters, double* xf,
+                                 double* xb, int nthreads) {
+    if (P->formulation != HVP_FORM_ADMM) return HVP_E_ARG;
+    switch (P->N) {
+#define HVP_CASE(n) \
+    case n: solve_range<n>(*P, systems, B, sys, role, params, u, x, region, cost, status, nodes, iters, nthreads, xf, xb); return 0;
         HVP_CASE(2) HVP_CASE(3) HVP_CASE(4) HVP_CASE(5) HVP_CASE(6) HVP_CASE(7) HVP_CASE(8)
         HVP_CASE(9) HVP_CASE(10) HVP_CASE(11) HVP_CASE(12) HVP_CASE(13) HVP_CASE(14) HVP_CASE(15) HVP_CASE(16)
 #undef HVP_CASE

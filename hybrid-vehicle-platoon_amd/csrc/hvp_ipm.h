@@ -49,6 +49,9 @@ struct Consts {
     double tol;
     int max_iter;
     int N;
+    int form;      // HVP_FORM_*
+    int stride;    // parameter block stride (doubles)
+    double rho;    // ADMM penalty
 };
 
 struct QpOut {

@@ -28,6 +28,7 @@
 
 #define HVP_HD __host__ __device__
 #include "hvp.h"
+#include "hvp_admm.h"
 #include "hvp_bnb.h"
 #include "hvp_gi.h"
 #include "hvp_ipm.h"
@@ -126,6 +127,9 @@ hvp::Consts make_consts(const hvp_problem& p) {
     C.tol = p.tol > 0 ? p.tol : 1e-12;
     C.max_iter = p.max_iter > 0 ? p.max_iter : 60;
     C.N = p.N;
+    C.form = p.formulation;
+    C.stride = p.formulation == HVP_FORM_ADMM ? hvp_params_stride_admm(p.N) : hvp_params_stride(p.N);
+    C.rho = p.rho;
     return C;
 }
 
@@ -356,10 +360,15 @@ __device__ inline double inc_of(const Workspace& ws, int inst) { return __longlo
 template <int N, int BS>
 __device__ inline int bnb_qp(hvp::LaneQp<N, LdsMem<N, BS>>& q, const hvp_system& S, const hvp::Consts& C, int rl,
                              const double* prm, uint64_t code, int K, double& cost) {
-    hvp::setup_lane<N>(q, S, C, rl, prm, code, K);
-    int it = 0;
-    const int st = hvp::solve_gi<N>(q, C, kGiMaxIter<N>, it);
-    cost = st == hvp::GI_OK ? hvp::direct_cost<N>(q, S, C, rl, prm, code, K) : 0.0;
+    int it = 0, st;
+    if (C.form == HVP_FORM_ADMM) {
+        st = hvp::solve_admm_lane<N>(q, S, C, rl, prm, code, K, kGiMaxIter<N>, it);
+        cost = st == hvp::GI_OK ? hvp::admm_direct_cost<N>(q, S, C, rl, prm, code, K) : 0.0;
+    } else {
+        hvp::setup_lane<N>(q, S, C, rl, prm, code, K);
+        st = hvp::solve_gi<N>(q, C, kGiMaxIter<N>, it);
+        cost = st == hvp::GI_OK ? hvp::direct_cost<N>(q, S, C, rl, prm, code, K) : 0.0;
+    }
     return st == hvp::GI_OK ? it : -1 - it;
 }
 
@@ -375,7 +384,7 @@ __global__ __launch_bounds__(kBnbBlock<N>) void k_bnb_root(int B, const hvp_syst
     if (i >= B) return;
     const hvp_system& S = systems[sys[i]];
     const int rl = role[i];
-    const double* prm = params + (size_t)i * (2 + 6 * (N + 1));
+    const double* prm = params + (size_t)i * C.stride;
     const double v0 = prm[1], P1 = prm[0] + S.ts * v0;
     const bool ok = P1 >= S.pmin - 1e-9 * (1.0 + fabs(S.pmin)) && P1 <= S.pmax + 1e-9 * (1.0 + fabs(S.pmax));
     ws.key[i] = ~0ull;
@@ -493,7 +502,7 @@ __global__ __launch_bounds__(kBnbBlock<N>) void k_bnb_bound(int k, const hvp_sys
         const uint64_t code = ws.nd_code[dst][t];
         const hvp_system& S = systems[sys[inst]];
         const int rl = role[inst];
-        const double* prm = params + (size_t)inst * (2 + 6 * (N + 1));
+        const double* prm = params + (size_t)inst * C.stride;
         hvp::LaneQp<N, LdsMem<N, BS>> q;
         q.mem.lane = threadIdx.x;
         double c;
@@ -519,7 +528,7 @@ __global__ __launch_bounds__(kBnbBlock<N>) void k_bnb_bound(int k, const hvp_sys
             } else {
                 ++fails;
                 atomicOr(&ws.inst_flag[inst], 8);  // a velocity-feasible sequence exists
-                if (N <= HVP_MAX_N_ENUM) {  // the interior-point fallback (K_bnb_ipm) re-solves it
+                if (N <= HVP_MAX_N_ENUM && C.form == HVP_FORM_DECENT) {  // K_bnb_ipm re-solves it
                     const unsigned long long r = atomicAdd(&ws.counter[2], 1ull);
                     if (r < (unsigned long long)ws.cap) ws.redo[r] = (int32_t)t;
                 }
@@ -551,7 +560,7 @@ __global__ __launch_bounds__(kBnbBlock<N>) void k_bnb_ipm(const hvp_system* __re
         const uint64_t code = ws.nd_code[src][t];
         const hvp_system& S = systems[sys[inst]];
         const int rl = role[inst];
-        const double* prm = params + (size_t)inst * (2 + 6 * (N + 1));
+        const double* prm = params + (size_t)inst * C.stride;
         hvp::LaneQp<N, LdsMem<N, BS>> q;
         q.mem.lane = threadIdx.x;
         hvp::setup_lane<N>(q, S, C, rl, prm, code);
@@ -569,7 +578,7 @@ __global__ __launch_bounds__(kBnbBlock<N>) void k_bnb_ipm(const hvp_system* __re
 
 // tie rule: the lexicographically first leaf within 1e-9 relative of the minimum
 template <int N>
-__global__ __launch_bounds__(kBlock) void k_bnb_key(Workspace ws) {
+__global__ __launch_bounds__(kBlock) void k_bnb_key(Workspace ws, int form) {
     const int src = N & 1;
     const unsigned long long nn = ws.lvl[N];
     const long long total = (long long)(nn < (unsigned long long)ws.cap ? nn : ws.cap);
@@ -583,7 +592,8 @@ __global__ __launch_bounds__(kBlock) void k_bnb_key(Workspace ws) {
             // fallback is an infeasible QP (position box), excluded exactly as the enumeration
             // path and the oracle exclude it.  Beyond, there is no fallback: a failed leaf still
             // in contention makes the instance MAXITER rather than a possibly wrong answer.
-            if (N > HVP_MAX_N_ENUM && !hvp::bnb_pruned(ws.nd_lb[src][t], best)) atomicOr(&ws.inst_flag[inst], 4);
+            if ((N > HVP_MAX_N_ENUM || form != HVP_FORM_DECENT) && !hvp::bnb_pruned(ws.nd_lb[src][t], best))
+                atomicOr(&ws.inst_flag[inst], 4);
             continue;
         }
         if (ws.nd_lb[src][t] <= best + 1e-9 * fmax(1.0, fabs(best)))
@@ -617,13 +627,44 @@ __device__ inline void write_solution(int i, const hvp_system& S, const double* 
     }
 }
 
+// optimal neighbour copies of an ADMM solution (fleet_naive_admm.py: mpc.x_front.X / x_back.X)
+template <int N>
+__device__ inline void write_copies(int i, const hvp_system& S, const hvp::Consts& C, int rl, const double* prm,
+                                    bool win, const double* y, double* xf_out, double* xb_out) {
+    const bool side_on[2] = {(rl & HVP_ROLE_SAFE_FRONT) != 0, (rl & HVP_ROLE_SAFE_BACK) != 0};
+    const bool track[2] = {(rl & HVP_ROLE_TRACK_FRONT) != 0, (rl & HVP_ROLE_TRACK_BACK) != 0};
+    double* outs[2] = {xf_out, xb_out};
+    const int K1 = N + 1;
+    for (int side = 0; side < 2; ++side) {
+        double* o = outs[side];
+        if (!o) continue;
+        o += (size_t)i * 2 * K1;
+        double p = prm[0], v = prm[1];
+        for (int k = 0; k <= N; ++k) {
+            double e = 0.0, g = 0.0;
+            if (win && side_on[side])
+                hvp::admm_copy_value(C, track[side], side, hvp::admm_y(prm, side, N)[k],
+                                     hvp::admm_y(prm, side, N)[K1 + k], hvp::admm_z(prm, side, N)[k],
+                                     hvp::admm_z(prm, side, N)[K1 + k], p, v, &e, &g);
+            o[k] = e;
+            o[K1 + k] = g;
+            if (k < N) {
+                p = p + S.ts * v;
+                v = win ? y[k] : v;
+            }
+        }
+    }
+}
+
 template <int N>
 __global__ __launch_bounds__(kBlock) void k_bnb_write(const hvp_system* __restrict__ systems,
                                                       const int32_t* __restrict__ sys,
-                                                      const double* __restrict__ params, Workspace ws,
+                                                      const int32_t* __restrict__ role,
+                                                      const double* __restrict__ params, hvp::Consts C, Workspace ws,
                                                       double* __restrict__ u_out, double* __restrict__ x_out,
                                                       int8_t* __restrict__ region_out, int8_t* __restrict__ gear_out,
-                                                      double* __restrict__ cost_out) {
+                                                      double* __restrict__ cost_out, double* __restrict__ xf_out,
+                                                      double* __restrict__ xb_out) {
     const int src = N & 1;
     const unsigned long long nn = ws.lvl[N];
     const long long total = (long long)(nn < (unsigned long long)ws.cap ? nn : ws.cap);
@@ -638,8 +679,9 @@ __global__ __launch_bounds__(kBlock) void k_bnb_write(const hvp_system* __restri
         double y[N];
 #pragma unroll
         for (int j = 0; j < N; ++j) y[j] = ws.task_y[t * N + j];
-        write_solution<N>(inst, S, params + (size_t)inst * (2 + 6 * (N + 1)), true, code, y, u_out, x_out,
-                          region_out, gear_out);
+        const double* prm = params + (size_t)inst * C.stride;
+        write_solution<N>(inst, S, prm, true, code, y, u_out, x_out, region_out, gear_out);
+        if (C.form == HVP_FORM_ADMM) write_copies<N>(inst, S, C, role[inst], prm, true, y, xf_out, xb_out);
         if (cost_out) cost_out[inst] = ws.nd_lb[src][t];
     }
 }
@@ -647,12 +689,14 @@ __global__ __launch_bounds__(kBlock) void k_bnb_write(const hvp_system* __restri
 template <int N>
 __global__ __launch_bounds__(kBlock) void k_bnb_finish(int B, const hvp_system* __restrict__ systems,
                                                        const int32_t* __restrict__ sys,
-                                                       const double* __restrict__ params, Workspace ws,
+                                                       const int32_t* __restrict__ role,
+                                                       const double* __restrict__ params, hvp::Consts C, Workspace ws,
                                                        double* __restrict__ u_out, double* __restrict__ x_out,
                                                        int8_t* __restrict__ region_out, int8_t* __restrict__ gear_out,
                                                        double* __restrict__ cost_out, int32_t* __restrict__ status_out,
                                                        int32_t* __restrict__ nodes_out,
-                                                       int32_t* __restrict__ iters_out) {
+                                                       int32_t* __restrict__ iters_out,
+                                                       double* __restrict__ xf_out, double* __restrict__ xb_out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= B) return;
     const int flag = ws.inst_flag[i];
@@ -668,8 +712,9 @@ __global__ __launch_bounds__(kBlock) void k_bnb_finish(int B, const hvp_system* 
     if (iters_out) iters_out[i] = ws.iters[i];
     if (!win || status != HVP_OPTIMAL) {
         if (cost_out) cost_out[i] = 1e300;
-        write_solution<N>(i, systems[sys[i]], params + (size_t)i * (2 + 6 * (N + 1)), false, 0, nullptr, u_out, x_out,
-                          region_out, gear_out);
+        const double* prm = params + (size_t)i * C.stride;
+        write_solution<N>(i, systems[sys[i]], prm, false, 0, nullptr, u_out, x_out, region_out, gear_out);
+        if (C.form == HVP_FORM_ADMM) write_copies<N>(i, systems[sys[i]], C, role[i], prm, false, nullptr, xf_out, xb_out);
     }
 }
 
@@ -731,12 +776,60 @@ __global__ __launch_bounds__(kBlock) void k_evaluate(int B, const hvp_system* __
     status_out[i] = ok ? HVP_OPTIMAL : HVP_INFEASIBLE;
 }
 
+// ================================================================== ADMM consensus update
+// ADMMCoordinator.get_control z/y update (fleet_naive_admm.py:421-468), one thread per
+// (platoon, vehicle, state entry).  Thread (p, i, e) recomputes z of i-1, i, i+1 (3 loads each),
+// so the y-updates and the next parameter blocks of vehicle i need no second pass:
+//   y_front_i += rho (xf_i - z_{i-1}),  y_back_i += rho (xb_i - z_{i+1}),
+//   params_i: y_front_i, z_front = z_{i-1}, y_back_i, z_back = z_{i+1}.
+__device__ inline double admm_z_of(int i, int n, const double* x, const double* xf, const double* xb, size_t base,
+                                   int stride2, int e) {
+    // base = platoon's first instance; entries of instance j at (base + j) * stride2 + e
+    double s = x[(base + i) * stride2 + e];
+    int cnt = 1;
+    if (i + 1 < n) { s += xf[(base + i + 1) * stride2 + e]; ++cnt; }
+    if (i >= 1) { s += xb[(base + i - 1) * stride2 + e]; ++cnt; }
+    return cnt == 3 ? s * (1.0 / 3.0) : (cnt == 2 ? 0.5 * s : s);
+}
+
+__global__ __launch_bounds__(kBlock) void k_admm_update(int P, int n, int N, double rho, int pstride,
+                                                        const double* __restrict__ x, const double* __restrict__ xf,
+                                                        const double* __restrict__ xb, double* __restrict__ y_front,
+                                                        double* __restrict__ y_back, double* __restrict__ params,
+                                                        double* __restrict__ z_out) {
+    const int E = 2 * (N + 1);
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (long long)P * n * E) return;
+    const int e = (int)(t % E);
+    const long long inst = t / E;
+    const int i = (int)(inst % n);
+    const size_t base = (size_t)(inst - i);
+    const double zi = admm_z_of(i, n, x, xf, xb, base, E, e);
+    if (z_out) z_out[inst * E + e] = zi;
+    double* prm = params + inst * pstride;
+    if (i >= 1) {
+        const double zm = admm_z_of(i - 1, n, x, xf, xb, base, E, e);
+        const double yf = y_front[inst * E + e] + rho * (xf[inst * E + e] - zm);
+        y_front[inst * E + e] = yf;
+        prm[2 + e] = yf;
+        prm[2 + E + e] = zm;
+    }
+    if (i + 1 < n) {
+        const double zp = admm_z_of(i + 1, n, x, xf, xb, base, E, e);
+        const double yb = y_back[inst * E + e] + rho * (xb[inst * E + e] - zp);
+        y_back[inst * E + e] = yb;
+        prm[2 + 2 * E + e] = yb;
+        prm[2 + 3 * E + e] = zp;
+    }
+}
+
 int grid_for(long long n) { return (int)std::max<long long>(1, (n + kBlock - 1) / kBlock); }
 
 template <int N>
 int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, const double* params, double* u_out,
                double* x_out, int8_t* region_out, int8_t* gear_out, double* cost_out, int32_t* status_out,
-               int32_t* nodes_out, int32_t* iters_out, hipStream_t st) {
+               int32_t* nodes_out, int32_t* iters_out, hipStream_t st, double* xf_out = nullptr,
+               double* xb_out = nullptr) {
     Workspace ws = h->ws;
     constexpr int BS = kBnbBlock<N>;
     HIP_TRY(hipMemsetAsync(ws.counter, 0, 8 * sizeof(unsigned long long), st));
@@ -763,17 +856,19 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
     }
     HIP_TRY(hipEventRecord(h->evq1, st));
     if constexpr (N <= HVP_MAX_N_ENUM) {
+        if (h->C.form == HVP_FORM_DECENT)
         hipLaunchKernelGGL(k_bnb_ipm<N>, dim3(std::max(1, h->n_cu)), dim3(BS), lds, st, h->d_sys, sys, role, params,
                            h->C, ws);
         HIP_TRY(hipGetLastError());
     }
-    hipLaunchKernelGGL(k_bnb_key<N>, dim3(g_small), dim3(kBlock), 0, st, ws);
+    hipLaunchKernelGGL(k_bnb_key<N>, dim3(g_small), dim3(kBlock), 0, st, ws, h->C.form);
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_bnb_write<N>, dim3(g_small), dim3(kBlock), 0, st, h->d_sys, sys, params, ws, u_out, x_out,
-                       region_out, gear_out, cost_out);
+    hipLaunchKernelGGL(k_bnb_write<N>, dim3(g_small), dim3(kBlock), 0, st, h->d_sys, sys, role, params, h->C, ws,
+                       u_out, x_out, region_out, gear_out, cost_out, xf_out, xb_out);
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_bnb_finish<N>, dim3(grid_for(B)), dim3(kBlock), 0, st, B, h->d_sys, sys, params, ws, u_out,
-                       x_out, region_out, gear_out, cost_out, status_out, nodes_out, iters_out);
+    hipLaunchKernelGGL(k_bnb_finish<N>, dim3(grid_for(B)), dim3(kBlock), 0, st, B, h->d_sys, sys, role, params, h->C,
+                       ws, u_out, x_out, region_out, gear_out, cost_out, status_out, nodes_out, iters_out, xf_out,
+                       xb_out);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(h->ev1, st));
     h->last_stream = st;
@@ -905,6 +1000,12 @@ int hvp_create(hvp_handle** out, const hvp_problem* problem, const hvp_system* s
     if (problem->method == HVP_METHOD_ENUMERATE && problem->N > HVP_MAX_N_ENUM)
         return fail(HVP_E_UNSUPPORTED, "hvp_create: enumeration supports N <= " + std::to_string(HVP_MAX_N_ENUM) +
                                            " (use HVP_METHOD_BNB)");
+    if (problem->formulation != HVP_FORM_DECENT && problem->formulation != HVP_FORM_ADMM)
+        return fail(HVP_E_ARG, "hvp_create: unknown formulation");
+    if (problem->formulation == HVP_FORM_ADMM && problem->method == HVP_METHOD_ENUMERATE)
+        return fail(HVP_E_UNSUPPORTED, "hvp_create: the ADMM formulation is solved by branch and bound only");
+    if (problem->formulation == HVP_FORM_ADMM && !(problem->rho > 0))
+        return fail(HVP_E_ARG, "hvp_create: the ADMM formulation needs rho > 0");
     if (problem->quadratic_cost != 1)
         return fail(HVP_E_UNSUPPORTED, "hvp_create: only the quadratic cost (min_2_norm) runs on the GPU");
     for (int i = 0; i < n_systems; ++i) {
@@ -976,9 +1077,32 @@ int hvp_reserve(hvp_handle* h, int max_batch, int64_t cap) {
     return 0;
 }
 
+static int solve_impl(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, const double* params,
+                      double* u_out, double* x_out, int8_t* region_out, int8_t* gear_out, double* cost_out,
+                      int32_t* status_out, int32_t* nodes_out, int32_t* iters_out, void* stream, double* xf_out,
+                      double* xb_out);
+
 int hvp_solve_batch(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, const double* params,
                     double* u_out, double* x_out, int8_t* region_out, int8_t* gear_out, double* cost_out,
                     int32_t* status_out, int32_t* nodes_out, int32_t* iters_out, void* stream) {
+    return solve_impl(h, B, sys, role, params, u_out, x_out, region_out, gear_out, cost_out, status_out, nodes_out,
+                      iters_out, stream, nullptr, nullptr);
+}
+
+int hvp_solve_admm_batch(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, const double* params,
+                         double* u_out, double* x_out, int8_t* region_out, int8_t* gear_out, double* cost_out,
+                         int32_t* status_out, int32_t* nodes_out, int32_t* iters_out, double* xf_out, double* xb_out,
+                         void* stream) {
+    if (h && h->prob.formulation != HVP_FORM_ADMM)
+        return fail(HVP_E_ARG, "hvp_solve_admm_batch: the handle is not an HVP_FORM_ADMM problem");
+    return solve_impl(h, B, sys, role, params, u_out, x_out, region_out, gear_out, cost_out, status_out, nodes_out,
+                      iters_out, stream, xf_out, xb_out);
+}
+
+static int solve_impl(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, const double* params,
+                      double* u_out, double* x_out, int8_t* region_out, int8_t* gear_out, double* cost_out,
+                      int32_t* status_out, int32_t* nodes_out, int32_t* iters_out, void* stream, double* xf_out,
+                      double* xb_out) {
     if (!h || B < 0 || (B > 0 && (!sys || !role || !params || !cost_out || !status_out)))
         return fail(HVP_E_ARG, "hvp_solve_batch: bad argument");
     if (B == 0) return 0;
@@ -991,7 +1115,7 @@ int hvp_solve_batch(hvp_handle* h, int B, const int32_t* sys, const int32_t* rol
     if (h->bnb) {
         switch (h->prob.N) {
 #define HVP_CASE(n) \
-    case n: return launch_bnb<n>(h, B, sys, role, params, u_out, x_out, region_out, gear_out, cost_out, status_out, nodes_out, iters_out, st);
+    case n: return launch_bnb<n>(h, B, sys, role, params, u_out, x_out, region_out, gear_out, cost_out, status_out, nodes_out, iters_out, st, xf_out, xb_out);
             HVP_CASE(2) HVP_CASE(3) HVP_CASE(4) HVP_CASE(5) HVP_CASE(6) HVP_CASE(7) HVP_CASE(8)
             HVP_CASE(9) HVP_CASE(10) HVP_CASE(11) HVP_CASE(12) HVP_CASE(13) HVP_CASE(14) HVP_CASE(15) HVP_CASE(16)
 #undef HVP_CASE
@@ -1012,6 +1136,8 @@ int hvp_evaluate_batch(hvp_handle* h, int B, const int32_t* sys, const int32_t* 
                        void* stream) {
     if (!h || B < 0 || (B > 0 && (!sys || !role || !params || !gear_in || !u_in || !cost_out || !status_out)))
         return fail(HVP_E_ARG, "hvp_evaluate_batch: bad argument");
+    if (h->prob.formulation != HVP_FORM_DECENT)
+        return fail(HVP_E_UNSUPPORTED, "hvp_evaluate_batch: HVP_FORM_DECENT problems only");
     if (B == 0) return 0;
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t st = (hipStream_t)stream;
@@ -1026,6 +1152,22 @@ int hvp_evaluate_batch(hvp_handle* h, int B, const int32_t* sys, const int32_t* 
 #undef HVP_CASE
         default: return fail(HVP_E_UNSUPPORTED, "hvp_evaluate_batch: unsupported N");
     }
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int hvp_admm_update(hvp_handle* h, int P, int n, const double* x, const double* xf, const double* xb,
+                    double* y_front, double* y_back, double* params, double* z_out, void* stream) {
+    if (!h || P < 0 || n < 1 || (P > 0 && (!x || !xf || !xb || !y_front || !y_back || !params)))
+        return fail(HVP_E_ARG, "hvp_admm_update: bad argument");
+    if (h->prob.formulation != HVP_FORM_ADMM)
+        return fail(HVP_E_ARG, "hvp_admm_update: the handle is not an HVP_FORM_ADMM problem");
+    if (P == 0) return 0;
+    HIP_TRY(hipSetDevice(h->device));
+    const int N = h->prob.N;
+    const long long total = (long long)P * n * 2 * (N + 1);
+    hipLaunchKernelGGL(k_admm_update, dim3(grid_for(total)), dim3(kBlock), 0, (hipStream_t)stream, P, n, N,
+                       h->prob.rho, h->C.stride, x, xf, xb, y_front, y_back, params, z_out);
     HIP_TRY(hipGetLastError());
     return 0;
 }
@@ -1079,7 +1221,7 @@ int hvp_solve_batch_host(hvp_handle* h, int B, const int32_t* sys, const int32_t
     if (!h || B < 0) return fail(HVP_E_ARG, "hvp_solve_batch_host: bad argument");
     if (B == 0) return 0;
     const int N = h->prob.N;
-    const size_t P = (2 + 6 * (N + 1));
+    const size_t P = (size_t)h->C.stride;
     // staging layout (8-byte aligned pieces)
     const size_t s_sys = sizeof(int32_t) * B, s_role = s_sys, s_prm = sizeof(double) * P * B;
     const size_t s_u = sizeof(double) * N * B, s_x = sizeof(double) * 2 * (N + 1) * B;

@@ -15,6 +15,7 @@ MAX_N_ENUM = 8
 ABI_VERSION = 2
 
 METHOD_AUTO, METHOD_ENUMERATE, METHOD_BNB = 0, 1, 2
+FORM_DECENT, FORM_ADMM = 0, 1
 
 ROLE_SAFE_FRONT = 1
 ROLE_SAFE_BACK = 2
@@ -67,6 +68,9 @@ class HvpProblem(ctypes.Structure):
         ("max_iter", ctypes.c_int32),
         ("method", ctypes.c_int32),
         ("tol", ctypes.c_double),
+        ("formulation", ctypes.c_int32),
+        ("pad_", ctypes.c_int32),
+        ("rho", ctypes.c_double),
     ]
 
 
@@ -83,8 +87,8 @@ class HvpStats(ctypes.Structure):
     ]
 
 
-def params_stride(N: int) -> int:
-    return 2 + 6 * (N + 1)
+def params_stride(N: int, formulation: int = 0) -> int:
+    return 2 + (10 if formulation == FORM_ADMM else 6) * (N + 1)
 
 
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -108,6 +112,8 @@ EXPORTS = {
     "hvp_solve_batch_host": ([_P, ctypes.c_int, _I32P, _I32P, _DP, _DP, _DP, _I8P, _I8P, _DP, _I32P, _I32P,
                               _I32P], ctypes.c_int),
     "hvp_evaluate_batch": ([_P, ctypes.c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
+    "hvp_solve_admm_batch": ([_P, ctypes.c_int] + [_P] * 14, ctypes.c_int),
+    "hvp_admm_update": ([_P, ctypes.c_int, ctypes.c_int] + [_P] * 8, ctypes.c_int),
     "hvp_sync": ([_P, _P], ctypes.c_int),
     "hvp_get_stats": ([_P, ctypes.POINTER(HvpStats)], ctypes.c_int),
     "hvp_destroy": ([_P], None),

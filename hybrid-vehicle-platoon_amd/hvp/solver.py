@@ -65,7 +65,7 @@ class BatchSolver:
 
     @property
     def params_stride(self) -> int:
-        return _abi.params_stride(self.N)
+        return _abi.params_stride(self.N, int(self.problem.formulation))
 
     def stats(self) -> _abi.HvpStats:
         s = _abi.HvpStats()
@@ -210,3 +210,53 @@ class BatchSolver:
                                    t(u, torch.float64).reshape(B, self.N))
         torch.cuda.synchronize(dev)
         return {k: v.cpu().numpy() for k, v in out.items()}
+
+    # -------------------------------------------------------------- ADMM formulation
+    def solve_admm_device(self, sys_idx, roles, params, out: dict, stream=None) -> dict:
+        """hvp_solve_admm_batch on device tensors; ``out`` also needs "x_front", "x_back"."""
+        import torch
+
+        B = int(roles.shape[0])
+        if params.numel() != B * self.params_stride:
+            raise ValueError("params must be (B, hvp_params_stride_admm)")
+        if stream is None:
+            stream = torch.cuda.current_stream(params.device)
+        ptr = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        rc = self._lib.hvp_solve_admm_batch(
+            self._h, B, ptr(sys_idx), ptr(roles), ptr(params), ptr(out["u"]), ptr(out["x"]), ptr(out["region"]),
+            ptr(out["gear"]), ptr(out["cost"]), ptr(out["status"]), ptr(out["nodes"]), ptr(out["iters"]),
+            ptr(out["x_front"]), ptr(out["x_back"]), ctypes.c_void_p(stream.cuda_stream))
+        _abi.check(rc, "hvp_solve_admm_batch")
+        return out
+
+    def admm_update(self, P: int, n: int, x, xf, xb, y_front, y_back, params, z=None, stream=None) -> None:
+        """hvp_admm_update: z / y update and next parameter blocks (device tensors, async)."""
+        import torch
+
+        if stream is None:
+            stream = torch.cuda.current_stream(params.device)
+        ptr = lambda t: ctypes.c_void_p(t.data_ptr() if t is not None else 0)  # noqa: E731
+        rc = self._lib.hvp_admm_update(self._h, int(P), int(n), ptr(x), ptr(xf), ptr(xb), ptr(y_front), ptr(y_back),
+                                       ptr(params), ptr(z), ctypes.c_void_p(stream.cuda_stream))
+        _abi.check(rc, "hvp_admm_update")
+
+    def solve_admm(self, sys_idx, roles, params) -> BatchResult:
+        """Host-array form of :meth:`solve_admm_device` (synchronous); the result also carries
+        x_front / x_back (B, 2, N+1)."""
+        import torch
+
+        dev = torch.device("cuda", self.device)
+        roles = np.asarray(roles, np.int32).reshape(-1)
+        B = len(roles)
+        t = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a), dtype=dt).to(dev)  # noqa: E731
+        out = self.alloc_outputs(B, dev)
+        out["x_front"] = torch.zeros((B, 2, self.N + 1), dtype=torch.float64, device=dev)
+        out["x_back"] = torch.zeros((B, 2, self.N + 1), dtype=torch.float64, device=dev)
+        self.solve_admm_device(t(np.asarray(sys_idx).reshape(-1), torch.int32), t(roles, torch.int32),
+                               t(np.asarray(params).reshape(B, -1), torch.float64), out)
+        torch.cuda.synchronize(dev)
+        h = {k: v.cpu().numpy() for k, v in out.items()}
+        res = BatchResult(u=h["u"], x=h["x"], region=h["region"], gear=h["gear"], cost=h["cost"], status=h["status"],
+                          nodes=h["nodes"], iters=h["iters"])
+        res.x_front, res.x_back = h["x_front"], h["x_back"]
+        return res

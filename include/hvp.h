@@ -81,7 +81,17 @@ typedef struct hvp_problem {
     int32_t max_iter;       /* fallback IPM iteration cap per candidate (<=0: 60)      */
     int32_t method;         /* HVP_METHOD_*: how the region sequences are searched     */
     double tol;             /* fallback IPM relative tolerance (<=0: 1e-12)            */
+    int32_t formulation;    /* HVP_FORM_*: which local MPC (parameter layout, cost)    */
+    int32_t pad_;
+    double rho;             /* ADMM penalty (HVP_FORM_ADMM; fleet_naive_admm.py:600)   */
 } hvp_problem;
+
+/* Local MPC formulation (hvp_problem.formulation). */
+enum {
+    HVP_FORM_DECENT = 0, /* LocalMpcMld (fleet_decent_mld.py:21-223): fixed neighbour predictions   */
+    HVP_FORM_ADMM = 1    /* LocalMpcADMM (fleet_naive_admm.py:24-253): neighbour COPIES as decision
+                            variables with ADMM terms y'(c - z) + rho/2 |c - z|^2; needs B&B      */
+};
 
 /* Search over the region sequences (hvp_problem.method).  Both give the same sequence: the
  * exact argmin with ties to the lexicographically first sequence (DESIGN.md "Algorithm"). */
@@ -126,6 +136,11 @@ enum {
  * Blocks a role does not use are ignored. */
 static inline int hvp_params_stride(int N) { return 2 + 6 * (N + 1); }
 
+/* HVP_FORM_ADMM parameter block, stride hvp_params_stride_admm(N) doubles:
+ *   [0..1] x0 | y_front | z_front | y_back | z_back | leader_x   (each (2, N+1) row-major)
+ * (set_front_vars / set_back_vars / set_leader_x, fleet_naive_admm.py:239-258). */
+static inline int hvp_params_stride_admm(int N) { return 2 + 10 * (N + 1); }
+
 typedef struct hvp_handle hvp_handle;
 
 typedef struct hvp_stats {
@@ -152,6 +167,24 @@ int hvp_solve_batch_host(hvp_handle* h, int B, const int32_t* sys, const int32_t
                          const double* params, double* u_out, double* x_out,
                          int8_t* region_out, int8_t* gear_out, double* cost_out,
                          int32_t* status_out, int32_t* nodes_out, int32_t* iters_out);
+/* HVP_FORM_ADMM solve: as hvp_solve_batch, plus the optimal neighbour copies the coordinator
+ * reads as mpc.x_front.X / mpc.x_back.X (fleet_naive_admm.py:413-446): xf_out, xb_out
+ * [B][2][N+1] (may be NULL; zero for a side the role does not have). */
+int hvp_solve_admm_batch(hvp_handle* h, int B, const int32_t* sys, const int32_t* role,
+                         const double* params, double* u_out, double* x_out, int8_t* region_out,
+                         int8_t* gear_out, double* cost_out, int32_t* status_out, int32_t* nodes_out,
+                         int32_t* iters_out, double* xf_out, double* xb_out, void* stream);
+
+/* ADMM z- and y-update of ADMMCoordinator.get_control (fleet_naive_admm.py:421-468) for P
+ * platoons of n vehicles (instance p*n + i), device pointers, async on stream:
+ *   z_i = mean of x_i, vehicle (i+1)'s front copy and vehicle (i-1)'s back copy;
+ *   y_front_{i+1} += rho (xf_{i+1} - z_i);  y_back_{i-1} += rho (xb_{i-1} - z_i);
+ * then writes every vehicle's next parameter blocks  (y_front_i, z_{i-1}) and (y_back_i, z_{i+1})
+ * into params (HVP_FORM_ADMM layout) and z into z_out [P*n][2][N+1] (may be NULL).
+ * y_front / y_back [P*n][2][N+1] are updated in place. */
+int hvp_admm_update(hvp_handle* h, int P, int n, const double* x, const double* xf, const double* xb,
+                    double* y_front, double* y_back, double* params, double* z_out, void* stream);
+
 /* Cost of FIXED controls (device pointers, async on stream): replaces MpcGear.evaluate_cost
  * (mpcs/mpc_gear.py:137-170).  gear_in[B][N] = gear label per step (for the 7-region gear model
  * the label of the region the velocity lies in), u_in[B][N] = the control (u_g for the gear

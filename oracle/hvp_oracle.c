@@ -55,6 +55,11 @@ typedef struct {
     int quadratic;
     double Qx[2][2], Qu, Qdu, w, a_acc, a_dec, ts, d_safe, tight, d0, t0;
     int role; /* HVP_ROLE_* bits, see include/hvp.h */
+    /* naive ADMM local problem (fleet_naive_admm.py:24-253): the neighbour trajectories are
+     * decision variables (copies) with ADMM terms; y/z blocks (2, N+1) replace xf / xb */
+    int admm;
+    double rho;
+    const double *yf, *zf, *yb, *zb;
 } or_cfg;
 
 enum { R_SF = 1, R_SB = 2, R_TF = 4, R_TB = 8, R_TL = 16, R_LSP = 32 };
@@ -192,7 +197,12 @@ static int build_qp_k(or_qp* qp, const or_model* md, const or_cfg* cf, const int
     if (cf->role & R_SF) nz += N + 1;
     int sb0 = nz;
     if (cf->role & R_SB) nz += N + 1;
-    L.nsb_idx = nz; /* aux (L1) variables are appended after the slacks */
+    int cf_idx = -1, cb_idx = -1; /* ADMM copies x_front, x_back (2, N+1), fleet_naive_admm.py:84-102 */
+    if (cf->admm) {
+        if (cf->role & R_SF) { cf_idx = nz; nz += 2 * (N + 1); }
+        if (cf->role & R_SB) { cb_idx = nz; nz += 2 * (N + 1); }
+    }
+    L.nsb_idx = nz; /* aux (L1) variables are appended after the slacks (and copies) */
     L.naux = 0;
     int aux_needed = cf->quadratic ? 0 : (N + 1) * 2 * 3 + N * 2;
     if (nz + aux_needed > OR_MAX_NZ) return 0;
@@ -252,6 +262,10 @@ static int build_qp_k(or_qp* qp, const or_model* md, const or_cfg* cf, const int
             lin ns = lin_axpy(-1.0, &s, &(lin){.n = 0, .cst = 0.0});
             qp_add_le(qp, &ns, 0.0);
             lin e = lin_axpy(-1.0, &s, &pk); /* p_k - s_f <= pf_k - d_safe */
+            if (cf->admm) { /* pf_k is the copy's position (fleet_naive_admm.py:217-226) */
+                lin_add(&e, cf_idx + k, -1.0);
+                qp_add_le(qp, &e, -cf->d_safe);
+            } else
             qp_add_le(qp, &e, par(xf, N, 0, k) - cf->d_safe);
             lin ws = lin_axpy(cf->w, &s, &(lin){.n = 0, .cst = 0.0});
             qp_add_lin(qp, &ws);
@@ -262,6 +276,10 @@ static int build_qp_k(or_qp* qp, const or_model* md, const or_cfg* cf, const int
             lin ns = lin_axpy(-1.0, &s, &(lin){.n = 0, .cst = 0.0});
             qp_add_le(qp, &ns, 0.0);
             lin e = lin_axpy(-1.0, &pk, &ns); /* -p_k - s_b <= -(pb_k + d_safe) */
+            if (cf->admm) { /* (:227-236) */
+                lin_add(&e, cb_idx + k, 1.0);
+                qp_add_le(qp, &e, -cf->d_safe);
+            } else
             qp_add_le(qp, &e, -(par(xb, N, 0, k) + cf->d_safe));
             lin ws = lin_axpy(cf->w, &s, &(lin){.n = 0, .cst = 0.0});
             qp_add_lin(qp, &ws);
@@ -273,15 +291,40 @@ static int build_qp_k(or_qp* qp, const or_model* md, const or_cfg* cf, const int
         lin e[2];
         if (cf->role & R_TF) { /* x_k - xf_k - spacing(x_k) ; spacing(x) = [-d0 - t0 v, 0] */
             e[0] = lin_axpy(cf->t0, &v, &p);
-            e[0].cst += cf->d0 - par(xf, N, 0, k);
-            e[1] = v; e[1].cst -= par(xf, N, 1, k);
+            e[0].cst += cf->d0;
+            e[1] = v;
+            if (cf->admm) { lin_add(&e[0], cf_idx + k, -1.0); lin_add(&e[1], cf_idx + N + 1 + k, -1.0); }
+            else { e[0].cst -= par(xf, N, 0, k); e[1].cst -= par(xf, N, 1, k); }
             add_norm(qp, &L, cf, e, cf->Qx, 2);
         }
         if (cf->role & R_TB) { /* xb_k - x_k - spacing(xb_k) */
-            double pb = par(xb, N, 0, k), vb = par(xb, N, 1, k);
-            e[0] = lin_axpy(-1.0, &p, &(lin){.n = 0, .cst = pb + cf->d0 + cf->t0 * vb});
-            e[1] = lin_axpy(-1.0, &v, &(lin){.n = 0, .cst = vb});
+            if (cf->admm) {
+                e[0] = lin_axpy(-1.0, &p, &(lin){.n = 0, .cst = cf->d0});
+                lin_add(&e[0], cb_idx + k, 1.0);
+                lin_add(&e[0], cb_idx + N + 1 + k, cf->t0);
+                e[1] = lin_axpy(-1.0, &v, &(lin){.n = 0, .cst = 0.0});
+                lin_add(&e[1], cb_idx + N + 1 + k, 1.0);
+            } else {
+                double pb = par(xb, N, 0, k), vb = par(xb, N, 1, k);
+                e[0] = lin_axpy(-1.0, &p, &(lin){.n = 0, .cst = pb + cf->d0 + cf->t0 * vb});
+                e[1] = lin_axpy(-1.0, &v, &(lin){.n = 0, .cst = vb});
+            }
             add_norm(qp, &L, cf, e, cf->Qx, 2);
+        }
+        if (cf->admm) { /* y'(c - z) + rho/2 |c - z|^2 per copy (fleet_naive_admm.py:172-198) */
+            const int idx[2] = {cf_idx, cb_idx};
+            const double* yy[2] = {cf->yf, cf->yb};
+            const double* zz[2] = {cf->zf, cf->zb};
+            for (int side = 0; side < 2; ++side) {
+                if (idx[side] < 0) continue;
+                for (int i = 0; i < 2; ++i) {
+                    lin d = lin_const(-par(zz[side], N, i, k));
+                    lin_add(&d, idx[side] + i * (N + 1) + k, 1.0);
+                    qp_add_prod(qp, 0.5 * cf->rho, &d, &d);
+                    lin yd = lin_axpy(par(yy[side], N, i, k), &d, &(lin){.n = 0, .cst = 0.0});
+                    qp_add_lin(qp, &yd);
+                }
+            }
         }
         if (cf->role & R_TL) { /* x_k - xl_k (- spacing(x_k) for real_vehicle_as_reference) */
             if (cf->role & R_LSP) { e[0] = lin_axpy(cf->t0, &v, &p); e[0].cst += cf->d0; }
@@ -672,6 +715,22 @@ static double direct_objective_k(const or_cfg* cf, const double* x0, const doubl
                                  const double* xl, const double* z, int K) {
     const int N = cf->N;
     double J = 0.0;
+    if (cf->admm) { /* the copies are part of the solution; price their ADMM terms */
+        int idx = 3 * N + ((cf->role & R_SF) ? N + 1 : 0) + ((cf->role & R_SB) ? N + 1 : 0);
+        if (cf->role & R_SF) { xf = z + idx; idx += 2 * (N + 1); }
+        if (cf->role & R_SB) xb = z + idx;
+        const double* cc[2] = {(cf->role & R_SF) ? xf : NULL, (cf->role & R_SB) ? xb : NULL};
+        const double* yy[2] = {cf->yf, cf->yb};
+        const double* zz[2] = {cf->zf, cf->zb};
+        for (int side = 0; side < 2; ++side) {
+            if (!cc[side]) continue;
+            for (int k = 0; k <= N; ++k)
+                for (int i = 0; i < 2; ++i) {
+                    double d = par(cc[side], N, i, k) - par(zz[side], N, i, k);
+                    J += par(yy[side], N, i, k) * d + 0.5 * cf->rho * d * d;
+                }
+        }
+    }
     for (int k = 0; k <= N; ++k) {
         double p = k == 0 ? x0[0] : z[2 * (k - 1)], v = k == 0 ? x0[1] : z[2 * (k - 1) + 1];
         double e[3][2];
@@ -977,6 +1036,7 @@ static int unpack_model(or_model* md, int nreg, int nsr, const double* S, const 
 static void unpack_cfg(or_cfg* cf, int N, int quadratic, int role, const double* p) {
     /* p = [Qx00 Qx01 Qx10 Qx11 Qu Qdu w a_acc a_dec ts d_safe tight d0 t0] */
     cf->N = N; cf->quadratic = quadratic; cf->role = role;
+    cf->admm = 0; cf->rho = 0.0; cf->yf = cf->zf = cf->yb = cf->zb = NULL;
     cf->Qx[0][0] = p[0]; cf->Qx[0][1] = p[1]; cf->Qx[1][0] = p[2]; cf->Qx[1][1] = p[3];
     cf->Qu = p[4]; cf->Qdu = p[5]; cf->w = p[6]; cf->a_acc = p[7]; cf->a_dec = p[8]; cf->ts = p[9];
     cf->d_safe = p[10]; cf->tight = p[11]; cf->d0 = p[12]; cf->t0 = p[13];
@@ -1071,6 +1131,82 @@ int oracle_solve_miqp(int N, int nreg, int nsr, const double* S, const double* R
     free(C.obj); free(C.sig); free(C.cert);
     info_out[0] = best_obj;
     info_out[1] = count;
+    info_out[2] = C.n_conv;
+    info_out[3] = C.n_cert;
+    info_out[4] = best_cert;
+    info_out[5] = status;
+    info_out[6] = C.iters;
+    free(qp);
+    free(w);
+    return 0;
+}
+
+/* Naive-ADMM local MIQP (LocalMpcADMM, fleet_naive_admm.py:24-253), by branch and bound.
+ * p = [x0 (2) | y_front | z_front | y_back | z_back | leader_x] (each (2, N+1)), as
+ * hvp_params_stride_admm.  Outputs as oracle_solve_miqp plus the copies xf_out / xb_out. */
+int oracle_solve_admm_miqp(int N, int nreg, int nsr, const double* S, const double* R, const double* T,
+                           const double* A, const double* B, const double* c, int nd, const double* D, const double* E,
+                           int nf, const double* F, const double* G, const double* cfgp, int role, double rho,
+                           const double* p, int maxit, double* x_out, double* u_out, int* sigma_out, double* info_out,
+                           double* xf_out, double* xb_out) {
+    or_model md;
+    or_cfg cf;
+    or_vmodel vm;
+    if (N > OR_MAX_N || unpack_model(&md, nreg, nsr, S, R, T, A, B, c, nd, D, E, nf, F, G)) return -1;
+    unpack_cfg(&cf, N, 1, role, cfgp);
+    const int K1 = 2 * (N + 1);
+    cf.admm = 1;
+    cf.rho = rho;
+    cf.yf = p + 2; cf.zf = p + 2 + K1; cf.yb = p + 2 + 2 * K1; cf.zb = p + 2 + 3 * K1;
+    const double* xl = p + 2 + 4 * K1;
+    if (make_vmodel(&md, &vm) || !oracle_bnb_ok(&md)) return -2;
+    or_qp* qp = (or_qp*)malloc(sizeof(or_qp));
+    or_work* w = (or_work*)malloc(sizeof(or_work));
+    if (!qp || !w) { free(qp); free(w); return -3; }
+    static const double zero[2 * (OR_MAX_N + 1)] = {0};
+    or_ctx C;
+    memset(&C, 0, sizeof(C));
+    C.md = &md; C.cf = &cf; C.x0 = p; C.xf = zero; C.xb = zero; C.xl = xl; C.qp = qp; C.w = w;
+    C.maxit = maxit > 0 ? maxit : 200;
+    int sigma[OR_MAX_N], count = 0;
+    double inc = INFINITY;
+    bnb_dfs(&C, &vm, md.nreg, 0, p[1], p[1], sigma, &inc, &count);
+    int win = -1;
+    if (isfinite(inc)) {
+        double tol = 1e-9 * fmax(1.0, fabs(inc));
+        for (int i = 0; i < C.ncand; ++i) {
+            if (!(C.obj[i] <= inc + tol)) continue;
+            int less = win < 0;
+            for (int k = 0; k < N && !less; ++k) {
+                int a = C.sig[(size_t)i * N + k], b = C.sig[(size_t)win * N + k];
+                if (a != b) { less = a < b; break; }
+            }
+            if (less) win = i;
+        }
+    }
+    int status = win >= 0 ? 0 : (count == 0 ? 1 : 2);
+    double best_obj = INFINITY;
+    int best_cert = 0;
+    memset(xf_out, 0, sizeof(double) * K1);
+    memset(xb_out, 0, sizeof(double) * K1);
+    if (win >= 0) {
+        const int* ws = C.sig + (size_t)win * N;
+        build_qp(qp, &md, &cf, ws, p, zero, zero, xl);
+        or_result r = ipm_solve(qp, w, C.maxit);
+        best_obj = direct_objective(&cf, p, zero, zero, xl, w->z);
+        best_cert = r.certified;
+        for (int i = 0; i < 2; ++i) x_out[i * (N + 1)] = p[i];
+        for (int k = 1; k <= N; ++k)
+            for (int i = 0; i < 2; ++i) x_out[i * (N + 1) + k] = w->z[2 * (k - 1) + i];
+        for (int k = 0; k < N; ++k) u_out[k] = w->z[2 * N + k];
+        for (int k = 0; k < N; ++k) sigma_out[k] = ws[k];
+        int idx = 3 * N + ((role & R_SF) ? N + 1 : 0) + ((role & R_SB) ? N + 1 : 0);
+        if (role & R_SF) { memcpy(xf_out, w->z + idx, sizeof(double) * K1); idx += K1; }
+        if (role & R_SB) memcpy(xb_out, w->z + idx, sizeof(double) * K1);
+    }
+    free(C.obj); free(C.sig); free(C.cert);
+    info_out[0] = best_obj;
+    info_out[1] = count ? C.n_qp : 0;
     info_out[2] = C.n_conv;
     info_out[3] = C.n_cert;
     info_out[4] = best_cert;

@@ -239,6 +239,9 @@ def lib():
         L.oracle_solve_batch.argtypes = [c_int, c_int, c_int, c_int, c_int, dp, dp, dp, dp, dp, dp, c_int, dp, dp,
                                          c_int, dp, dp, dp, c_int, ip, ip, dp, c_int, dp, dp, ip, dp, c_int]
         L.oracle_solve_batch.restype = c_int
+        L.oracle_solve_admm_miqp.argtypes = model_args + [dp, c_int, ctypes.c_double, dp, c_int, dp, dp, ip, dp,
+                                                          dp, dp]
+        L.oracle_solve_admm_miqp.restype = c_int
         L.oracle_set_method.argtypes = [c_int]
         L.oracle_set_method.restype = None
         _lib = L
@@ -321,6 +324,44 @@ def solve_miqp(sysd: dict, cfg: Cfg, N: int, role: int, x0, xf, xb, xl, quadrati
     return res
 
 
+@dataclass
+class AdmmResult:
+    x: np.ndarray        # (2, N+1)
+    u: np.ndarray        # (N,)
+    sigma: np.ndarray    # (N,)
+    cost: float
+    x_front: np.ndarray  # (2, N+1) optimal front copy (zeros if the role has none)
+    x_back: np.ndarray   # (2, N+1)
+    n_qps: int
+    status: int
+    certified: bool
+
+
+def admm_params(x0, y_front, z_front, y_back, z_back, leader_x) -> np.ndarray:
+    """Parameter row of the ADMM local problem (include/hvp.h hvp_params_stride_admm)."""
+    blocks = [np.asarray(b, dtype=np.float64).reshape(-1) for b in (y_front, z_front, y_back, z_back, leader_x)]
+    return np.concatenate([np.asarray(x0, dtype=np.float64).reshape(-1)[:2]] + blocks)
+
+
+def solve_admm_miqp(sysd: dict, cfg: Cfg, N: int, role: int, rho: float, params, maxit: int = 200) -> AdmmResult:
+    """LocalMpcADMM's MIQP (fleet_naive_admm.py:24-253) in the full (x, u, s, copies) space,
+    branch and bound over the region sequences; see hvp_oracle.c oracle_solve_admm_miqp."""
+    L = lib()
+    args, keep = _model_args(sysd)
+    cv = cfg.vector()
+    p = np.ascontiguousarray(np.asarray(params, dtype=np.float64).reshape(-1))
+    assert p.size == 2 + 10 * (N + 1)
+    x_out, u_out = np.zeros((2, N + 1)), np.zeros(N)
+    sig, info = np.zeros(N, dtype=np.int32), np.zeros(7)
+    xf, xb = np.zeros((2, N + 1)), np.zeros((2, N + 1))
+    rc = L.oracle_solve_admm_miqp(N, *args, _d(cv), int(role), float(rho), _d(p), maxit, _d(x_out), _d(u_out), _i(sig),
+                                  _d(info), _d(xf), _d(xb))
+    del keep
+    if rc != 0:
+        raise RuntimeError(f"oracle_solve_admm_miqp failed ({rc})")
+    return AdmmResult(x_out, u_out, sig, float(info[0]), xf, xb, int(info[1]), int(info[5]), bool(info[4]))
+
+
 def candidates(sysd: dict, cfg: Cfg, N: int, x0, cap: int = 200000) -> np.ndarray:
     L = lib()
     args, keep = _model_args(sysd)
@@ -401,3 +442,70 @@ def export_qp(sysd: dict, cfg: Cfg, N: int, role: int, sigma, x0, xf, xb, xl, qu
     nz, ne, m = int(dims[0]), int(dims[1]), int(dims[2])
     return (P[: nz * nz].reshape(nz, nz), q[:nz].copy(), float(dims[3]), A[: ne * nz].reshape(ne, nz), b[:ne].copy(),
             G[: m * nz].reshape(m, nz), h[:m].copy())
+
+
+class AdmmCoordinator:
+    """Restatement of ADMMCoordinator.get_control (fleet_naive_admm.py:379-468) on oracle local
+    solves, for the end-to-end parity of the ADMM iteration (test infrastructure).
+
+    State carried across time steps as in the reference: y_front / y_back (never reset), the
+    parameter blocks each local MPC was last given, and the last local solutions (warm start)."""
+
+    def __init__(self, sysd: dict, cfg: Cfg, N: int, n: int, rho: float = 0.5, leader_index: int = 0):
+        self.sysd, self.cfg, self.N, self.n, self.rho = sysd, cfg, N, n, rho
+        self.leader_index = leader_index
+        K = (2, N + 1)
+        self.y_front = [np.zeros(K) for _ in range(n)]
+        self.y_back = [np.zeros(K) for _ in range(n)]
+        self.z = [np.zeros(K) for _ in range(n)]
+        self.blocks = [{"yf": np.zeros(K), "zf": np.zeros(K), "yb": np.zeros(K), "zb": np.zeros(K),
+                        "xl": np.zeros(K)} for _ in range(n)]
+        self.x_pred = [None] * n
+        self.roles = [role_bits(i, n, leader_index) for i in range(n)]
+
+    def set_leader_x(self, xl) -> None:
+        self.blocks[self.leader_index]["xl"] = np.asarray(xl, dtype=float)
+
+    def step(self, state, admm_iters: int):
+        n, N, rho = self.n, self.N, self.rho
+        x = np.asarray(state, dtype=float).reshape(n, 2)
+        for i in range(n):  # warm start (:392-402)
+            if i != 0 and self.x_pred[i - 1] is not None:
+                xp = self.x_pred[i - 1]
+                self.blocks[i]["yf"] = self.y_front[i].copy()
+                self.blocks[i]["zf"] = np.hstack((xp[:, 1:], xp[:, [-1]]))
+            if i != n - 1 and self.x_pred[i + 1] is not None:
+                xp = self.x_pred[i + 1]
+                self.blocks[i]["yb"] = self.y_back[i].copy()
+                self.blocks[i]["zb"] = np.hstack((xp[:, 1:], xp[:, [-1]]))
+        history = []
+        for _ in range(admm_iters):
+            res = []
+            for i in range(n):  # x-update (:407-419)
+                b = self.blocks[i]
+                p = admm_params(x[i], b["yf"], b["zf"], b["yb"], b["zb"], b["xl"])
+                r = solve_admm_miqp(self.sysd, self.cfg, N, self.roles[i], rho, p)
+                if r.status != 0:
+                    raise RuntimeError(f"oracle ADMM local MIQP {i} status {r.status}")
+                res.append(r)
+            history.append(res)
+            for i in range(n):  # z- and y-update (:421-447)
+                if i == 0:
+                    self.z[i] = 0.5 * (res[i].x + res[i + 1].x_front)
+                    self.y_front[i + 1] = self.y_front[i + 1] + rho * (res[i + 1].x_front - self.z[i])
+                elif i == n - 1:
+                    self.z[i] = 0.5 * (res[i].x + res[i - 1].x_back)
+                    self.y_back[i - 1] = self.y_back[i - 1] + rho * (res[i - 1].x_back - self.z[i])
+                else:
+                    self.z[i] = (res[i].x + res[i + 1].x_front + res[i - 1].x_back) / 3.0
+                    self.y_front[i + 1] = self.y_front[i + 1] + rho * (res[i + 1].x_front - self.z[i])
+                    self.y_back[i - 1] = self.y_back[i - 1] + rho * (res[i - 1].x_back - self.z[i])
+            for i in range(n):  # set the local vars (:453-468)
+                if i != 0:
+                    self.blocks[i]["yf"], self.blocks[i]["zf"] = self.y_front[i].copy(), self.z[i - 1].copy()
+                if i != n - 1:
+                    self.blocks[i]["yb"], self.blocks[i]["zb"] = self.y_back[i].copy(), self.z[i + 1].copy()
+        last = history[-1]
+        for i in range(n):
+            self.x_pred[i] = last[i].x
+        return np.array([r.u[0] for r in last]), history

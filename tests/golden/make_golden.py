@@ -27,7 +27,9 @@ Files (numpy .npz, no pickles):
 
   gear_n4_N5.npz, gear_n5_N8.npz  LocalMpcGear on the pwa_friction model ("model" = 1):
                       (gear, friction region) modes, oracle gear_friction_mld_system
-Run:  python tests/golden/make_golden.py [sweep | gear]
+  admm_local_N{5,10}.npz, admm_steps_n4_N5.npz  naive ADMM (configs[2]): local problems with
+                      copies, and 3 closed-loop time steps x 4 ADMM iterations (oracle coordinator)
+Run:  python tests/golden/make_golden.py [sweep | gear | admm]
 """
 
 from __future__ import annotations
@@ -187,7 +189,55 @@ def sweep():
         O.set_method(O.METHOD_ENUMERATE)
 
 
+def admm_fixtures():
+    """Naive ADMM (fleet_naive_admm.py, configs[2]): local problems with copies (random y, z
+    around the neighbours' predictions) and two closed-loop ADMM time steps of a 4-vehicle
+    platoon, all from the oracle (full (x, u, s, copies) space, branch and bound)."""
+    rng = np.random.default_rng(7)
+    sysd = O.gear_pwa_system(800.0)
+    for N, seeds in ((5, range(4)), (10, range(2))):
+        P, R, X, U, XF, XB, C, S, REG = [], [], [], [], [], [], [], [], []
+        for seed in seeds:
+            n = 4
+            st = O.env_initial_state(n, seed).astype(float)
+            for i in range(n):
+                pred = lambda j: O.constant_velocity_prediction(st[2 * j], st[2 * j + 1], N)  # noqa: E731
+                zf = pred(i - 1) + rng.normal(0, 3, (2, N + 1)) if i > 0 else np.zeros((2, N + 1))
+                zb = pred(i + 1) + rng.normal(0, 3, (2, N + 1)) if i < n - 1 else np.zeros((2, N + 1))
+                yf = rng.normal(0, 2, (2, N + 1)) if i > 0 else np.zeros((2, N + 1))
+                yb = rng.normal(0, 2, (2, N + 1)) if i < n - 1 else np.zeros((2, N + 1))
+                if seed == 0:  # the first time step of the reference: y = z = 0
+                    yf, zf, yb, zb = (np.zeros((2, N + 1)),) * 4
+                xl = leader_window(N) if i == 0 else np.zeros((2, N + 1))
+                p = O.admm_params(st[2 * i:2 * i + 2], yf, zf, yb, zb, xl)
+                r = O.solve_admm_miqp(sysd, O.Cfg(), N, O.role_bits(i, n), 0.5, p)
+                P.append(p); R.append(O.role_bits(i, n)); X.append(r.x); U.append(r.u); XF.append(r.x_front)
+                XB.append(r.x_back); C.append(r.cost); S.append(r.status); REG.append(r.sigma)
+        np.savez_compressed(os.path.join(HERE, f"admm_local_N{N}.npz"), N=N, rho=0.5, params=np.array(P),
+                            roles=np.array(R, np.int32), exp_x=np.array(X), exp_u=np.array(U), exp_xf=np.array(XF),
+                            exp_xb=np.array(XB), exp_cost=np.array(C), exp_status=np.array(S, np.int32),
+                            exp_region=np.array(REG, np.int32))
+        print(f"admm_local_N{N}.npz: {len(R)} instances")
+    # closed-loop ADMM steps (the state advances by the local solutions' x_1)
+    n, N, iters = 4, 5, 4
+    coord = O.AdmmCoordinator(sysd, O.Cfg(), N, n)
+    st = O.env_initial_state(n, 3).astype(float)
+    states, us, xs = [], [], []
+    for t in range(3):
+        coord.set_leader_x(leader_window(N, t))
+        u, hist = coord.step(st, iters)
+        states.append(st.copy()); us.append(np.array([[r.u for r in res] for res in hist]))
+        xs.append(np.array([[r.x for r in res] for res in hist]))
+        st = np.concatenate([r.x[:, 1] for r in hist[-1]])
+    np.savez_compressed(os.path.join(HERE, "admm_steps_n4_N5.npz"), N=N, n=n, iters=iters, rho=0.5,
+                        states=np.array(states), exp_u=np.array(us), exp_x=np.array(xs))
+    print("admm_steps_n4_N5.npz written")
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "admm":
+        admm_fixtures()
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "sweep":
         sweep()
         return
