@@ -355,7 +355,16 @@ __global__ __launch_bounds__(kBlock) void k_select(int B, const hvp_system* __re
 template <int N>
 constexpr int kBnbBlock = N <= 8 ? 256 : 64;  // LDS rows: 7 N doubles per lane
 
-__device__ inline double inc_of(const Workspace& ws, int inst) { return __longlong_as_double((long long)ws.inc[inst]); }
+// The incumbent is kept as an order-preserving 64-bit key of the double so that atomicMin on the
+// key is a min on the cost -- for negative costs too (the ADMM objective carries y'(c - z)).
+__device__ inline unsigned long long cost_key(double c) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(c);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+__device__ inline double key_cost(unsigned long long k) {
+    return __longlong_as_double((long long)((k >> 63) ? (k & 0x7fffffffffffffffull) : ~k));
+}
+__device__ inline double inc_of(const Workspace& ws, int inst) { return key_cost(ws.inc[inst]); }
 
 template <int N, int BS>
 __device__ inline int bnb_qp(hvp::LaneQp<N, LdsMem<N, BS>>& q, const hvp_system& S, const hvp::Consts& C, int rl,
@@ -419,7 +428,7 @@ __global__ __launch_bounds__(kBnbBlock<N>) void k_bnb_root(int B, const hvp_syst
         }
     }
     ws.nd_lb[0][i] = lb;
-    ws.inc[i] = (unsigned long long)__double_as_longlong(inc);
+    ws.inc[i] = cost_key(inc);
     ws.nodes[i] = nodes;
     ws.iters[i] = iters;
     atomicAdd(&ws.counter[3], (unsigned long long)nodes);
@@ -524,7 +533,7 @@ __global__ __launch_bounds__(kBnbBlock<N>) void k_bnb_bound(int k, const hvp_sys
 #pragma unroll
             for (int j = 0; j < N; ++j) ws.task_y[t * N + j] = q.y[j];
             if (ok) {
-                atomicMin(&ws.inc[inst], (unsigned long long)__double_as_longlong(c));
+                atomicMin(&ws.inc[inst], cost_key(c));
             } else {
                 ++fails;
                 atomicOr(&ws.inst_flag[inst], 8);  // a velocity-feasible sequence exists
@@ -572,7 +581,7 @@ __global__ __launch_bounds__(kBnbBlock<N>) void k_bnb_ipm(const hvp_system* __re
         for (int j = 0; j < N; ++j) ws.task_y[t * N + j] = q.y[j];
         ws.nd_lb[src][t] = c;
         ws.leaf_stat[t] = 0;
-        atomicMin(&ws.inc[inst], (unsigned long long)__double_as_longlong(c));
+        atomicMin(&ws.inc[inst], cost_key(c));
     }
 }
 

@@ -190,7 +190,7 @@ class AdmmEngine:
         o = self.out
         stream = stream or torch.cuda.current_stream(self.dev)
         for _ in range(admm_iters):
-            self.solver.solve_admm_device(self.sys, self.roles, self.params, o, stream)
+            self.solver.solve_admm_device(self.sys, self.roles, self.params, o, stream, retry_overflow=True)
             if on_solve is not None:
                 on_solve(self.solver)
             self.solver.admm_update(self.P, n, o["x"], o["x_front"], o["x_back"], self.y_front, self.y_back,

@@ -212,8 +212,26 @@ class BatchSolver:
         return {k: v.cpu().numpy() for k, v in out.items()}
 
     # -------------------------------------------------------------- ADMM formulation
-    def solve_admm_device(self, sys_idx, roles, params, out: dict, stream=None) -> dict:
-        """hvp_solve_admm_batch on device tensors; ``out`` also needs "x_front", "x_back"."""
+    def solve_admm_device(self, sys_idx, roles, params, out: dict, stream=None, retry_overflow: bool = False) -> dict:
+        """hvp_solve_admm_batch on device tensors; ``out`` also needs "x_front", "x_back".
+        ``retry_overflow`` as in :meth:`solve_device`."""
+        import torch
+
+        self._launch_admm(sys_idx, roles, params, out, stream)
+        for attempt in range(4 if retry_overflow else 0):
+            over = torch.nonzero(out["status"] == _abi.OVERFLOW).reshape(-1)
+            if over.numel() == 0:
+                break
+            if attempt:
+                self.reserve(int(roles.shape[0]), 4 * self.stats().capacity)
+            sub = {k: torch.empty_like(v[over]) for k, v in out.items()}
+            self._launch_admm(sys_idx[over].contiguous(), roles[over].contiguous(), params[over].contiguous(), sub,
+                              stream)
+            for k, v in sub.items():
+                out[k][over] = v
+        return out
+
+    def _launch_admm(self, sys_idx, roles, params, out: dict, stream=None) -> dict:
         import torch
 
         B = int(roles.shape[0])
