@@ -1,0 +1,695 @@
+// hvp_coop.h -- the fixed-sequence QP solved by a GROUP of 16 lanes (long horizons, N <= 16).
+//
+// The lane-per-QP solver (hvp_gi.h) keeps J (N x N) and R (N x N) of the Goldfarb-Idnani method
+// in registers: fine up to N ~ 8, but at N = 10 / 15 (C3, C5) it needs 200 / 450 doubles per
+// lane and the kernel lives in scratch.  Here one QP is owned by a 16-lane DPP row of the
+// wavefront (4 QPs per wave):
+//
+//   lane t      owns variable y_t = v_{t+1}, the rows of step t+1 (V/U/A) and the position /
+//               safe-distance rows of step t+1 (prefix rows of m = t - 1), their active and
+//               saturation bits, the multiplier and row id of active position t, and row t of
+//               the Hessian during setup;
+//   LDS         the group's J (row t of J is lane t's) and R (upper triangular), row stride
+//               17 doubles (bank-conflict-free column walks), plus two scratch vectors;
+//   shuffles    sums / argmax / scans within the 16-lane group (__shfl*, width 16).
+//
+// Same algorithm as hvp_gi.h (most violated row, dual step, soft rows with saturation and the
+// reversed rows that unsaturate them, the same verification), same velocity-space QP as
+// setup_lane / setup_lane_admm (the Hessian rows are assembled in closed form from the per-step
+// quadratic forms), so the results agree with the lane solver to rounding.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "hvp_admm.h"
+#include "hvp_gi.h"
+#include "hvp_ipm.h"
+
+namespace hvp {
+namespace coop {
+
+constexpr int G = 16;
+constexpr int LD = 17;  // padded LDS row stride (doubles)
+
+struct GroupLds {
+    double J[G * LD];
+    double R[G * LD];
+    double v[G];  // broadcast vector (dv, y*, ...)
+    double pad[G];
+};
+
+__device__ inline int lane16() { return (int)(threadIdx.x & (G - 1)); }
+__device__ inline void gsync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+__device__ inline double gsum(double x) {
+    x += __shfl_xor(x, 8, G);
+    x += __shfl_xor(x, 4, G);
+    x += __shfl_xor(x, 2, G);
+    x += __shfl_xor(x, 1, G);
+    return x;
+}
+__device__ inline int gor(int x) {
+    x |= __shfl_xor(x, 8, G);
+    x |= __shfl_xor(x, 4, G);
+    x |= __shfl_xor(x, 2, G);
+    x |= __shfl_xor(x, 1, G);
+    return x;
+}
+__device__ inline unsigned long long gor64(unsigned long long x) {
+    x |= __shfl_xor(x, 8, G);
+    x |= __shfl_xor(x, 4, G);
+    x |= __shfl_xor(x, 2, G);
+    x |= __shfl_xor(x, 1, G);
+    return x;
+}
+template <class T>
+__device__ inline T bcast(T x, int src) { return __shfl(x, src, G); }
+// inclusive prefix sum over the group
+__device__ inline double gscan(double x) {
+    const int t = lane16();
+#pragma unroll
+    for (int d = 1; d < G; d <<= 1) {
+        const double o = __shfl_up(x, d, G);
+        if (t >= d) x += o;
+    }
+    return x;
+}
+// group argmin of (key, lane) -> (key, lane); ties to the lower lane
+__device__ inline void gargmin(double& key, int& who) {
+#pragma unroll
+    for (int d = G / 2; d > 0; d >>= 1) {
+        const double ok = __shfl_xor(key, d, G);
+        const int ow = __shfl_xor(who, d, G);
+        if (ok < key || (ok == key && ow < who)) { key = ok; who = ow; }
+    }
+}
+// select x[t] of a register array with a lane-dependent index (predicated, no scratch)
+template <int N>
+__device__ inline double pick(const double* x, int t) {
+    double r = 0.0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) r = i == t ? x[i] : r;
+    return r;
+}
+
+// ------------------------------------------------------------------ per-lane problem data
+template <int N>
+struct Lane {
+    // uniform
+    double v0, P1, ts, pmin, pmax;
+    bool has_sf, has_sb;
+    // step t = lane (valid if t < N)
+    double am, vlo, vhi, ulo, uhi, dec, acc;
+    double hf, hb;  // prefix rows of m = t - 1 (t >= 1)
+    double y;       // y_t
+    double f;       // linear term f_t
+};
+
+// Per-step quadratic form of the tracking / copy terms at step k = 1..N (setup_lane's
+// Wpp, Wpv, Wvv, lp, lv with the constant folded at pbar = P1).
+struct StepForm {
+    double Wpp, Wpv, Wvv, lp, lv;
+};
+
+template <int N>
+__device__ inline StepForm decent_form(const Consts& C, int role, const double* prm, int k) {
+    const double* xf = prm + 2;
+    const double* xb = prm + 2 + 2 * (N + 1);
+    const double* xl = prm + 2 + 4 * (N + 1);
+    const bool tf = (role & HVP_ROLE_TRACK_FRONT) != 0, tb = (role & HVP_ROLE_TRACK_BACK) != 0;
+    const bool tl = (role & HVP_ROLE_TRACK_LEADER) != 0, lsp = (role & HVP_ROLE_LEADER_SPACING) != 0;
+    const double Qpp = C.Qpp, Qpv = C.Qpv, Qvv = C.Qvv, t0 = C.t0, d0 = C.d0;
+    StepForm F{0, 0, 0, 0, 0};
+    auto add = [&](double m00, double m01, double m11, double r0, double r1) {
+        const double qa = Qpp * m00;
+        const double qc = Qpp * m01 + Qpv * m11, qd = Qpv * m01 + Qvv * m11;
+        F.Wpp += m00 * qa;
+        F.Wpv += m00 * qc;
+        F.Wvv += m01 * qc + m11 * qd;
+        const double Qr0 = Qpp * r0 + Qpv * r1, Qr1 = Qpv * r0 + Qvv * r1;
+        F.lp += m00 * Qr0;
+        F.lv += m01 * Qr0 + m11 * Qr1;
+    };
+    const int K1 = N + 1;
+    if (tf) add(1.0, t0, 1.0, d0 - xf[k], -xf[K1 + k]);
+    if (tb) add(-1.0, 0.0, -1.0, xb[k] + t0 * xb[K1 + k] + d0, xb[K1 + k]);
+    if (tl) {
+        if (lsp) add(1.0, t0, 1.0, d0 - xl[k], -xl[K1 + k]);
+        else add(1.0, 0.0, 1.0, -xl[k], -xl[K1 + k]);
+    }
+    return F;
+}
+
+template <int N>
+__device__ inline StepForm admm_form(const Consts& C, int role, const double* prm, int k, uint64_t hs) {
+    const double* xl = admm_leader(prm, N);
+    const bool hf = (role & HVP_ROLE_SAFE_FRONT) != 0, hb = (role & HVP_ROLE_SAFE_BACK) != 0;
+    const bool tf = (role & HVP_ROLE_TRACK_FRONT) != 0, tb = (role & HVP_ROLE_TRACK_BACK) != 0;
+    const bool tl = (role & HVP_ROLE_TRACK_LEADER) != 0;
+    const int K1 = N + 1;
+    double Wpp = 0, Wpv = 0, Wvv = 0, lp = 0, lv = 0, cc = 0;
+    if (tl) {
+        const double r0 = -xl[k], r1 = -xl[K1 + k];
+        Wpp += C.Qpp;
+        Wpv += C.Qpv;
+        Wvv += C.Qvv;
+        lp += C.Qpp * r0 + C.Qpv * r1;
+        lv += C.Qpv * r0 + C.Qvv * r1;
+    }
+    for (int side = 0; side < 2; ++side) {
+        if (!(side == 0 ? hf : hb)) continue;
+        const double* yy = admm_y(prm, side, N);
+        const double* zz = admm_z(prm, side, N);
+        CopyTerm T;
+        admm_copy(C, side == 0 ? tf : tb, side, yy[k], yy[K1 + k], zz[k], zz[K1 + k], T);
+        Wpp += T.Wpp;
+        Wpv += T.Wpv;
+        Wvv += T.Wvv;
+        lp += T.lp;
+        lv += T.lv;
+        hub_add(T, hub_get(hs, k, side), C.w, Wpp, Wpv, Wvv, lp, lv, cc);
+    }
+    return StepForm{Wpp, Wpv, Wvv, lp, lv};
+}
+
+// Lane data + this lane's Hessian row (into LDS J area, row t) for region code / relaxation K.
+template <int N>
+__device__ inline bool setup(Lane<N>& L, GroupLds& S_lds, const hvp_system& S, const Consts& C, int role,
+                             const double* prm, uint64_t code, int K, uint64_t hs) {
+    const int t = lane16();
+    const bool admm = C.form == HVP_FORM_ADMM;
+    const double p0 = prm[0], v0 = prm[1], ts = S.ts;
+    L.v0 = v0;
+    L.ts = ts;
+    L.P1 = p0 + ts * v0;
+    L.pmin = S.pmin;
+    L.pmax = S.pmax;
+    L.has_sf = !admm && (role & HVP_ROLE_SAFE_FRONT) != 0;
+    L.has_sb = !admm && (role & HVP_ROLE_SAFE_BACK) != 0;
+    // dynamics of step k (relaxed beyond K)
+    auto dyn = [&](int k, double& a, double& b, double& c) {
+        const int r = code_region(code, k);
+        const bool fx = k < K;
+        a = fx ? S.a[r] : 1.0;
+        b = fx ? S.b[r] : 1.0;
+        c = fx ? S.c[r] : 0.0;
+    };
+    const int tt = t < N ? t : N - 1;
+    {
+        double a, b, c;
+        dyn(tt, a, b, c);
+        const bool fx = tt < K;
+        L.am = a;
+        L.ulo = fx ? c + b * S.umin : -1e30;
+        L.uhi = fx ? c + b * S.umax : 1e30;
+        if (tt + 1 < K) {
+            const int r1 = code_region(code, tt + 1);
+            L.vlo = fmax(S.vmin, S.vlo[r1]);
+            L.vhi = fmin(S.vmax, S.vhi[r1]);
+        } else {
+            L.vlo = S.vmin;
+            L.vhi = S.vmax;
+        }
+        L.dec = C.dec[tt];
+        L.acc = C.acc[tt];
+        // prefix rows of m = t - 1: safe rows at step k = t + 1 (inert when absent)
+        const double* xf = prm + 2;
+        const double* xb = prm + 2 + 2 * (N + 1);
+        const int m = tt >= 1 ? tt - 1 : 0;
+        const double reach = ts * (m + 1);
+        L.hf = L.has_sf ? xf[m + 2] - C.d_safe : L.P1 + reach * S.vmax + 100.0;
+        L.hb = L.has_sb ? xb[m + 2] + C.d_safe : L.P1 + reach * S.vmin - 100.0;
+    }
+    // ---- Hessian row t and f_t
+    double Hrow[N];
+#pragma unroll
+    for (int c = 0; c < N; ++c) Hrow[c] = 0.0;
+    double f = 0.0;
+    // tracking / copy forms: suffix sums over k of 2 Wpp ts^2 and ts * gp
+    const double P1 = L.P1;
+    double Spp[N + 2], Sgp[N + 2], Wpv2[N + 1];
+#pragma unroll
+    for (int i = 0; i < N + 2; ++i) { Spp[i] = 0.0; Sgp[i] = 0.0; }
+    double Wvv_t = 0.0, gv_t = 0.0;
+#pragma unroll
+    for (int k = N; k >= 1; --k) {
+        const StepForm F = admm ? admm_form<N>(C, role, prm, k, hs) : decent_form<N>(C, role, prm, k);
+        Spp[k] = Spp[k + 1] + 2.0 * F.Wpp * ts * ts;
+        Sgp[k] = Sgp[k + 1] + ts * 2.0 * (F.Wpp * P1 + F.lp);
+        Wpv2[k] = 2.0 * F.Wpv * ts;
+        if (k == t + 1) {
+            Wvv_t = 2.0 * F.Wvv;
+            gv_t = 2.0 * (F.Wpv * P1 + F.lv);
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < N; ++c) {
+        const int mx = c > t ? c : t;
+        double h = mx + 2 <= N ? Spp[mx + 2] : 0.0;
+        if (c < t) h += Wpv2[t + 1 <= N ? t + 1 : N];
+        if (c > t) h += Wpv2[c + 1];
+        if (c == t) h += Wvv_t;
+        Hrow[c] = h;
+    }
+    f = gv_t + (t + 2 <= N ? Sgp[t + 2] : 0.0);
+    // input cost Qu u_k^2 (k < K) and variation Qdu (u_{k+1} - u_k)^2 (k + 1 < K)
+    auto ucoef = [&](int k, double& ub, double& gk, double& gkm) {
+        double a, b, c;
+        dyn(k, a, b, c);
+        const double ib = 1.0 / b;
+        ub = k == 0 ? -(a * v0 + c) * ib : -c * ib;
+        gk = ib;
+        gkm = k == 0 ? 0.0 : -a * ib;
+    };
+    const double w2 = 2.0 * C.Qu;
+    if (t < N) {
+        double ub, gk, gkm;
+        ucoef(t, ub, gk, gkm);
+        if (t < K) {
+            Hrow[t] += w2 * gk * gk;
+            f += w2 * ub * gk;
+#pragma unroll
+            for (int c = 0; c < N; ++c)
+                if (c + 1 == t) Hrow[c] += w2 * gk * gkm;
+        }
+        if (t + 1 < N && t + 1 < K) {
+            double ub1, gk1, gkm1;
+            ucoef(t + 1, ub1, gk1, gkm1);
+            Hrow[t] += w2 * gkm1 * gkm1;
+            f += w2 * ub1 * gkm1;
+#pragma unroll
+            for (int c = 0; c < N; ++c)
+                if (c == t + 1) Hrow[c] += w2 * gk1 * gkm1;
+        }
+        if (C.Qdu != 0.0) {
+            const double wd = 2.0 * C.Qdu;
+            for (int k = t - 1; k <= t + 1; ++k) {
+                if (k < 0 || k + 1 >= N || !(k + 1 < K)) continue;
+                double ubk, gkk, gkmk, ubk1, gkk1, gkmk1;
+                ucoef(k, ubk, gkk, gkmk);
+                ucoef(k + 1, ubk1, gkk1, gkmk1);
+                // e = u_{k+1} - u_k: entries k+1: gk_{k+1}; k: gkm_{k+1} - gk_k; k-1: -gkm_k
+                const double g_kp = gkk1, g_k = gkmk1 - gkk, g_km = k >= 1 ? -gkmk : 0.0;
+                const double eb = ubk1 - ubk;
+                const double gt = t == k + 1 ? g_kp : (t == k ? g_k : (t == k - 1 ? g_km : 0.0));
+                if (gt == 0.0) continue;
+                f += wd * eb * gt;
+#pragma unroll
+                for (int c = 0; c < N; ++c) {
+                    const double gc = c == k + 1 ? g_kp : (c == k ? g_k : (c == k - 1 ? g_km : 0.0));
+                    Hrow[c] += wd * gt * gc;
+                }
+            }
+        }
+    }
+    if (t < N) {
+#pragma unroll
+        for (int c = 0; c < N; ++c) S_lds.J[t * LD + c] = Hrow[c];
+    }
+    L.f = t < N ? f : 0.0;
+    return L.P1 >= S.pmin - 1e-9 * (1.0 + fabs(S.pmin)) && L.P1 <= S.pmax + 1e-9 * (1.0 + fabs(S.pmax));
+}
+
+// Row-local constraint evaluation: the rows lane t owns, in the order of hvp_gi.h.
+// id < 6N: 6t + {V_lo, V_hi, U_lo, U_hi, A_lo, A_hi}; prefix rows 6N + 4(t-1) + {P_lo, P_hi, SF, SB}.
+template <int N>
+__device__ inline void most_violated_lane(const Lane<N>& L, const Consts& C, double y, double yprev, double cum,
+                                          unsigned act, unsigned sat, double tol, double& best_score, int& best_id,
+                                          double& best_slack) {
+    const int t = lane16();
+    best_score = -1.0;
+    best_id = -1;
+    best_slack = 0.0;
+    if (t >= N) return;
+    double best_v2 = 0.0, best_nn = 1.0;
+    auto consider = [&](int local, int id, double slack, double nn, double scale) {
+        if (((act >> local) & 1u) || !(slack < -tol * scale)) return;
+        const double v2 = slack * slack;
+        if (best_id < 0 || v2 * best_nn > best_v2 * nn) {
+            best_id = id;
+            best_v2 = v2;
+            best_nn = nn;
+            best_slack = slack;
+        }
+    };
+    const int j = t;
+    const double a = L.am;
+    const double gv = y, gu = y - a * yprev, ga = y - yprev;
+    const double nu = j ? 1.0 + a * a : 1.0, na = j ? 2.0 : 1.0;
+    consider(0, 6 * j + 0, gv - L.vlo, 1.0, 1.0 + fabs(L.vlo));
+    consider(1, 6 * j + 1, L.vhi - gv, 1.0, 1.0 + fabs(L.vhi));
+    consider(2, 6 * j + 2, gu - L.ulo, nu, 1.0 + fabs(L.ulo) + fabs(a * yprev));
+    consider(3, 6 * j + 3, L.uhi - gu, nu, 1.0 + fabs(L.uhi) + fabs(a * yprev));
+    consider(4, 6 * j + 4, ga - L.dec, na, 1.0 + fabs(yprev));
+    consider(5, 6 * j + 5, L.acc - ga, na, 1.0 + fabs(yprev));
+    if (t >= 1) {
+        const int m = t - 1;
+        const double p = L.P1 + L.ts * cum;  // cum = y_0 + .. + y_m
+        const double nn = L.ts * L.ts * (m + 1);
+        const double sc = 1.0 + fabs(p);
+        const int b = 6 * N + 4 * m;
+        consider(6, b + 0, p - L.pmin, nn, sc);
+        consider(7, b + 1, L.pmax - p, nn, sc);
+        const double sfw = L.hf - p, sbw = p - L.hb;
+        const bool satf = sat & 1u, satb = (sat >> 1) & 1u;
+        consider(8, satf ? (b + 2) | GI_REV : b + 2, satf ? -sfw : sfw, nn, sc);
+        consider(9, satb ? (b + 3) | GI_REV : b + 3, satb ? -sbw : sbw, nn, sc);
+    }
+    if (best_id >= 0) best_score = best_v2 / best_nn;
+}
+
+// owner lane and local bit of a row id
+template <int N>
+__device__ inline void row_owner(int id_in, int& lane, int& bit) {
+    const int id = id_in & (GI_REV - 1);
+    if (id < 6 * N) {
+        lane = id / 6;
+        bit = id % 6;
+    } else {
+        const int m = (id - 6 * N) / 4;
+        lane = m + 1;
+        bit = 6 + (id - 6 * N) % 4;
+    }
+}
+
+// Cooperative Goldfarb-Idnani.  On GI_OK lane t < N holds y_t in L.y.
+template <int N>
+__device__ inline int solve(Lane<N>& L, GroupLds& Sg, const Consts& C, int max_iter, int& iters) {
+    const int t = lane16();
+    iters = 0;
+    double* J = Sg.J;  // holds H on entry (row t written by lane t)
+    double* R = Sg.R;
+    gsync();
+    // ---- Cholesky H = L L' into R area (lower, row-major), column by column
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        // diagonal (lane j)
+        if (t == j) {
+            double s = J[j * LD + j];
+            for (int k = 0; k < j; ++k) s -= R[j * LD + k] * R[j * LD + k];
+            R[j * LD + j] = s > 0.0 ? sqrt(s) : -1.0;
+        }
+        gsync();
+        const double d = R[j * LD + j];
+        if (!(d > 0.0)) return GI_FAIL_CHOL;
+        if (t > j && t < N) {
+            double v = J[t * LD + j];
+            for (int k = 0; k < j; ++k) v -= R[t * LD + k] * R[j * LD + k];
+            R[t * LD + j] = v / d;
+        }
+        gsync();
+    }
+    // ---- unconstrained minimiser: L w = -f, L' y = w
+    double w = 0.0;  // w_t at lane t
+    {
+        double acc = -L.f;
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            double wi = 0.0;
+            if (t == i) wi = acc / R[i * LD + i];
+            wi = bcast(wi, i);
+            if (t == i) w = wi;
+            if (t > i && t < N) acc -= R[t * LD + i] * wi;
+        }
+        // back substitution: y_i = (w_i - sum_{k>i} L[k][i] y_k) / L[i][i]
+        double acc2 = w;
+        L.y = 0.0;
+#pragma unroll
+        for (int i = N - 1; i >= 0; --i) {
+            double yi = 0.0;
+            if (t == i) yi = acc2 / R[i * LD + i];
+            yi = bcast(yi, i);
+            if (t == i) L.y = yi;
+            // lanes k < i need L[i][k] (row i, column k): read from LDS
+            if (t < i) acc2 -= R[i * LD + t] * yi;
+        }
+    }
+    // ---- J = L^-T: row t of J = column t of L^-1 (forward substitution of e_t, all lanes)
+    {
+        double x[N];
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            double v = i == t ? 1.0 : 0.0;
+#pragma unroll
+            for (int k = 0; k < i; ++k) v -= R[i * LD + k] * x[k];
+            x[i] = v / R[i * LD + i];
+        }
+        gsync();
+        if (t < N) {
+#pragma unroll
+            for (int c = 0; c < N; ++c) J[t * LD + c] = x[c];
+        }
+        // R starts empty
+        if (t < N) {
+#pragma unroll
+            for (int c = 0; c < N; ++c) R[t * LD + c] = 0.0;
+        }
+        gsync();
+    }
+    double u = 0.0;  // multiplier of active position t
+    int id = -1;     // row id of active position t
+    int nact = 0;
+    unsigned act = 0;  // active bits of the rows lane t owns
+    unsigned sat = 0;  // saturation bits (SF = 1, SB = 2) of lane t's prefix rows
+    const double wgt = C.w;
+    const double tol = 1e-11;
+    int iter = 0;
+    for (;;) {
+        // ---------------- most violated row
+        const double yv = t < N ? L.y : 0.0;
+        double yprev = __shfl_up(yv, 1, G);
+        if (t == 0) yprev = L.v0;
+        const double cum = gscan(yv) - yv;  // y_0 + .. + y_{t-1}
+        double score;
+        int bid;
+        double bsl;
+        most_violated_lane<N>(L, C, yv, yprev, cum, act, sat, tol, score, bid, bsl);
+        double key = -score;
+        int who = t;
+        gargmin(key, who);
+        if (!(key < 0.0)) break;  // no violated row
+        const int p = bcast(bid, who);
+        const bool psoft = gi_soft<N>(p);
+        // row normal: np_i = -c_i (>= form), rhs dp = -d
+        const int base = p & (GI_REV - 1);
+        const bool rev = (p & GI_REV) != 0;
+        int rj = 0, rtype = 0, rm = 0;
+        double rsgn = 1.0, ra = 0.0, d = 0.0;
+        // bound d computed by the owner lane
+        double dloc = 0.0;
+        {
+            int ol, ob;
+            row_owner<N>(p, ol, ob);
+            if (base < 6 * N) {
+                rj = base / 6;
+                const int r = base % 6, pair = r / 2;
+                rtype = 0;
+                rsgn = (r & 1) ? 1.0 : -1.0;
+                if (t == rj) {
+                    const double a = pair == 1 ? L.am : (pair == 2 ? 1.0 : 0.0);
+                    double lo, hi;
+                    if (pair == 0) { lo = L.vlo; hi = L.vhi; }
+                    else if (pair == 1) { lo = L.ulo; hi = L.uhi; }
+                    else { lo = L.dec; hi = L.acc; }
+                    const double cst = rj == 0 ? -a * L.v0 : 0.0;
+                    dloc = (r & 1) ? hi - cst : -(lo - cst);
+                }
+                ra = bcast(pair == 1 ? L.am : (pair == 2 ? 1.0 : 0.0), rj);
+            } else {
+                rm = (base - 6 * N) / 4;
+                const int r = (base - 6 * N) % 4;
+                rtype = 1;
+                rsgn = (r == 1 || r == 2) ? 1.0 : -1.0;
+                if (t == rm + 1) {
+                    if (r == 0) dloc = L.P1 - L.pmin;
+                    else if (r == 1) dloc = L.pmax - L.P1;
+                    else if (r == 2) dloc = L.hf - L.P1;
+                    else dloc = L.P1 - L.hb;
+                }
+            }
+            d = bcast(dloc, ol);
+        }
+        const double flip = rev ? -1.0 : 1.0;
+        // c_i of row p for index i (uniform across lanes)
+        auto cof = [&](int i) -> double {
+            double c;
+            if (rtype == 0) c = (i == rj ? rsgn : 0.0) + (i + 1 == rj ? -rsgn * ra : 0.0);
+            else c = i <= rm ? rsgn * L.ts : 0.0;
+            return flip * c;
+        };
+        const double dd = flip * d;
+        const double np_t = t < N ? -cof(t) : 0.0;
+        const double dp = -dd;
+        double unew = 0.0;
+        for (;;) {
+            if (++iter > max_iter) { iters = iter; return GI_FAIL_ITER; }
+            // ---- dv_c = sum_i J[i][c] np_i  (lane c)
+            double dv = 0.0;
+            if (t < N) {
+#pragma unroll
+                for (int i = 0; i < N; ++i) {
+                    const double ni = -cof(i);
+                    if (ni != 0.0) dv += J[i * LD + t] * ni;
+                }
+            }
+            Sg.v[t] = dv;
+            gsync();
+            double dvr[N];
+#pragma unroll
+            for (int c = 0; c < N; ++c) dvr[c] = Sg.v[c];
+            double d2n = 0.0, dn = 0.0;
+#pragma unroll
+            for (int c = 0; c < N; ++c) {
+                dn += dvr[c] * dvr[c];
+                if (c >= nact) d2n += dvr[c] * dvr[c];
+            }
+            // ---- z_t = sum_{c >= nact} J[t][c] dv_c
+            double z = 0.0;
+            if (t < N) {
+#pragma unroll
+                for (int c = 0; c < N; ++c)
+                    if (c >= nact) z += J[t * LD + c] * dvr[c];
+            }
+            // ---- r = R^-1 dv (active part), column-oriented back substitution
+            double r = 0.0;
+            {
+                double accr = t < nact ? pick<N>(dvr, t) : 0.0;
+#pragma unroll
+                for (int j = N - 1; j >= 0; --j) {
+                    if (j >= nact) continue;
+                    double rj_ = 0.0;
+                    if (t == j) rj_ = accr / R[j * LD + j];
+                    rj_ = bcast(rj_, j);
+                    if (t == j) r = rj_;
+                    if (t < j) accr -= R[t * LD + j] * rj_;
+                }
+            }
+            // ---- step lengths
+            double k1key = 1e300;
+            int k1 = t;
+            if (t < nact && r > 0.0) k1key = u / r;
+            gargmin(k1key, k1);
+            const double t1 = k1key;
+            double k3key = 1e300;
+            int k3 = t;
+            if (t < nact && gi_soft<N>(id) && r < 0.0) k3key = (wgt - u) / (-r);
+            gargmin(k3key, k3);
+            double t3 = k3key;
+            bool new_sat = false;
+            if (psoft && wgt - unew <= t3) {
+                t3 = wgt - unew;
+                new_sat = true;
+            }
+            const bool zstep = d2n > 1e-14 * dn;
+            const double zn = d2n;
+            const double sp_now = dp + gsum(np_t * (t < N ? L.y : 0.0));
+            const double t2 = zstep && zn > 0.0 ? fmax(-sp_now, 0.0) / zn : 1e300;
+            const double tstep = fmin(t1, fmin(t2, t3));
+            if (!(tstep < 1e299)) { iters = iter; return GI_FAIL_DUAL; }
+            if (t2 < 1e299 && t < N) L.y += tstep * z;
+            if (t < nact) u -= tstep * r;
+            unew += tstep;
+            if (t2 <= t1 && t2 <= t3) {
+                // ---- add p: Givens zeroing dv[nact+1 .. N-1] bottom-up, rotating J's columns
+#pragma unroll
+                for (int i = N - 1; i >= 1; --i) {
+                    if (i > nact) {
+                        double gc, gs;
+                        givens(dvr[i - 1], dvr[i], gc, gs);
+                        dvr[i - 1] = gc * dvr[i - 1] + gs * dvr[i];
+                        dvr[i] = 0.0;
+                        if (t < N) {
+                            const double a0 = J[t * LD + i - 1], a1 = J[t * LD + i];
+                            J[t * LD + i - 1] = gc * a0 + gs * a1;
+                            J[t * LD + i] = -gs * a0 + gc * a1;
+                        }
+                    }
+                }
+                if (t <= nact && t < N) R[t * LD + nact] = pick<N>(dvr, t);
+                if (t == nact) { u = unew; id = p; }
+                {
+                    int ol, ob;
+                    row_owner<N>(p, ol, ob);
+                    if (t == ol) act |= 1u << ob;
+                }
+                ++nact;
+                gsync();
+                break;
+            }
+            // ---- a row leaves the active set
+            int drop;
+            const bool by_sat = t3 <= t1;
+            if (by_sat) {
+                if (new_sat) {
+                    // the new soft row saturates: it joins the objective
+                    int ol, ob;
+                    row_owner<N>(p, ol, ob);
+                    if (t == ol) sat ^= 1u << (ob - 8);  // SF -> bit 0, SB -> bit 1 (GI_REV toggles back)
+                    gsync();
+                    break;
+                }
+                drop = k3;
+            } else {
+                drop = k1;
+            }
+            const int dropped = bcast(id, drop);
+            {
+                int ol, ob;
+                row_owner<N>(dropped, ol, ob);
+                if (t == ol) {
+                    act &= ~(1u << ob);
+                    if (by_sat) sat ^= 1u << (ob - 8);
+                }
+            }
+            // shift positions drop.. nact-2 (u, id, R columns)
+            const double u_n = __shfl_down(u, 1, G);
+            const int id_n = __shfl_down(id, 1, G);
+            if (t >= drop && t < nact - 1) { u = u_n; id = id_n; }
+            if (t == nact - 1) { u = 0.0; id = -1; }
+            if (t < N) {
+#pragma unroll
+                for (int j = 0; j < N - 1; ++j)
+                    if (j >= drop && j < nact - 1) R[t * LD + j] = R[t * LD + j + 1];
+#pragma unroll
+                for (int j = 0; j < N; ++j)
+                    if (j == nact - 1) R[t * LD + j] = 0.0;
+            }
+            gsync();
+            // re-triangularise: rotations of rows (i, i+1), i = drop .. nact-2
+#pragma unroll
+            for (int i = 0; i < N - 1; ++i) {
+                if (i >= drop && i < nact - 1) {
+                    double gc, gs;
+                    givens(R[i * LD + i], R[(i + 1) * LD + i], gc, gs);
+                    gsync();
+                    if (t >= i && t < nact - 1) {
+                        const double a0 = R[i * LD + t], a1 = R[(i + 1) * LD + t];
+                        R[i * LD + t] = gc * a0 + gs * a1;
+                        R[(i + 1) * LD + t] = -gs * a0 + gc * a1;
+                    }
+                    if (t < N) {
+                        const double a0 = J[t * LD + i], a1 = J[t * LD + i + 1];
+                        J[t * LD + i] = gc * a0 + gs * a1;
+                        J[t * LD + i + 1] = -gs * a0 + gc * a1;
+                    }
+                    gsync();
+                }
+            }
+            --nact;
+        }
+    }
+    iters = iter;
+    // ---- verification: multipliers in [0, w] (soft) or >= 0
+    int bad = 0;
+    if (t < nact) {
+        if (u < -1e-9 * wgt) bad = 1;
+        if (gi_soft<N>(id) && u > wgt * (1.0 + 1e-9)) bad = 1;
+    }
+    return gor(bad) ? GI_FAIL_VERIFY : GI_OK;
+}
+
+}  // namespace coop
+}  // namespace hvp
