@@ -294,6 +294,7 @@ def main() -> None:
     if dist:
         dist.barrier()
     dt = time.perf_counter() - t0
+    ok = bool((out["status"] == 0).all().item())  # the timed steps' own results
     if dist:
         tt = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -311,7 +312,6 @@ def main() -> None:
         iters += s.qp_iterations
         fallback += s.n_fallback
 
-    ok = bool((out["status"] == 0).all().item())
     steps_total = S * world * args.steps
     value = steps_total / dt
     bnb = method != 1

@@ -223,38 +223,35 @@ __device__ inline bool setup(Lane<N>& L, GroupLds& S_lds, const hvp_system& S, c
         L.hf = L.has_sf ? xf[m + 2] - C.d_safe : L.P1 + reach * S.vmax + 100.0;
         L.hb = L.has_sb ? xb[m + 2] + C.d_safe : L.P1 + reach * S.vmin - 100.0;
     }
-    // ---- Hessian row t and f_t
-    double Hrow[N];
-#pragma unroll
-    for (int c = 0; c < N; ++c) Hrow[c] = 0.0;
-    double f = 0.0;
-    // tracking / copy forms: suffix sums over k of 2 Wpp ts^2 and ts * gp
+    // ---- Hessian row t and f_t from the per-step forms: lane t evaluates the form of ITS step
+    // k = t + 1 only; the suffix sums over k (Spp(m) = sum_{k >= m} 2 Wpp_k ts^2, likewise the
+    // prefix gradient) are group scans, and the entries right of the diagonal come from the
+    // column owner's lane:
+    //   H[t][c] = Spp(max(t, c) + 2) + 2 Wpv_{max(t,c)+1} ts (c != t),  H[t][t] = 2 Wvv_{t+1} + Spp(t + 2)
+    //   f_t = 2 (Wpv_{t+1} P1 + lv_{t+1}) + sum_{k >= t+2} ts 2 (Wpp_k P1 + lp_k)
+    double* Hrow = S_lds.J + (t < N ? t : 0) * LD;  // row t (lanes >= N never store)
     const double P1 = L.P1;
-    double Spp[N + 2], Sgp[N + 2], Wpv2[N + 1];
-#pragma unroll
-    for (int i = 0; i < N + 2; ++i) { Spp[i] = 0.0; Sgp[i] = 0.0; }
-    double Wvv_t = 0.0, gv_t = 0.0;
-#pragma unroll
-    for (int k = N; k >= 1; --k) {
-        const StepForm F = admm ? admm_form<N>(C, role, prm, k, hs) : decent_form<N>(C, role, prm, k);
-        Spp[k] = Spp[k + 1] + 2.0 * F.Wpp * ts * ts;
-        Sgp[k] = Sgp[k + 1] + ts * 2.0 * (F.Wpp * P1 + F.lp);
-        Wpv2[k] = 2.0 * F.Wpv * ts;
-        if (k == t + 1) {
-            Wvv_t = 2.0 * F.Wvv;
-            gv_t = 2.0 * (F.Wpv * P1 + F.lv);
-        }
-    }
+    StepForm F{0, 0, 0, 0, 0};
+    if (t < N) F = admm ? admm_form<N>(C, role, prm, t + 1, hs) : decent_form<N>(C, role, prm, t + 1);
+    const double wpp = t < N ? 2.0 * F.Wpp * ts * ts : 0.0;
+    const double wgp = t < N ? ts * 2.0 * (F.Wpp * P1 + F.lp) : 0.0;
+    // suffix sums: total - inclusive prefix + own
+    const double pre_pp = gscan(wpp), pre_gp = gscan(wgp);
+    const double tot_pp = bcast(pre_pp, G - 1), tot_gp = bcast(pre_gp, G - 1);
+    const double suf_pp = tot_pp - pre_pp + wpp;  // Spp(t + 1) at lane t
+    const double suf_gp = tot_gp - pre_gp + wgp;
+    const double spp_next = __shfl_down(suf_pp, 1, G);  // Spp(t + 2)
+    const double sgp_next = __shfl_down(suf_gp, 1, G);
+    const double spp2 = t + 1 < N ? spp_next : 0.0;
+    const double sgp2 = t + 1 < N ? sgp_next : 0.0;
+    const double wpv2 = 2.0 * F.Wpv * ts;
+    const double colv = spp2 + wpv2;  // value of column t in the rows above it
 #pragma unroll
     for (int c = 0; c < N; ++c) {
-        const int mx = c > t ? c : t;
-        double h = mx + 2 <= N ? Spp[mx + 2] : 0.0;
-        if (c < t) h += Wpv2[t + 1 <= N ? t + 1 : N];
-        if (c > t) h += Wpv2[c + 1];
-        if (c == t) h += Wvv_t;
-        Hrow[c] = h;
+        const double cv = bcast(colv, c);
+        if (t < N) Hrow[c] = c < t ? spp2 + wpv2 : (c > t ? cv : 2.0 * F.Wvv + spp2);
     }
-    f = gv_t + (t + 2 <= N ? Sgp[t + 2] : 0.0);
+    double f = 2.0 * (F.Wpv * P1 + F.lv) + sgp2;
     // input cost Qu u_k^2 (k < K) and variation Qdu (u_{k+1} - u_k)^2 (k + 1 < K)
     auto ucoef = [&](int k, double& ub, double& gk, double& gkm) {
         double a, b, c;
@@ -271,18 +268,14 @@ __device__ inline bool setup(Lane<N>& L, GroupLds& S_lds, const hvp_system& S, c
         if (t < K) {
             Hrow[t] += w2 * gk * gk;
             f += w2 * ub * gk;
-#pragma unroll
-            for (int c = 0; c < N; ++c)
-                if (c + 1 == t) Hrow[c] += w2 * gk * gkm;
+            if (t >= 1) Hrow[t - 1] += w2 * gk * gkm;
         }
         if (t + 1 < N && t + 1 < K) {
             double ub1, gk1, gkm1;
             ucoef(t + 1, ub1, gk1, gkm1);
             Hrow[t] += w2 * gkm1 * gkm1;
             f += w2 * ub1 * gkm1;
-#pragma unroll
-            for (int c = 0; c < N; ++c)
-                if (c == t + 1) Hrow[c] += w2 * gk1 * gkm1;
+            Hrow[t + 1] += w2 * gk1 * gkm1;
         }
         if (C.Qdu != 0.0) {
             const double wd = 2.0 * C.Qdu;
@@ -297,17 +290,11 @@ __device__ inline bool setup(Lane<N>& L, GroupLds& S_lds, const hvp_system& S, c
                 const double gt = t == k + 1 ? g_kp : (t == k ? g_k : (t == k - 1 ? g_km : 0.0));
                 if (gt == 0.0) continue;
                 f += wd * eb * gt;
-#pragma unroll
-                for (int c = 0; c < N; ++c) {
-                    const double gc = c == k + 1 ? g_kp : (c == k ? g_k : (c == k - 1 ? g_km : 0.0));
-                    Hrow[c] += wd * gt * gc;
-                }
+                Hrow[k + 1] += wd * gt * g_kp;
+                Hrow[k] += wd * gt * g_k;
+                if (k >= 1) Hrow[k - 1] += wd * gt * g_km;
             }
         }
-    }
-    if (t < N) {
-#pragma unroll
-        for (int c = 0; c < N; ++c) S_lds.J[t * LD + c] = Hrow[c];
     }
     L.f = t < N ? f : 0.0;
     return L.P1 >= S.pmin - 1e-9 * (1.0 + fabs(S.pmin)) && L.P1 <= S.pmax + 1e-9 * (1.0 + fabs(S.pmax));
@@ -429,24 +416,19 @@ __device__ inline int solve(Lane<N>& L, GroupLds& Sg, const Consts& C, int max_i
     }
     // ---- J = L^-T: row t of J = column t of L^-1 (forward substitution of e_t, all lanes)
     {
-        double x[N];
-#pragma unroll
-        for (int i = 0; i < N; ++i) {
-            double v = i == t ? 1.0 : 0.0;
-#pragma unroll
-            for (int k = 0; k < i; ++k) v -= R[i * LD + k] * x[k];
-            x[i] = v / R[i * LD + i];
-        }
+        // row t of J is column t of L^-1: forward substitution written in place (H is dead)
         gsync();
         if (t < N) {
-#pragma unroll
-            for (int c = 0; c < N; ++c) J[t * LD + c] = x[c];
+            for (int i = 0; i < N; ++i) {
+                double v = i == t ? 1.0 : 0.0;
+                for (int k = 0; k < i; ++k) v -= R[i * LD + k] * J[t * LD + k];
+                J[t * LD + i] = v / R[i * LD + i];
+            }
         }
+        gsync();
         // R starts empty
-        if (t < N) {
-#pragma unroll
+        if (t < N)
             for (int c = 0; c < N; ++c) R[t * LD + c] = 0.0;
-        }
         gsync();
     }
     double u = 0.0;  // multiplier of active position t
@@ -522,7 +504,7 @@ __device__ inline int solve(Lane<N>& L, GroupLds& Sg, const Consts& C, int max_i
         };
         const double dd = flip * d;
         const double np_t = t < N ? -cof(t) : 0.0;
-        const double dp = -dd;
+        const double dp = dd;  // slack of row p at y: n.y + dp = d - c.y
         double unew = 0.0;
         for (;;) {
             if (++iter > max_iter) { iters = iter; return GI_FAIL_ITER; }
@@ -535,28 +517,20 @@ __device__ inline int solve(Lane<N>& L, GroupLds& Sg, const Consts& C, int max_i
                     if (ni != 0.0) dv += J[i * LD + t] * ni;
                 }
             }
-            Sg.v[t] = dv;
+            double* dvr = Sg.v;  // dv, shared by the group
+            dvr[t] = dv;
             gsync();
-            double dvr[N];
-#pragma unroll
-            for (int c = 0; c < N; ++c) dvr[c] = Sg.v[c];
-            double d2n = 0.0, dn = 0.0;
-#pragma unroll
-            for (int c = 0; c < N; ++c) {
-                dn += dvr[c] * dvr[c];
-                if (c >= nact) d2n += dvr[c] * dvr[c];
-            }
+            const double dn = gsum(dv * dv);
+            const double d2n = gsum(t >= nact ? dv * dv : 0.0);
             // ---- z_t = sum_{c >= nact} J[t][c] dv_c
             double z = 0.0;
             if (t < N) {
-#pragma unroll
-                for (int c = 0; c < N; ++c)
-                    if (c >= nact) z += J[t * LD + c] * dvr[c];
+                for (int c = nact; c < N; ++c) z += J[t * LD + c] * dvr[c];
             }
             // ---- r = R^-1 dv (active part), column-oriented back substitution
             double r = 0.0;
             {
-                double accr = t < nact ? pick<N>(dvr, t) : 0.0;
+                double accr = t < nact ? dv : 0.0;
 #pragma unroll
                 for (int j = N - 1; j >= 0; --j) {
                     if (j >= nact) continue;
@@ -594,21 +568,22 @@ __device__ inline int solve(Lane<N>& L, GroupLds& Sg, const Consts& C, int max_i
             unew += tstep;
             if (t2 <= t1 && t2 <= t3) {
                 // ---- add p: Givens zeroing dv[nact+1 .. N-1] bottom-up, rotating J's columns
-#pragma unroll
-                for (int i = N - 1; i >= 1; --i) {
-                    if (i > nact) {
-                        double gc, gs;
-                        givens(dvr[i - 1], dvr[i], gc, gs);
-                        dvr[i - 1] = gc * dvr[i - 1] + gs * dvr[i];
-                        dvr[i] = 0.0;
-                        if (t < N) {
-                            const double a0 = J[t * LD + i - 1], a1 = J[t * LD + i];
-                            J[t * LD + i - 1] = gc * a0 + gs * a1;
-                            J[t * LD + i] = -gs * a0 + gc * a1;
-                        }
+                // (every lane runs the same rotation sequence on its register copy of the pair)
+                double carry = N - 1 > nact ? dvr[N - 1] : 0.0;
+                for (int i = N - 1; i > nact; --i) {
+                    const double lo = dvr[i - 1];
+                    double gc, gs;
+                    givens(lo, carry, gc, gs);
+                    carry = gc * lo + gs * carry;
+                    if (t < N) {
+                        const double a0 = J[t * LD + i - 1], a1 = J[t * LD + i];
+                        J[t * LD + i - 1] = gc * a0 + gs * a1;
+                        J[t * LD + i] = -gs * a0 + gc * a1;
                     }
                 }
-                if (t <= nact && t < N) R[t * LD + nact] = pick<N>(dvr, t);
+                // after the sweep dv[nact] = carry, dv[0..nact-1] unchanged
+                if (t < nact) R[t * LD + nact] = dv;
+                if (t == nact) R[t * LD + nact] = N - 1 > nact ? carry : dv;
                 if (t == nact) { u = unew; id = p; }
                 {
                     int ol, ob;
@@ -689,6 +664,182 @@ __device__ inline int solve(Lane<N>& L, GroupLds& Sg, const Consts& C, int max_i
         if (gi_soft<N>(id) && u > wgt * (1.0 + 1e-9)) bad = 1;
     }
     return gor(bad) ? GI_FAIL_VERIFY : GI_OK;
+}
+
+// ------------------------------------------------------------------ trajectory helpers
+// lane t: v_t (velocity entering step t), p_{t+1}, v_{t+1} of the group's trajectory y.
+template <int N>
+__device__ inline void lane_state(const Lane<N>& L, double& v_prev, double& p_next, double& v_next) {
+    const int t = lane16();
+    const double yv = t < N ? L.y : 0.0;
+    double vp = __shfl_up(yv, 1, G);
+    if (t == 0) vp = L.v0;
+    const double excl = gscan(yv) - yv;
+    v_prev = vp;
+    p_next = L.P1 + L.ts * excl;  // p_{t+1} = P1 + ts (y_0 + .. + y_{t-1})
+    v_next = yv;
+}
+
+// Objective (direct, term by term) of the decentralised local problem: lane t adds the terms
+// of state k = t + 1 and of input step t; lane 0 also those of x_0 (as direct_cost).
+template <int N>
+__device__ inline double direct_cost_decent(const Lane<N>& L, const hvp_system& S, const Consts& C, int role,
+                                            const double* prm, uint64_t code, int K) {
+    const int t = lane16();
+    const double* xf = prm + 2;
+    const double* xb = prm + 2 + 2 * (N + 1);
+    const double* xl = prm + 2 + 4 * (N + 1);
+    const bool tf = (role & HVP_ROLE_TRACK_FRONT) != 0, tb = (role & HVP_ROLE_TRACK_BACK) != 0;
+    const bool tl = (role & HVP_ROLE_TRACK_LEADER) != 0, lsp = (role & HVP_ROLE_LEADER_SPACING) != 0;
+    const bool sf = (role & HVP_ROLE_SAFE_FRONT) != 0, sb = (role & HVP_ROLE_SAFE_BACK) != 0;
+    const double Qpv2 = 2.0 * C.Qpv;
+    auto quad = [&](double ep, double ev) { return C.Qpp * ep * ep + Qpv2 * ep * ev + C.Qvv * ev * ev; };
+    auto state_terms = [&](int k, double p, double v) {
+        double J = 0.0;
+        if (tf) J += quad(p + C.t0 * v + C.d0 - xf[k], v - xf[N + 1 + k]);
+        if (tb) J += quad(xb[k] + C.t0 * xb[N + 1 + k] + C.d0 - p, xb[N + 1 + k] - v);
+        if (tl) J += quad(p - xl[k] + (lsp ? C.t0 * v + C.d0 : 0.0), v - xl[N + 1 + k]);
+        if (sf) J += C.w * fmax(0.0, p - xf[k] + C.d_safe);
+        if (sb) J += C.w * fmax(0.0, xb[k] + C.d_safe - p);
+        return J;
+    };
+    double vprev, pn, vn;
+    lane_state<N>(L, vprev, pn, vn);
+    double J = 0.0, u = 0.0;
+    if (t < N) {
+        J += state_terms(t + 1, pn, vn);
+        const int r = code_region(code, t);
+        u = (vn - S.a[r] * vprev - S.c[r]) / S.b[r];
+        if (t < K) J += C.Qu * u * u;
+    }
+    const double uprev = __shfl_up(u, 1, G);
+    if (t >= 1 && t < N && t < K) J += C.Qdu * (u - uprev) * (u - uprev);
+    if (t == 0) J += state_terms(0, prm[0], prm[1]);
+    return gsum(J);
+}
+
+template <int N>
+__device__ inline double direct_cost_admm(const Lane<N>& L, const hvp_system& S, const Consts& C, int role,
+                                          const double* prm, uint64_t code, int K) {
+    const int t = lane16();
+    const double* xl = admm_leader(prm, N);
+    const bool hf = (role & HVP_ROLE_SAFE_FRONT) != 0, hb = (role & HVP_ROLE_SAFE_BACK) != 0;
+    const bool tf = (role & HVP_ROLE_TRACK_FRONT) != 0, tb = (role & HVP_ROLE_TRACK_BACK) != 0;
+    const bool tl = (role & HVP_ROLE_TRACK_LEADER) != 0;
+    const int K1 = N + 1;
+    auto state_terms = [&](int k, double p, double v) {
+        double J = 0.0;
+        if (tl) {
+            const double ep = p - xl[k], ev = v - xl[K1 + k];
+            J += C.Qpp * ep * ep + 2.0 * C.Qpv * ep * ev + C.Qvv * ev * ev;
+        }
+        if (hf)
+            J += admm_copy_value(C, tf, 0, admm_y(prm, 0, N)[k], admm_y(prm, 0, N)[K1 + k], admm_z(prm, 0, N)[k],
+                                 admm_z(prm, 0, N)[K1 + k], p, v, nullptr, nullptr);
+        if (hb)
+            J += admm_copy_value(C, tb, 1, admm_y(prm, 1, N)[k], admm_y(prm, 1, N)[K1 + k], admm_z(prm, 1, N)[k],
+                                 admm_z(prm, 1, N)[K1 + k], p, v, nullptr, nullptr);
+        return J;
+    };
+    double vprev, pn, vn;
+    lane_state<N>(L, vprev, pn, vn);
+    double J = 0.0, u = 0.0;
+    if (t < N) {
+        J += state_terms(t + 1, pn, vn);
+        const int r = code_region(code, t);
+        u = (vn - S.a[r] * vprev - S.c[r]) / S.b[r];
+        if (t < K) J += C.Qu * u * u;
+    }
+    const double uprev = __shfl_up(u, 1, G);
+    if (t >= 1 && t < N && t < K) J += C.Qdu * (u - uprev) * (u - uprev);
+    if (t == 0) J += state_terms(0, prm[0], prm[1]);
+    return gsum(J);
+}
+
+// ADMM hinge states at the group's trajectory (k = t + 1 per lane); *consistent = no change
+template <int N>
+__device__ inline uint64_t admm_classify_group(const Lane<N>& L, const Consts& C, int role, const double* prm,
+                                               uint64_t hs, bool* consistent) {
+    const int t = lane16();
+    const bool hf = (role & HVP_ROLE_SAFE_FRONT) != 0, hb = (role & HVP_ROLE_SAFE_BACK) != 0;
+    const bool tf = (role & HVP_ROLE_TRACK_FRONT) != 0, tb = (role & HVP_ROLE_TRACK_BACK) != 0;
+    const int K1 = N + 1;
+    double vprev, p, v;
+    lane_state<N>(L, vprev, p, v);
+    unsigned long long mine = 0;
+    int changed = 0;
+    if (t < N) {
+        const int k = t + 1;
+        for (int side = 0; side < 2; ++side) {
+            if (!(side == 0 ? hf : hb)) continue;
+            const double* yy = admm_y(prm, side, N);
+            const double* zz = admm_z(prm, side, N);
+            CopyTerm T;
+            admm_copy(C, side == 0 ? tf : tb, side, yy[k], yy[K1 + k], zz[k], zz[K1 + k], T);
+            const double uu = T.gp * p + T.gv * v + T.g0;
+            const int old = hub_get(hs, k, side);
+            int st = hub_state(uu, C.w, T.kappa);
+            const double tol = 1e-10 * (1.0 + fabs(uu) + fabs(p));
+            if (st != old) {
+                const double lo = old == HUB_OFF ? -1e300 : (old == HUB_QUAD ? 0.0 : C.w * T.kappa);
+                const double hi = old == HUB_OFF ? 0.0 : (old == HUB_QUAD ? C.w * T.kappa : 1e300);
+                if (uu >= lo - tol && uu <= hi + tol) st = old;
+            }
+            if (st != old) changed = 1;
+            mine = hub_set(mine, k, side, st);
+        }
+    }
+    *consistent = gor(changed) == 0;
+    return gor64(mine);
+}
+
+// initial hinge states: those at the constant-velocity trajectory (as solve_admm_lane)
+template <int N>
+__device__ inline uint64_t admm_initial_states(Lane<N>& L, const Consts& C, int role, const double* prm) {
+    const double ysave = L.y;
+    L.y = prm[1];
+    bool c;
+    const uint64_t hs = admm_classify_group<N>(L, C, role, prm, 0, &c);
+    L.y = ysave;
+    return hs;
+}
+
+// One fixed-sequence (relaxed beyond K) QP of either formulation, solved by the group.
+// Returns GI_OK with y in L.y (lane t < N) and the direct objective in *cost.
+template <int N>
+__device__ inline int solve_qp(Lane<N>& L, GroupLds& Sg, const hvp_system& S, const Consts& C, int role,
+                               const double* prm, uint64_t code, int K, int max_iter, int& iters, double* cost) {
+    iters = 0;
+    if (C.form == HVP_FORM_ADMM) {
+        uint64_t hs;
+        {
+            // lane data for the classification helpers
+            Lane<N> L0;
+            setup<N>(L0, Sg, S, C, role, prm, code, K, 0);
+            hs = admm_initial_states<N>(L0, C, role, prm);
+        }
+        for (int round = 0; round < kHubRounds; ++round) {
+            gsync();
+            setup<N>(L, Sg, S, C, role, prm, code, K, hs);
+            int it = 0;
+            const int st = solve<N>(L, Sg, C, max_iter, it);
+            iters += it;
+            if (st != GI_OK) return st;
+            bool consistent;
+            hs = admm_classify_group<N>(L, C, role, prm, hs, &consistent);
+            if (consistent) {
+                *cost = direct_cost_admm<N>(L, S, C, role, prm, code, K);
+                return GI_OK;
+            }
+        }
+        return GI_FAIL_ITER;
+    }
+    gsync();
+    setup<N>(L, Sg, S, C, role, prm, code, K, 0);
+    const int st = solve<N>(L, Sg, C, max_iter, iters);
+    if (st != GI_OK) return st;
+    *cost = direct_cost_decent<N>(L, S, C, role, prm, code, K);
+    return GI_OK;
 }
 
 }  // namespace coop

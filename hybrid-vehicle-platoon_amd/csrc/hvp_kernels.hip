@@ -30,6 +30,7 @@
 #include "hvp.h"
 #include "hvp_admm.h"
 #include "hvp_bnb.h"
+#include "hvp_coop.h"
 #include "hvp_gi.h"
 #include "hvp_ipm.h"
 
@@ -433,6 +434,126 @@ __global__ __launch_bounds__(kBnbBlock<N>) void k_bnb_root(int B, const hvp_syst
     ws.iters[i] = iters;
     atomicAdd(&ws.counter[3], (unsigned long long)nodes);
     atomicAdd(&ws.counter[1], (unsigned long long)iters);
+}
+
+// ---- long horizons: one QP per 16-lane group (hvp_coop.h), 4 groups per 64-lane block
+template <int N>
+constexpr bool kCoop = N > HVP_MAX_N_ENUM;
+constexpr int kCoopBlock = 64;
+constexpr int kCoopGroups = kCoopBlock / hvp::coop::G;
+
+template <int N>
+__global__ __launch_bounds__(kCoopBlock) void k_bnb_root_coop(int B, const hvp_system* __restrict__ systems,
+                                                              const int32_t* __restrict__ sys,
+                                                              const int32_t* __restrict__ role,
+                                                              const double* __restrict__ params, hvp::Consts C,
+                                                              Workspace ws) {
+    __shared__ hvp::coop::GroupLds lds[kCoopGroups];
+    const int g = threadIdx.x / hvp::coop::G, t = threadIdx.x % hvp::coop::G;
+    const int i = blockIdx.x * kCoopGroups + g;
+    if (blockIdx.x == 0 && threadIdx.x == 0) ws.lvl[0] = (unsigned long long)B;
+    if (i >= B) return;  // group-uniform
+    const hvp_system& S = systems[sys[i]];
+    const int rl = role[i];
+    const double* prm = params + (size_t)i * C.stride;
+    const double v0 = prm[1], P1 = prm[0] + S.ts * v0;
+    const bool ok = P1 >= S.pmin - 1e-9 * (1.0 + fabs(S.pmin)) && P1 <= S.pmax + 1e-9 * (1.0 + fabs(S.pmax));
+    double inc = __longlong_as_double(0x7ff0000000000000ll);
+    double lb = -1e300;
+    int nodes = 0, iters = 0;
+    if (ok) {
+        hvp::coop::Lane<N> L;
+        double c0 = 0.0;
+        int it = 0;
+        int st = hvp::coop::solve_qp<N>(L, lds[g], S, C, rl, prm, 0, 0, kGiMaxIter<N>, it, &c0);
+        ++nodes;
+        iters += it;
+        if (st == hvp::GI_OK) {
+            lb = c0;
+            lds[g].v[t] = t < N ? L.y : 0.0;
+            hvp::coop::gsync();
+            unsigned long long code = 0;
+            int dive_ok = 0;
+            if (t == 0) {
+                double ystar[N];
+#pragma unroll
+                for (int k = 0; k < N; ++k) ystar[k] = lds[g].v[k];
+                uint64_t c64;
+                dive_ok = hvp::bnb_dive<N>(S, C, v0, ystar, &c64) ? 1 : 0;
+                code = c64;
+            }
+            dive_ok = hvp::coop::bcast(dive_ok, 0);
+            code = hvp::coop::bcast(code, 0);
+            if (dive_ok) {
+                double c1 = 0.0;
+                st = hvp::coop::solve_qp<N>(L, lds[g], S, C, rl, prm, code, N, kGiMaxIter<N>, it, &c1);
+                ++nodes;
+                iters += it;
+                if (st == hvp::GI_OK) inc = c1;
+            }
+        }
+    }
+    if (t == 0) {
+        ws.key[i] = ~0ull;
+        ws.inst_flag[i] = ok ? 0 : 1;
+        ws.nd_inst[0][i] = ok ? i : -1;
+        ws.nd_code[0][i] = 0;
+        ws.nd_lo[0][i] = v0;
+        ws.nd_hi[0][i] = v0;
+        ws.nd_lb[0][i] = lb;
+        ws.inc[i] = cost_key(inc);
+        ws.nodes[i] = nodes;
+        ws.iters[i] = iters;
+        atomicAdd(&ws.counter[3], (unsigned long long)nodes);
+        atomicAdd(&ws.counter[1], (unsigned long long)iters);
+    }
+}
+
+template <int N>
+__global__ __launch_bounds__(kCoopBlock) void k_bnb_bound_coop(int k, const hvp_system* __restrict__ systems,
+                                                               const int32_t* __restrict__ sys,
+                                                               const int32_t* __restrict__ role,
+                                                               const double* __restrict__ params, hvp::Consts C,
+                                                               Workspace ws) {
+    __shared__ hvp::coop::GroupLds lds[kCoopGroups];
+    const int g = threadIdx.x / hvp::coop::G, t = threadIdx.x % hvp::coop::G;
+    const int dst = k & 1;
+    const unsigned long long nn = ws.lvl[k];
+    const long long total = (long long)(nn < (unsigned long long)ws.cap ? nn : ws.cap);
+    for (long long q = (long long)blockIdx.x * kCoopGroups + g; q < total; q += (long long)gridDim.x * kCoopGroups) {
+        const int inst = ws.nd_inst[dst][q];
+        if (inst < 0) {
+            if (t == 0) {
+                if (k == N) ws.leaf_stat[q] = HVP_OVERFLOW;
+                else ws.nd_lb[dst][q] = 1e300;
+            }
+            continue;
+        }
+        const uint64_t code = ws.nd_code[dst][q];
+        const hvp_system& S = systems[sys[inst]];
+        const int rl = role[inst];
+        const double* prm = params + (size_t)inst * C.stride;
+        hvp::coop::Lane<N> L;
+        double c = 0.0;
+        int it = 0;
+        const int st = hvp::coop::solve_qp<N>(L, lds[g], S, C, rl, prm, code, k, kGiMaxIter<N>, it, &c);
+        const bool ok = st == hvp::GI_OK;
+        if (k == N && t < N) ws.task_y[q * N + t] = L.y;
+        if (t == 0) {
+            atomicAdd(&ws.nodes[inst], 1);
+            atomicAdd(&ws.iters[inst], it);
+            atomicAdd(&ws.counter[1], (unsigned long long)it);
+            if (k < N) {
+                ws.nd_lb[dst][q] = ok ? c : -1e300;
+                if (!ok) atomicAdd(&ws.counter[4], 1ull);
+            } else {
+                if (ok) ws.nd_lb[dst][q] = c;
+                ws.leaf_stat[q] = ok ? 0 : HVP_MAXITER;
+                if (ok) atomicMin(&ws.inc[inst], cost_key(c));
+                else atomicOr(&ws.inst_flag[inst], 8);
+            }
+        }
+    }
 }
 
 // children of the level-(k-1) nodes that survive the incumbent test
@@ -847,8 +968,13 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
     HIP_TRY(hipEventRecord(h->evq0, st));
     const size_t lds = sizeof(double) * hvp::F_COUNT * N * BS;
     HIP_TRY(hipEventRecord(h->evb[0], st));
-    hipLaunchKernelGGL(k_bnb_root<N>, dim3((B + BS - 1) / BS), dim3(BS), lds, st, B, h->d_sys, sys, role, params,
-                       h->C, ws);
+    if constexpr (kCoop<N>) {
+        hipLaunchKernelGGL(k_bnb_root_coop<N>, dim3((B + kCoopGroups - 1) / kCoopGroups), dim3(kCoopBlock), 0, st, B,
+                           h->d_sys, sys, role, params, h->C, ws);
+    } else {
+        hipLaunchKernelGGL(k_bnb_root<N>, dim3((B + BS - 1) / BS), dim3(BS), lds, st, B, h->d_sys, sys, role, params,
+                           h->C, ws);
+    }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(h->evb[1], st));
     const int g_small = (int)std::min<long long>(grid_for(h->ws.cap), (long long)h->n_cu * 8);
@@ -859,7 +985,15 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
         hipLaunchKernelGGL(k_bnb_expand<N>, dim3(g_small), dim3(kBlock), 0, st, k, quota, h->d_sys, sys, h->C, ws);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(h->evb[2 * k], st));
-        hipLaunchKernelGGL(k_bnb_bound<N>, dim3(g_qp), dim3(BS), lds, st, k, h->d_sys, sys, role, params, h->C, ws);
+        if constexpr (kCoop<N>) {
+            const int g_coop = (int)std::min<long long>((h->ws.cap + kCoopGroups - 1) / kCoopGroups,
+                                                        (long long)h->n_cu * 32);
+            hipLaunchKernelGGL(k_bnb_bound_coop<N>, dim3(g_coop), dim3(kCoopBlock), 0, st, k, h->d_sys, sys, role,
+                               params, h->C, ws);
+        } else {
+            hipLaunchKernelGGL(k_bnb_bound<N>, dim3(g_qp), dim3(BS), lds, st, k, h->d_sys, sys, role, params, h->C,
+                               ws);
+        }
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(h->evb[2 * k + 1], st));
     }
