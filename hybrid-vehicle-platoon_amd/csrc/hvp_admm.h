@@ -157,6 +157,46 @@ HVP_HD inline const double* admm_y(const double* prm, int side, int N) { return 
 HVP_HD inline const double* admm_z(const double* prm, int side, int N) { return prm + 2 + (2 * side + 1) * 2 * (N + 1); }
 HVP_HD inline const double* admm_leader(const double* prm, int N) { return prm + 2 + 8 * (N + 1); }
 
+// ---------------------------------------------------------------- switching ADMM (HVP_FORM_GADMM)
+// fleet_g_admm.LocalMpc (:22-205) for a GIVEN region sequence.  Same velocity-space problem as
+// the naive-ADMM local problem with two differences: the vehicle's OWN trajectory is part of
+// the augmented state (MpcAdmm [EXT]: y_own'(x_k - z_own,k) + rho/2 |x_k - z_own,k|^2 for
+// k = 0..N), and the copy of the vehicle behind (HVP_ROLE_BACK_COPY) carries its ADMM term only
+// (the cost tracks the front copy only, :136-158; safety only w.r.t. it, :98-109), so it
+// decouples: c_b = z_b - y_b / rho with value -|y_b|^2 / (2 rho) per step.
+// Parameter block (hvp_params_stride_gadmm(N)): the ADMM block followed by y_own | z_own.
+HVP_HD inline const double* gadmm_yo(const double* prm, int N) { return prm + 2 + 10 * (N + 1); }
+HVP_HD inline const double* gadmm_zo(const double* prm, int N) { return prm + 2 + 12 * (N + 1); }
+
+// own-state ADMM term at step k as a form x'Wx + 2 l'x + cc
+HVP_HD inline void gadmm_own_add(const Consts& C, const double* prm, int N, int k, double& Wpp, double& Wvv,
+                                 double& lp, double& lv, double& cc) {
+    const int K1 = N + 1;
+    const double* yo = gadmm_yo(prm, N);
+    const double* zo = gadmm_zo(prm, N);
+    const double y0 = yo[k], y1 = yo[K1 + k], z0 = zo[k], z1 = zo[K1 + k];
+    Wpp += 0.5 * C.rho;
+    Wvv += 0.5 * C.rho;
+    lp += 0.5 * (y0 - C.rho * z0);
+    lv += 0.5 * (y1 - C.rho * z1);
+    cc += 0.5 * C.rho * (z0 * z0 + z1 * z1) - (y0 * z0 + y1 * z1);
+}
+
+// own-state ADMM term of state k and the back-copy term, evaluated directly
+HVP_HD inline double gadmm_state_terms(const Consts& C, int role, const double* prm, int N, int k, double p,
+                                       double v) {
+    const int K1 = N + 1;
+    const double* yo = gadmm_yo(prm, N);
+    const double* zo = gadmm_zo(prm, N);
+    const double dp = p - zo[k], dv = v - zo[K1 + k];
+    double J = yo[k] * dp + yo[K1 + k] * dv + 0.5 * C.rho * (dp * dp + dv * dv);
+    if (role & HVP_ROLE_BACK_COPY) {
+        const double* yb = admm_y(prm, 1, N);
+        J -= (yb[k] * yb[k] + yb[K1 + k] * yb[K1 + k]) / (2.0 * C.rho);
+    }
+    return J;
+}
+
 // Velocity-space QP of the ADMM local problem for region code (first K steps fixed) and the
 // hinge states hs.  Same row set and input-cost terms as setup_lane; the safe-distance rows are
 // inert (the safety lives in the copies' hinges).
@@ -238,6 +278,7 @@ HVP_HD inline bool setup_lane_admm(LaneQp<N, M>& q, const hvp_system& S, const C
             cc += T.cc;
             hub_add(T, hub_get(hs, k, side), C.w, Wpp, Wpv, Wvv, lp, lv, cc);
         }
+        if (C.form == HVP_FORM_GADMM) gadmm_own_add(C, prm, N, k, Wpp, Wvv, lp, lv, cc);
         // x_k = xbar + Gamma y : p = P1 + ts prefix(0..k-2), v = e_{k-1}
         const double pbar = q.P1;
         const double gp = 2.0 * (Wpp * pbar + lp);
@@ -388,6 +429,7 @@ HVP_HD inline double admm_direct_cost(const LaneQp<N, M>& q, const hvp_system& S
         if (hb)
             J += admm_copy_value(C, tb, 1, admm_y(prm, 1, N)[k], admm_y(prm, 1, N)[K1 + k], admm_z(prm, 1, N)[k],
                                  admm_z(prm, 1, N)[K1 + k], p, v, nullptr, nullptr);
+        if (C.form == HVP_FORM_GADMM) J += gadmm_state_terms(C, role, prm, N, k, p, v);
         if (k < N) {
             const int r = code_region(code, k);
             const double vn = q.y[k];
@@ -408,7 +450,7 @@ HVP_HD inline double admm_direct_cost(const LaneQp<N, M>& q, const hvp_system& S
 constexpr int kHubRounds = 12;
 template <int N, class M>
 HVP_HD inline int solve_admm_lane(LaneQp<N, M>& q, const hvp_system& S, const Consts& C, int role, const double* prm,
-                                  uint64_t code, int K, int max_iter, int& iters) {
+                                  uint64_t code, int K, int max_iter, int& iters, uint32_t* edge = nullptr) {
     uint64_t hs = 0;
     iters = 0;
     // initial states: those of the unconstrained copies at the constant-velocity trajectory
@@ -422,7 +464,7 @@ HVP_HD inline int solve_admm_lane(LaneQp<N, M>& q, const hvp_system& S, const Co
     for (int round = 0; round < kHubRounds; ++round) {
         setup_lane_admm<N>(q, S, C, role, prm, code, K, hs);
         int it = 0;
-        const int st = solve_gi<N>(q, C, max_iter, it);
+        const int st = solve_gi<N>(q, C, max_iter, it, edge);
         iters += it;
         if (st != GI_OK) return st;
         bool consistent;

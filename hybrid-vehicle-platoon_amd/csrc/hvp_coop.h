@@ -172,6 +172,7 @@ __device__ inline StepForm admm_form(const Consts& C, int role, const double* pr
         lv += T.lv;
         hub_add(T, hub_get(hs, k, side), C.w, Wpp, Wpv, Wvv, lp, lv, cc);
     }
+    if (C.form == HVP_FORM_GADMM) gadmm_own_add(C, prm, N, k, Wpp, Wvv, lp, lv, cc);
     return StepForm{Wpp, Wpv, Wvv, lp, lv};
 }
 
@@ -180,7 +181,7 @@ template <int N>
 __device__ inline bool setup(Lane<N>& L, GroupLds& S_lds, const hvp_system& S, const Consts& C, int role,
                              const double* prm, uint64_t code, int K, uint64_t hs) {
     const int t = lane16();
-    const bool admm = C.form == HVP_FORM_ADMM;
+    const bool admm = C.form == HVP_FORM_ADMM || C.form == HVP_FORM_GADMM;
     const double p0 = prm[0], v0 = prm[1], ts = S.ts;
     L.v0 = v0;
     L.ts = ts;
@@ -364,7 +365,8 @@ __device__ inline void row_owner(int id_in, int& lane, int& bit) {
 
 // Cooperative Goldfarb-Idnani.  On GI_OK lane t < N holds y_t in L.y.
 template <int N>
-__device__ inline int solve(Lane<N>& L, GroupLds& Sg, const Consts& C, int max_iter, int& iters) {
+__device__ inline int solve(Lane<N>& L, GroupLds& Sg, const Consts& C, int max_iter, int& iters,
+                            unsigned* edge = nullptr) {
     const int t = lane16();
     iters = 0;
     double* J = Sg.J;  // holds H on entry (row t written by lane t)
@@ -663,6 +665,11 @@ __device__ inline int solve(Lane<N>& L, GroupLds& Sg, const Consts& C, int max_i
         if (u < -1e-9 * wgt) bad = 1;
         if (gi_soft<N>(id) && u > wgt * (1.0 + 1e-9)) bad = 1;
     }
+    if (edge) {
+        int bit = 0;
+        if (t < nact && id >= 0 && id < 6 * N && id % 6 < 2 && u > kEdgeMultTol) bit = 1 << (2 * (id / 6) + id % 6);
+        *edge = (unsigned)gor(bit);
+    }
     return gor(bad) ? GI_FAIL_VERIFY : GI_OK;
 }
 
@@ -739,6 +746,7 @@ __device__ inline double direct_cost_admm(const Lane<N>& L, const hvp_system& S,
         if (hb)
             J += admm_copy_value(C, tb, 1, admm_y(prm, 1, N)[k], admm_y(prm, 1, N)[K1 + k], admm_z(prm, 1, N)[k],
                                  admm_z(prm, 1, N)[K1 + k], p, v, nullptr, nullptr);
+        if (C.form == HVP_FORM_GADMM) J += gadmm_state_terms(C, role, prm, N, k, p, v);
         return J;
     };
     double vprev, pn, vn;
@@ -808,9 +816,10 @@ __device__ inline uint64_t admm_initial_states(Lane<N>& L, const Consts& C, int 
 // Returns GI_OK with y in L.y (lane t < N) and the direct objective in *cost.
 template <int N>
 __device__ inline int solve_qp(Lane<N>& L, GroupLds& Sg, const hvp_system& S, const Consts& C, int role,
-                               const double* prm, uint64_t code, int K, int max_iter, int& iters, double* cost) {
+                               const double* prm, uint64_t code, int K, int max_iter, int& iters, double* cost,
+                               unsigned* edge = nullptr) {
     iters = 0;
-    if (C.form == HVP_FORM_ADMM) {
+    if (C.form == HVP_FORM_ADMM || C.form == HVP_FORM_GADMM) {
         uint64_t hs;
         {
             // lane data for the classification helpers
@@ -822,7 +831,7 @@ __device__ inline int solve_qp(Lane<N>& L, GroupLds& Sg, const hvp_system& S, co
             gsync();
             setup<N>(L, Sg, S, C, role, prm, code, K, hs);
             int it = 0;
-            const int st = solve<N>(L, Sg, C, max_iter, it);
+            const int st = solve<N>(L, Sg, C, max_iter, it, edge);
             iters += it;
             if (st != GI_OK) return st;
             bool consistent;

@@ -170,8 +170,13 @@ HVP_HD inline void givens(double a, double b, double& c, double& s) {
 // penalty term turns inactive again (c_i.y < d_i) shows up as a violated REVERSED soft row
 // -c_i.y <= -d_i; saturating that reversed row (multiplier w) cancels the linear term, i.e. the
 // row leaves S.  Returns GI_OK with the optimum in q.y, or a GI_FAIL_* reason.
+// Multiplier above which an active velocity row counts for the switching rule (hvp_gadmm.h).
+constexpr double kEdgeMultTol = 1e-6;
+
+// edge (optional): bit 2 j + 0 / + 1 set when the V_lo / V_hi row of y_j (= v_{j+1}) is active
+// at the optimum with multiplier > kEdgeMultTol.
 template <int N, class M>
-HVP_HD inline int solve_gi(LaneQp<N, M>& q, const Consts& C, int max_iter, int& iters) {
+HVP_HD inline int solve_gi(LaneQp<N, M>& q, const Consts& C, int max_iter, int& iters, uint32_t* edge = nullptr) {
     iters = 0;
     // ---- unconstrained minimiser and J = L^-T
     double L[N * (N + 1) / 2];
@@ -415,6 +420,15 @@ HVP_HD inline int solve_gi(LaneQp<N, M>& q, const Consts& C, int max_iter, int& 
         }
     }
     // primal feasibility and the saturated rows' sides hold by the exit condition of step 1
+    if (edge) {
+        uint32_t m = 0;
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            if (j < nact && ids[j] >= 0 && ids[j] < 6 * N && ids[j] % 6 < 2 && u[j] > kEdgeMultTol)
+                m |= 1u << (2 * (ids[j] / 6) + ids[j] % 6);
+        }
+        *edge = m;
+    }
     return ok ? GI_OK : GI_FAIL_VERIFY;
 }
 

@@ -41,7 +41,9 @@ hvp::Consts make_consts(const hvp_problem& p) {
     C.max_iter = p.max_iter > 0 ? p.max_iter : 60;
     C.N = p.N;
     C.form = p.formulation;
-    C.stride = p.formulation == HVP_FORM_ADMM ? hvp_params_stride_admm(p.N) : hvp_params_stride(p.N);
+    C.stride = p.formulation == HVP_FORM_ADMM    ? hvp_params_stride_admm(p.N)
+               : p.formulation == HVP_FORM_GADMM ? hvp_params_stride_gadmm(p.N)
+                                                 : hvp_params_stride(p.N);
     C.rho = p.rho;
     return C;
 }
@@ -306,9 +308,79 @@ void solve_range(const hvp_problem& P, const hvp_system* systems, int B, const i
     }
 }
 
+// switching-ADMM local QP of one vehicle for its sequence (the lane path of k_gadmm_qp)
+template <int N>
+void gadmm_one(const hvp_system& S, const hvp::Consts& C, int role, const double* prm, const int8_t* seq, double* u,
+               double* x, double* xf, double* xb, double* cost, int32_t* status, uint32_t* edge) {
+    uint64_t code = 0;
+    for (int k = 0; k < N; ++k) code = hvp::code_with(code, k, seq[k]);
+    hvp::LaneQp<N> q;
+    int it = 0;
+    uint32_t raw = 0;
+    const int st = hvp::solve_admm_lane<N>(q, S, C, role, prm, code, N, 8 * hvp::GiConstraintSet<N>::NC, it, &raw);
+    if (st != hvp::GI_OK) {
+        *status = st == hvp::GI_FAIL_DUAL ? HVP_INFEASIBLE : HVP_MAXITER;
+        *cost = 1e300;
+        *edge = 0;
+        return;
+    }
+    *status = HVP_OPTIMAL;
+    *cost = hvp::admm_direct_cost<N>(q, S, C, role, prm, code, N);
+    uint32_t e = 0;  // region edges strictly inside the state box (k_gadmm_qp's gadmm_edges)
+    for (int j = 0; j + 1 < N; ++j) {
+        const int r = hvp::code_region(code, j + 1);
+        if (((raw >> (2 * j)) & 1u) && S.vlo[r] > S.vmin + 1e-9 * (1.0 + fabs(S.vlo[r]))) e |= 1u << (2 * j);
+        if (((raw >> (2 * j + 1)) & 1u) && S.vhi[r] < S.vmax - 1e-9 * (1.0 + fabs(S.vhi[r]))) e |= 1u << (2 * j + 1);
+    }
+    *edge = e;
+    const int K1 = N + 1;
+    double p = prm[0], v = prm[1];
+    for (int k = 0; k <= N; ++k) {
+        x[k] = p;
+        x[K1 + k] = v;
+        double fe = 0.0, fg = 0.0;
+        if (role & HVP_ROLE_SAFE_FRONT)
+            hvp::admm_copy_value(C, (role & HVP_ROLE_TRACK_FRONT) != 0, 0, hvp::admm_y(prm, 0, N)[k],
+                                 hvp::admm_y(prm, 0, N)[K1 + k], hvp::admm_z(prm, 0, N)[k],
+                                 hvp::admm_z(prm, 0, N)[K1 + k], p, v, &fe, &fg);
+        xf[k] = fe;
+        xf[K1 + k] = fg;
+        const bool back = (role & HVP_ROLE_BACK_COPY) != 0;
+        xb[k] = back ? hvp::admm_z(prm, 1, N)[k] - hvp::admm_y(prm, 1, N)[k] / C.rho : 0.0;
+        xb[K1 + k] = back ? hvp::admm_z(prm, 1, N)[K1 + k] - hvp::admm_y(prm, 1, N)[K1 + k] / C.rho : 0.0;
+        if (k < N) {
+            const int r = hvp::code_region(code, k);
+            u[k] = (q.y[k] - S.a[r] * v - S.c[r]) / S.b[r];
+            p = p + S.ts * v;
+            v = q.y[k];
+        }
+    }
+}
+
 }  // namespace
 
 extern "C" {
+
+// HVP_FORM_GADMM local QPs for given sequences (test use only): the lane algorithm on the host.
+int hvp_hostref_gadmm_solve(const hvp_problem* P, const hvp_system* systems, int B, const int32_t* sys,
+                            const int32_t* role, const double* params, const int8_t* seq, double* u, double* x,
+                            double* xf, double* xb, double* cost, int32_t* status, uint32_t* edge) {
+    if (P->formulation != HVP_FORM_GADMM) return HVP_E_ARG;
+    const hvp::Consts C = make_consts(*P);
+    const int N = P->N, E = 2 * (N + 1);
+    for (int i = 0; i < B; ++i) {
+        const double* prm = params + (size_t)i * C.stride;
+        switch (N) {
+#define HVP_CASE(n) \
+    case n: gadmm_one<n>(systems[sys[i]], C, role[i], prm, seq + (size_t)i * N, u + (size_t)i * N, x + (size_t)i * E, xf + (size_t)i * E, xb + (size_t)i * E, cost + i, status + i, edge + i); break;
+            HVP_CASE(2) HVP_CASE(3) HVP_CASE(4) HVP_CASE(5) HVP_CASE(6) HVP_CASE(7) HVP_CASE(8)
+            HVP_CASE(9) HVP_CASE(10) HVP_CASE(11) HVP_CASE(12) HVP_CASE(13) HVP_CASE(14) HVP_CASE(15) HVP_CASE(16)
+#undef HVP_CASE
+            default: return HVP_E_UNSUPPORTED;
+        }
+    }
+    return 0;
+}
 
 void hvp_hostref_set_solver(int s) { g_solver = s; }
 void hvp_hostref_gi_stats(long long* out) {

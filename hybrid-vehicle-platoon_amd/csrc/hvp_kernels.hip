@@ -105,6 +105,7 @@ struct hvp_handle {
     // host-pointer entry point staging (grown on demand)
     size_t stage_bytes = 0;
     char* d_stage = nullptr;
+    unsigned long long* g_counter = nullptr;  // [8] switching-ADMM counters (QP iterations at [1])
 };
 
 namespace {
@@ -129,7 +130,9 @@ hvp::Consts make_consts(const hvp_problem& p) {
     C.max_iter = p.max_iter > 0 ? p.max_iter : 60;
     C.N = p.N;
     C.form = p.formulation;
-    C.stride = p.formulation == HVP_FORM_ADMM ? hvp_params_stride_admm(p.N) : hvp_params_stride(p.N);
+    C.stride = p.formulation == HVP_FORM_ADMM    ? hvp_params_stride_admm(p.N)
+               : p.formulation == HVP_FORM_GADMM ? hvp_params_stride_gadmm(p.N)
+                                                 : hvp_params_stride(p.N);
     C.rho = p.rho;
     return C;
 }
@@ -953,6 +956,296 @@ __global__ __launch_bounds__(kBlock) void k_admm_update(int P, int n, int N, dou
     }
 }
 
+// ================================================================== switching ADMM (HVP_FORM_GADMM)
+// TrackingGAdmmCoordinator / GAdmmCoordinator (fleet_g_admm.py:208-301, dmpcpwa [EXT]) for P
+// platoons: rollout of the warm start, per ADMM iteration one local-QP launch + one consensus
+// launch, sequence switching per round (include/hvp.h "Switching ADMM").  Instance b holds
+// vehicle i = lo + b % m of platoon p = b / m; trajectories live in full-platoon slots p n + i.
+__device__ inline int gadmm_slot(int b, int n, int lo, int m) { return (b / m) * n + lo + b % m; }
+
+__device__ inline void gadmm_fail(int32_t* state, int p) {
+    atomicOr(&state[p], 2);
+    atomicAnd(&state[p], ~1);
+}
+
+// first region whose closed velocity band holds v (buf widens the lower edge: the [0, 1e-4]
+// buffer of PwaGearVehicle.find_region used by get_u_for_constant_vel, models.py:519-540)
+__device__ inline int gadmm_region(const hvp_system& S, double v, double buf) {
+    for (int r = 0; r < S.n_regions; ++r)
+        if (v >= S.vlo[r] - buf && v <= S.vhi[r]) return r;
+    return -1;
+}
+
+template <int N>
+__global__ __launch_bounds__(kBlock) void k_gadmm_rollout(int P, int n, int lo, int m,
+                                                          const hvp_system* __restrict__ systems,
+                                                          const int32_t* __restrict__ sys,
+                                                          const double* __restrict__ params, int stride, int mode,
+                                                          const double* __restrict__ u_prev, double* __restrict__ x,
+                                                          int8_t* __restrict__ seq, double* __restrict__ u_ws,
+                                                          int32_t* __restrict__ state) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= P * m) return;
+    const int p = b / m;
+    const hvp_system& S = systems[sys[b]];
+    const double* prm = params + (size_t)b * stride;
+    double pk = prm[0], vk = prm[1];
+    double* xs = x + (size_t)gadmm_slot(b, n, lo, m) * 2 * (N + 1);
+    bool ok = true;
+    double ucv = 0.0;
+    if (mode == 0) {
+        const int r = gadmm_region(S, vk, 1e-4);
+        if (r < 0) ok = false;
+        else ucv = ((1.0 - S.a[r]) * vk - S.c[r]) / S.b[r];
+    }
+    xs[0] = pk;
+    xs[N + 1] = vk;
+    for (int k = 0; k < N; ++k) {
+        const double u = mode == 0 ? ucv : u_prev[(size_t)b * N + (k + 1 < N ? k + 1 : N - 1)];
+        int r = gadmm_region(S, vk, 0.0);
+        if (r < 0) { ok = false; r = 0; }
+        seq[(size_t)b * N + k] = (int8_t)r;
+        if (u_ws) u_ws[(size_t)b * N + k] = u;
+        const double vn = S.a[r] * vk + S.b[r] * u + S.c[r];
+        pk = pk + S.ts * vk;
+        vk = vn;
+        xs[k + 1] = pk;
+        xs[N + 1 + k + 1] = vk;
+    }
+    if (!ok) gadmm_fail(state, p);
+}
+
+// edge bits of the switching rule: active V rows at a region edge strictly inside the state box
+template <int N>
+__device__ inline uint32_t gadmm_edges(const hvp_system& S, uint64_t code, uint32_t raw) {
+    uint32_t out = 0;
+#pragma unroll
+    for (int j = 0; j + 1 < N; ++j) {
+        const int r = hvp::code_region(code, j + 1);
+        const double lo = S.vlo[r], hi = S.vhi[r];
+        if (((raw >> (2 * j)) & 1u) && lo > S.vmin + 1e-9 * (1.0 + fabs(lo))) out |= 1u << (2 * j);
+        if (((raw >> (2 * j + 1)) & 1u) && hi < S.vmax - 1e-9 * (1.0 + fabs(hi))) out |= 1u << (2 * j + 1);
+    }
+    return out;
+}
+
+// outputs of one solved local problem: u, trajectory slot, copies (front: closed-form optimum of
+// its hinge problem, back: z_b - y_b / rho)
+template <int N>
+__device__ inline void gadmm_write(int b, int slot, const hvp_system& S, const hvp::Consts& C, int rl,
+                                   const double* prm, uint64_t code, const double* y, double* u_out, double* x,
+                                   double* xf, double* xb) {
+    const int K1 = N + 1;
+    double* xs = x + (size_t)slot * 2 * K1;
+    double* fs = xf + (size_t)slot * 2 * K1;
+    double* bs = xb + (size_t)slot * 2 * K1;
+    const bool front = (rl & HVP_ROLE_SAFE_FRONT) != 0, back = (rl & HVP_ROLE_BACK_COPY) != 0;
+    const bool tf = (rl & HVP_ROLE_TRACK_FRONT) != 0;
+    const double* yb = hvp::admm_y(prm, 1, N);
+    const double* zb = hvp::admm_z(prm, 1, N);
+    double p = prm[0], v = prm[1];
+    for (int k = 0; k <= N; ++k) {
+        xs[k] = p;
+        xs[K1 + k] = v;
+        double e = 0.0, g = 0.0;
+        if (front)
+            hvp::admm_copy_value(C, tf, 0, hvp::admm_y(prm, 0, N)[k], hvp::admm_y(prm, 0, N)[K1 + k],
+                                 hvp::admm_z(prm, 0, N)[k], hvp::admm_z(prm, 0, N)[K1 + k], p, v, &e, &g);
+        fs[k] = e;
+        fs[K1 + k] = g;
+        bs[k] = back ? zb[k] - yb[k] / C.rho : 0.0;
+        bs[K1 + k] = back ? zb[K1 + k] - yb[K1 + k] / C.rho : 0.0;
+        if (k < N) {
+            const int r = hvp::code_region(code, k);
+            const double vn = y[k];
+            u_out[(size_t)b * N + k] = (vn - S.a[r] * v - S.c[r]) / S.b[r];
+            p = p + S.ts * v;
+            v = vn;
+        }
+    }
+}
+
+template <int N>
+__device__ inline uint64_t gadmm_code(const int8_t* seq, int b) {
+    uint64_t code = 0;
+#pragma unroll
+    for (int k = 0; k < N; ++k) code = hvp::code_with(code, k, seq[(size_t)b * N + k]);
+    return code;
+}
+
+// x-update, one lane per local QP (N <= 8)
+template <int N>
+__global__ __launch_bounds__(kBnbBlock<N>) void k_gadmm_qp(int P, int n, int lo, int m,
+                                                           const hvp_system* __restrict__ systems,
+                                                           const int32_t* __restrict__ sys,
+                                                           const int32_t* __restrict__ role,
+                                                           const double* __restrict__ params, hvp::Consts C,
+                                                           const int8_t* __restrict__ seq,
+                                                           int32_t* __restrict__ state, double* __restrict__ u_out,
+                                                           double* __restrict__ x, double* __restrict__ xf,
+                                                           double* __restrict__ xb, double* __restrict__ cost_out,
+                                                           int32_t* __restrict__ status_out,
+                                                           uint32_t* __restrict__ edge_out,
+                                                           int32_t* __restrict__ iters_out,
+                                                           unsigned long long* __restrict__ counter) {
+    constexpr int BS = kBnbBlock<N>;
+    const int b = blockIdx.x * BS + threadIdx.x;
+    if (b >= P * m) return;
+    const int p = b / m;
+    if (!(state[p] & 1)) return;
+    const hvp_system& S = systems[sys[b]];
+    const int rl = role[b];
+    const double* prm = params + (size_t)b * C.stride;
+    const uint64_t code = gadmm_code<N>(seq, b);
+    hvp::LaneQp<N, LdsMem<N, BS>> q;
+    q.mem.lane = threadIdx.x;
+    int it = 0;
+    uint32_t raw = 0;
+    const int st = hvp::solve_admm_lane<N>(q, S, C, rl, prm, code, N, kGiMaxIter<N>, it, &raw);
+    if (iters_out) iters_out[b] = it;
+    atomicAdd(&counter[1], (unsigned long long)it);
+    if (st == hvp::GI_OK) {
+        cost_out[b] = hvp::admm_direct_cost<N>(q, S, C, rl, prm, code, N);
+        status_out[b] = HVP_OPTIMAL;
+        edge_out[b] = gadmm_edges<N>(S, code, raw);
+        gadmm_write<N>(b, gadmm_slot(b, n, lo, m), S, C, rl, prm, code, q.y, u_out, x, xf, xb);
+    } else {
+        cost_out[b] = 1e300;
+        status_out[b] = st == hvp::GI_FAIL_DUAL ? HVP_INFEASIBLE : HVP_MAXITER;
+        edge_out[b] = 0;
+        gadmm_fail(state, p);
+    }
+}
+
+// x-update, one 16-lane group per local QP (long horizons, hvp_coop.h)
+template <int N>
+__global__ __launch_bounds__(kCoopBlock) void k_gadmm_qp_coop(int P, int n, int lo, int m,
+                                                              const hvp_system* __restrict__ systems,
+                                                              const int32_t* __restrict__ sys,
+                                                              const int32_t* __restrict__ role,
+                                                              const double* __restrict__ params, hvp::Consts C,
+                                                              const int8_t* __restrict__ seq,
+                                                              int32_t* __restrict__ state, double* __restrict__ u_out,
+                                                              double* __restrict__ x, double* __restrict__ xf,
+                                                              double* __restrict__ xb, double* __restrict__ cost_out,
+                                                              int32_t* __restrict__ status_out,
+                                                              uint32_t* __restrict__ edge_out,
+                                                              int32_t* __restrict__ iters_out,
+                                                              unsigned long long* __restrict__ counter) {
+    __shared__ hvp::coop::GroupLds lds[kCoopGroups];
+    const int g = threadIdx.x / hvp::coop::G, t = threadIdx.x % hvp::coop::G;
+    const int b = blockIdx.x * kCoopGroups + g;
+    if (b >= P * m) return;  // group-uniform
+    const int p = b / m;
+    if (!(state[p] & 1)) return;
+    const hvp_system& S = systems[sys[b]];
+    const int rl = role[b];
+    const double* prm = params + (size_t)b * C.stride;
+    const uint64_t code = gadmm_code<N>(seq, b);
+    hvp::coop::Lane<N> L;
+    double cost = 0.0;
+    int it = 0;
+    unsigned raw = 0;
+    const int st = hvp::coop::solve_qp<N>(L, lds[g], S, C, rl, prm, code, N, kGiMaxIter<N>, it, &cost, &raw);
+    if (st == hvp::GI_OK) {
+        lds[g].v[t] = t < N ? L.y : 0.0;
+        hvp::coop::gsync();
+    }
+    if (t != 0) return;
+    if (iters_out) iters_out[b] = it;
+    atomicAdd(&counter[1], (unsigned long long)it);
+    if (st == hvp::GI_OK) {
+        double y[N];
+#pragma unroll
+        for (int k = 0; k < N; ++k) y[k] = lds[g].v[k];
+        cost_out[b] = cost;
+        status_out[b] = HVP_OPTIMAL;
+        edge_out[b] = gadmm_edges<N>(S, code, raw);
+        gadmm_write<N>(b, gadmm_slot(b, n, lo, m), S, C, rl, prm, code, y, u_out, x, xf, xb);
+    } else {
+        cost_out[b] = 1e300;
+        status_out[b] = st == hvp::GI_FAIL_DUAL ? HVP_INFEASIBLE : HVP_MAXITER;
+        edge_out[b] = 0;
+        gadmm_fail(state, p);
+    }
+}
+
+// consensus step, one thread per (held vehicle, state entry); z of i-1, i, i+1 recomputed per
+// thread so the y-updates need no second pass
+__device__ inline double gadmm_z(int j, int n, size_t base, const double* x, const double* xf, const double* xb,
+                                 int E, int e, bool init) {
+    double s = x[(base + j) * E + e];
+    if (init) return s;
+    int cnt = 1;
+    if (j >= 1) { s += xb[(base + j - 1) * E + e]; ++cnt; }
+    if (j + 1 < n) { s += xf[(base + j + 1) * E + e]; ++cnt; }
+    return cnt == 3 ? s * (1.0 / 3.0) : (cnt == 2 ? 0.5 * s : s);
+}
+
+__global__ __launch_bounds__(kBlock) void k_gadmm_update(int P, int n, int lo, int m, int N, double rho, int stride,
+                                                         const double* __restrict__ x, const double* __restrict__ xf,
+                                                         const double* __restrict__ xb, double* __restrict__ params,
+                                                         const int32_t* __restrict__ state, int init) {
+    const int E = 2 * (N + 1);
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (long long)P * m * E) return;
+    const int e = (int)(t % E);
+    const int b = (int)(t / E);
+    const int p = b / m, i = lo + b % m;
+    if (!(state[p] & 1)) return;
+    const size_t base = (size_t)p * n;
+    double* prm = params + (size_t)b * stride;
+    const bool in = init != 0;
+    const double zi = gadmm_z(i, n, base, x, xf, xb, E, e, in);
+    prm[2 + 6 * E + e] = zi;
+    prm[2 + 5 * E + e] = in ? 0.0 : prm[2 + 5 * E + e] + rho * (x[(base + i) * E + e] - zi);
+    if (i >= 1) {
+        const double zm = gadmm_z(i - 1, n, base, x, xf, xb, E, e, in);
+        prm[2 + E + e] = zm;
+        prm[2 + e] = in ? 0.0 : prm[2 + e] + rho * (xf[(base + i) * E + e] - zm);
+    }
+    if (i + 1 < n) {
+        const double zp = gadmm_z(i + 1, n, base, x, xf, xb, E, e, in);
+        prm[2 + 3 * E + e] = zp;
+        prm[2 + 2 * E + e] = in ? 0.0 : prm[2 + 2 * E + e] + rho * (xb[(base + i) * E + e] - zp);
+    }
+}
+
+__device__ inline int gadmm_neighbour(const hvp_system& S, int r, bool up) {
+    const double edge = up ? S.vhi[r] : S.vlo[r];
+    const double tol = 1e-9 * (1.0 + fabs(edge));
+    for (int q = 0; q < S.n_regions; ++q) {
+        if (q == r) continue;
+        if (fabs((up ? S.vlo[q] : S.vhi[q]) - edge) <= tol) return q;
+    }
+    return -1;
+}
+
+__global__ __launch_bounds__(kBlock) void k_gadmm_switch(int P, int n, int lo, int m, int N,
+                                                         const hvp_system* __restrict__ systems,
+                                                         const int32_t* __restrict__ sys,
+                                                         const uint32_t* __restrict__ edge, int8_t* __restrict__ seq,
+                                                         int32_t* __restrict__ state) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= P * m) return;
+    const int p = b / m;
+    if (!(state[p] & 1)) return;
+    const hvp_system& S = systems[sys[b]];
+    const uint32_t bits = edge[b];
+    bool changed = false;
+    for (int k = 1; k < N; ++k) {
+        const int r = seq[(size_t)b * N + k];
+        int q = -1;
+        if ((bits >> (2 * (k - 1))) & 1u) q = gadmm_neighbour(S, r, false);
+        else if ((bits >> (2 * (k - 1) + 1)) & 1u) q = gadmm_neighbour(S, r, true);
+        if (q >= 0) {
+            seq[(size_t)b * N + k] = (int8_t)q;
+            changed = true;
+        }
+    }
+    if (changed) atomicOr(&state[p], 4);
+}
+
 int grid_for(long long n) { return (int)std::max<long long>(1, (n + kBlock - 1) / kBlock); }
 
 template <int N>
@@ -1143,8 +1436,11 @@ int hvp_create(hvp_handle** out, const hvp_problem* problem, const hvp_system* s
     if (problem->method == HVP_METHOD_ENUMERATE && problem->N > HVP_MAX_N_ENUM)
         return fail(HVP_E_UNSUPPORTED, "hvp_create: enumeration supports N <= " + std::to_string(HVP_MAX_N_ENUM) +
                                            " (use HVP_METHOD_BNB)");
-    if (problem->formulation != HVP_FORM_DECENT && problem->formulation != HVP_FORM_ADMM)
+    if (problem->formulation != HVP_FORM_DECENT && problem->formulation != HVP_FORM_ADMM &&
+        problem->formulation != HVP_FORM_GADMM)
         return fail(HVP_E_ARG, "hvp_create: unknown formulation");
+    if (problem->formulation == HVP_FORM_GADMM && !(problem->rho > 0))
+        return fail(HVP_E_ARG, "hvp_create: the switching-ADMM formulation needs rho > 0");
     if (problem->formulation == HVP_FORM_ADMM && problem->method == HVP_METHOD_ENUMERATE)
         return fail(HVP_E_UNSUPPORTED, "hvp_create: the ADMM formulation is solved by branch and bound only");
     if (problem->formulation == HVP_FORM_ADMM && !(problem->rho > 0))
@@ -1167,6 +1463,8 @@ int hvp_create(hvp_handle** out, const hvp_problem* problem, const hvp_system* s
         hipMemcpy(h->d_sys, systems, sizeof(hvp_system) * n_systems, hipMemcpyHostToDevice) != hipSuccess ||
         hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess ||
         hipEventCreate(&h->evq0) != hipSuccess || hipEventCreate(&h->evq1) != hipSuccess ||
+        hipMalloc(&h->g_counter, 8 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(h->g_counter, 0, 8 * sizeof(unsigned long long)) != hipSuccess ||
         !create_events(h->evb, 2 * (HVP_MAX_N + 1))) {
         hvp_destroy(h);
         return fail(HVP_E_HIP, "hvp_create: device allocation failed");
@@ -1248,6 +1546,8 @@ static int solve_impl(hvp_handle* h, int B, const int32_t* sys, const int32_t* r
                       double* xb_out) {
     if (!h || B < 0 || (B > 0 && (!sys || !role || !params || !cost_out || !status_out)))
         return fail(HVP_E_ARG, "hvp_solve_batch: bad argument");
+    if (h->prob.formulation == HVP_FORM_GADMM)
+        return fail(HVP_E_ARG, "hvp_solve_batch: HVP_FORM_GADMM handles are solved by hvp_gadmm_solve");
     if (B == 0) return 0;
     if (B > h->ws.max_batch) {
         int rc = hvp_reserve(h, B, default_capacity(h->prob.N, B, h->bnb));
@@ -1315,6 +1615,117 @@ int hvp_admm_update(hvp_handle* h, int P, int n, const double* x, const double* 
     return 0;
 }
 
+// ---------------------------------------------------------------- switching ADMM
+static int gadmm_check(hvp_handle* h, int P, int n, int lo, int m, const char* who) {
+    if (!h) return fail(HVP_E_ARG, std::string(who) + ": null handle");
+    if (h->prob.formulation != HVP_FORM_GADMM)
+        return fail(HVP_E_ARG, std::string(who) + ": the handle is not an HVP_FORM_GADMM problem");
+    if (P < 0 || n < 1 || m < 1 || lo < 0 || lo + m > n)
+        return fail(HVP_E_ARG, std::string(who) + ": bad platoon layout (P, n, lo, m)");
+    return 0;
+}
+
+int hvp_gadmm_rollout(hvp_handle* h, int P, int n, int lo, int m, const int32_t* sys, const double* params, int mode,
+                      const double* u_prev, double* x, int8_t* seq, double* u_ws, int32_t* state, void* stream) {
+    if (int rc = gadmm_check(h, P, n, lo, m, "hvp_gadmm_rollout")) return rc;
+    if (P == 0) return 0;
+    if (!sys || !params || !x || !seq || !state || (mode != 0 && mode != 1) || (mode == 1 && !u_prev))
+        return fail(HVP_E_ARG, "hvp_gadmm_rollout: bad argument");
+    HIP_TRY(hipSetDevice(h->device));
+    const int B = P * m;
+    HIP_TRY(hipMemsetAsync(h->g_counter, 0, 8 * sizeof(unsigned long long), (hipStream_t)stream));
+    switch (h->prob.N) {
+#define HVP_CASE(nn)                                                                                                \
+    case nn:                                                                                                        \
+        hipLaunchKernelGGL(k_gadmm_rollout<nn>, dim3(grid_for(B)), dim3(kBlock), 0, (hipStream_t)stream, P, n, lo, m, \
+                           h->d_sys, sys, params, h->C.stride, mode, u_prev, x, seq, u_ws, state);                  \
+        break;
+        HVP_CASE(2) HVP_CASE(3) HVP_CASE(4) HVP_CASE(5) HVP_CASE(6) HVP_CASE(7) HVP_CASE(8)
+        HVP_CASE(9) HVP_CASE(10) HVP_CASE(11) HVP_CASE(12) HVP_CASE(13) HVP_CASE(14) HVP_CASE(15) HVP_CASE(16)
+#undef HVP_CASE
+        default: return fail(HVP_E_UNSUPPORTED, "hvp_gadmm_rollout: unsupported N");
+    }
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+}  // extern "C"
+
+template <int N>
+static int launch_gadmm_qp(hvp_handle* h, int P, int n, int lo, int m, const int32_t* sys, const int32_t* role,
+                           const double* params, const int8_t* seq, int32_t* state, double* u_out, double* x,
+                           double* xf, double* xb, double* cost_out, int32_t* status_out, uint32_t* edge_out,
+                           int32_t* iters_out, hipStream_t st) {
+    const int B = P * m;
+    HIP_TRY(hipEventRecord(h->evq0, st));
+    if constexpr (kCoop<N>) {
+        hipLaunchKernelGGL(k_gadmm_qp_coop<N>, dim3((B + kCoopGroups - 1) / kCoopGroups), dim3(kCoopBlock), 0, st, P, n,
+                           lo, m, h->d_sys, sys, role, params, h->C, seq, state, u_out, x, xf, xb, cost_out,
+                           status_out, edge_out, iters_out, h->g_counter);
+    } else {
+        constexpr int BS = kBnbBlock<N>;
+        const size_t lds = sizeof(double) * hvp::F_COUNT * N * BS;
+        hipLaunchKernelGGL(k_gadmm_qp<N>, dim3((B + BS - 1) / BS), dim3(BS), lds, st, P, n, lo, m, h->d_sys, sys, role,
+                           params, h->C, seq, state, u_out, x, xf, xb, cost_out, status_out, edge_out, iters_out,
+                           h->g_counter);
+    }
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(h->evq1, st));
+    h->last_stream = st;
+    h->last_B = B;
+    h->last_bnb = false;
+    return 0;
+}
+
+extern "C" {
+
+int hvp_gadmm_solve(hvp_handle* h, int P, int n, int lo, int m, const int32_t* sys, const int32_t* role,
+                    const double* params, const int8_t* seq, int32_t* state, double* u_out, double* x, double* xf,
+                    double* xb, double* cost_out, int32_t* status_out, uint32_t* edge_out, int32_t* iters_out,
+                    void* stream) {
+    if (int rc = gadmm_check(h, P, n, lo, m, "hvp_gadmm_solve")) return rc;
+    if (P == 0) return 0;
+    if (!sys || !role || !params || !seq || !state || !u_out || !x || !xf || !xb || !cost_out || !status_out ||
+        !edge_out)
+        return fail(HVP_E_ARG, "hvp_gadmm_solve: bad argument");
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t st = (hipStream_t)stream;
+    switch (h->prob.N) {
+#define HVP_CASE(nn) \
+    case nn: return launch_gadmm_qp<nn>(h, P, n, lo, m, sys, role, params, seq, state, u_out, x, xf, xb, cost_out, status_out, edge_out, iters_out, st);
+        HVP_CASE(2) HVP_CASE(3) HVP_CASE(4) HVP_CASE(5) HVP_CASE(6) HVP_CASE(7) HVP_CASE(8)
+        HVP_CASE(9) HVP_CASE(10) HVP_CASE(11) HVP_CASE(12) HVP_CASE(13) HVP_CASE(14) HVP_CASE(15) HVP_CASE(16)
+#undef HVP_CASE
+        default: return fail(HVP_E_UNSUPPORTED, "hvp_gadmm_solve: unsupported N");
+    }
+}
+
+int hvp_gadmm_update(hvp_handle* h, int P, int n, int lo, int m, const double* x, const double* xf, const double* xb,
+                     double* params, const int32_t* state, int init, void* stream) {
+    if (int rc = gadmm_check(h, P, n, lo, m, "hvp_gadmm_update")) return rc;
+    if (P == 0) return 0;
+    if (!x || !xf || !xb || !params || !state) return fail(HVP_E_ARG, "hvp_gadmm_update: bad argument");
+    HIP_TRY(hipSetDevice(h->device));
+    const int N = h->prob.N;
+    const long long total = (long long)P * m * 2 * (N + 1);
+    hipLaunchKernelGGL(k_gadmm_update, dim3(grid_for(total)), dim3(kBlock), 0, (hipStream_t)stream, P, n, lo, m, N,
+                       h->prob.rho, h->C.stride, x, xf, xb, params, state, init);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int hvp_gadmm_switch(hvp_handle* h, int P, int n, int lo, int m, const int32_t* sys, const uint32_t* edge,
+                     int8_t* seq, int32_t* state, void* stream) {
+    if (int rc = gadmm_check(h, P, n, lo, m, "hvp_gadmm_switch")) return rc;
+    if (P == 0) return 0;
+    if (!sys || !edge || !seq || !state) return fail(HVP_E_ARG, "hvp_gadmm_switch: bad argument");
+    HIP_TRY(hipSetDevice(h->device));
+    hipLaunchKernelGGL(k_gadmm_switch, dim3(grid_for((long long)P * m)), dim3(kBlock), 0, (hipStream_t)stream, P, n,
+                       lo, m, h->prob.N, h->d_sys, sys, edge, seq, state);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
 int hvp_sync(hvp_handle* h, void* stream) {
     if (!h) return fail(HVP_E_ARG, "hvp_sync: null handle");
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
@@ -1325,7 +1736,12 @@ int hvp_get_stats(hvp_handle* h, hvp_stats* out) {
     if (!h || !out) return fail(HVP_E_ARG, "hvp_get_stats: bad argument");
     HIP_TRY(hipStreamSynchronize(h->last_stream));
     unsigned long long c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (h->ws.counter) HIP_TRY(hipMemcpy(c, h->ws.counter, sizeof(c), hipMemcpyDeviceToHost));
+    if (h->prob.formulation == HVP_FORM_GADMM) {
+        // cumulative since the last hvp_gadmm_rollout (one g_admm_control warm start)
+        HIP_TRY(hipMemcpy(c, h->g_counter, sizeof(c), hipMemcpyDeviceToHost));
+    } else if (h->ws.counter) {
+        HIP_TRY(hipMemcpy(c, h->ws.counter, sizeof(c), hipMemcpyDeviceToHost));
+    }
     float ms = 0.f, qms = 0.f;
     if (h->last_B > 0) {
         HIP_TRY(hipEventElapsedTime(&ms, h->ev0, h->ev1));
@@ -1418,6 +1834,7 @@ void hvp_destroy(hvp_handle* h) {
     free_ws(h->ws);
     if (h->d_sys) (void)hipFree(h->d_sys);
     if (h->d_stage) (void)hipFree(h->d_stage);
+    if (h->g_counter) (void)hipFree(h->g_counter);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
     if (h->evq0) (void)hipEventDestroy(h->evq0);

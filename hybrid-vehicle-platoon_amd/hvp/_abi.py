@@ -12,10 +12,10 @@ import os
 MAX_REGIONS = 16
 MAX_N = 16
 MAX_N_ENUM = 8
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 METHOD_AUTO, METHOD_ENUMERATE, METHOD_BNB = 0, 1, 2
-FORM_DECENT, FORM_ADMM = 0, 1
+FORM_DECENT, FORM_ADMM, FORM_GADMM = 0, 1, 2
 
 ROLE_SAFE_FRONT = 1
 ROLE_SAFE_BACK = 2
@@ -23,6 +23,10 @@ ROLE_TRACK_FRONT = 4
 ROLE_TRACK_BACK = 8
 ROLE_TRACK_LEADER = 16
 ROLE_LEADER_SPACING = 32
+ROLE_BACK_COPY = 64
+
+# switching-ADMM platoon state bits (include/hvp.h)
+GADMM_LIVE, GADMM_FAILED, GADMM_CHANGED = 1, 2, 4
 
 OPTIMAL, INFEASIBLE, MAXITER, OVERFLOW = 0, 1, 2, 3
 STATUS_NAMES = {OPTIMAL: "OPTIMAL", INFEASIBLE: "INFEASIBLE", MAXITER: "MAXITER", OVERFLOW: "OVERFLOW"}
@@ -88,7 +92,7 @@ class HvpStats(ctypes.Structure):
 
 
 def params_stride(N: int, formulation: int = 0) -> int:
-    return 2 + (10 if formulation == FORM_ADMM else 6) * (N + 1)
+    return 2 + {FORM_ADMM: 10, FORM_GADMM: 14}.get(formulation, 6) * (N + 1)
 
 
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -114,6 +118,10 @@ EXPORTS = {
     "hvp_evaluate_batch": ([_P, ctypes.c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
     "hvp_solve_admm_batch": ([_P, ctypes.c_int] + [_P] * 14, ctypes.c_int),
     "hvp_admm_update": ([_P, ctypes.c_int, ctypes.c_int] + [_P] * 8, ctypes.c_int),
+    "hvp_gadmm_rollout": ([_P] + [ctypes.c_int] * 4 + [_P, _P, ctypes.c_int] + [_P] * 6, ctypes.c_int),
+    "hvp_gadmm_solve": ([_P] + [ctypes.c_int] * 4 + [_P] * 14, ctypes.c_int),
+    "hvp_gadmm_update": ([_P] + [ctypes.c_int] * 4 + [_P] * 5 + [ctypes.c_int, _P], ctypes.c_int),
+    "hvp_gadmm_switch": ([_P] + [ctypes.c_int] * 4 + [_P] * 5, ctypes.c_int),
     "hvp_sync": ([_P, _P], ctypes.c_int),
     "hvp_get_stats": ([_P, ctypes.POINTER(HvpStats)], ctypes.c_int),
     "hvp_destroy": ([_P], None),

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define HVP_ABI_VERSION 2
+#define HVP_ABI_VERSION 3
 #define HVP_MAX_REGIONS 16
 #define HVP_MAX_N 16     /* longest horizon (branch-and-bound path)            */
 #define HVP_MAX_N_ENUM 8 /* longest horizon of the exhaustive-enumeration path */
@@ -89,8 +89,11 @@ typedef struct hvp_problem {
 /* Local MPC formulation (hvp_problem.formulation). */
 enum {
     HVP_FORM_DECENT = 0, /* LocalMpcMld (fleet_decent_mld.py:21-223): fixed neighbour predictions   */
-    HVP_FORM_ADMM = 1    /* LocalMpcADMM (fleet_naive_admm.py:24-253): neighbour COPIES as decision
+    HVP_FORM_ADMM = 1,   /* LocalMpcADMM (fleet_naive_admm.py:24-253): neighbour COPIES as decision
                             variables with ADMM terms y'(c - z) + rho/2 |c - z|^2; needs B&B      */
+    HVP_FORM_GADMM = 2   /* fleet_g_admm.LocalMpc (:22-205) under MpcSwitching [EXT]: convex QP for
+                            a GIVEN region sequence; own state and copies in the augmented
+                            Lagrangian; solved by hvp_gadmm_solve only                          */
 };
 
 /* Search over the region sequences (hvp_problem.method).  Both give the same sequence: the
@@ -108,7 +111,9 @@ enum {
     HVP_ROLE_TRACK_FRONT = 4,    /* not is_front and not is_leader                         */
     HVP_ROLE_TRACK_BACK = 8,     /* not is_trailer and not is_leader                       */
     HVP_ROLE_TRACK_LEADER = 16,  /* is_leader                                              */
-    HVP_ROLE_LEADER_SPACING = 32 /* is_leader and real_vehicle_as_reference                */
+    HVP_ROLE_LEADER_SPACING = 32,/* is_leader and real_vehicle_as_reference                */
+    HVP_ROLE_BACK_COPY = 64      /* HVP_FORM_GADMM: holds a copy of the vehicle behind (ADMM term
+                                    only; G[i] contains i + 1, fleet_g_admm.py:341-353)     */
 };
 
 /* Per-instance status (Gurobi Status 2 <-> HVP_OPTIMAL). */
@@ -140,6 +145,12 @@ static inline int hvp_params_stride(int N) { return 2 + 6 * (N + 1); }
  *   [0..1] x0 | y_front | z_front | y_back | z_back | leader_x   (each (2, N+1) row-major)
  * (set_front_vars / set_back_vars / set_leader_x, fleet_naive_admm.py:239-258). */
 static inline int hvp_params_stride_admm(int N) { return 2 + 10 * (N + 1); }
+
+/* HVP_FORM_GADMM parameter block, stride hvp_params_stride_gadmm(N) doubles:
+ *   [0..1] x0 | y_front | z_front | y_back | z_back | leader_x | y_own | z_own  (each (2, N+1))
+ * i.e. the ADMM block plus the own-state multiplier / consensus value (MpcAdmm's augmented state
+ * [EXT]: the y / z parameters of fleet_g_admm.LocalMpc cover own state and copies). */
+static inline int hvp_params_stride_gadmm(int N) { return 2 + 14 * (N + 1); }
 
 typedef struct hvp_handle hvp_handle;
 
@@ -194,6 +205,44 @@ int hvp_admm_update(hvp_handle* h, int P, int n, const double* x, const double* 
 int hvp_evaluate_batch(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, const double* params,
                        const int8_t* gear_in, const double* u_in, double* cost_out, int32_t* status_out,
                        double* x_out, void* stream);
+/* ---- Switching ADMM (fleet_g_admm.py: TrackingGAdmmCoordinator over GAdmmCoordinator /
+ * MpcSwitching of dmpcpwa [EXT]; the restated rule is documented in DESIGN.md and
+ * oracle/oracle.py GAdmmCoordinator).  Layout: P platoons of n vehicles; a process holds the
+ * vehicles [lo, lo + m) of every platoon (m = n unsharded), instance b = p * m + (i - lo).
+ * Trajectory arrays x / xf / xb are FULL-platoon [P][n][2][N+1] (vehicle slot p * n + i):
+ * the solve writes the held vehicles' slots, a sharded caller fills the neighbouring slots
+ * (halo) before hvp_gadmm_update.  state[P] (int32, device): bit 0 = still iterating (live),
+ * bit 1 = failed (a rollout or local QP failed: the reference's error / infeasibility flag),
+ * bit 2 = sequence changed in the last hvp_gadmm_switch. */
+
+/* Warm start (fleet_g_admm.py:256-272): mode 0 = constant-velocity throttle of each vehicle's
+ * v0 (Vehicle.get_u_for_constant_vel, models.py:537-556), mode 1 = u_prev [B][N] shifted by one
+ * step (last column repeated).  Rolls the controls out through the PWA dynamics (region = first
+ * closed velocity band holding v_k) from x0 = params[b][0..1]: x [P][n][2][N+1] slots, seq
+ * [B][N] regions, u_ws [B][N] (may be NULL).  A velocity in no band sets state bit 1. */
+int hvp_gadmm_rollout(hvp_handle* h, int P, int n, int lo, int m, const int32_t* sys, const double* params,
+                      int mode, const double* u_prev, double* x, int8_t* seq, double* u_ws, int32_t* state,
+                      void* stream);
+/* One ADMM x-update: the local QP of every held vehicle of every live platoon for its sequence
+ * seq [B][N].  Writes u_out [B][N], the vehicle's trajectory / optimal copies into the x / xf /
+ * xb slots, cost_out [B] (the local objective incl. ADMM terms: sol.f), status_out [B],
+ * edge_out [B] (bit 2(k-1) + 0/1: the lower / upper velocity edge of region seq_k, k = 1..N-1,
+ * strictly inside the state box, is active with multiplier > 1e-6), iters_out [B] (may be
+ * NULL).  A failed QP sets state bit 1 of its platoon and clears bit 0. */
+int hvp_gadmm_solve(hvp_handle* h, int P, int n, int lo, int m, const int32_t* sys, const int32_t* role,
+                    const double* params, const int8_t* seq, int32_t* state, double* u_out, double* x,
+                    double* xf, double* xb, double* cost_out, int32_t* status_out, uint32_t* edge_out,
+                    int32_t* iters_out, void* stream);
+/* z- and y-update (consensus over G[i] = {i-1, i, i+1}):  z_j = mean(x_j, xb_{j-1}, xf_{j+1}),
+ * y_own_i += rho (x_i - z_i), y_front_i += rho (xf_i - z_{i-1}), y_back_i += rho (xb_i - z_{i+1}),
+ * and the z blocks of params <- z_i, z_{i-1}, z_{i+1}; for live platoons only.  init != 0
+ * starts an ADMM run: z_j <- x_j (the rollout), every y <- 0. */
+int hvp_gadmm_update(hvp_handle* h, int P, int n, int lo, int m, const double* x, const double* xf,
+                     const double* xb, double* params, const int32_t* state, int init, void* stream);
+/* Sequence switching after an ADMM run (live platoons): seq_k moves across every edge flagged
+ * in edge [B] into the region on the other side; sets state bit 2 when a sequence changed. */
+int hvp_gadmm_switch(hvp_handle* h, int P, int n, int lo, int m, const int32_t* sys, const uint32_t* edge,
+                     int8_t* seq, int32_t* state, void* stream);
 int hvp_sync(hvp_handle* h, void* stream);
 int hvp_get_stats(hvp_handle* h, hvp_stats* out); /* synchronises the handle's last stream */
 void hvp_destroy(hvp_handle* h);

@@ -60,6 +60,13 @@ typedef struct {
     int admm;
     double rho;
     const double *yf, *zf, *yb, *zb;
+    /* switching-ADMM local problem of fleet_g_admm.LocalMpc (fleet_g_admm.py:22-205): on top of
+     * the copies, the OWN state enters the augmented Lagrangian (MpcAdmm augmented state [EXT]:
+     * y_own'(x - z_own) + rho/2 |x - z_own|^2, k = 0..N); the back copy is priced by its ADMM
+     * term only (the cost tracks the front copy only, :136-158; safety only w.r.t. the front
+     * copy, :98-109). */
+    int gadmm, back_copy;
+    const double *yo, *zo;
 } or_cfg;
 
 enum { R_SF = 1, R_SB = 2, R_TF = 4, R_TB = 8, R_TL = 16, R_LSP = 32 };
@@ -95,6 +102,7 @@ typedef struct {
     double Aeq[OR_MAX_EQ][OR_MAX_NZ], beq[OR_MAX_EQ];
     double G[OR_MAX_M][OR_MAX_NZ], h[OR_MAX_M];
     int infeasible_const; /* a variable-free row was violated */
+    int reg_row[OR_MAX_N][4]; /* inequality index of region row (k, row), -1 if variable-free */
 } or_qp;
 
 static void qp_add_prod(or_qp* qp, double wgt, const lin* a, const lin* b) { /* wgt * a * b */
@@ -200,7 +208,7 @@ static int build_qp_k(or_qp* qp, const or_model* md, const or_cfg* cf, const int
     int cf_idx = -1, cb_idx = -1; /* ADMM copies x_front, x_back (2, N+1), fleet_naive_admm.py:84-102 */
     if (cf->admm) {
         if (cf->role & R_SF) { cf_idx = nz; nz += 2 * (N + 1); }
-        if (cf->role & R_SB) { cb_idx = nz; nz += 2 * (N + 1); }
+        if ((cf->role & R_SB) || cf->back_copy) { cb_idx = nz; nz += 2 * (N + 1); }
     }
     L.nsb_idx = nz; /* aux (L1) variables are appended after the slacks (and copies) */
     L.naux = 0;
@@ -222,6 +230,8 @@ static int build_qp_k(or_qp* qp, const or_model* md, const or_cfg* cf, const int
         }
     }
     /* region rows S x_k + R u_k <= T (k = 0..N-1) */
+    for (int k = 0; k < OR_MAX_N; ++k)
+        for (int row = 0; row < 4; ++row) qp->reg_row[k][row] = -1;
     for (int k = 0; k < K; ++k) {
         int r = sigma[k];
         for (int row = 0; row < md->nsr; ++row) {
@@ -229,7 +239,9 @@ static int build_qp_k(or_qp* qp, const or_model* md, const or_cfg* cf, const int
             for (int j = 0; j < 2; ++j) { lin xj = X(&L, k, j); e = lin_axpy(md->S[r][row][j], &xj, &e); }
             lin uk = U(&L, k);
             e = lin_axpy(md->R[r][row], &uk, &e);
+            const int m0 = qp->m;
             qp_add_le(qp, &e, md->T[r][row]);
+            if (qp->m > m0) qp->reg_row[k][row] = m0;
         }
     }
     /* state box k = 1..N, input box k = 0..N-1 */
@@ -324,6 +336,16 @@ static int build_qp_k(or_qp* qp, const or_model* md, const or_cfg* cf, const int
                     lin yd = lin_axpy(par(yy[side], N, i, k), &d, &(lin){.n = 0, .cst = 0.0});
                     qp_add_lin(qp, &yd);
                 }
+            }
+        }
+        if (cf->gadmm) { /* own state in the augmented Lagrangian: y_own'(x_k - z_k) + rho/2 |x_k - z_k|^2 */
+            lin xs[2] = {p, v};
+            for (int i = 0; i < 2; ++i) {
+                lin d = xs[i];
+                d.cst -= par(cf->zo, N, i, k);
+                qp_add_prod(qp, 0.5 * cf->rho, &d, &d);
+                lin yd = lin_axpy(par(cf->yo, N, i, k), &d, &(lin){.n = 0, .cst = 0.0});
+                qp_add_lin(qp, &yd);
             }
         }
         if (cf->role & R_TL) { /* x_k - xl_k (- spacing(x_k) for real_vehicle_as_reference) */
@@ -596,6 +618,8 @@ static int polish(const or_qp* qp, or_work* w) {
             continue;
         }
         for (int j = 0; j < nz; ++j) w->z[j] = x[j];
+        for (int i = 0; i < m; ++i) w->lam[i] = 0.0; /* multipliers of the certified active set */
+        for (int a = 0; a < na; ++a) w->lam[act[a]] = x[nz + ne + a];
         return 1;
     }
     return 0;
@@ -717,9 +741,10 @@ static double direct_objective_k(const or_cfg* cf, const double* x0, const doubl
     double J = 0.0;
     if (cf->admm) { /* the copies are part of the solution; price their ADMM terms */
         int idx = 3 * N + ((cf->role & R_SF) ? N + 1 : 0) + ((cf->role & R_SB) ? N + 1 : 0);
+        const int has_b = (cf->role & R_SB) || cf->back_copy;
         if (cf->role & R_SF) { xf = z + idx; idx += 2 * (N + 1); }
-        if (cf->role & R_SB) xb = z + idx;
-        const double* cc[2] = {(cf->role & R_SF) ? xf : NULL, (cf->role & R_SB) ? xb : NULL};
+        if (has_b) xb = z + idx;
+        const double* cc[2] = {(cf->role & R_SF) ? xf : NULL, has_b ? xb : NULL};
         const double* yy[2] = {cf->yf, cf->yb};
         const double* zz[2] = {cf->zf, cf->zb};
         for (int side = 0; side < 2; ++side) {
@@ -731,6 +756,13 @@ static double direct_objective_k(const or_cfg* cf, const double* x0, const doubl
                 }
         }
     }
+    if (cf->gadmm)
+        for (int k = 0; k <= N; ++k)
+            for (int i = 0; i < 2; ++i) {
+                double xi = k == 0 ? x0[i] : z[2 * (k - 1) + i];
+                double d = xi - par(cf->zo, N, i, k);
+                J += par(cf->yo, N, i, k) * d + 0.5 * cf->rho * d * d;
+            }
     for (int k = 0; k <= N; ++k) {
         double p = k == 0 ? x0[0] : z[2 * (k - 1)], v = k == 0 ? x0[1] : z[2 * (k - 1) + 1];
         double e[3][2];
@@ -1037,6 +1069,7 @@ static void unpack_cfg(or_cfg* cf, int N, int quadratic, int role, const double*
     /* p = [Qx00 Qx01 Qx10 Qx11 Qu Qdu w a_acc a_dec ts d_safe tight d0 t0] */
     cf->N = N; cf->quadratic = quadratic; cf->role = role;
     cf->admm = 0; cf->rho = 0.0; cf->yf = cf->zf = cf->yb = cf->zb = NULL;
+    cf->gadmm = 0; cf->back_copy = 0; cf->yo = cf->zo = NULL;
     cf->Qx[0][0] = p[0]; cf->Qx[0][1] = p[1]; cf->Qx[1][0] = p[2]; cf->Qx[1][1] = p[3];
     cf->Qu = p[4]; cf->Qdu = p[5]; cf->w = p[6]; cf->a_acc = p[7]; cf->a_dec = p[8]; cf->ts = p[9];
     cf->d_safe = p[10]; cf->tight = p[11]; cf->d0 = p[12]; cf->t0 = p[13];
@@ -1300,5 +1333,73 @@ int oracle_export_qp(int N, int nreg, int nsr, const double* S, const double* R,
     dims_out[0] = nz; dims_out[1] = qp->neq; dims_out[2] = qp->m; dims_out[3] = qp->r0;
     dims_out[4] = qp->infeasible_const;
     free(qp);
+    return 0;
+}
+
+/* Local QP of the switching ADMM (fleet_g_admm.LocalMpc, :22-205) for a GIVEN region sequence
+ * (MpcSwitching [EXT]: dynamics and region rows of sigma_k at every step, no binaries).
+ * p = [x0 (2) | y_front | z_front | y_back | z_back | leader_x | y_own | z_own], each (2, N+1).
+ * back_copy: the vehicle holds a copy of the one behind (ADMM term only).
+ * Outputs: x (2, N+1), u (N), xf / xb (2, N+1) (zero when absent), info = [objective (the
+ * local cost incl. every ADMM term, sol.f), status (0 ok, 1 infeasible / not converged),
+ * certified, switch bits].  Switch bits (the switching rule, see oracle.py GAdmmCoordinator):
+ * bit 2 (k - 1) + 0 / + 1 for k = 1..N-1 when the lower / upper velocity edge of region
+ * sigma_k is an active region row with multiplier > 1e-6 and lies strictly inside the state
+ * box (crossing it leads into the neighbouring region). */
+int oracle_solve_gadmm_qp(int N, int nreg, int nsr, const double* S, const double* R, const double* T,
+                          const double* A, const double* B, const double* c, int nd, const double* D,
+                          const double* E, int nf, const double* F, const double* G, const double* cfgp, int role,
+                          int back_copy, double rho, const double* p, const int* sigma, double* x_out,
+                          double* u_out, double* xf_out, double* xb_out, double* info_out) {
+    or_model md;
+    or_cfg cf;
+    or_vmodel vm;
+    if (N > OR_MAX_N || unpack_model(&md, nreg, nsr, S, R, T, A, B, c, nd, D, E, nf, F, G)) return -1;
+    if (make_vmodel(&md, &vm)) return -2;
+    unpack_cfg(&cf, N, 1, role, cfgp);
+    const int K1 = 2 * (N + 1);
+    cf.admm = 1; cf.gadmm = 1; cf.back_copy = back_copy; cf.rho = rho;
+    cf.yf = p + 2; cf.zf = p + 2 + K1; cf.yb = p + 2 + 2 * K1; cf.zb = p + 2 + 3 * K1;
+    const double* xl = p + 2 + 4 * K1;
+    cf.yo = p + 2 + 5 * K1; cf.zo = p + 2 + 6 * K1;
+    static const double zero[2 * (OR_MAX_N + 1)] = {0};
+    or_qp* qp = (or_qp*)malloc(sizeof(or_qp));
+    or_work* w = (or_work*)malloc(sizeof(or_work));
+    if (!qp || !w) { free(qp); free(w); return -3; }
+    int nz = build_qp(qp, &md, &cf, sigma, p, zero, zero, xl);
+    or_result r = {0, 0, 0, INFINITY};
+    if (nz > 0 && !qp->infeasible_const) r = ipm_solve(qp, w, 200);
+    memset(xf_out, 0, sizeof(double) * K1);
+    memset(xb_out, 0, sizeof(double) * K1);
+    double bits = 0.0;
+    if (r.converged) {
+        for (int i = 0; i < 2; ++i) x_out[i * (N + 1)] = p[i];
+        for (int k = 1; k <= N; ++k)
+            for (int i = 0; i < 2; ++i) x_out[i * (N + 1) + k] = w->z[2 * (k - 1) + i];
+        for (int k = 0; k < N; ++k) u_out[k] = w->z[2 * N + k];
+        int idx = 3 * N + ((role & R_SF) ? N + 1 : 0);
+        if (role & R_SF) { memcpy(xf_out, w->z + idx, sizeof(double) * K1); idx += K1; }
+        if (back_copy) memcpy(xb_out, w->z + idx, sizeof(double) * K1);
+        unsigned mask = 0;
+        for (int k = 1; k < N; ++k) {
+            const int rg = sigma[k];
+            for (int row = 0; row < md.nsr; ++row) {
+                const int m = qp->reg_row[k][row];
+                if (m < 0 || !(w->lam[m] > 1e-6)) continue;
+                const double s = md.S[rg][row][1];
+                if (md.S[rg][row][0] != 0.0 || s == 0.0) continue;
+                const double edge = md.T[rg][row] / s;
+                if (s > 0 && edge < vm.bhi - 1e-9 * (1.0 + fabs(edge))) mask |= 1u << (2 * (k - 1) + 1);
+                if (s < 0 && edge > vm.blo + 1e-9 * (1.0 + fabs(edge))) mask |= 1u << (2 * (k - 1));
+            }
+        }
+        bits = (double)mask;
+    }
+    info_out[0] = r.converged ? direct_objective(&cf, p, zero, zero, xl, w->z) : INFINITY;
+    info_out[1] = r.converged ? 0 : 1;
+    info_out[2] = r.certified;
+    info_out[3] = bits;
+    free(qp);
+    free(w);
     return 0;
 }

@@ -242,6 +242,9 @@ def lib():
         L.oracle_solve_admm_miqp.argtypes = model_args + [dp, c_int, ctypes.c_double, dp, c_int, dp, dp, ip, dp,
                                                           dp, dp]
         L.oracle_solve_admm_miqp.restype = c_int
+        L.oracle_solve_gadmm_qp.argtypes = model_args + [dp, c_int, c_int, ctypes.c_double, dp, ip, dp, dp, dp, dp,
+                                                         dp]
+        L.oracle_solve_gadmm_qp.restype = c_int
         L.oracle_set_method.argtypes = [c_int]
         L.oracle_set_method.restype = None
         _lib = L
@@ -509,3 +512,222 @@ class AdmmCoordinator:
         for i in range(n):
             self.x_pred[i] = last[i].x
         return np.array([r.u[0] for r in last]), history
+
+
+# ------------------------------------------------------------------ switching ADMM (fleet_g_admm.py)
+@dataclass
+class GAdmmQpResult:
+    x: np.ndarray        # (2, N+1)
+    u: np.ndarray        # (N,)
+    x_front: np.ndarray  # (2, N+1) optimal copy of the vehicle ahead (zeros if none)
+    x_back: np.ndarray   # (2, N+1) optimal copy of the vehicle behind (zeros if none)
+    cost: float          # the local objective incl. every ADMM term (sol.f)
+    status: int          # 0 ok, 1 infeasible / not converged
+    certified: bool
+    switch: int          # region-edge multiplier bits, see hvp_oracle.c oracle_solve_gadmm_qp
+
+
+def gadmm_params(x0, y_front, z_front, y_back, z_back, leader_x, y_own, z_own) -> np.ndarray:
+    """Parameter row of the switching-ADMM local problem (include/hvp.h hvp_params_stride_gadmm)."""
+    blocks = [np.asarray(b, dtype=np.float64).reshape(-1)
+              for b in (y_front, z_front, y_back, z_back, leader_x, y_own, z_own)]
+    return np.concatenate([np.asarray(x0, dtype=np.float64).reshape(-1)[:2]] + blocks)
+
+
+def solve_gadmm_qp(sysd: dict, cfg: Cfg, N: int, role: int, back_copy: bool, rho: float, params,
+                   sigma) -> GAdmmQpResult:
+    """fleet_g_admm.LocalMpc (:22-205) for a fixed switching sequence, in the full
+    (x, u, s, copies) space; see hvp_oracle.c oracle_solve_gadmm_qp."""
+    L = lib()
+    args, keep = _model_args(sysd)
+    cv = cfg.vector()
+    p = np.ascontiguousarray(np.asarray(params, dtype=np.float64).reshape(-1))
+    assert p.size == 2 + 14 * (N + 1)
+    sig = np.ascontiguousarray(np.asarray(sigma, dtype=np.int32).reshape(-1))
+    x_out, u_out = np.zeros((2, N + 1)), np.zeros(N)
+    xf, xb, info = np.zeros((2, N + 1)), np.zeros((2, N + 1)), np.zeros(4)
+    rc = L.oracle_solve_gadmm_qp(N, *args, _d(cv), int(role), int(bool(back_copy)), float(rho), _d(p), _i(sig),
+                                 _d(x_out), _d(u_out), _d(xf), _d(xb), _d(info))
+    del keep
+    if rc != 0:
+        raise RuntimeError(f"oracle_solve_gadmm_qp failed ({rc})")
+    return GAdmmQpResult(x_out, u_out, xf, xb, float(info[0]), int(info[1]), bool(info[2]), int(info[3]))
+
+
+def region_bands(sysd: dict) -> tuple[np.ndarray, np.ndarray]:
+    """Velocity interval [vlo_r, vhi_r] of every region from its rows S x <= T (v-only rows)."""
+    S, T = np.asarray(sysd["S"], dtype=float), np.asarray(sysd["T"], dtype=float).reshape(len(sysd["S"]), -1)
+    lo, hi = np.full(len(S), -np.inf), np.full(len(S), np.inf)
+    for r in range(len(S)):
+        for row in range(S.shape[1]):
+            s = S[r, row, 1]
+            if S[r, row, 0] != 0.0 or s == 0.0:
+                continue
+            if s > 0:
+                hi[r] = min(hi[r], T[r, row] / s)
+            else:
+                lo[r] = max(lo[r], T[r, row] / s)
+    return lo, hi
+
+
+def gadmm_role(i: int, n: int) -> tuple[int, bool]:
+    """(role bits, back_copy) of vehicle i of a g_admm chain (fleet_g_admm.py:341-389: vehicle 0
+    leads and tracks x_ref; every other vehicle tracks / keeps its distance to its front copy)."""
+    role = ROLE_TRACK_LEADER if i == 0 else (ROLE_SAFE_FRONT | ROLE_TRACK_FRONT)
+    return role, i < n - 1
+
+
+class GAdmmCoordinator:
+    """Restatement (test infrastructure) of TrackingGAdmmCoordinator.g_admm_control
+    (fleet_g_admm.py:255-301) on top of GAdmmCoordinator / MpcSwitching of dmpcpwa 0.0.2 [EXT,
+    absent: parity unpinned against it].  The switching-ADMM rule restated here (and run on the
+    device by hvp/gadmm.py) -- Mallick, Dabiri, De Schutter, "switching ADMM" for PWA systems:
+
+    per warm start u (n, N):
+      1. rollout: x_{i,0} = state_i, sigma_{i,k} = first region whose closed velocity band holds
+         v_{i,k}, x_{i,k+1} = A x + B u + c of that region (the discrete system dicts);
+      2. z_i <- the rollout of vehicle i, y <- 0 (own block and both copies);
+      3. rounds (at most max_rounds): admm_iters x [every vehicle solves its local QP for its
+         sequence (x-update, Jacobi), z_j = mean of x_j and its copies held by j-1 (back copy)
+         and j+1 (front copy), y += rho (x_aug - z)]; then every vehicle moves sigma_{i,k}
+         (k = 1..N-1) across a velocity edge of its region whose row is active with multiplier
+         > 1e-6 (into the region on the other side of that edge); no change anywhere -> stop;
+      4. cost = sum of the local objectives of the last iteration (sol.f).
+    Warm starts (:256-272): constant-velocity throttle (Vehicle.get_u_for_constant_vel,
+    models.py:537-556) and, from the second step on, the shifted previous solution; the lowest
+    cost wins, ties to the first (:285-293); the previous solution is that of the last warm start
+    that succeeded."""
+
+    def __init__(self, systems: list[dict], cfg: Cfg, N: int, rho: float = 0.5, admm_iters: int = 100,
+                 max_rounds: int = 10):
+        self.systems, self.cfg, self.N, self.rho = systems, cfg, N, rho
+        self.n = len(systems)
+        self.admm_iters, self.max_rounds = admm_iters, max_rounds
+        self.bands = [region_bands(s) for s in systems]
+        self.prev_u = None
+        self.leader_x = np.zeros((2, N + 1))
+        self.trace: list | None = None  # set to a list to record every local QP (fixtures)
+
+    def set_leader_traj(self, leader_x) -> None:
+        self.leader_x = np.asarray(leader_x, dtype=np.float64).reshape(2, self.N + 1)
+
+    def u_const_vel(self, i: int, v: float) -> float:
+        """get_u_for_constant_vel (models.py:537-556): region by the [0, 1e-4] buffer rule."""
+        lo, hi = self.bands[i]
+        s = self.systems[i]
+        for r in range(len(lo)):
+            if lo[r] - 1e-4 <= v <= hi[r]:
+                a = float(np.asarray(s["A"][r])[1, 1])
+                b = float(np.asarray(s["B"][r]).reshape(2)[1])
+                c = float(np.asarray(s["c"][r]).reshape(2)[1])
+                return ((1.0 - a) * v - c) / b
+        raise RuntimeError("Didn't find any PWA region for the given speed!")
+
+    def rollout(self, i: int, x0, u) -> tuple[np.ndarray, np.ndarray] | None:
+        lo, hi = self.bands[i]
+        s = self.systems[i]
+        N = self.N
+        X = np.zeros((2, N + 1))
+        X[:, 0] = x0
+        sig = np.zeros(N, dtype=np.int32)
+        for k in range(N):
+            v = X[1, k]
+            r = next((r for r in range(len(lo)) if lo[r] <= v <= hi[r]), None)
+            if r is None:
+                return None
+            sig[k] = r
+            A, B, c = np.asarray(s["A"][r]), np.asarray(s["B"][r]).reshape(2), np.asarray(s["c"][r]).reshape(2)
+            X[:, k + 1] = A @ X[:, k] + B * u[k] + c
+        return X, sig
+
+    def switch(self, i: int, sig: np.ndarray, bits: int) -> np.ndarray:
+        lo, hi = self.bands[i]
+        out = sig.copy()
+        tol = lambda e: 1e-9 * (1.0 + abs(e))  # noqa: E731
+        for k in range(1, self.N):
+            r = int(sig[k])
+            if (bits >> (2 * (k - 1))) & 1:  # lower edge of r active: into the region below
+                cand = [q for q in range(len(lo)) if q != r and abs(hi[q] - lo[r]) <= tol(lo[r])]
+            elif (bits >> (2 * (k - 1) + 1)) & 1:
+                cand = [q for q in range(len(lo)) if q != r and abs(lo[q] - hi[r]) <= tol(hi[r])]
+            else:
+                continue
+            if cand:
+                out[k] = cand[0]
+        return out
+
+    def run(self, state, u_ws):
+        """One GAdmmCoordinator.g_admm_control(state, warm_start=u_ws): (u (n, N), cost, info)
+        or None when a rollout or a local QP fails (error / infeasibility flag)."""
+        n, N, rho = self.n, self.N, self.rho
+        x = np.asarray(state, dtype=np.float64).reshape(n, 2)
+        X, sig = [], []
+        for i in range(n):
+            r = self.rollout(i, x[i], u_ws[i])
+            if r is None:
+                return None
+            X.append(r[0])
+            sig.append(r[1])
+        Z = [X[i].copy() for i in range(n)]
+        K = (2, N + 1)
+        yo = [np.zeros(K) for _ in range(n)]
+        yf = [np.zeros(K) for _ in range(n)]
+        yb = [np.zeros(K) for _ in range(n)]
+        rounds, res = 0, None
+        for rounds in range(1, self.max_rounds + 1):
+            for _ in range(self.admm_iters):
+                res = []
+                for i in range(n):
+                    role, bc = gadmm_role(i, n)
+                    zf = Z[i - 1] if i > 0 else np.zeros(K)
+                    zb = Z[i + 1] if i < n - 1 else np.zeros(K)
+                    xl = self.leader_x if i == 0 else np.zeros(K)
+                    p = gadmm_params(x[i], yf[i], zf, yb[i], zb, xl, yo[i], Z[i])
+                    r = solve_gadmm_qp(self.systems[i], self.cfg, N, role, bc, rho, p, sig[i])
+                    if self.trace is not None:
+                        self.trace.append((i, role, bc, p, sig[i].copy(), r))
+                    if r.status != 0:
+                        return None
+                    res.append(r)
+                for j in range(n):  # z-update
+                    parts = [res[j].x]
+                    if j > 0:
+                        parts.append(res[j - 1].x_back)
+                    if j < n - 1:
+                        parts.append(res[j + 1].x_front)
+                    Z[j] = sum(parts[1:], parts[0]) / len(parts)
+                for i in range(n):  # y-update
+                    yo[i] = yo[i] + rho * (res[i].x - Z[i])
+                    if i > 0:
+                        yf[i] = yf[i] + rho * (res[i].x_front - Z[i - 1])
+                    if i < n - 1:
+                        yb[i] = yb[i] + rho * (res[i].x_back - Z[i + 1])
+            new = [self.switch(i, sig[i], res[i].switch) for i in range(n)]
+            changed = any((new[i] != sig[i]).any() for i in range(n))
+            sig = new
+            if not changed:
+                break
+        u = np.stack([r.u for r in res])
+        cost = float(sum(r.cost for r in res))
+        return u, cost, {"rounds": rounds, "sigma": np.stack(sig), "x": np.stack([r.x for r in res])}
+
+    def control(self, state):
+        """TrackingGAdmmCoordinator.g_admm_control: best of the warm starts; returns the
+        control trajectories u (n, N) of the winner and the per-warm-start details."""
+        n, N = self.n, self.N
+        x = np.asarray(state, dtype=np.float64).reshape(n, 2)
+        warm = [np.stack([np.full(N, self.u_const_vel(i, x[i, 1])) for i in range(n)])]
+        if self.prev_u is not None:
+            warm.append(np.concatenate([self.prev_u[:, 1:], self.prev_u[:, -1:]], axis=1))
+        best, best_cost, runs = None, float("inf"), []
+        for w in warm:
+            r = self.run(state, w)
+            runs.append(r)
+            if r is None:
+                continue
+            self.prev_u = r[0]
+            if r[1] < best_cost:
+                best, best_cost = r, r[1]
+        if best is None:
+            raise RuntimeError("No solution found for any of the warm starts")
+        return best[0], best_cost, runs

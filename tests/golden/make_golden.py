@@ -29,7 +29,11 @@ Files (numpy .npz, no pickles):
                       (gear, friction region) modes, oracle gear_friction_mld_system
   admm_local_N{5,10}.npz, admm_steps_n4_N5.npz  naive ADMM (configs[2]): local problems with
                       copies, and 3 closed-loop time steps x 4 ADMM iterations (oracle coordinator)
-Run:  python tests/golden/make_golden.py [sweep | gear | admm]
+  gadmm_local_N{5,10}.npz, gadmm_steps_n4_N5.npz, gadmm_steps_n3_N10.npz  switching ADMM
+                      (fleet_g_admm.py, configs[3]): every local QP of oracle coordinator runs
+                      (sampled), and two time steps of the restated coordinator (warm starts,
+                      rollouts, rounds of ADMM + switching) for several platoons
+Run:  python tests/golden/make_golden.py [sweep | gear | admm | gadmm]
 """
 
 from __future__ import annotations
@@ -234,7 +238,56 @@ def admm_fixtures():
     print("admm_steps_n4_N5.npz written")
 
 
+def gadmm_fixtures():
+    """Switching ADMM (fleet_g_admm.py, configs[3]): the oracle's restated coordinator
+    (oracle.py GAdmmCoordinator) on t = 0 platoon states; every local QP it solves is traced and
+    a sample kept as local-problem fixtures; two consecutive time steps (the state advances
+    along the winner's predicted x_1, the second step has both warm starts) as coordinator
+    fixtures."""
+    rng = np.random.default_rng(11)
+    for N, n, iters, seeds in ((5, 4, 20, range(4)), (10, 3, 10, range(3))):
+        systems = [O.gear_pwa_system(800.0) for _ in range(n)]
+        co = O.GAdmmCoordinator(systems, O.Cfg(), N, admm_iters=iters)
+        co.trace = []
+        states, exp_u, exp_cost, exp_ws, exp_rounds, exp_seq, exp_runcost = [], [], [], [], [], [], []
+        for seed in seeds:
+            co.prev_u = None
+            st = O.env_initial_state(n, seed).astype(float)
+            for t in range(2):
+                co.set_leader_traj(leader_window(N, t))
+                u, c, runs = co.control(st)
+                ws = next(k for k, r in enumerate(runs) if r is not None and r[1] == c)
+                states.append(st.copy()); exp_u.append(u); exp_cost.append(c); exp_ws.append(ws + 1)
+                exp_rounds.append([r[2]["rounds"] if r else -1 for r in runs] + [-1] * (2 - len(runs)))
+                exp_seq.append([r[2]["sigma"] if r else np.full((n, N), -1) for r in runs] +
+                               [np.full((n, N), -1)] * (2 - len(runs)))
+                exp_runcost.append([r[1] if r else np.inf for r in runs] + [np.nan] * (2 - len(runs)))
+                st = np.concatenate([runs[ws][2]["x"][i][:, 1] for i in range(n)])
+        name = f"gadmm_steps_n{n}_N{N}.npz"
+        np.savez_compressed(os.path.join(HERE, name), N=N, n=n, iters=iters, rho=0.5, max_rounds=co.max_rounds,
+                            steps=2, states=np.array(states), exp_u=np.array(exp_u), exp_cost=np.array(exp_cost),
+                            exp_warm_start=np.array(exp_ws, np.int32), exp_rounds=np.array(exp_rounds, np.int32),
+                            exp_seq=np.array(exp_seq, np.int32), exp_run_cost=np.array(exp_runcost))
+        print(f"{name}: {len(states)} coordinator calls")
+        T = co.trace
+        keep = np.sort(rng.choice(len(T), size=min(300, len(T)), replace=False))
+        T = [T[k] for k in keep]
+        roles = np.array([t[1] | (64 if t[2] else 0) for t in T], np.int32)
+        np.savez_compressed(os.path.join(HERE, f"gadmm_local_N{N}.npz"), N=N, rho=0.5,
+                            params=np.stack([t[3] for t in T]), roles=roles,
+                            seq=np.stack([t[4] for t in T]).astype(np.int32),
+                            exp_u=np.stack([t[5].u for t in T]), exp_x=np.stack([t[5].x for t in T]),
+                            exp_xf=np.stack([t[5].x_front for t in T]), exp_xb=np.stack([t[5].x_back for t in T]),
+                            exp_cost=np.array([t[5].cost for t in T]),
+                            exp_status=np.array([t[5].status for t in T], np.int32),
+                            exp_edge=np.array([t[5].switch for t in T], np.int64))
+        print(f"gadmm_local_N{N}.npz: {len(T)} local QPs, {int((roles & 64).sum() // 64)} with a back copy")
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "gadmm":
+        gadmm_fixtures()
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "admm":
         admm_fixtures()
         return

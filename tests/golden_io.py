@@ -13,7 +13,7 @@ GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 def fixture_names() -> list[str]:
     """The decentralised local-MIQP fixtures (the ADMM ones have their own layout: admm_*)."""
     return sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLDEN, "*.npz"))
-                  if not os.path.basename(p).startswith("admm_"))
+                  if not os.path.basename(p).startswith(("admm_", "gadmm_")))
 
 
 def load(name: str) -> dict:
