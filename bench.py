@@ -227,6 +227,140 @@ def cpu_baseline_admm(n: int, N: int, iters: int, budget_s: float):
             "sample": f"{done} platoon steps x {iters} ADMM iterations x {n} local MIQPs (N={N}), oracle, {dt:.1f} s"}
 
 
+def gadmm_qp_bytes(N: int) -> int:
+    """SURVEY 8(d) dense-QP bytes of one switching-ADMM local QP (fleet_g_admm.LocalMpc with x
+    condensed): n_w = u (N) + slack (N+1) + two neighbour copies 2 (N+1) each, m = 14 N + 4."""
+    nw, m = 6 * N + 5, 14 * N + 4
+    return 8 * (nw * nw + m * nw + m + nw)
+
+
+def bench_gadmm(args, world: int, rank: int, local: int, dist) -> None:
+    """configs[3]: fleet_g_admm, one step = TrackingGAdmmCoordinator.g_admm_control (both warm
+    starts: constant velocity + shifted previous solution; each a rollout and rounds of
+    admm_iters x (local QPs + consensus) + switching) for every platoon on the device.
+    --gadmm-layout replicas: every rank owns whole platoons (seed-sharded, no collective);
+    vehicles: every rank owns a block of vehicles of all platoons, RCCL halo send/recv of the
+    boundary vehicles after every local-QP launch."""
+    import torch
+
+    from hvp import tables
+    from hvp.env import derive_env_seed, initial_platoon_state
+    from hvp.gadmm import GAdmmEngine, HaloExchange, gadmm_problem
+    from hvp.models import PwaGearVehicle
+
+    n, N, S, iters = args.n, args.N, args.platoons, args.admm_iters
+    sharded = args.gadmm_layout == "vehicles" and world > 1
+    veh = PwaGearVehicle(800)
+    system = tables.system_from_dict(veh.get_discrete_system(1), tables.gears_of(veh))
+    seed0 = 0 if sharded else rank * S
+    states = np.stack([initial_platoon_state(n, derive_env_seed(int(s))).reshape(-1).astype(np.float64)
+                       for s in range(seed0, seed0 + S)])
+    ex = HaloExchange(S, n, N, rank, world) if sharded else None
+    eng = GAdmmEngine(gadmm_problem(N, 0.5), [system] * n, n, S, device=local, admm_iters=iters,
+                      max_rounds=args.max_rounds, exchange=ex)
+    lead = np.stack([3000.0 + 20.0 * np.arange(N + 1), np.full(N + 1, 20.0)])
+    eng.set_leader(lead)
+    t_states = torch.from_numpy(states).to(eng.dev)
+    eng.control(t_states)  # t = 0 (one warm start): establishes the previous solution
+    for _ in range(args.warmup):
+        eng.control(t_states)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rounds = launches = 0
+    for _ in range(args.steps):
+        out = eng.control(t_states)
+        rounds += sum(r["rounds"] for r in out["runs"])
+        launches += sum(r["launches"] for r in out["runs"])
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    ok = bool(torch.isfinite(out["cost"]).all().item())
+    if dist:
+        tt = torch.tensor([dt], device=eng.dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    # per-launch time of the local-QP kernel: HIP events on the launch stream over one more step
+    qp_ev = []
+    solve = eng.solve
+
+    def timed_solve(stream=None):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        solve(stream)
+        b.record()
+        qp_ev.append((a, b))
+
+    eng.solve = timed_solve
+    out2 = eng.control(t_states)
+    torch.cuda.synchronize()
+    eng.solve = solve
+    qp_ms = [a.elapsed_time(b) for a, b in qp_ev]
+    n_qp_launch = len(qp_ms)
+    qp_avg = float(np.mean(qp_ms))
+    live_qps = S * eng.m  # upper bound: platoons that stopped switching skip their lanes
+    alg_bytes = live_qps * (gadmm_qp_bytes(N) + 8 * (2 + 14 * (N + 1)))
+    achieved = alg_bytes / (qp_avg * 1e-3) / 1e9
+    platoons_total = S * (1 if sharded else world)
+    value = platoons_total * args.steps / dt
+    result = {
+        "metric": f"MPC timesteps/sec (whole platoon) at n={n} N={N} g_admm ({iters} ADMM iterations)",
+        "value": value, "unit": "platoon-timesteps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "strong" if sharded else "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic: env.reset random-init platoon states (seeded), constant-velocity leader; every timed "
+                "step is a g_admm_control with both warm starts (previous solution from the preceding call)",
+        "config": {"workload": f"fleet_g_admm n={n} N={N} pwa_gear (configs[3])", "n_vehicles": n, "horizon": N,
+                   "admm_iters": iters, "max_rounds": args.max_rounds, "rho": 0.5, "platoons_per_gpu": S,
+                   "parallelism": (f"vehicles-sharded x{world} (RCCL halo send/recv per ADMM iteration)" if sharded
+                                   else f"seeds-sharded x{world} (replicas, no collective)")},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "k_gadmm_qp_coop" if N > 8
+                     else "k_gadmm_qp", "kernel_avg_ms": qp_avg, "launches_measured": n_qp_launch,
+                     "note": "SURVEY 8(d) dense bytes of the local QP (n_w = 6N+5, m = 14N+4) + its parameter "
+                             "block, for every held vehicle of every platoon, / HIP-event time per QP launch"},
+        "admm_rounds_per_step": rounds / args.steps, "qp_launches_per_step": launches / args.steps,
+        "all_feasible": ok,
+    }
+    if ex is not None:
+        result["halo_bytes_per_exchange"] = ex.bytes_per_call
+    if rank == 0 and not args.no_cpu and args.cpu_budget > 0 and world == 1:
+        result["cpu_baseline"] = cpu_baseline_gadmm(n, N, iters, args.max_rounds, min(args.cpu_budget, 30.0))
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+def cpu_baseline_gadmm(n: int, N: int, iters: int, max_rounds: int, budget_s: float):
+    """The oracle coordinator (oracle.GAdmmCoordinator, full-space local QPs), one platoon's
+    g_admm_control at a time on one core, both warm starts (a preceding untimed call)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    lead = np.stack([3000.0 + 20.0 * np.arange(N + 1), np.full(N + 1, 20.0)])
+    systems = [O.gear_pwa_system(800.0)] * n
+    done, qps, seed, t_run = 0, 0, 40_000_000, 0.0
+    while t_run < budget_s:
+        co = O.GAdmmCoordinator(systems, O.Cfg(), N, admm_iters=iters, max_rounds=max_rounds)
+        co.set_leader_traj(lead)
+        st = O.env_initial_state(n, seed).astype(float)
+        co.control(st)
+        co.trace = []
+        t0 = time.perf_counter()
+        co.control(st)
+        t_run += time.perf_counter() - t0
+        qps += len(co.trace)
+        seed += 1
+        done += 1
+    return {"value": done / t_run, "unit": "platoon-timesteps/s", "cores": 1, "kind": "port",
+            "sample": f"{done} g_admm_control calls (n={n}, N={N}, {iters} ADMM iterations, {qps} local QPs), "
+                      f"oracle, {t_run:.1f} s"}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -239,9 +373,12 @@ def main() -> None:
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--method", choices=["auto", "enum", "bnb"], default="auto",
                     help="region-sequence search (include/hvp.h HVP_METHOD_*)")
-    ap.add_argument("--controller", choices=["decent", "admm"], default="decent",
-                    help="decent: fleet_decent_mld (configs[1]); admm: fleet_naive_admm (configs[2])")
-    ap.add_argument("--admm-iters", type=int, default=20)
+    ap.add_argument("--controller", choices=["decent", "admm", "gadmm"], default="decent",
+                    help="decent: fleet_decent_mld (configs[1]); admm: fleet_naive_admm (configs[2]); "
+                         "gadmm: fleet_g_admm (configs[3])")
+    ap.add_argument("--admm-iters", type=int, default=None, help="default 20 (admm) / 100 (gadmm)")
+    ap.add_argument("--max-rounds", type=int, default=10, help="gadmm: switching rounds cap")
+    ap.add_argument("--gadmm-layout", choices=["replicas", "vehicles"], default="replicas")
     args = ap.parse_args()
 
     import torch
@@ -260,8 +397,12 @@ def main() -> None:
     from hvp.models import PwaGearVehicle
     from hvp.solver import BatchSolver
 
+    if args.admm_iters is None:
+        args.admm_iters = 100 if args.controller == "gadmm" else 20
     if args.controller == "admm":
         return bench_admm(args, world, rank, local, dist)
+    if args.controller == "gadmm":
+        return bench_gadmm(args, world, rank, local, dist)
     n, N, S = args.n, args.N, args.platoons
     veh = PwaGearVehicle(800)
     system = tables.system_from_dict(veh.get_discrete_system(1), tables.gears_of(veh))

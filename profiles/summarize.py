@@ -34,7 +34,8 @@ def per_kernel(path: str) -> dict:
 
 def short(name: str) -> str:
     for k in ("k_qp_gi", "k_qp_ipm", "k_enum", "k_cost", "k_select", "k_bnb_root", "k_bnb_expand", "k_bnb_bound",
-              "k_bnb_key", "k_bnb_write", "k_bnb_finish"):
+              "k_bnb_key", "k_bnb_write", "k_bnb_finish", "k_gadmm_qp_coop", "k_gadmm_qp", "k_gadmm_update",
+              "k_gadmm_rollout", "k_gadmm_switch", "k_admm_update"):
         if k in name:
             return k
     return name[:48]
@@ -50,6 +51,16 @@ def main() -> None:
             out.setdefault(k, {})["avg_ms"] = float(r["AverageNs"]) / 1e6
             out[k]["calls"] = int(r["Calls"])
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(here, f"{rnd}_kernel_stats.csv"))
+    # extra workloads traced on their own (e.g. gadmm/): kernel stats kept as <round>_<name>_kernel_stats.csv
+    extra = {}
+    for name in sorted(os.listdir(src)):
+        p = os.path.join(src, name, "trace", "run_kernel_stats.csv")
+        if name == "trace" or not os.path.exists(p):
+            continue
+        shutil.copy(p, os.path.join(here, f"{rnd}_{name}_kernel_stats.csv"))
+        with open(p) as f:
+            extra[name] = {short(r["Name"]): {"avg_ms": float(r["AverageNs"]) / 1e6, "calls": int(r["Calls"])}
+                           for r in csv.DictReader(f)}
     for sub in ("fetch", "write", "f64"):
         p = os.path.join(src, sub, "run_counter_collection.csv")
         if not os.path.exists(p):
@@ -71,7 +82,7 @@ def main() -> None:
             if d.get("avg_ms"):
                 d["f64_tflops"] = d["f64_flop"] / (d["avg_ms"] * 1e-3) / 1e12
     meta = {"round": rnd, "source": "profiles/run_profiles.sh (rocprofv3 kernel trace + separate PMC passes)",
-            "kernels": out}
+            "kernels": out, "workloads": extra}
     with open(os.path.join(here, f"{rnd}_summary.json"), "w") as f:
         json.dump(meta, f, indent=1, sort_keys=True)
     print(json.dumps(meta, indent=1, sort_keys=True))
