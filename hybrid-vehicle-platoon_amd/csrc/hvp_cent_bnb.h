@@ -1,0 +1,282 @@
+// hvp_cent_bnb.h -- depth-first branch and bound of the centralised platoon MIQP (MpcMldCent,
+// mpcs/cent_mld.py:21-182), one 64-lane wavefront per platoon, on top of the wave QP of
+// hvp_cent.h.
+//
+// Decision d = k n + i fixes sigma_{i,k} (time-major, the order of oracle/hvp_oracle.c
+// cent_dfs).  A node's children are the regions reachable from the exact velocity interval of
+// v_{i,k} (bnb_child); each child's bound is the platoon QP with the assigned prefix fixed and
+// every later step relaxed (a valid lower bound: the feasible set grows, nonnegative input-cost
+// terms are dropped).  Children are visited in increasing (bound, region) order and pruned when
+// bound > incumbent + kPruneRel (1 + |incumbent|); leaves (all n N steps fixed) are exact QPs.
+// The answer is the lexicographically first (time-major) joint sequence within 1e-9 relative of
+// the minimum -- the oracle's rule -- and the exploration order, hence the QP count, is the
+// oracle's too.
+//
+// Storage: the DFS frame headers live in lane d's registers (depth d < 64), the children of each
+// frame in the platoon's global slice `frames` [D][nreg_max], the near-optimal leaves of the tie
+// rule in `tie_codes` [kTie][n] (codes) and lane j's register (cost).
+#pragma once
+
+#include "hvp_bnb.h"
+#include "hvp_cent.h"
+
+namespace hvp {
+namespace cent {
+
+constexpr int kTie = 16;  // near-optimal leaves kept for the tie rule
+
+enum { QP_OK = 0, QP_INFEASIBLE = 1, QP_FAILED = 2 };
+
+struct Child {
+    double lb, lo, hi;
+    int32_t r, pad;
+};
+
+struct Result {
+    double cost;
+    int status;  // HVP_*
+    int nodes;   // QPs solved: bounds, leaves and the final re-solve (the oracle's count)
+    int iters;   // active-set iterations
+};
+
+// Register state of the search.  Lane i < n: vehicle i's region code and the reachable interval
+// of its next undecided velocity.  Lane d < D: DFS frame d (children, cursor, the interval of
+// vehicle d % n before the frame's decision, the bound of the child taken).  Lane j < ntie: cost
+// of near-optimal leaf j.
+struct Search {
+    uint64_t vcode;
+    double vlo, vhi;
+    int f_n, f_cur;
+    double f_slo, f_shi, f_lb;
+    double tie_c;
+};
+
+// fixed steps of vehicle i once the first d decisions (time-major) are taken
+__device__ inline int fixed_steps(int d, int n, int i) { return d / n + (i < d % n ? 1 : 0); }
+
+// Platoon QP with the first `d` decisions fixed.  QP_OK with the cost and the lanes' y.
+__device__ inline int platoon_qp(Lane& L, const Lds& S, const Consts& C, const Inst& I, uint64_t vcode, int d,
+                                 int max_iter, double& cost, int& iters) {
+    const int t = lane();
+    const int i = t < I.V ? t / I.N : 0;
+    const uint64_t ci = bc(vcode, i);
+    const int Ki = fixed_steps(d, I.n, i);
+    int it = 0;
+    iters = 0;
+    wsync();
+    if (!setup(L, S, C, I, ci, Ki)) return QP_INFEASIBLE;
+    const int r = solve(L, S, C, I, max_iter, it);
+    iters = it;
+    if (r == GI_FAIL_DUAL) return QP_INFEASIBLE;
+    if (r != GI_OK) return QP_FAILED;
+    cost = direct_cost(L, C, I, ci, Ki);
+    return QP_OK;
+}
+
+// time-major lexicographic "a < b" of two joint sequences (lane i < n holds vehicle i's code)
+__device__ inline bool joint_less(uint64_t a_code, uint64_t b_code, int n, int N) {
+    const int t = lane();
+    const int D = n * N;
+    const int vi = t < D ? t % n : 0, vk = t < D ? t / n : 0;
+    const uint64_t ca = bc(a_code, vi), cb = bc(b_code, vi);
+    const int ra = t < D ? code_region(ca, vk) : 0, rb = t < D ? code_region(cb, vk) : 0;
+    const unsigned long long diff = __ballot(t < D && ra != rb);
+    if (!diff) return false;
+    const int first = __ffsll((long long)diff) - 1;
+    return bc(ra, first) < bc(rb, first);
+}
+
+// One child record, read with lane-dependent addresses (vector loads: the slice is rewritten
+// during the search, so it must not go through the scalar cache) and broadcast.
+__device__ inline Child load_child(const Child* c) {
+    const int t = lane();
+    const double* w = reinterpret_cast<const double*>(c);
+    const double v = t < 4 ? w[t] : 0.0;
+    Child ch;
+    ch.lb = bc(v, 0);
+    ch.lo = bc(v, 1);
+    ch.hi = bc(v, 2);
+    ch.r = (int32_t)(__double_as_longlong(bc(v, 3)) & 0xffffffffll);
+    ch.pad = 0;
+    return ch;
+}
+
+// Branch and bound of one platoon.  On return with status HVP_OPTIMAL the lanes' L.y and
+// st.vcode hold the winner.
+__device__ inline void bnb_platoon(Lane& L, const Lds& S, const Consts& C, const Inst& I, Search& st, Child* frames,
+                                   int nreg_max, uint64_t* tie_codes, int max_nodes, bool exhaustive, int max_iter,
+                                   Result& res) {
+    const int t = lane();
+    const int n = I.n, N = I.N, D = n * N;
+    const double INF = __builtin_inf();
+    st.vcode = 0;
+    st.vlo = st.vhi = t < n ? I.x0[2 * t + 1] : 0.0;
+    st.f_n = st.f_cur = 0;
+    st.f_slo = st.f_shi = st.f_lb = 0.0;
+    st.tie_c = INF;
+    int ntie = 0;
+    double inc = INF;
+    bool have_best = false, node_limit = false, tie_over = false;
+    double fail_lb = INF;  // smallest bound of a leaf whose QP failed (not infeasible)
+    int nodes = 0, iters = 0;
+
+    auto qp = [&](int dfix, double& cost) -> int {
+        int it = 0;
+        ++nodes;
+        const int r = platoon_qp(L, S, C, I, st.vcode, dfix, max_iter, cost, it);
+        iters += it;
+        return r;
+    };
+    // children of the node with d decisions taken, sorted by (bound, region) into frame d
+    auto expand = [&](int d) {
+        const int k = d / n, i = d % n;
+        const hvp_system& Si = I.systems[I.vsys[i]];
+        const double lo = bc(st.vlo, i), hi = bc(st.vhi, i);
+        bool ok = false;
+        double nlo = 0.0, nhi = 0.0;
+        if (t < Si.n_regions) ok = bnb_child(Si, C, k, lo, hi, t, &nlo, &nhi);
+        const unsigned long long mask = __ballot(ok);
+        double clb = 0.0;
+        if (d + 1 < D && !exhaustive) {
+            const uint64_t save = st.vcode;
+            for (unsigned long long m = mask; m; m &= m - 1) {
+                const int r = __ffsll((long long)m) - 1;
+                if (t == i) st.vcode = code_with(save, k, r);
+                double c = 0.0;
+                const int q = qp(d + 1, c);
+                const double lb = q == QP_OK ? c : (q == QP_INFEASIBLE ? INF : -INF);
+                if (t == r) clb = lb;
+            }
+            if (t == i) st.vcode = save;
+        }
+        int rank = 0;
+        for (int c = 0; c < Si.n_regions; ++c) {
+            const double lc = bc(clb, c);
+            if (((mask >> c) & 1ull) && (lc < clb || (lc == clb && c < t))) ++rank;
+        }
+        if (ok) {
+            Child ch;
+            ch.lb = clb;
+            ch.lo = nlo;
+            ch.hi = nhi;
+            ch.r = t;
+            ch.pad = 0;
+            frames[(size_t)d * nreg_max + rank] = ch;
+        }
+        if (t == d) {
+            st.f_n = __popcll(mask);
+            st.f_cur = 0;
+            st.f_slo = lo;
+            st.f_shi = hi;
+        }
+        __threadfence_block();
+        wsync();
+    };
+    // a feasible leaf with the current codes: incumbent and tie set
+    auto record = [&](double cost) {
+        if (cost < inc) {
+            inc = cost;
+            const double tol = 1e-9 * fmax(1.0, fabs(inc));
+            int w = 0;  // drop entries beyond the new window (rows only move down: serial copy)
+            for (int j = 0; j < ntie; ++j) {
+                const double cj = bc(st.tie_c, j);
+                if (!(cj <= inc + tol)) continue;
+                if (w != j) {
+                    if (t < n) tie_codes[(size_t)w * n + t] = tie_codes[(size_t)j * n + t];
+                    if (t == w) st.tie_c = cj;
+                }
+                ++w;
+            }
+            ntie = w;
+            if (t >= ntie) st.tie_c = INF;
+        }
+        if (cost <= inc + 1e-9 * fmax(1.0, fabs(inc))) {
+            if (ntie < kTie) {
+                if (t < n) tie_codes[(size_t)ntie * n + t] = st.vcode;
+                if (t == ntie) st.tie_c = cost;
+                ++ntie;
+            } else {
+                tie_over = true;
+            }
+        }
+        have_best = true;
+    };
+
+    expand(0);
+    int d = 0;
+    while (d >= 0) {
+        if (nodes >= max_nodes) {
+            node_limit = true;
+            break;
+        }
+        const int nch = bc(st.f_n, d), cur = bc(st.f_cur, d);
+        const int i = d % n, k = d / n;
+        if (cur >= nch) {  // frame done: vehicle i's interval back to the parent's
+            const double slo = bc(st.f_slo, d), shi = bc(st.f_shi, d);
+            if (t == i) {
+                st.vlo = slo;
+                st.vhi = shi;
+            }
+            --d;
+            continue;
+        }
+        if (t == d) st.f_cur = cur + 1;
+        const Child ch = load_child(frames + (size_t)d * nreg_max + cur);
+        if (have_best && bnb_pruned(ch.lb, inc)) continue;
+        if (!(ch.lb < INF)) continue;
+        if (t == i) {
+            st.vcode = code_with(st.vcode, k, ch.r);
+            st.vlo = ch.lo;
+            st.vhi = ch.hi;
+        }
+        if (t == d) st.f_lb = ch.lb;
+        if (d + 1 == D) {  // leaf: every step of every vehicle fixed
+            double c = 0.0;
+            const int q = qp(D, c);
+            if (q == QP_OK) {
+                record(c);
+            } else if (q == QP_FAILED) {
+                const double plb = D >= 2 ? bc(st.f_lb, D - 2) : -INF;
+                fail_lb = fmin(fail_lb, plb);
+            }
+        } else {
+            ++d;
+            expand(d);
+        }
+    }
+    res.status = HVP_INFEASIBLE;
+    res.cost = INF;
+    if (node_limit) {
+        res.status = HVP_MAXITER;
+    } else if (tie_over) {
+        res.status = HVP_OVERFLOW;
+    } else if (have_best) {
+        // the lexicographically first (time-major) leaf within the tie window
+        const double tol = 1e-9 * fmax(1.0, fabs(inc));
+        int win = -1;
+        uint64_t wcode = 0;
+        for (int j = 0; j < ntie; ++j) {
+            const double cj = bc(st.tie_c, j);
+            if (!(cj <= inc + tol)) continue;
+            const uint64_t cj_code = t < n ? tie_codes[(size_t)j * n + t] : 0;
+            if (win < 0 || joint_less(cj_code, wcode, n, N)) {
+                win = j;
+                wcode = cj_code;
+            }
+        }
+        st.vcode = wcode;
+        // a failed leaf whose bound is not above the incumbent could hide the optimum
+        res.status = (fail_lb < INF && !bnb_pruned(fail_lb, inc)) ? HVP_MAXITER : HVP_OPTIMAL;
+        double c = 0.0;
+        const int q = qp(D, c);  // re-solve the winner for its trajectory (counted, as the oracle)
+        if (q != QP_OK) res.status = HVP_MAXITER;
+        res.cost = c;
+    } else if (fail_lb < INF) {
+        res.status = HVP_MAXITER;
+    }
+    res.nodes = nodes;
+    res.iters = iters;
+}
+
+}  // namespace cent
+}  // namespace hvp

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define HVP_ABI_VERSION 3
+#define HVP_ABI_VERSION 4
 #define HVP_MAX_REGIONS 16
 #define HVP_MAX_N 16     /* longest horizon (branch-and-bound path)            */
 #define HVP_MAX_N_ENUM 8 /* longest horizon of the exhaustive-enumeration path */
@@ -91,9 +91,11 @@ enum {
     HVP_FORM_DECENT = 0, /* LocalMpcMld (fleet_decent_mld.py:21-223): fixed neighbour predictions   */
     HVP_FORM_ADMM = 1,   /* LocalMpcADMM (fleet_naive_admm.py:24-253): neighbour COPIES as decision
                             variables with ADMM terms y'(c - z) + rho/2 |c - z|^2; needs B&B      */
-    HVP_FORM_GADMM = 2   /* fleet_g_admm.LocalMpc (:22-205) under MpcSwitching [EXT]: convex QP for
+    HVP_FORM_GADMM = 2,  /* fleet_g_admm.LocalMpc (:22-205) under MpcSwitching [EXT]: convex QP for
                             a GIVEN region sequence; own state and copies in the augmented
                             Lagrangian; solved by hvp_gadmm_solve only                          */
+    HVP_FORM_CENT = 3    /* MpcMldCent (mpcs/cent_mld.py:21-182): ONE MIQP over the whole platoon;
+                            solved by hvp_cent_solve_batch only                                  */
 };
 
 /* Search over the region sequences (hvp_problem.method).  Both give the same sequence: the
@@ -243,6 +245,26 @@ int hvp_gadmm_update(hvp_handle* h, int P, int n, int lo, int m, const double* x
  * in edge [B] into the region on the other side; sets state bit 2 when a sequence changed. */
 int hvp_gadmm_switch(hvp_handle* h, int P, int n, int lo, int m, const int32_t* sys, const uint32_t* edge,
                      int8_t* seq, int32_t* state, void* stream);
+/* ---- Centralised MLD (mpcs/cent_mld.py MpcMldCent, fleet_cent_mld.py): replaces
+ * MpcMldCent.__init__ + setup_cost_and_constraints (:21-177; the handle, formulation
+ * HVP_FORM_CENT, and leader_index / real_vehicle_as_reference here), set_leader_traj (:179-182;
+ * leader_x) and MldAgent.get_control -> solve_mpc -> Model.optimize() (fleet_cent_mld.py:183) for
+ * P independent platoons of n vehicles in one call (device pointers, async on stream):
+ *   sys [P*n] system index of vehicle i of platoon p at p*n + i; x0 [P][n][2] (p, v);
+ *   leader_x [P][2][N+1] the leader window; n*N <= 64; real_vehicle_as_reference needs
+ *   leader_index == 0 (the reference raises NotImplementedError otherwise, :63-66).
+ * Exact branch and bound over the joint region sequence (time-major), ties to the
+ * lexicographically first sequence in that order; hvp_problem.method == HVP_METHOD_ENUMERATE
+ * visits every velocity-feasible joint sequence instead (cross-check, tiny instances only).
+ * max_nodes (<= 0: 200000) caps the QPs per platoon; a platoon that reaches it is HVP_MAXITER.
+ * Outputs: u [P][n][N], x [P][n][2][N+1] (may be NULL), region / gear [P][n][N] int8 (may be
+ * NULL), cost [P], status [P], nodes [P] (QPs solved, Gurobi NodeCount analogue), iters [P] (may
+ * be NULL).  Workspace grows on demand (one synchronisation when it does). */
+int hvp_cent_solve_batch(hvp_handle* h, int P, int n, int leader_index, int real_vehicle_as_reference,
+                         const int32_t* sys, const double* x0, const double* leader_x, int max_nodes,
+                         double* u_out, double* x_out, int8_t* region_out, int8_t* gear_out,
+                         double* cost_out, int32_t* status_out, int32_t* nodes_out, int32_t* iters_out,
+                         void* stream);
 int hvp_sync(hvp_handle* h, void* stream);
 int hvp_get_stats(hvp_handle* h, hvp_stats* out); /* synchronises the handle's last stream */
 void hvp_destroy(hvp_handle* h);

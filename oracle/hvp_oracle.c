@@ -36,9 +36,9 @@
 
 #define OR_MAX_N 16
 #define OR_MAX_REG 16
-#define OR_MAX_NZ 200
-#define OR_MAX_EQ 40
-#define OR_MAX_M 420
+#define OR_MAX_NZ 264
+#define OR_MAX_EQ 128
+#define OR_MAX_M 760
 #define OR_MAX_KKT (OR_MAX_NZ + OR_MAX_EQ + OR_MAX_M)
 #define OR_BIG 1e6
 
@@ -1401,5 +1401,350 @@ int oracle_solve_gadmm_qp(int N, int nreg, int nsr, const double* S, const doubl
     info_out[3] = bits;
     free(qp);
     free(w);
+    return 0;
+}
+
+/* ================================================================== centralised MLD (a20)
+ * MpcMldCent (mpcs/cent_mld.py:21-182): ONE MIQP over the platoon.  Per vehicle i the MLD model
+ * of MpcMldCentDecup [EXT] (region rows / dynamics of sigma_{i,k}, D x <= E for k >= 1, F u <= G),
+ * the acceleration rows (:145-163); cost: leader tracking of x_ref by vehicle L (:85-105, with
+ * spacing when real_vehicle_as_reference), the chain terms |x_i - x_{i-1} - spacing(x_i)|^2_Q for
+ * i >= 1 (:106-117), Q_u u^2, Q_du (du)^2 (:119-135) and w s (:137-140) with the soft safe rows
+ * p_i <= p_{i-1} - d_safe + s_i (:170-177) and, with real_vehicle_as_reference, the leader's row
+ * p_0 <= x_ref - d_safe + s_0 (:164-169).  Vehicle i's steps k >= K[i] are relaxed as in
+ * build_qp_k (branch and bound).  Layout per vehicle: x (2N) | u (N) | s (N+1, if it has a safe
+ * row).  x0 = [p0 v0] per vehicle, xl = leader_x (2, N+1). */
+#define OR_MAX_VEH 16
+typedef struct {
+    int n, lsp, L;
+    int xo[OR_MAX_VEH], uo[OR_MAX_VEH], so[OR_MAX_VEH];
+} or_cent_layout;
+
+static lin CX(const or_cent_layout* CL, const double* x0, int N, int i, int k, int c) {
+    if (k == 0) return lin_const(x0[2 * i + c]);
+    lin e = lin_const(0.0);
+    lin_add(&e, CL->xo[i] + 2 * (k - 1) + c, 1.0);
+    return e;
+    (void)N;
+}
+
+static int build_cent_qp(or_qp* qp, const or_model* md, const or_cfg* cf, or_cent_layout* CL, const int* sigma,
+                         const int* K, const double* x0, const double* xl) {
+    const int N = cf->N, n = CL->n;
+    int nz = 0;
+    for (int i = 0; i < n; ++i) {
+        CL->xo[i] = nz; nz += 2 * N;
+        CL->uo[i] = nz; nz += N;
+        const int has_s = i >= 1 || (CL->lsp && CL->L == 0);
+        CL->so[i] = has_s ? nz : -1;
+        if (has_s) nz += N + 1;
+    }
+    if (nz > OR_MAX_NZ) return 0;
+    memset(qp->P, 0, sizeof(qp->P));
+    memset(qp->q, 0, sizeof(qp->q));
+    qp->r0 = 0.0; qp->neq = 0; qp->m = 0; qp->infeasible_const = 0;
+    for (int i = 0; i < n; ++i) {
+        const or_model* m = &md[i];
+        const int* sg = sigma + i * N;
+        for (int k = 0; k < N; ++k) {
+            int r = k < K[i] ? sg[k] : 0;
+            for (int c = 0; c < (k < K[i] ? 2 : 1); ++c) {
+                lin e = CX(CL, x0, N, i, k + 1, c);
+                for (int j = 0; j < 2; ++j) { lin xj = CX(CL, x0, N, i, k, j); e = lin_axpy(-m->A[r][c][j], &xj, &e); }
+                lin uk = lin_const(0.0);
+                lin_add(&uk, CL->uo[i] + k, 1.0);
+                e = lin_axpy(-m->B[r][c], &uk, &e);
+                if (qp->neq >= OR_MAX_EQ) return 0;
+                qp_add_eq(qp, &e, m->c[r][c]);
+            }
+        }
+        for (int k = 0; k < K[i]; ++k) {
+            int r = sg[k];
+            for (int row = 0; row < m->nsr; ++row) {
+                lin e = lin_const(0.0);
+                for (int j = 0; j < 2; ++j) { lin xj = CX(CL, x0, N, i, k, j); e = lin_axpy(m->S[r][row][j], &xj, &e); }
+                lin uk = lin_const(0.0);
+                lin_add(&uk, CL->uo[i] + k, 1.0);
+                e = lin_axpy(m->R[r][row], &uk, &e);
+                qp_add_le(qp, &e, m->T[r][row]);
+            }
+        }
+        for (int k = 1; k <= N; ++k)
+            for (int row = 0; row < m->nd; ++row) {
+                lin e = lin_const(0.0);
+                for (int j = 0; j < 2; ++j) { lin xj = CX(CL, x0, N, i, k, j); e = lin_axpy(m->D[row][j], &xj, &e); }
+                qp_add_le(qp, &e, m->E[row]);
+            }
+        for (int k = 0; k < N; ++k)
+            for (int row = 0; row < m->nf; ++row) {
+                lin e = lin_const(0.0);
+                lin_add(&e, CL->uo[i] + k, m->F[row]);
+                qp_add_le(qp, &e, m->G[row]);
+            }
+        for (int k = 0; k < N; ++k) {
+            lin v1 = CX(CL, x0, N, i, k + 1, 1), v0 = CX(CL, x0, N, i, k, 1);
+            lin dv = lin_axpy(-1.0, &v0, &v1);
+            lin ndv = lin_axpy(-1.0, &dv, &(lin){.n = 0, .cst = 0.0});
+            qp_add_le(qp, &ndv, -(cf->a_dec * cf->ts) - k * cf->tight);
+            qp_add_le(qp, &dv, cf->a_acc * cf->ts - k * cf->tight);
+        }
+        if (CL->so[i] >= 0)
+            for (int k = 0; k <= N; ++k) {
+                lin s = lin_const(0.0);
+                lin_add(&s, CL->so[i] + k, 1.0);
+                lin ns = lin_axpy(-1.0, &s, &(lin){.n = 0, .cst = 0.0});
+                qp_add_le(qp, &ns, 0.0);
+                lin pk = CX(CL, x0, N, i, k, 0);
+                lin e = lin_axpy(-1.0, &s, &pk); /* p_i - s <= p_{i-1} - d_safe  (or x_ref) */
+                if (i >= 1) {
+                    lin pm = CX(CL, x0, N, i - 1, k, 0);
+                    e = lin_axpy(-1.0, &pm, &e);
+                    qp_add_le(qp, &e, -cf->d_safe);
+                } else {
+                    qp_add_le(qp, &e, par(xl, N, 0, k) - cf->d_safe);
+                }
+                lin ws = lin_axpy(cf->w, &s, &(lin){.n = 0, .cst = 0.0});
+                qp_add_lin(qp, &ws);
+            }
+    }
+    /* tracking: leader and chain terms, k = 0..N */
+    for (int k = 0; k <= N; ++k) {
+        for (int i = 0; i < n; ++i) {
+            lin p = CX(CL, x0, N, i, k, 0), v = CX(CL, x0, N, i, k, 1);
+            lin e[2];
+            if (i == CL->L) {
+                if (CL->lsp) { e[0] = lin_axpy(cf->t0, &v, &p); e[0].cst += cf->d0; }
+                else e[0] = p;
+                e[0].cst -= par(xl, N, 0, k);
+                e[1] = v; e[1].cst -= par(xl, N, 1, k);
+                add_norm(qp, NULL, cf, e, cf->Qx, 2);
+            }
+            if (i >= 1) {
+                lin pm = CX(CL, x0, N, i - 1, k, 0), vm = CX(CL, x0, N, i - 1, k, 1);
+                e[0] = lin_axpy(cf->t0, &v, &p);
+                e[0].cst += cf->d0;
+                e[0] = lin_axpy(-1.0, &pm, &e[0]);
+                e[1] = lin_axpy(-1.0, &vm, &v);
+                add_norm(qp, NULL, cf, e, cf->Qx, 2);
+            }
+        }
+    }
+    double Qu[2][2] = {{cf->Qu, 0}, {0, 0}}, Qdu[2][2] = {{cf->Qdu, 0}, {0, 0}};
+    for (int i = 0; i < n; ++i) {
+        for (int k = 0; k < K[i]; ++k) {
+            lin e[2]; e[0] = lin_const(0.0); lin_add(&e[0], CL->uo[i] + k, 1.0); e[1] = lin_const(0.0);
+            add_norm(qp, NULL, cf, e, Qu, 1);
+        }
+        for (int k = 0; k + 1 < K[i]; ++k) {
+            if (cf->Qdu == 0.0) continue;
+            lin e[2]; e[0] = lin_const(0.0);
+            lin_add(&e[0], CL->uo[i] + k + 1, 1.0);
+            lin_add(&e[0], CL->uo[i] + k, -1.0);
+            e[1] = lin_const(0.0);
+            add_norm(qp, NULL, cf, e, Qdu, 1);
+        }
+    }
+    qp->nz = nz;
+    return nz;
+}
+
+/* direct objective of a centralised solution z (relaxed steps without input cost) */
+static double cent_objective(const or_cfg* cf, const or_cent_layout* CL, const int* K, const double* x0,
+                             const double* xl, const double* z) {
+    const int N = cf->N, n = CL->n;
+    double J = 0.0;
+    for (int k = 0; k <= N; ++k)
+        for (int i = 0; i < n; ++i) {
+            double p = k ? z[CL->xo[i] + 2 * (k - 1)] : x0[2 * i], v = k ? z[CL->xo[i] + 2 * (k - 1) + 1] : x0[2 * i + 1];
+            double e0, e1;
+            if (i == CL->L) {
+                e0 = p - par(xl, N, 0, k) + (CL->lsp ? cf->t0 * v + cf->d0 : 0.0);
+                e1 = v - par(xl, N, 1, k);
+                J += cf->Qx[0][0] * e0 * e0 + (cf->Qx[0][1] + cf->Qx[1][0]) * e0 * e1 + cf->Qx[1][1] * e1 * e1;
+            }
+            if (i >= 1) {
+                double pm = k ? z[CL->xo[i - 1] + 2 * (k - 1)] : x0[2 * (i - 1)];
+                double vm = k ? z[CL->xo[i - 1] + 2 * (k - 1) + 1] : x0[2 * (i - 1) + 1];
+                e0 = p + cf->t0 * v + cf->d0 - pm;
+                e1 = v - vm;
+                J += cf->Qx[0][0] * e0 * e0 + (cf->Qx[0][1] + cf->Qx[1][0]) * e0 * e1 + cf->Qx[1][1] * e1 * e1;
+                J += cf->w * fmax(0.0, p - pm + cf->d_safe);
+            } else if (CL->lsp && CL->L == 0) {
+                J += cf->w * fmax(0.0, p - par(xl, N, 0, k) + cf->d_safe);
+            }
+        }
+    for (int i = 0; i < n; ++i)
+        for (int k = 0; k < K[i]; ++k) {
+            double u = z[CL->uo[i] + k];
+            J += cf->Qu * u * u;
+            if (k + 1 < K[i]) { double du = z[CL->uo[i] + k + 1] - u; J += cf->Qdu * du * du; }
+        }
+    return J;
+}
+
+typedef struct {
+    const or_model* md;
+    const or_vmodel* vm;
+    const or_cfg* cf;
+    or_cent_layout CL;
+    const double *x0, *xl;
+    or_qp* qp;
+    or_work* w;
+    int n, N, maxit, n_qp, exhaustive;
+    double inc;
+    int best[OR_MAX_VEH * OR_MAX_N], have_best;
+    long iters;
+    int nleaf, capleaf; /* every leaf evaluated: the tie rule is applied at the end */
+    double* leaf_obj;
+    int* leaf_sig;
+} or_cent;
+
+static double cent_qp(or_cent* C, const int* sigma, const int* K, int leaf) {
+    C->n_qp++;
+    if (build_cent_qp(C->qp, C->md, C->cf, &C->CL, sigma, K, C->x0, C->xl) <= 0 || C->qp->infeasible_const)
+        return INFINITY;
+    or_result r = ipm_solve(C->qp, C->w, C->maxit);
+    C->iters += r.iters;
+    if (!r.converged) return leaf ? INFINITY : -INFINITY;
+    return cent_objective(C->cf, &C->CL, K, C->x0, C->xl, C->w->z);
+}
+
+/* time-major decision order d -> (k = d / n, i = d % n); lexicographic key in that order */
+static int cent_less(const int* a, const int* b, int n, int N) {
+    for (int k = 0; k < N; ++k)
+        for (int i = 0; i < n; ++i)
+            if (a[i * N + k] != b[i * N + k]) return a[i * N + k] < b[i * N + k];
+    return 0;
+}
+
+static void cent_leaf(or_cent* C, const int* sigma, const int* K) {
+    double obj = cent_qp(C, sigma, K, 1);
+    if (!isfinite(obj)) return;
+    const int nN = C->n * C->N;
+    if (C->nleaf == C->capleaf) {
+        C->capleaf = C->capleaf ? 2 * C->capleaf : 64;
+        C->leaf_obj = (double*)realloc(C->leaf_obj, sizeof(double) * C->capleaf);
+        C->leaf_sig = (int*)realloc(C->leaf_sig, sizeof(int) * (size_t)C->capleaf * nN);
+    }
+    C->leaf_obj[C->nleaf] = obj;
+    memcpy(C->leaf_sig + (size_t)C->nleaf * nN, sigma, sizeof(int) * nN);
+    C->nleaf++;
+    if (obj < C->inc) C->inc = obj;
+    C->have_best = 1;
+}
+
+static void cent_dfs(or_cent* C, int d, int* sigma, int* K, double* lo, double* hi) {
+    const int n = C->n, N = C->N;
+    if (d == n * N) { cent_leaf(C, sigma, K); return; }
+    const int k = d / n, i = d % n;
+    const or_vmodel* vm = &C->vm[i];
+    const or_cfg* cf = C->cf;
+    double dec = cf->a_dec * cf->ts + k * cf->tight, acc = cf->a_acc * cf->ts - k * cf->tight;
+    int child[OR_MAX_REG], nch = 0;
+    double clo[OR_MAX_REG], chi[OR_MAX_REG], lb[OR_MAX_REG];
+    for (int r = 0; r < C->md[i].nreg; ++r) {
+        if (!vm->rok[r]) continue;
+        double ilo = fmax(lo[i], vm->rlo[r]), ihi = fmin(hi[i], vm->rhi[r]);
+        if (ilo > ihi + 1e-9 * (1.0 + fabs(ihi))) continue;
+        if (ilo > ihi) ilo = ihi = 0.5 * (ilo + ihi);
+        double nlo, nhi;
+        if (!next_interval(ilo, ihi, vm->a[r], vm->b[r], vm->c[r], vm->ul, vm->uh, dec, acc, vm->blo, vm->bhi, &nlo,
+                           &nhi))
+            continue;
+        sigma[i * N + k] = r;
+        K[i] = k + 1;
+        lb[nch] = (d + 1 == n * N || C->exhaustive) ? 0.0 : cent_qp(C, sigma, K, 0);
+        K[i] = k;
+        child[nch] = r; clo[nch] = nlo; chi[nch] = nhi;
+        nch++;
+    }
+    /* visit in increasing bound order (ties: lower region first) */
+    for (int a = 0; a < nch; ++a) {
+        int m = a;
+        for (int b = a + 1; b < nch; ++b)
+            if (lb[b] < lb[m] || (lb[b] == lb[m] && child[b] < child[m])) m = b;
+        double tl = lb[a]; lb[a] = lb[m]; lb[m] = tl;
+        int tc = child[a]; child[a] = child[m]; child[m] = tc;
+        double t1 = clo[a]; clo[a] = clo[m]; clo[m] = t1;
+        double t2 = chi[a]; chi[a] = chi[m]; chi[m] = t2;
+    }
+    for (int a = 0; a < nch; ++a) {
+        if (C->have_best && lb[a] > C->inc + 1e-7 * (1.0 + fabs(C->inc))) continue;
+        if (!(lb[a] < INFINITY)) continue;
+        const double slo = lo[i], shi = hi[i];
+        sigma[i * N + k] = child[a];
+        K[i] = k + 1;
+        lo[i] = clo[a]; hi[i] = chi[a];
+        cent_dfs(C, d + 1, sigma, K, lo, hi);
+        lo[i] = slo; hi[i] = shi;
+        K[i] = k;
+    }
+}
+
+/* Centralised MIQP of one platoon: sys models stacked per vehicle (as oracle_solve_batch), x0
+ * (2n), xl (2, N+1), role = leader index | real_vehicle_as_reference << 8.  Outputs x (n, 2, N+1),
+ * u (n, N), sigma (n, N), info = [objective, status (0 optimal, 1 infeasible), QPs solved].
+ * role bit 16: exhaustive enumeration of the joint sequences instead of branch and bound. */
+int oracle_solve_cent(int n, int N, int nreg, int nsr, const double* S, const double* R, const double* T,
+                      const double* A, const double* B, const double* c, int nd, const double* D, const double* E, int nf,
+                      const double* F, const double* G, const double* cfgp, int role, const double* x0,
+                      const double* xl, double* x_out, double* u_out, int* sigma_out, double* info_out) {
+    if (n < 1 || n > OR_MAX_VEH || N > OR_MAX_N) return -1;
+    or_model md[OR_MAX_VEH];
+    or_vmodel vm[OR_MAX_VEH];
+    for (int i = 0; i < n; ++i) {
+        const size_t so = (size_t)i * nreg * nsr, ao = (size_t)i * nreg;
+        if (unpack_model(&md[i], nreg, nsr, S + 2 * so, R + so, T + so, A + 4 * ao, B + 2 * ao, c + 2 * ao, nd,
+                         D + (size_t)i * 2 * nd, E + (size_t)i * nd, nf, F + (size_t)i * nf, G + (size_t)i * nf))
+            return -1;
+        if (make_vmodel(&md[i], &vm[i]) || !oracle_bnb_ok(&md[i])) return -2;
+    }
+    or_cfg cf;
+    unpack_cfg(&cf, N, 1, 0, cfgp);
+    or_cent* C = (or_cent*)calloc(1, sizeof(or_cent));
+    or_qp* qp = (or_qp*)malloc(sizeof(or_qp));
+    or_work* w = (or_work*)malloc(sizeof(or_work));
+    if (!C || !qp || !w) { free(C); free(qp); free(w); return -3; }
+    C->md = md; C->vm = vm; C->cf = &cf; C->x0 = x0; C->xl = xl; C->qp = qp; C->w = w;
+    C->n = n; C->N = N; C->maxit = 200; C->inc = INFINITY;
+    C->CL.n = n; C->CL.L = role & 0xff; C->CL.lsp = (role >> 8) & 1;
+    C->exhaustive = (role >> 16) & 1; /* every velocity-feasible joint sequence (cross-check) */
+    int sigma[OR_MAX_VEH * OR_MAX_N] = {0}, K[OR_MAX_VEH] = {0};
+    double lo[OR_MAX_VEH], hi[OR_MAX_VEH];
+    for (int i = 0; i < n; ++i) lo[i] = hi[i] = x0[2 * i + 1];
+    cent_dfs(C, 0, sigma, K, lo, hi);
+    if (C->have_best) { /* lexicographically first (time-major) leaf within 1e-9 relative of the minimum */
+        const double tol = 1e-9 * fmax(1.0, fabs(C->inc));
+        int win = -1;
+        for (int l = 0; l < C->nleaf; ++l) {
+            if (!(C->leaf_obj[l] <= C->inc + tol)) continue;
+            if (win < 0 || cent_less(C->leaf_sig + (size_t)l * n * N, C->leaf_sig + (size_t)win * n * N, n, N)) win = l;
+        }
+        memcpy(C->best, C->leaf_sig + (size_t)win * n * N, sizeof(int) * n * N);
+    }
+    free(C->leaf_obj);
+    free(C->leaf_sig);
+    info_out[0] = C->have_best ? C->inc : INFINITY;
+    info_out[1] = C->have_best ? 0 : 1;
+    info_out[2] = C->n_qp;
+    if (C->have_best) {
+        for (int i = 0; i < n; ++i) {
+            K[i] = N;
+            for (int k = 0; k < N; ++k) sigma_out[i * N + k] = C->best[i * N + k];
+        }
+        /* re-evaluate the winner for its exact objective and trajectory */
+        double obj = cent_qp(C, C->best, K, 1);
+        info_out[0] = obj;
+        for (int i = 0; i < n; ++i) {
+            x_out[i * 2 * (N + 1)] = x0[2 * i];
+            x_out[i * 2 * (N + 1) + N + 1] = x0[2 * i + 1];
+            for (int k = 1; k <= N; ++k) {
+                x_out[i * 2 * (N + 1) + k] = w->z[C->CL.xo[i] + 2 * (k - 1)];
+                x_out[i * 2 * (N + 1) + N + 1 + k] = w->z[C->CL.xo[i] + 2 * (k - 1) + 1];
+            }
+            for (int k = 0; k < N; ++k) u_out[i * N + k] = w->z[C->CL.uo[i] + k];
+        }
+    }
+    free(C); free(qp); free(w);
     return 0;
 }

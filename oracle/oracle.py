@@ -245,6 +245,9 @@ def lib():
         L.oracle_solve_gadmm_qp.argtypes = model_args + [dp, c_int, c_int, ctypes.c_double, dp, ip, dp, dp, dp, dp,
                                                          dp]
         L.oracle_solve_gadmm_qp.restype = c_int
+        L.oracle_solve_cent.argtypes = [c_int, c_int, c_int, c_int, dp, dp, dp, dp, dp, dp, c_int, dp, dp, c_int, dp,
+                                        dp, dp, c_int, dp, dp, dp, dp, ip, dp]
+        L.oracle_solve_cent.restype = c_int
         L.oracle_set_method.argtypes = [c_int]
         L.oracle_set_method.restype = None
         _lib = L
@@ -731,3 +734,38 @@ class GAdmmCoordinator:
         if best is None:
             raise RuntimeError("No solution found for any of the warm starts")
         return best[0], best_cost, runs
+
+
+# ------------------------------------------------------------------ centralised MLD (mpcs/cent_mld.py)
+@dataclass
+class CentResult:
+    x: np.ndarray      # (n, 2, N+1)
+    u: np.ndarray      # (n, N)
+    sigma: np.ndarray  # (n, N)
+    cost: float
+    status: int        # 0 optimal, 1 infeasible
+    n_qps: int
+
+
+def solve_cent(systems: list[dict], cfg: Cfg, N: int, x0, leader_x, leader_index: int = 0,
+               real_vehicle_as_reference: bool = False, exhaustive: bool = False) -> CentResult:
+    """MpcMldCent's MIQP (mpcs/cent_mld.py:48-182) for one platoon: full (x, u, s) space, branch
+    and bound over the joint region sequences in time-major order (or exhaustive enumeration);
+    ties to the lexicographically first joint sequence in that order (hvp_oracle.c oracle_solve_cent)."""
+    L = lib()
+    n = len(systems)
+    arrs = [_model_arrays(s)[2] for s in systems]
+    nreg, nsr = _model_arrays(systems[0])[:2]
+    st = {k: np.ascontiguousarray(np.stack([a[k] for a in arrs])) for k in "SRTABcDEFG"}
+    cv = cfg.vector()
+    x0 = np.ascontiguousarray(np.asarray(x0, dtype=np.float64).reshape(-1))
+    xl = np.ascontiguousarray(np.asarray(leader_x, dtype=np.float64).reshape(2, N + 1))
+    x_out, u_out = np.zeros((n, 2, N + 1)), np.zeros((n, N))
+    sig, info = np.zeros((n, N), dtype=np.int32), np.zeros(3)
+    role = int(leader_index) | (256 if real_vehicle_as_reference else 0) | (65536 if exhaustive else 0)
+    rc = L.oracle_solve_cent(n, N, nreg, nsr, _d(st["S"]), _d(st["R"]), _d(st["T"]), _d(st["A"]), _d(st["B"]),
+                             _d(st["c"]), st["D"].shape[1], _d(st["D"]), _d(st["E"]), st["F"].shape[1], _d(st["F"]),
+                             _d(st["G"]), _d(cv), role, _d(x0), _d(xl), _d(x_out), _d(u_out), _i(sig), _d(info))
+    if rc != 0:
+        raise RuntimeError(f"oracle_solve_cent failed ({rc})")
+    return CentResult(x_out, u_out, sig, float(info[0]), int(info[1]), int(info[2]))
