@@ -361,6 +361,116 @@ def cpu_baseline_gadmm(n: int, N: int, iters: int, max_rounds: int, budget_s: fl
                       f"oracle, {t_run:.1f} s"}
 
 
+def cent_qp_bytes(n: int, N: int) -> int:
+    """SURVEY.md 8(d) dense bytes of one centralised fixed-sequence QP (condensed like the local
+    QP: u (nN) and slacks (n(N+1)) free, m = 13N + 3 rows per vehicle), 8 (n_w^2 + m n_w + m + n_w)."""
+    nw, m = n * (2 * N + 1), n * (13 * N + 3)
+    return 8 * (nw * nw + m * nw + m + nw)
+
+
+def bench_cent(args, world: int, rank: int, local: int, dist) -> None:
+    """fleet_cent_mld.py (mpcs/cent_mld.py MpcMldCent): one step = the centralised MIQP of every
+    platoon of the rank's seed range (MldAgent.get_control -> solve_mpc), one wavefront per
+    platoon running the whole branch and bound (csrc/hvp_cent_bnb.h); platoons are independent
+    (seed-sharded, no collective)."""
+    import torch
+
+    from hvp import tables
+    from hvp.cent import CentSolver, cent_problem
+    from hvp.env import derive_env_seed, initial_platoon_state
+    from hvp.models import PwaGearVehicle
+
+    n, N, S = args.n, args.N, args.platoons
+    veh = PwaGearVehicle(800)
+    system = tables.system_from_dict(veh.get_discrete_system(1), tables.gears_of(veh))
+    solver = CentSolver(cent_problem(N), [system], device=local)
+    dev = torch.device("cuda", local)
+    seeds = range(rank * S, (rank + 1) * S)
+    x0 = np.stack([initial_platoon_state(n, derive_env_seed(int(s))).reshape(n, 2).astype(np.float64) for s in seeds])
+    lead = np.stack([3000.0 + 20.0 * np.arange(N + 1), np.full(N + 1, 20.0)])
+    t_x0 = torch.from_numpy(x0).to(dev)
+    t_sys = torch.zeros((S, n), dtype=torch.int32, device=dev)
+    t_lead = torch.from_numpy(np.ascontiguousarray(np.broadcast_to(lead, (S, 2, N + 1)))).to(dev)
+    out = solver.alloc_outputs(S, n, dev)
+    run = lambda: solver.solve_device(t_sys, t_x0, t_lead, max_nodes=args.max_nodes, out=out)  # noqa: E731
+    for _ in range(args.warmup):
+        run()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    status = out["status"].cpu().numpy()
+    nodes = out["nodes"].cpu().numpy()
+    iters = out["iters"].cpu().numpy()
+    if dist:
+        tt = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    # kernel time: HIP events the library records around k_cent_bnb on the solve stream
+    run()
+    st = solver.stats()
+    kernel_ms = st.last_ms
+    qps = int(nodes.sum())
+    alg_bytes = qps * cent_qp_bytes(n, N) + S * 8 * (2 * n + 2 * (N + 1) + n * (3 * N + 2) + 1)
+    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+    value = S * world * args.steps / dt
+    q = np.percentile(nodes, [50, 90, 99, 100])
+    result = {
+        "metric": f"MPC timesteps/sec (whole platoon) at n={n} N={N} cent_mld",
+        "value": value, "unit": "platoon-timesteps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic: env.reset random-init platoon states (seeded), constant-velocity leader",
+        "config": {"workload": f"fleet_cent_mld n={n} N={N} pwa_gear (MpcMldCent)", "n_vehicles": n, "horizon": N,
+                   "platoons_per_gpu": S, "max_nodes": args.max_nodes, "parallelism": f"seeds-sharded x{world}"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "k_cent_bnb",
+                     "kernel_avg_ms": kernel_ms, "launches_per_step": 1,
+                     "note": "SURVEY 8(d) notional dense bytes of every platoon QP solved (n_w = n(2N+1), "
+                             "m = n(13N+3)) + platoon I/O / the HIP-event time of the search kernel. The wave "
+                             "builds each QP in LDS from the platoon block: the kernel is FP64-latency bound "
+                             "(one wavefront per platoon, sequential active-set steps)"},
+        "qps_per_step": qps, "qp_iters_per_qp": float(iters.sum()) / max(qps, 1),
+        "nodes_per_platoon": {"p50": float(q[0]), "p90": float(q[1]), "p99": float(q[2]), "max": float(q[3])},
+        "status_counts": {"optimal": int((status == 0).sum()), "infeasible": int((status == 1).sum()),
+                          "node_limit": int((status == 2).sum()), "overflow": int((status == 3).sum())},
+    }
+    if rank == 0 and not args.no_cpu and args.cpu_budget > 0 and world == 1:
+        result["cpu_baseline"] = cpu_baseline_cent(n, N, min(args.cpu_budget, 60.0))
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+def cpu_baseline_cent(n: int, N: int, budget_s: float):
+    """The oracle's centralised MIQP (oracle_solve_cent: full-space dense IPM per QP, the same
+    joint branch and bound) one platoon at a time on one core, seeds from 10^7 up, until the
+    budget is spent (at least one platoon)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    systems = [O.gear_pwa_system(800.0)] * n
+    lead = np.stack([3000.0 + 20.0 * np.arange(N + 1), np.full(N + 1, 20.0)])
+    done, qps, seed = 0, 0, 10_000_000
+    t0 = time.perf_counter()
+    while done == 0 or time.perf_counter() - t0 < budget_s:
+        r = O.solve_cent(systems, O.Cfg(), N, O.env_initial_state(n, seed).astype(float), lead)
+        qps += r.n_qps
+        done += 1
+        seed += 1
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "platoon-timesteps/s", "cores": 1, "kind": "port",
+            "sample": f"{done} platoons (n={n}, N={N}, {qps} QPs) by oracle_solve_cent, {dt:.1f} s"}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -373,9 +483,10 @@ def main() -> None:
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--method", choices=["auto", "enum", "bnb"], default="auto",
                     help="region-sequence search (include/hvp.h HVP_METHOD_*)")
-    ap.add_argument("--controller", choices=["decent", "admm", "gadmm"], default="decent",
+    ap.add_argument("--controller", choices=["decent", "admm", "gadmm", "cent"], default="decent",
                     help="decent: fleet_decent_mld (configs[1]); admm: fleet_naive_admm (configs[2]); "
-                         "gadmm: fleet_g_admm (configs[3])")
+                         "gadmm: fleet_g_admm (configs[3]); cent: fleet_cent_mld (MpcMldCent)")
+    ap.add_argument("--max-nodes", type=int, default=200000, help="cent: QPs per platoon cap")
     ap.add_argument("--admm-iters", type=int, default=None, help="default 20 (admm) / 100 (gadmm)")
     ap.add_argument("--max-rounds", type=int, default=10, help="gadmm: switching rounds cap")
     ap.add_argument("--gadmm-layout", choices=["replicas", "vehicles"], default="replicas")
@@ -403,6 +514,8 @@ def main() -> None:
         return bench_admm(args, world, rank, local, dist)
     if args.controller == "gadmm":
         return bench_gadmm(args, world, rank, local, dist)
+    if args.controller == "cent":
+        return bench_cent(args, world, rank, local, dist)
     n, N, S = args.n, args.N, args.platoons
     veh = PwaGearVehicle(800)
     system = tables.system_from_dict(veh.get_discrete_system(1), tables.gears_of(veh))

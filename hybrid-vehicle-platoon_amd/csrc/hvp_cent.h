@@ -97,6 +97,7 @@ struct Inst {
     const int32_t* vsys;        // [n] system index per vehicle
     const double* x0;           // [2n] (p0, v0) per vehicle
     const double* xl;           // leader_x (2, N+1)
+    int debug;                  // HVP_CENT_DEBUG: printf diagnostics of failing QPs
 };
 
 struct Lane {
@@ -459,10 +460,12 @@ __device__ inline int solve(Lane& L, const Lds& Sg, const Consts& C, const Inst&
                 n2 = oa >= 1 && pair != 0 ? 1 : 0;
                 cf2 = -flip * sgn * ra;
                 if (t == owner) {
-                    double lo, hi;
-                    if (pair == 0) { lo = L.vlo; hi = L.vhi; }
-                    else if (pair == 1) { lo = L.ulo; hi = L.uhi; }
-                    else { lo = L.dec; hi = L.acc; }
+                    // value selects: opaque copies keep the compiler from turning this into a
+                    // select of field addresses (which would put the whole Lane in scratch)
+                    double vlo = L.vlo, vhi = L.vhi, ulo = L.ulo, uhi = L.uhi, dlo = L.dec, dhi = L.acc;
+                    asm volatile("" : "+v"(vlo), "+v"(vhi), "+v"(ulo), "+v"(uhi), "+v"(dlo), "+v"(dhi));
+                    const double lo = pair == 0 ? vlo : (pair == 1 ? ulo : dlo);
+                    const double hi = pair == 0 ? vhi : (pair == 1 ? uhi : dhi);
                     const double cst = oa == 0 ? -ra * L.v0 : 0.0;
                     dloc = (rr & 1) ? hi - cst : -(lo - cst);
                 }
@@ -542,7 +545,13 @@ __device__ inline int solve(Lane& L, const Lds& Sg, const Consts& C, const Inst&
             const double sp_now = dp + wsum(np_t * (t < V ? L.y : 0.0));
             const double t2 = zstep && zn > 0.0 ? fmax(-sp_now, 0.0) / zn : 1e300;
             const double tstep = fmin(t1, fmin(t2, t3));
-            if (!(tstep < 1e299)) { iters = iter; return GI_FAIL_DUAL; }
+            if (!(tstep < 1e299)) {
+                if (I.debug && t == 0)
+                    printf("[cent] GI_FAIL_DUAL iter %d nact %d row %d (owner %d rr %d rev %d) d2n %.3e dn %.3e "
+                           "sp %.6e\n", iter, nact, pr, owner, rr, (int)rev, d2n, dn, sp_now);
+                iters = iter;
+                return GI_FAIL_DUAL;
+            }
             if (t2 < 1e299 && t < V) L.y += tstep * z;
             if (t < nact) u -= tstep * r;
             unew += tstep;

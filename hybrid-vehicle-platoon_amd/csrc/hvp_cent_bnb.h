@@ -35,7 +35,8 @@ struct Child {
 struct Result {
     double cost;
     int status;  // HVP_*
-    int nodes;   // QPs solved: bounds, leaves and the final re-solve (the oracle's count)
+    int nodes;   // QPs of the search: bounds and leaves (the oracle's count; the final re-solve of
+                 // the winner is not counted)
     int iters;   // active-set iterations
 };
 
@@ -102,7 +103,9 @@ __device__ inline Child load_child(const Child* c) {
 }
 
 // Branch and bound of one platoon.  On return with status HVP_OPTIMAL the lanes' L.y and
-// st.vcode hold the winner.
+// st.vcode hold the winner.  Written as a loop with ONE platoon-QP call site (bound QPs of a
+// node's children, leaf QPs and the final re-solve all go through it), so the large QP body is
+// inlined once and its state stays in registers.
 __device__ inline void bnb_platoon(Lane& L, const Lds& S, const Consts& C, const Inst& I, Search& st, Child* frames,
                                    int nreg_max, uint64_t* tie_codes, int max_nodes, bool exhaustive, int max_iter,
                                    Result& res) {
@@ -118,56 +121,51 @@ __device__ inline void bnb_platoon(Lane& L, const Lds& S, const Consts& C, const
     double inc = INF;
     bool have_best = false, node_limit = false, tie_over = false;
     double fail_lb = INF;  // smallest bound of a leaf whose QP failed (not infeasible)
-    int nodes = 0, iters = 0;
+    int nodes = 0, iters = 0, searched = 0;
 
-    auto qp = [&](int dfix, double& cost) -> int {
-        int it = 0;
-        ++nodes;
-        const int r = platoon_qp(L, S, C, I, st.vcode, dfix, max_iter, cost, it);
-        iters += it;
-        return r;
-    };
-    // children of the node with d decisions taken, sorted by (bound, region) into frame d
-    auto expand = [&](int d) {
-        const int k = d / n, i = d % n;
+    // expansion of the node with d decisions taken: lane r holds child r's interval and bound
+    enum { EXPAND = 0, VISIT = 1, FINAL = 2 };
+    int phase = EXPAND, d = 0;
+    unsigned long long ex_mask = 0, ex_todo = 0;
+    uint64_t ex_save = 0;
+    bool ex_ok = false;
+    double ex_nlo = 0.0, ex_nhi = 0.0, ex_lb = 0.0;
+    int ex_r = 0;
+
+    auto begin_expand = [&](int dd) {
+        const int k = dd / n, i = dd % n;
         const hvp_system& Si = I.systems[I.vsys[i]];
         const double lo = bc(st.vlo, i), hi = bc(st.vhi, i);
-        bool ok = false;
-        double nlo = 0.0, nhi = 0.0;
-        if (t < Si.n_regions) ok = bnb_child(Si, C, k, lo, hi, t, &nlo, &nhi);
-        const unsigned long long mask = __ballot(ok);
-        double clb = 0.0;
-        if (d + 1 < D && !exhaustive) {
-            const uint64_t save = st.vcode;
-            for (unsigned long long m = mask; m; m &= m - 1) {
-                const int r = __ffsll((long long)m) - 1;
-                if (t == i) st.vcode = code_with(save, k, r);
-                double c = 0.0;
-                const int q = qp(d + 1, c);
-                const double lb = q == QP_OK ? c : (q == QP_INFEASIBLE ? INF : -INF);
-                if (t == r) clb = lb;
-            }
-            if (t == i) st.vcode = save;
-        }
-        int rank = 0;
-        for (int c = 0; c < Si.n_regions; ++c) {
-            const double lc = bc(clb, c);
-            if (((mask >> c) & 1ull) && (lc < clb || (lc == clb && c < t))) ++rank;
-        }
-        if (ok) {
-            Child ch;
-            ch.lb = clb;
-            ch.lo = nlo;
-            ch.hi = nhi;
-            ch.r = t;
-            ch.pad = 0;
-            frames[(size_t)d * nreg_max + rank] = ch;
-        }
-        if (t == d) {
-            st.f_n = __popcll(mask);
+        ex_ok = false;
+        ex_nlo = ex_nhi = 0.0;
+        if (t < Si.n_regions) ex_ok = bnb_child(Si, C, k, lo, hi, t, &ex_nlo, &ex_nhi);
+        ex_mask = __ballot(ex_ok);
+        ex_todo = (dd + 1 < D && !exhaustive) ? ex_mask : 0ull;
+        ex_lb = 0.0;
+        ex_save = st.vcode;
+        if (t == dd) {
+            st.f_n = __popcll(ex_mask);
             st.f_cur = 0;
             st.f_slo = lo;
             st.f_shi = hi;
+        }
+    };
+    // children sorted by (bound, region) into frame dd
+    auto finish_expand = [&](int dd) {
+        const hvp_system& Si = I.systems[I.vsys[dd % n]];
+        int rank = 0;
+        for (int c = 0; c < Si.n_regions; ++c) {
+            const double lc = bc(ex_lb, c);
+            if (((ex_mask >> c) & 1ull) && (lc < ex_lb || (lc == ex_lb && c < t))) ++rank;
+        }
+        if (ex_ok) {
+            Child ch;
+            ch.lb = ex_lb;
+            ch.lo = ex_nlo;
+            ch.hi = ex_nhi;
+            ch.r = t;
+            ch.pad = 0;
+            frames[(size_t)dd * nreg_max + rank] = ch;
         }
         __threadfence_block();
         wsync();
@@ -202,79 +200,115 @@ __device__ inline void bnb_platoon(Lane& L, const Lds& S, const Consts& C, const
         have_best = true;
     };
 
-    expand(0);
-    int d = 0;
-    while (d >= 0) {
-        if (nodes >= max_nodes) {
-            node_limit = true;
-            break;
-        }
-        const int nch = bc(st.f_n, d), cur = bc(st.f_cur, d);
-        const int i = d % n, k = d / n;
-        if (cur >= nch) {  // frame done: vehicle i's interval back to the parent's
-            const double slo = bc(st.f_slo, d), shi = bc(st.f_shi, d);
-            if (t == i) {
-                st.vlo = slo;
-                st.vhi = shi;
+    begin_expand(0);
+    for (;;) {
+        // ---- decide the next QP (dfix decisions fixed), or move the search without one
+        int dfix = -1;
+        if (phase == EXPAND) {
+            if (!ex_todo) {
+                if (t == d % n) st.vcode = ex_save;
+                finish_expand(d);
+                phase = VISIT;
+                continue;
             }
-            --d;
-            continue;
+            ex_r = __ffsll((long long)ex_todo) - 1;
+            if (t == d % n) st.vcode = code_with(ex_save, d / n, ex_r);
+            dfix = d + 1;
+        } else if (phase == VISIT) {
+            if (nodes >= max_nodes) {
+                node_limit = true;
+                break;
+            }
+            if (d < 0) {  // search done
+                searched = nodes;
+                if (!have_best || tie_over) break;
+                // the lexicographically first (time-major) leaf within the tie window
+                const double tol = 1e-9 * fmax(1.0, fabs(inc));
+                int win = -1;
+                uint64_t wcode = 0;
+                for (int j = 0; j < ntie; ++j) {
+                    const double cj = bc(st.tie_c, j);
+                    if (!(cj <= inc + tol)) continue;
+                    const uint64_t cj_code = t < n ? tie_codes[(size_t)j * n + t] : 0;
+                    if (win < 0 || joint_less(cj_code, wcode, n, N)) {
+                        win = j;
+                        wcode = cj_code;
+                    }
+                }
+                st.vcode = wcode;
+                phase = FINAL;
+                dfix = D;  // re-solve the winner for its trajectory (not counted)
+            } else {
+                const int nch = bc(st.f_n, d), cur = bc(st.f_cur, d);
+                const int i = d % n, k = d / n;
+                if (cur >= nch) {  // frame done: vehicle i's interval back to the parent's
+                    const double slo = bc(st.f_slo, d), shi = bc(st.f_shi, d);
+                    if (t == i) {
+                        st.vlo = slo;
+                        st.vhi = shi;
+                    }
+                    --d;
+                    continue;
+                }
+                if (t == d) st.f_cur = cur + 1;
+                const Child ch = load_child(frames + (size_t)d * nreg_max + cur);
+                if (have_best && bnb_pruned(ch.lb, inc)) continue;
+                if (!(ch.lb < INF)) continue;
+                if (t == i) {
+                    st.vcode = code_with(st.vcode, k, ch.r);
+                    st.vlo = ch.lo;
+                    st.vhi = ch.hi;
+                }
+                if (t == d) st.f_lb = ch.lb;
+                if (d + 1 < D) {
+                    ++d;
+                    begin_expand(d);
+                    phase = EXPAND;
+                    continue;
+                }
+                dfix = D;  // leaf: every step of every vehicle fixed
+            }
         }
-        if (t == d) st.f_cur = cur + 1;
-        const Child ch = load_child(frames + (size_t)d * nreg_max + cur);
-        if (have_best && bnb_pruned(ch.lb, inc)) continue;
-        if (!(ch.lb < INF)) continue;
-        if (t == i) {
-            st.vcode = code_with(st.vcode, k, ch.r);
-            st.vlo = ch.lo;
-            st.vhi = ch.hi;
+        // ---- the one QP call site
+        double c = 0.0;
+        int it = 0;
+        ++nodes;
+        const int q = platoon_qp(L, S, C, I, st.vcode, dfix, max_iter, c, it);
+        iters += it;
+        if (I.debug && q != QP_OK) {
+            const uint64_t c0 = bc(st.vcode, 0), c1 = bc(st.vcode, 1 < n ? 1 : 0), c2 = bc(st.vcode, 2 < n ? 2 : 0);
+            if (t == 0)
+                printf("[cent] platoon %d QP %d dfix %d phase %d -> %d (codes v0 %llx v1 %llx v2 %llx)\n",
+                       (int)blockIdx.x, nodes, dfix, phase, q, (unsigned long long)c0, (unsigned long long)c1,
+                       (unsigned long long)c2);
         }
-        if (t == d) st.f_lb = ch.lb;
-        if (d + 1 == D) {  // leaf: every step of every vehicle fixed
-            double c = 0.0;
-            const int q = qp(D, c);
+        // ---- use its result
+        if (phase == EXPAND) {
+            const double lb = q == QP_OK ? c : (q == QP_INFEASIBLE ? INF : -INF);
+            if (t == ex_r) ex_lb = lb;
+            ex_todo &= ex_todo - 1;
+        } else if (phase == VISIT) {
             if (q == QP_OK) {
                 record(c);
             } else if (q == QP_FAILED) {
                 const double plb = D >= 2 ? bc(st.f_lb, D - 2) : -INF;
                 fail_lb = fmin(fail_lb, plb);
             }
-        } else {
-            ++d;
-            expand(d);
+        } else {  // FINAL
+            // a failed leaf whose bound is not above the incumbent could hide the optimum
+            res.status = (fail_lb < INF && !bnb_pruned(fail_lb, inc)) ? HVP_MAXITER : HVP_OPTIMAL;
+            if (q != QP_OK) res.status = HVP_MAXITER;
+            res.cost = c;
+            res.nodes = searched;
+            res.iters = iters;
+            return;
         }
     }
-    res.status = HVP_INFEASIBLE;
     res.cost = INF;
-    if (node_limit) {
-        res.status = HVP_MAXITER;
-    } else if (tie_over) {
-        res.status = HVP_OVERFLOW;
-    } else if (have_best) {
-        // the lexicographically first (time-major) leaf within the tie window
-        const double tol = 1e-9 * fmax(1.0, fabs(inc));
-        int win = -1;
-        uint64_t wcode = 0;
-        for (int j = 0; j < ntie; ++j) {
-            const double cj = bc(st.tie_c, j);
-            if (!(cj <= inc + tol)) continue;
-            const uint64_t cj_code = t < n ? tie_codes[(size_t)j * n + t] : 0;
-            if (win < 0 || joint_less(cj_code, wcode, n, N)) {
-                win = j;
-                wcode = cj_code;
-            }
-        }
-        st.vcode = wcode;
-        // a failed leaf whose bound is not above the incumbent could hide the optimum
-        res.status = (fail_lb < INF && !bnb_pruned(fail_lb, inc)) ? HVP_MAXITER : HVP_OPTIMAL;
-        double c = 0.0;
-        const int q = qp(D, c);  // re-solve the winner for its trajectory (counted, as the oracle)
-        if (q != QP_OK) res.status = HVP_MAXITER;
-        res.cost = c;
-    } else if (fail_lb < INF) {
-        res.status = HVP_MAXITER;
-    }
-    res.nodes = nodes;
+    if (node_limit) res.status = HVP_MAXITER;
+    else if (tie_over) res.status = HVP_OVERFLOW;
+    else res.status = fail_lb < INF ? HVP_MAXITER : HVP_INFEASIBLE;
+    res.nodes = node_limit ? nodes : searched;
     res.iters = iters;
 }
 

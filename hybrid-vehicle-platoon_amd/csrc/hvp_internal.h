@@ -1,0 +1,87 @@
+// hvp_internal.h -- definitions shared by the translation units of libhvpsolve.so
+// (hvp_kernels.hip: decentralised / ADMM paths and the common C ABI; hvp_cent.hip: the
+// centralised MLD path).  Not part of the public ABI (include/hvp.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "hvp.h"
+#include "hvp_ipm.h"
+
+namespace hvp {
+namespace cent {
+struct Child;  // hvp_cent_bnb.h (only the centralised unit needs its layout)
+}  // namespace cent
+}  // namespace hvp
+
+namespace hvp_detail {
+
+// sets the thread's last-error text (hvp_last_error) and returns code
+int fail(int code, const std::string& msg);
+
+#define HIP_TRY(expr)                                                                                     \
+    do {                                                                                                  \
+        hipError_t e_ = (expr);                                                                           \
+        if (e_ != hipSuccess) return hvp_detail::fail(HVP_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+struct Workspace {
+    int max_batch = 0;
+    int64_t cap = 0;
+    int32_t* inst_off = nullptr;   // [max_batch] first candidate slot (-1: overflow)
+    int32_t* inst_cnt = nullptr;   // [max_batch] candidates of the instance
+    int32_t* inst_flag = nullptr;  // [max_batch] 0 ok, 1 infeasible constant rows
+    unsigned long long* counter = nullptr;  // [8] reserved slots, qp iterations, fallback count, root QPs, failed bounds
+    int32_t* redo = nullptr;       // [cap] candidates the active-set method hands to the IPM
+    int32_t* task_inst = nullptr;  // [cap]
+    uint32_t* task_code = nullptr; // [cap]
+    double* task_cost = nullptr;   // [cap]
+    int32_t* task_stat = nullptr;  // [cap] status | iters << 8
+    double* task_y = nullptr;      // [cap * N]
+    // branch and bound (hvp_bnb.h): two node lists (parents / children of a level, ping-pong),
+    // per-instance incumbent and winner key
+    int32_t* nd_inst[2] = {nullptr, nullptr};    // [cap] owning instance (-1: dead)
+    uint64_t* nd_code[2] = {nullptr, nullptr};   // [cap] region prefix, 4 bits per step
+    double* nd_lo[2] = {nullptr, nullptr};       // [cap] reachable interval of v_depth
+    double* nd_hi[2] = {nullptr, nullptr};
+    double* nd_lb[2] = {nullptr, nullptr};       // [cap] bound (relaxed QP) or leaf cost
+    int32_t* leaf_stat = nullptr;                // [cap] 0 ok, else the QP failed
+    unsigned long long* inc = nullptr;           // [max_batch] incumbent cost (bits of a double >= 0)
+    unsigned long long* key = nullptr;           // [max_batch] lexicographic key of the winner
+    int32_t* nodes = nullptr;                    // [max_batch] QPs solved for the instance
+    int32_t* iters = nullptr;                    // [max_batch] active-set iterations
+    unsigned long long* lvl = nullptr;           // [HVP_MAX_N + 1] nodes per level
+    int32_t* inst_lvl = nullptr;                 // [max_batch] children of the instance at this level
+};
+
+
+}  // namespace hvp_detail
+
+struct hvp_handle {
+    int device = 0;
+    hvp_problem prob{};
+    hvp::Consts C{};
+    int n_systems = 0;
+    hvp_system* d_sys = nullptr;
+    hvp_detail::Workspace ws;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;  // around the whole solve
+    hipEvent_t evq0 = nullptr, evq1 = nullptr; // around K_qp (the dominant kernel)
+    hipEvent_t evb[2 * (HVP_MAX_N + 1)] = {};    // B&B: around K_bnb_root and every K_bnb_bound
+    hipStream_t last_stream = nullptr;
+    int last_B = 0;
+    bool bnb = false;       // search method resolved at hvp_create (HVP_METHOD_*)
+    bool last_bnb = false;
+    int n_cu = 256;
+    // host-pointer entry point staging (grown on demand)
+    size_t stage_bytes = 0;
+    char* d_stage = nullptr;
+    unsigned long long* g_counter = nullptr;  // [8] switching-ADMM / centralised counters (QP iterations at [1])
+    // centralised MLD (hvp_cent_solve_batch): per-platoon DFS child slices and tie-rule rows
+    int nreg_max = 1;
+    size_t cent_frames_bytes = 0, cent_ties_bytes = 0;
+    hvp::cent::Child* cent_frames = nullptr;
+    uint64_t* cent_ties = nullptr;
+    hvp::Consts* d_consts = nullptr;  // device copy of C (the centralised kernel reads it by pointer)
+};

@@ -28,27 +28,28 @@
 
 #define HVP_HD __host__ __device__
 #include "hvp.h"
+#include "hvp_internal.h"
 #include "hvp_admm.h"
 #include "hvp_bnb.h"
-#include "hvp_cent_bnb.h"
 #include "hvp_coop.h"
 #include "hvp_gi.h"
 #include "hvp_ipm.h"
 
-namespace {
-
+namespace hvp_detail {
 thread_local std::string g_err;
-
 int fail(int code, const std::string& msg) {
     g_err = msg;
     return code;
 }
+}  // namespace hvp_detail
 
-#define HIP_TRY(expr)                                                                                     \
-    do {                                                                                                  \
-        hipError_t e_ = (expr);                                                                           \
-        if (e_ != hipSuccess) return fail(HVP_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
-    } while (0)
+namespace {
+
+using hvp_detail::fail;
+using hvp_detail::Workspace;
+
+
+
 
 constexpr int kBlock = 256;
 // HVP_METHOD_AUTO: exhaustive enumeration up to this horizon, branch and bound beyond
@@ -57,62 +58,7 @@ constexpr int kAutoEnumMaxN = 0;  // measured: B&B beats enumeration already at 
 template <int N>
 constexpr int kGiMaxIter = 8 * hvp::GiConstraintSet<N>::NC;
 
-struct Workspace {
-    int max_batch = 0;
-    int64_t cap = 0;
-    int32_t* inst_off = nullptr;   // [max_batch] first candidate slot (-1: overflow)
-    int32_t* inst_cnt = nullptr;   // [max_batch] candidates of the instance
-    int32_t* inst_flag = nullptr;  // [max_batch] 0 ok, 1 infeasible constant rows
-    unsigned long long* counter = nullptr;  // [8] reserved slots, qp iterations, fallback count, root QPs, failed bounds
-    int32_t* redo = nullptr;       // [cap] candidates the active-set method hands to the IPM
-    int32_t* task_inst = nullptr;  // [cap]
-    uint32_t* task_code = nullptr; // [cap]
-    double* task_cost = nullptr;   // [cap]
-    int32_t* task_stat = nullptr;  // [cap] status | iters << 8
-    double* task_y = nullptr;      // [cap * N]
-    // branch and bound (hvp_bnb.h): two node lists (parents / children of a level, ping-pong),
-    // per-instance incumbent and winner key
-    int32_t* nd_inst[2] = {nullptr, nullptr};    // [cap] owning instance (-1: dead)
-    uint64_t* nd_code[2] = {nullptr, nullptr};   // [cap] region prefix, 4 bits per step
-    double* nd_lo[2] = {nullptr, nullptr};       // [cap] reachable interval of v_depth
-    double* nd_hi[2] = {nullptr, nullptr};
-    double* nd_lb[2] = {nullptr, nullptr};       // [cap] bound (relaxed QP) or leaf cost
-    int32_t* leaf_stat = nullptr;                // [cap] 0 ok, else the QP failed
-    unsigned long long* inc = nullptr;           // [max_batch] incumbent cost (bits of a double >= 0)
-    unsigned long long* key = nullptr;           // [max_batch] lexicographic key of the winner
-    int32_t* nodes = nullptr;                    // [max_batch] QPs solved for the instance
-    int32_t* iters = nullptr;                    // [max_batch] active-set iterations
-    unsigned long long* lvl = nullptr;           // [HVP_MAX_N + 1] nodes per level
-    int32_t* inst_lvl = nullptr;                 // [max_batch] children of the instance at this level
-};
-
 }  // namespace
-
-struct hvp_handle {
-    int device = 0;
-    hvp_problem prob{};
-    hvp::Consts C{};
-    int n_systems = 0;
-    hvp_system* d_sys = nullptr;
-    Workspace ws;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;  // around the whole solve
-    hipEvent_t evq0 = nullptr, evq1 = nullptr; // around K_qp (the dominant kernel)
-    hipEvent_t evb[2 * (HVP_MAX_N + 1)] = {};    // B&B: around K_bnb_root and every K_bnb_bound
-    hipStream_t last_stream = nullptr;
-    int last_B = 0;
-    bool bnb = false;       // search method resolved at hvp_create (HVP_METHOD_*)
-    bool last_bnb = false;
-    int n_cu = 256;
-    // host-pointer entry point staging (grown on demand)
-    size_t stage_bytes = 0;
-    char* d_stage = nullptr;
-    unsigned long long* g_counter = nullptr;  // [8] switching-ADMM / centralised counters (QP iterations at [1])
-    // centralised MLD (hvp_cent_solve_batch): per-platoon DFS child slices and tie-rule rows
-    int nreg_max = 1;
-    size_t cent_frames_bytes = 0, cent_ties_bytes = 0;
-    hvp::cent::Child* cent_frames = nullptr;
-    uint64_t* cent_ties = nullptr;
-};
 
 namespace {
 
@@ -1413,80 +1359,6 @@ bool valid_system(const hvp_system& s, std::string* why) {
 
 }  // namespace
 
-// ================================================================== centralised MLD (MpcMldCent)
-// One workgroup = one wavefront per platoon: the platoon's whole branch and bound
-// (hvp_cent_bnb.h) runs inside the wave, J / R of its QPs in dynamic LDS (2 V (V+1) doubles,
-// 41 KB at n = 10, N = 5: three platoons per CU).  Then the wave writes the winner: lane
-// t = i N + a stores u_{i,a}, x_{i,a+1}, region and gear.
-__global__ __launch_bounds__(64) void k_cent_bnb(int P, int n, int N, int leader, int lsp,
-                                                 const hvp_system* __restrict__ systems,
-                                                 const int32_t* __restrict__ sys, const double* __restrict__ x0,
-                                                 const double* __restrict__ xl, hvp::Consts C, int nreg_max,
-                                                 int max_nodes, int exhaustive, int max_iter,
-                                                 hvp::cent::Child* frames, uint64_t* ties, double* __restrict__ u_out,
-                                                 double* __restrict__ x_out, int8_t* __restrict__ region_out,
-                                                 int8_t* __restrict__ gear_out, double* __restrict__ cost_out,
-                                                 int32_t* __restrict__ status_out, int32_t* __restrict__ nodes_out,
-                                                 int32_t* __restrict__ iters_out,
-                                                 unsigned long long* __restrict__ counter) {
-    using namespace hvp::cent;
-    extern __shared__ double cent_lds[];
-    const int p = blockIdx.x;
-    if (p >= P) return;
-    const int t = lane();
-    const int V = n * N;
-    const Lds S = lds_carve(cent_lds, V);
-    Inst I;
-    I.n = n;
-    I.N = N;
-    I.V = V;
-    I.L = leader;
-    I.lsp = lsp != 0;
-    I.systems = systems;
-    I.vsys = sys + (size_t)p * n;
-    I.x0 = x0 + (size_t)p * 2 * n;
-    I.xl = xl + (size_t)p * 2 * (N + 1);
-    Lane L;
-    Search st;
-    Result res;
-    bnb_platoon(L, S, C, I, st, frames + (size_t)p * V * nreg_max, nreg_max, ties + (size_t)p * kTie * n, max_nodes,
-                exhaustive != 0, max_iter, res);
-    const bool win = res.status == HVP_OPTIMAL;
-    const int i = t < V ? t / N : 0, a = t < V ? t % N : 0;
-    const uint64_t ci = bc(st.vcode, i);
-    double u = 0.0;
-    if (win) direct_cost(L, C, I, ci, N, &u);  // wave-uniform branch
-    const double yv = win && t < V ? L.y : 0.0;
-    const double cum = vehicle_prefix(yv, N);
-    if (t < V) {
-        const hvp_system& Sv = systems[I.vsys[i]];
-        const size_t veh = (size_t)p * n + i;
-        const double p0 = I.x0[2 * i], v0 = I.x0[2 * i + 1];
-        if (x_out) {
-            double* xo = x_out + veh * 2 * (N + 1);
-            if (a == 0) {
-                xo[0] = p0;
-                xo[N + 1] = v0;
-            }
-            // no solution: the constant-velocity trajectory with u = 0 (as k_bnb_finish)
-            xo[a + 1] = win ? p0 + Sv.ts * v0 + Sv.ts * cum : p0 + Sv.ts * v0 * (a + 1);
-            xo[N + 1 + a + 1] = win ? yv : v0;
-        }
-        if (u_out) u_out[veh * N + a] = win ? u : 0.0;
-        const int r = hvp::code_region(ci, a);
-        if (region_out) region_out[veh * N + a] = (int8_t)(win ? r : -1);
-        if (gear_out) gear_out[veh * N + a] = (int8_t)(win ? Sv.gear[r] : 0);
-    }
-    if (t == 0) {
-        cost_out[p] = win ? res.cost : 1e300;
-        status_out[p] = res.status;
-        if (nodes_out) nodes_out[p] = res.nodes;
-        if (iters_out) iters_out[p] = res.iters;
-        atomicAdd(&counter[0], (unsigned long long)res.nodes);
-        atomicAdd(&counter[1], (unsigned long long)res.iters);
-    }
-}
-
 // ===================================================================== C ABI
 extern "C" {
 
@@ -1502,7 +1374,7 @@ int hvp_abi_sizes(int32_t* sizes) {
 
 int hvp_last_error(char* buf, size_t len) {
     if (!buf || len == 0) return HVP_E_ARG;
-    std::snprintf(buf, len, "%s", g_err.c_str());
+    std::snprintf(buf, len, "%s", hvp_detail::g_err.c_str());
     return 0;
 }
 
@@ -1809,69 +1681,6 @@ int hvp_gadmm_switch(hvp_handle* h, int P, int n, int lo, int m, const int32_t* 
     return 0;
 }
 
-int hvp_cent_solve_batch(hvp_handle* h, int P, int n, int leader_index, int real_vehicle_as_reference,
-                         const int32_t* sys, const double* x0, const double* leader_x, int max_nodes, double* u_out,
-                         double* x_out, int8_t* region_out, int8_t* gear_out, double* cost_out, int32_t* status_out,
-                         int32_t* nodes_out, int32_t* iters_out, void* stream) {
-    if (!h) return fail(HVP_E_ARG, "hvp_cent_solve_batch: null handle");
-    if (h->prob.formulation != HVP_FORM_CENT)
-        return fail(HVP_E_ARG, "hvp_cent_solve_batch: the handle is not an HVP_FORM_CENT problem");
-    const int N = h->prob.N;
-    if (P < 0 || n < 1 || n > hvp::cent::kMaxVeh || n * N > hvp::cent::kMaxV)
-        return fail(HVP_E_UNSUPPORTED, "hvp_cent_solve_batch: need 1 <= n <= " + std::to_string(hvp::cent::kMaxVeh) +
-                                           " and n * N <= " + std::to_string(hvp::cent::kMaxV));
-    if (leader_index < 0 || leader_index >= n) return fail(HVP_E_ARG, "hvp_cent_solve_batch: leader_index out of range");
-    if (real_vehicle_as_reference && leader_index != 0)
-        return fail(HVP_E_UNSUPPORTED, "hvp_cent_solve_batch: real_vehicle_as_reference needs leader_index 0 "
-                                       "(mpcs/cent_mld.py:63-66)");
-    if (P == 0) return 0;
-    if (!sys || !x0 || !leader_x || !u_out || !cost_out || !status_out)
-        return fail(HVP_E_ARG, "hvp_cent_solve_batch: bad argument");
-    HIP_TRY(hipSetDevice(h->device));
-    hipStream_t st = (hipStream_t)stream;
-    const int V = n * N;
-    const size_t fb = (size_t)P * V * h->nreg_max * sizeof(hvp::cent::Child);
-    const size_t tb = (size_t)P * hvp::cent::kTie * n * sizeof(uint64_t);
-    if (fb > h->cent_frames_bytes || tb > h->cent_ties_bytes) {
-        HIP_TRY(hipDeviceSynchronize());
-        if (fb > h->cent_frames_bytes) {
-            (void)hipFree(h->cent_frames);
-            h->cent_frames = nullptr;
-            h->cent_frames_bytes = 0;
-            if (hipMalloc(&h->cent_frames, fb) != hipSuccess)
-                return fail(HVP_E_NOMEM, "hvp_cent_solve_batch: device allocation failed");
-            h->cent_frames_bytes = fb;
-        }
-        if (tb > h->cent_ties_bytes) {
-            (void)hipFree(h->cent_ties);
-            h->cent_ties = nullptr;
-            h->cent_ties_bytes = 0;
-            if (hipMalloc(&h->cent_ties, tb) != hipSuccess)
-                return fail(HVP_E_NOMEM, "hvp_cent_solve_batch: device allocation failed");
-            h->cent_ties_bytes = tb;
-        }
-    }
-    const size_t lds = hvp::cent::lds_doubles(V) * sizeof(double);
-    HIP_TRY(hipFuncSetAttribute((const void*)k_cent_bnb, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    HIP_TRY(hipMemsetAsync(h->g_counter, 0, 8 * sizeof(unsigned long long), st));
-    const int exhaustive = h->prob.method == HVP_METHOD_ENUMERATE ? 1 : 0;
-    const int cap = max_nodes > 0 ? max_nodes : 200000;
-    const int max_iter = 8 * hvp::cent::ROWS * V;  // active-set iterations per QP
-    HIP_TRY(hipEventRecord(h->ev0, st));
-    HIP_TRY(hipEventRecord(h->evq0, st));
-    hipLaunchKernelGGL(k_cent_bnb, dim3(P), dim3(64), lds, st, P, n, N, leader_index, real_vehicle_as_reference ? 1 : 0,
-                       h->d_sys, sys, x0, leader_x, h->C, h->nreg_max, cap, exhaustive, max_iter, h->cent_frames,
-                       h->cent_ties, u_out, x_out, region_out, gear_out, cost_out, status_out, nodes_out, iters_out,
-                       h->g_counter);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(h->evq1, st));
-    HIP_TRY(hipEventRecord(h->ev1, st));
-    h->last_stream = st;
-    h->last_B = P;
-    h->last_bnb = false;
-    return 0;
-}
-
 int hvp_sync(hvp_handle* h, void* stream) {
     if (!h) return fail(HVP_E_ARG, "hvp_sync: null handle");
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
@@ -1984,6 +1793,7 @@ void hvp_destroy(hvp_handle* h) {
     if (h->g_counter) (void)hipFree(h->g_counter);
     if (h->cent_frames) (void)hipFree(h->cent_frames);
     if (h->cent_ties) (void)hipFree(h->cent_ties);
+    if (h->d_consts) (void)hipFree(h->d_consts);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
     if (h->evq0) (void)hipEventDestroy(h->evq0);

@@ -12,10 +12,10 @@ import os
 MAX_REGIONS = 16
 MAX_N = 16
 MAX_N_ENUM = 8
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 METHOD_AUTO, METHOD_ENUMERATE, METHOD_BNB = 0, 1, 2
-FORM_DECENT, FORM_ADMM, FORM_GADMM = 0, 1, 2
+FORM_DECENT, FORM_ADMM, FORM_GADMM, FORM_CENT = 0, 1, 2, 3
 
 ROLE_SAFE_FRONT = 1
 ROLE_SAFE_BACK = 2
@@ -122,6 +122,8 @@ EXPORTS = {
     "hvp_gadmm_solve": ([_P] + [ctypes.c_int] * 4 + [_P] * 14, ctypes.c_int),
     "hvp_gadmm_update": ([_P] + [ctypes.c_int] * 4 + [_P] * 5 + [ctypes.c_int, _P], ctypes.c_int),
     "hvp_gadmm_switch": ([_P] + [ctypes.c_int] * 4 + [_P] * 5, ctypes.c_int),
+    "hvp_cent_solve_batch": ([_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P, _P, _P, ctypes.c_int]
+                             + [_P] * 9, ctypes.c_int),
     "hvp_sync": ([_P, _P], ctypes.c_int),
     "hvp_get_stats": ([_P, ctypes.POINTER(HvpStats)], ctypes.c_int),
     "hvp_destroy": ([_P], None),
@@ -135,6 +137,18 @@ class HvpError(RuntimeError):
     pass
 
 
+def _init_torch_runtime() -> None:
+    """Let torch's HIP runtime claim the devices first.  The library links the system HIP
+    runtime; when it touches a device before torch does, torch's own runtime (the device-tensor
+    marshalling) finds no GPU.  Without torch or without a GPU this is a no-op."""
+    try:
+        import torch
+    except ImportError:  # pragma: no cover - torch is part of the image
+        return
+    if torch.cuda.is_available():
+        torch.cuda.init()
+
+
 def load():
     """Load libhvpsolve.so (built by ``make -C hybrid-vehicle-platoon_amd``); raises if absent."""
     global _lib
@@ -145,6 +159,7 @@ def load():
             f"{LIB_PATH} not found: build the HIP library first (python -c 'import __graft_entry__ as g; g.build()' "
             "or make -C hybrid-vehicle-platoon_amd). There is no CPU fallback."
         )
+    _init_torch_runtime()
     lib = ctypes.CDLL(LIB_PATH)
     for name, (argt, rest) in EXPORTS.items():
         fn = getattr(lib, name)

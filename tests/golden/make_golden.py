@@ -33,7 +33,13 @@ Files (numpy .npz, no pickles):
                       (fleet_g_admm.py, configs[3]): every local QP of oracle coordinator runs
                       (sampled), and two time steps of the restated coordinator (warm starts,
                       rollouts, rounds of ADMM + switching) for several platoons
-Run:  python tests/golden/make_golden.py [sweep | gear | admm | gadmm]
+  cent_*.npz          centralised MLD (mpcs/cent_mld.py MpcMldCent, fleet_cent_mld.py): one MIQP per
+                      platoon from the oracle's joint branch and bound (oracle_solve_cent, cross-checked
+                      against its exhaustive joint enumeration by tests/test_cent.py); n = 2..8 at N = 5,
+                      n = 3 at N = 10, n = 10 at N = 3, variants (real_vehicle_as_reference, leader
+                      index, task_2 masses / ConstantTime / stop-and-go, Q_du), mid-rollout states,
+                      the gear model (MpcGearCent, model = 1)
+Run:  python tests/golden/make_golden.py [sweep | gear | admm | gadmm | cent [n10]]
 """
 
 from __future__ import annotations
@@ -284,7 +290,87 @@ def gadmm_fixtures():
         print(f"gadmm_local_N{N}.npz: {len(T)} local QPs, {int((roles & 64).sum() // 64)} with a back copy")
 
 
+def _cent_case(job):
+    """One oracle solve of the centralised MIQP (worker of cent_fixtures)."""
+    masses, model, cfg, N, x0, lead, leader_index, lsp = job
+    systems = [O.gear_friction_mld_system(m) if model == 1 else O.gear_pwa_system(m) for m in masses]
+    r = O.solve_cent(systems, cfg, N, x0, lead, leader_index, lsp)
+    gear = np.array([systems[i]["gear"][r.sigma[i]] for i in range(len(masses))]) if r.status == 0 else None
+    return r, gear
+
+
+def cent_save(name, N, jobs, results, cfg, model=0):
+    n = len(jobs[0][0])
+    ok = [r.status == 0 for r, _ in results]
+    np.savez_compressed(
+        os.path.join(HERE, name), N=N, n=n, model=model, cfg=cfg.vector(),
+        masses=np.array([j[0] for j in jobs], float), x0=np.array([np.reshape(j[4], (n, 2)) for j in jobs]),
+        leader_x=np.array([j[5] for j in jobs]), leader_index=np.array([j[6] for j in jobs], np.int32),
+        lsp=np.array([int(j[7]) for j in jobs], np.int32),
+        exp_status=np.array([r.status for r, _ in results], np.int32),
+        exp_region=np.array([r.sigma if r.status == 0 else np.full((n, N), -1) for r, _ in results], np.int32),
+        exp_gear=np.array([g if g is not None else np.zeros((n, N), int) for _, g in results], np.int32),
+        exp_u=np.array([r.u for r, _ in results]), exp_x=np.array([r.x for r, _ in results]),
+        exp_cost=np.array([r.cost for r, _ in results]), exp_nodes=np.array([r.n_qps for r, _ in results], np.int32))
+    print(f"{name}: {len(jobs)} platoons, optimal {sum(ok)}, QPs {[r.n_qps for r, _ in results]}", flush=True)
+
+
+def cent_fixtures(big: bool = False):
+    """Centralised MLD (configs: fleet_cent_mld.py): see the module docstring."""
+    from multiprocessing import Pool
+
+    def seeds_jobs(n, N, seeds, cfg=None, masses=None, model=0, leader_index=0, lsp=False, lead=None):
+        jobs = []
+        for s in seeds:
+            m = masses(s) if callable(masses) else [800.0] * n
+            jobs.append((m, model, cfg or O.Cfg(), N, O.env_initial_state(n, s).astype(float),
+                         leader_window(N) if lead is None else lead, leader_index, lsp))
+        return jobs
+
+    def rollout_jobs(n, N, seeds, steps):
+        jobs = []
+        for s in seeds:
+            st = O.env_initial_state(n, s).astype(float)
+            for t in range(steps):
+                job = ([800.0] * n, 0, O.Cfg(), N, st.copy(), leader_window(N, t), 0, False)
+                jobs.append(job)
+                r, _ = _cent_case(job)
+                if r.status != 0:
+                    break
+                st = r.x[:, :, 1].reshape(-1)  # along the controller's own prediction
+        return jobs
+
+    rng_mass = lambda s: np.random.RandomState(s).uniform(700, 1000, 5).tolist()  # noqa: E731
+    if big:
+        sets = [("cent_n10_N5.npz", 5, seeds_jobs(10, 5, range(2)), O.Cfg(), 0)]
+    else:
+        sets = [
+            ("cent_n2_N5.npz", 5, seeds_jobs(2, 5, range(10)), O.Cfg(), 0),
+            ("cent_n4_N5.npz", 5, seeds_jobs(4, 5, range(6)), O.Cfg(), 0),
+            ("cent_n6_N5.npz", 5, seeds_jobs(6, 5, range(4)), O.Cfg(), 0),
+            ("cent_n8_N5.npz", 5, seeds_jobs(8, 5, range(1)), O.Cfg(), 0),
+            ("cent_n3_N10.npz", 10, seeds_jobs(3, 10, range(2)), O.Cfg(), 0),
+            ("cent_n10_N3.npz", 3, seeds_jobs(10, 3, range(4)), O.Cfg(), 0),
+            ("cent_lsp_n4_N5.npz", 5, seeds_jobs(4, 5, range(3), lsp=True), O.Cfg(), 0),
+            ("cent_lead2_n4_N5.npz", 5, seeds_jobs(4, 5, range(3), leader_index=2), O.Cfg(), 0),
+            ("cent_qdu_n4_N5.npz", 5, seeds_jobs(4, 5, range(3), cfg=O.Cfg(Qdu=0.5)), O.Cfg(Qdu=0.5), 0),
+            ("cent_task2_n5_N5.npz", 5, seeds_jobs(5, 5, range(3), cfg=O.Cfg(d0=10.0, t0=3.0), masses=rng_mass,
+                                                   lead=stop_and_go(5, 29)), O.Cfg(d0=10.0, t0=3.0), 0),
+            ("cent_rollout_n4_N5.npz", 5, rollout_jobs(4, 5, range(2), 4), O.Cfg(), 0),
+            ("cent_gear_n3_N4.npz", 4, seeds_jobs(3, 4, range(3), model=1), O.Cfg(), 1),
+        ]
+    only = set(os.environ.get("CENT_ONLY", "").split(",")) - {""}
+    sets = [x for x in sets if not only or x[0] in only]
+    with Pool(min(8, os.cpu_count() or 1)) as pool:
+        pending = [[pool.apply_async(_cent_case, (j,)) for j in jobs] for _, _, jobs, _, _ in sets]
+        for (name, N, jobs, cfg, model), futs in zip(sets, pending):  # each set saved as it completes
+            cent_save(name, N, jobs, [f.get() for f in futs], cfg, model)
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "cent":
+        cent_fixtures(big=len(sys.argv) > 2 and sys.argv[2] == "n10")
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "gadmm":
         gadmm_fixtures()
         return

