@@ -527,12 +527,18 @@ __device__ inline int solve(Lane& L, const Lds& Sg, const Consts& C, const Inst&
             }
             double k1key = 1e300;
             int k1 = t;
-            if (t < nact && r > 0.0) k1key = u / r;
+            // blocking multipliers: r_j above the rounding level of r (a noise-level r_j > 0 with a
+            // rounding-level u_j < 0 would give a huge NEGATIVE step), u clamped at 0
+            double rmax = t < nact ? fabs(r) : 0.0;
+#pragma unroll
+            for (int o = W / 2; o > 0; o >>= 1) rmax = fmax(rmax, __shfl_xor(rmax, o, W));
+            if (t < nact && r > 1e-13 * rmax) k1key = fmax(u, 0.0) / r;
             wargmin(k1key, k1);
             const double t1 = k1key;
             double k3key = 1e300;
             int k3 = t;
-            if (t < nact && (id & (REV - 1)) % ROWS == 8 && id >= 0 && r < 0.0) k3key = (wgt - u) / (-r);
+            if (t < nact && id >= 0 && (id & (REV - 1)) % ROWS == 8 && r < -1e-13 * rmax)
+                k3key = fmax(wgt - u, 0.0) / (-r);
             wargmin(k3key, k3);
             double t3 = k3key;
             bool new_sat = false;
@@ -540,7 +546,7 @@ __device__ inline int solve(Lane& L, const Lds& Sg, const Consts& C, const Inst&
                 t3 = wgt - unew;
                 new_sat = true;
             }
-            const bool zstep = d2n > 1e-14 * dn;
+            const bool zstep = d2n > 1e-12 * dn;  // relative: V = 64 rows of rounding in d2n
             const double zn = d2n;
             const double sp_now = dp + wsum(np_t * (t < V ? L.y : 0.0));
             const double t2 = zstep && zn > 0.0 ? fmax(-sp_now, 0.0) / zn : 1e300;
@@ -549,9 +555,14 @@ __device__ inline int solve(Lane& L, const Lds& Sg, const Consts& C, const Inst&
                 if (I.debug && t == 0)
                     printf("[cent] GI_FAIL_DUAL iter %d nact %d row %d (owner %d rr %d rev %d) d2n %.3e dn %.3e "
                            "sp %.6e\n", iter, nact, pr, owner, rr, (int)rev, d2n, dn, sp_now);
+                if (I.debug && t < nact) printf("[cent]   act %d: id %d u %.6e r %.6e dv %.6e\n", t, id, u, r, dv);
+                if (I.debug && t < V) printf("[cent]   y %d = %.6e np %.3e\n", t, L.y, np_t);
                 iters = iter;
                 return GI_FAIL_DUAL;
             }
+            if (I.debug > 1 && t == 0)
+                printf("[cent] it %d row %d nact %d t1 %.4e(k%d) t2 %.4e t3 %.4e d2n/dn %.3e sp %.4e\n", iter, pr, nact,
+                       t1, k1, t2, t3, dn > 0 ? d2n / dn : 0.0, sp_now);
             if (t2 < 1e299 && t < V) L.y += tstep * z;
             if (t < nact) u -= tstep * r;
             unew += tstep;

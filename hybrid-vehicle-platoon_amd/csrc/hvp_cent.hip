@@ -147,7 +147,7 @@ int hvp_cent_solve_batch(hvp_handle* h, int P, int n, int leader_index, int real
     HIP_TRY(hipMemsetAsync(h->g_counter, 0, 8 * sizeof(unsigned long long), st));
     const int exhaustive = h->prob.method == HVP_METHOD_ENUMERATE ? 1 : 0;
     const char* dbg = std::getenv("HVP_CENT_DEBUG");  // diagnostics: printf of failing QPs
-    const int debug = dbg && dbg[0] && dbg[0] != '0' ? 1 : 0;
+    const int debug = dbg && dbg[0] ? std::atoi(dbg) : 0;  // 1: failures, 2: + every GI step
     const int cap = max_nodes > 0 ? max_nodes : 200000;
     const int max_iter = 8 * hvp::cent::ROWS * V;  // active-set iterations per QP
     HIP_TRY(hipEventRecord(h->ev0, st));

@@ -8,7 +8,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "hybrid-vehicle-platoon_amd"), os.path.join(ROOT, "oracle"),
                 os.path.join(ROOT, "tests")]
-os.environ["HVP_CENT_DEBUG"] = "1"
+os.environ.setdefault("HVP_CENT_DEBUG", "1")
 import oracle as O  # noqa: E402
 from instances import leader_window  # noqa: E402
 from hvp import tables  # noqa: E402
