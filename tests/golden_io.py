@@ -11,9 +11,9 @@ GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
 def fixture_names() -> list[str]:
-    """The decentralised local-MIQP fixtures (the ADMM ones have their own layout: admm_*)."""
+    """The decentralised local-MIQP fixtures (the ADMM and centralised ones have their own layouts)."""
     return sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLDEN, "*.npz"))
-                  if not os.path.basename(p).startswith(("admm_", "gadmm_")))
+                  if not os.path.basename(p).startswith(("admm_", "gadmm_", "cent_")))
 
 
 def load(name: str) -> dict:
