@@ -139,7 +139,7 @@ class CentSolver:
             raise ValueError("system index out of range")
         x0 = np.asarray(x0, dtype=np.float64).reshape(P, n, 2)
         lx = np.asarray(leader_x, dtype=np.float64)
-        lx = np.broadcast_to(lx.reshape(-1, 2, self.N + 1), (P, 2, self.N + 1))
+        lx = np.array(np.broadcast_to(lx.reshape(-1, 2, self.N + 1), (P, 2, self.N + 1)))
         dev = torch.device("cuda", self.device)
         t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
         out = self.solve_device(t(sys_idx), t(x0), t(lx), leader_index, real_vehicle_as_reference, max_nodes)

@@ -1633,8 +1633,13 @@ static void cent_leaf(or_cent* C, const int* sigma, const int* K) {
     C->have_best = 1;
 }
 
+/* QP budget of one oracle_solve_cent (0 = none): bench.py's bounded CPU sample of the search */
+static long g_cent_cap = 0;
+void oracle_set_cent_cap(long cap) { g_cent_cap = cap; }
+
 static void cent_dfs(or_cent* C, int d, int* sigma, int* K, double* lo, double* hi) {
     const int n = C->n, N = C->N;
+    if (g_cent_cap > 0 && C->n_qp >= g_cent_cap) return;
     if (d == n * N) { cent_leaf(C, sigma, K); return; }
     const int k = d / n, i = d % n;
     const or_vmodel* vm = &C->vm[i];

@@ -248,6 +248,8 @@ def lib():
         L.oracle_solve_cent.argtypes = [c_int, c_int, c_int, c_int, dp, dp, dp, dp, dp, dp, c_int, dp, dp, c_int, dp,
                                         dp, dp, c_int, dp, dp, dp, dp, ip, dp]
         L.oracle_solve_cent.restype = c_int
+        L.oracle_set_cent_cap.argtypes = [ctypes.c_long]
+        L.oracle_set_cent_cap.restype = None
         L.oracle_set_method.argtypes = [c_int]
         L.oracle_set_method.restype = None
         _lib = L
@@ -745,6 +747,11 @@ class CentResult:
     cost: float
     status: int        # 0 optimal, 1 infeasible
     n_qps: int
+
+
+def set_cent_cap(cap: int) -> None:
+    """QP budget per solve_cent call (0 = none; a capped search is a timing sample, not a result)."""
+    lib().oracle_set_cent_cap(int(cap))
 
 
 def solve_cent(systems: list[dict], cfg: Cfg, N: int, x0, leader_x, leader_index: int = 0,
