@@ -89,6 +89,31 @@ __device__ inline void wargmin(double& key, int& who) {
     }
 }
 
+// HVP_CENT_DEBUG >= 3: shader-clock cycles per phase of the wave QP, summed over the launch
+// (0 setup, 1 Cholesky, 2 minimiser + J, 3 most-violated search, 4 dv / z, 5 r back-substitution,
+// 6 step lengths, 7 add, 8 drop, 9 direct cost, 10 QPs, 11 iterations)
+__device__ unsigned long long g_cent_prof[16];
+struct Prof {
+    bool on;
+    long long last;
+    unsigned long long acc[12];
+    __device__ void start(bool enable) {
+        on = enable;
+        for (int k = 0; k < 12; ++k) acc[k] = 0;
+        last = on ? clock64() : 0;
+    }
+    __device__ void mark(int k) {
+        if (!on) return;
+        const long long now = clock64();
+        acc[k] += (unsigned long long)(now - last);
+        last = now;
+    }
+    __device__ void flush() {
+        if (!on || (threadIdx.x & 63) != 0) return;
+        for (int k = 0; k < 12; ++k) atomicAdd(&g_cent_prof[k], acc[k]);
+    }
+};
+
 // One platoon instance: n vehicles, horizon N, leader index / spacing flag, per-vehicle systems.
 struct Inst {
     int n, N, V, L;
@@ -362,7 +387,8 @@ __device__ inline void most_violated(const Lane& L, const Consts& C, double y, d
 }
 
 // Cooperative Goldfarb-Idnani over the wave (the algorithm of hvp_coop.h::solve).
-__device__ inline int solve(Lane& L, const Lds& Sg, const Consts& C, const Inst& I, int max_iter, int& iters) {
+__device__ inline int solve(Lane& L, const Lds& Sg, const Consts& C, const Inst& I, int max_iter, int& iters,
+                            Prof& pf) {
     const int t = lane();
     const int N = I.N, V = I.V, LD = Sg.LD;
     iters = 0;
@@ -386,6 +412,7 @@ __device__ inline int solve(Lane& L, const Lds& Sg, const Consts& C, const Inst&
         }
         wsync();
     }
+    pf.mark(1);
     // ---- unconstrained minimiser
     {
         double acc = -L.f, w = 0.0;
@@ -427,6 +454,7 @@ __device__ inline int solve(Lane& L, const Lds& Sg, const Consts& C, const Inst&
     const double tol = 1e-11;
     int iter = 0;
     for (;;) {
+        pf.mark(2);
         // ---------------- most violated row
         const double yv = t < V ? L.y : 0.0;
         double yprev = __shfl_up(yv, 1, W);
@@ -501,6 +529,7 @@ __device__ inline int solve(Lane& L, const Lds& Sg, const Consts& C, const Inst&
         double unew = 0.0;
         for (;;) {
             if (++iter > max_iter) { iters = iter; return GI_FAIL_ITER; }
+            pf.mark(3);
             // ---- dv_c = sum_i J[i][c] np_i over the row's support
             double dv = 0.0;
             if (t < V) {
@@ -514,6 +543,7 @@ __device__ inline int solve(Lane& L, const Lds& Sg, const Consts& C, const Inst&
             double z = 0.0;
             if (t < V)
                 for (int c = nact; c < V; ++c) z += J[t * LD + c] * Sg.v[c];
+            pf.mark(4);
             double r = 0.0;
             {
                 double accr = t < nact ? dv : 0.0;
@@ -527,6 +557,7 @@ __device__ inline int solve(Lane& L, const Lds& Sg, const Consts& C, const Inst&
             }
             double k1key = 1e300;
             int k1 = t;
+            pf.mark(5);
             // blocking multipliers: r_j above the rounding level of r (a noise-level r_j > 0 with a
             // rounding-level u_j < 0 would give a huge NEGATIVE step), u clamped at 0
             double rmax = t < nact ? fabs(r) : 0.0;
@@ -567,32 +598,43 @@ __device__ inline int solve(Lane& L, const Lds& Sg, const Consts& C, const Inst&
             if (t < nact) u -= tstep * r;
             unew += tstep;
             if (t2 <= t1 && t2 <= t3) {
-                double carry = V - 1 > nact ? Sg.v[V - 1] : 0.0;
-                for (int i = V - 1; i > nact; --i) {
-                    const double lo = Sg.v[i - 1];
-                    double gc, gs;
-                    givens(lo, carry, gc, gs);
-                    carry = gc * lo + gs * carry;
+                pf.mark(6);
+                pf.acc[11] += 1;
+                // ---- add p: one Householder reflection H of J's trailing columns maps
+                // d2 = dv[nact..V) onto alpha e_nact (J <- J diag(I, H), R gets the column
+                // (dv[0..nact), alpha)).  Every lane updates its own row of J: no serial
+                // rotation chain (the lane solver's Givens sweep is V - nact dependent steps).
+                const double x0 = Sg.v[nact];
+                double alpha = x0;
+                if (V - 1 > nact) {
+                    alpha = x0 >= 0.0 ? -sqrt(d2n) : sqrt(d2n);
+                    const double beta = 1.0 / (d2n - x0 * alpha);  // 2 / v'v, v = d2 - alpha e_0
                     if (t < V) {
-                        const double a0 = J[t * LD + i - 1], a1 = J[t * LD + i];
-                        J[t * LD + i - 1] = gc * a0 + gs * a1;
-                        J[t * LD + i] = -gs * a0 + gc * a1;
+                        double w = J[t * LD + nact] * (x0 - alpha);
+                        for (int c = nact + 1; c < V; ++c) w += J[t * LD + c] * Sg.v[c];
+                        const double bw = beta * w;
+                        J[t * LD + nact] -= bw * (x0 - alpha);
+                        for (int c = nact + 1; c < V; ++c) J[t * LD + c] -= bw * Sg.v[c];
                     }
                 }
                 if (t < nact) R[t * LD + nact] = dv;
-                if (t == nact) R[t * LD + nact] = V - 1 > nact ? carry : dv;
+                if (t == nact) R[t * LD + nact] = alpha;
                 if (t == nact) { u = unew; id = pr; }
                 if (t == owner) act |= 1u << rr;
                 ++nact;
                 wsync();
+                pf.mark(7);
                 break;
             }
+            pf.mark(6);
+            pf.acc[11] += 1;
             int drop;
             const bool by_sat = t3 <= t1;
             if (by_sat) {
                 if (new_sat) {
                     if (t == owner) sat ^= 1u;
                     wsync();
+                    pf.mark(8);
                     break;
                 }
                 drop = k3;
@@ -633,6 +675,7 @@ __device__ inline int solve(Lane& L, const Lds& Sg, const Consts& C, const Inst&
                 wsync();
             }
             --nact;
+            pf.mark(8);
         }
     }
     iters = iter;

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -157,6 +158,21 @@ int hvp_cent_solve_batch(hvp_handle* h, int P, int n, int leader_index, int real
                        h->cent_ties, u_out, x_out, region_out, gear_out, cost_out, status_out, nodes_out, iters_out,
                        h->g_counter);
     HIP_TRY(hipGetLastError());
+    if (debug >= 3) {  // phase profile of the wave QP (hvp_cent.h Prof), summed over all platoons
+        unsigned long long prof[16];
+        HIP_TRY(hipStreamSynchronize(st));
+        HIP_TRY(hipMemcpyFromSymbol(prof, HIP_SYMBOL(hvp::cent::g_cent_prof), sizeof(prof)));
+        const char* names[12] = {"setup", "cholesky", "minimiser+J", "most-violated", "dv+z", "r-backsolve",
+                                 "steps", "add", "drop", "direct-cost", "QPs", "GI-steps"};
+        unsigned long long tot = 0;
+        for (int k = 0; k < 10; ++k) tot += prof[k];
+        std::printf("[cent-prof] cycles %llu, QPs %llu, GI steps %llu\n", tot, prof[10], prof[11]);
+        for (int k = 0; k < 10; ++k)
+            std::printf("[cent-prof]   %-14s %6.2f%%  %8.0f cycles/QP\n", names[k], 100.0 * prof[k] / (tot ? tot : 1),
+                        (double)prof[k] / (prof[10] ? prof[10] : 1));
+        const unsigned long long zero[16] = {};
+        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(hvp::cent::g_cent_prof), zero, sizeof(zero)));
+    }
     HIP_TRY(hipEventRecord(h->evq1, st));
     HIP_TRY(hipEventRecord(h->ev1, st));
     h->last_stream = st;

@@ -57,7 +57,7 @@ __device__ inline int fixed_steps(int d, int n, int i) { return d / n + (i < d %
 
 // Platoon QP with the first `d` decisions fixed.  QP_OK with the cost and the lanes' y.
 __device__ inline int platoon_qp(Lane& L, const Lds& S, const Consts& C, const Inst& I, uint64_t vcode, int d,
-                                 int max_iter, double& cost, int& iters) {
+                                 int max_iter, double& cost, int& iters, Prof& pf) {
     const int t = lane();
     const int i = t < I.V ? t / I.N : 0;
     const uint64_t ci = bc(vcode, i);
@@ -65,12 +65,16 @@ __device__ inline int platoon_qp(Lane& L, const Lds& S, const Consts& C, const I
     int it = 0;
     iters = 0;
     wsync();
+    pf.mark(10);
+    pf.acc[10] += 1;
     if (!setup(L, S, C, I, ci, Ki)) return QP_INFEASIBLE;
-    const int r = solve(L, S, C, I, max_iter, it);
+    pf.mark(0);
+    const int r = solve(L, S, C, I, max_iter, it, pf);
     iters = it;
     if (r == GI_FAIL_DUAL) return QP_INFEASIBLE;
     if (r != GI_OK) return QP_FAILED;
     cost = direct_cost(L, C, I, ci, Ki);
+    pf.mark(9);
     return QP_OK;
 }
 
@@ -122,6 +126,8 @@ __device__ inline void bnb_platoon(Lane& L, const Lds& S, const Consts& C, const
     bool have_best = false, node_limit = false, tie_over = false;
     double fail_lb = INF;  // smallest bound of a leaf whose QP failed (not infeasible)
     int nodes = 0, iters = 0, searched = 0;
+    Prof pf;
+    pf.start(I.debug >= 3);
 
     // expansion of the node with d decisions taken: lane r holds child r's interval and bound
     enum { EXPAND = 0, VISIT = 1, FINAL = 2 };
@@ -273,7 +279,7 @@ __device__ inline void bnb_platoon(Lane& L, const Lds& S, const Consts& C, const
         double c = 0.0;
         int it = 0;
         ++nodes;
-        const int q = platoon_qp(L, S, C, I, st.vcode, dfix, max_iter, c, it);
+        const int q = platoon_qp(L, S, C, I, st.vcode, dfix, max_iter, c, it, pf);
         iters += it;
         if (I.debug && q != QP_OK) {
             const uint64_t c0 = bc(st.vcode, 0), c1 = bc(st.vcode, 1 < n ? 1 : 0), c2 = bc(st.vcode, 2 < n ? 2 : 0);
@@ -301,6 +307,7 @@ __device__ inline void bnb_platoon(Lane& L, const Lds& S, const Consts& C, const
             res.cost = c;
             res.nodes = searched;
             res.iters = iters;
+            pf.flush();
             return;
         }
     }
@@ -310,6 +317,7 @@ __device__ inline void bnb_platoon(Lane& L, const Lds& S, const Consts& C, const
     else res.status = fail_lb < INF ? HVP_MAXITER : HVP_INFEASIBLE;
     res.nodes = node_limit ? nodes : searched;
     res.iters = iters;
+    pf.flush();
 }
 
 }  // namespace cent

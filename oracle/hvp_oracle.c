@@ -1633,6 +1633,16 @@ static void cent_leaf(or_cent* C, const int* sigma, const int* K) {
     C->have_best = 1;
 }
 
+/* Pruning of the centralised search: gap = 0 is exact (bound above the incumbent by more than
+ * 1e-7 (1 + |inc|), 100x the tie window); gap > 0 is Gurobi's relative MIPGap rule (the node
+ * cannot improve the incumbent by more than gap |inc|; Gurobi's default is 1e-4). */
+static double g_cent_gap = 0.0;
+void oracle_set_cent_gap(double gap) { g_cent_gap = gap; }
+static int cent_pruned(double lb, double inc) {
+    if (g_cent_gap > 0.0) return lb >= inc - g_cent_gap * fabs(inc);
+    return lb > inc + 1e-7 * (1.0 + fabs(inc));
+}
+
 /* QP budget of one oracle_solve_cent (0 = none): bench.py's bounded CPU sample of the search */
 static long g_cent_cap = 0;
 void oracle_set_cent_cap(long cap) { g_cent_cap = cap; }
@@ -1674,7 +1684,7 @@ static void cent_dfs(or_cent* C, int d, int* sigma, int* K, double* lo, double* 
         double t2 = chi[a]; chi[a] = chi[m]; chi[m] = t2;
     }
     for (int a = 0; a < nch; ++a) {
-        if (C->have_best && lb[a] > C->inc + 1e-7 * (1.0 + fabs(C->inc))) continue;
+        if (C->have_best && cent_pruned(lb[a], C->inc)) continue;
         if (!(lb[a] < INFINITY)) continue;
         const double slo = lo[i], shi = hi[i];
         sigma[i * N + k] = child[a];

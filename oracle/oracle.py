@@ -248,6 +248,8 @@ def lib():
         L.oracle_solve_cent.argtypes = [c_int, c_int, c_int, c_int, dp, dp, dp, dp, dp, dp, c_int, dp, dp, c_int, dp,
                                         dp, dp, c_int, dp, dp, dp, dp, ip, dp]
         L.oracle_solve_cent.restype = c_int
+        L.oracle_set_cent_gap.argtypes = [ctypes.c_double]
+        L.oracle_set_cent_gap.restype = None
         L.oracle_set_cent_cap.argtypes = [ctypes.c_long]
         L.oracle_set_cent_cap.restype = None
         L.oracle_set_method.argtypes = [c_int]
@@ -747,6 +749,11 @@ class CentResult:
     cost: float
     status: int        # 0 optimal, 1 infeasible
     n_qps: int
+
+
+def set_cent_gap(gap: float) -> None:
+    """Relative MIP gap of solve_cent's pruning (0 = exact; Gurobi's default MIPGap is 1e-4)."""
+    lib().oracle_set_cent_gap(float(gap))
 
 
 def set_cent_cap(cap: int) -> None:
