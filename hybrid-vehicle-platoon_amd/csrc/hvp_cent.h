@@ -59,40 +59,113 @@ __device__ inline void wsync() {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 }
-__device__ inline double wsum(double x) {
-#pragma unroll
-    for (int d = W / 2; d > 0; d >>= 1) x += __shfl_xor(x, d, W);
-    return x;
-}
-__device__ inline int wor(int x) {
-#pragma unroll
-    for (int d = W / 2; d > 0; d >>= 1) x |= __shfl_xor(x, d, W);
-    return x;
-}
+
+// ---- cross-lane primitives.  A generic __shfl is a ds_bpermute round trip through the LDS
+// crossbar (~100+ cycles); the solver's chains of broadcasts and reductions use instead
+//   * v_readlane (SGPR result) for a broadcast from a wave-uniform source lane (bcu), and
+//   * DPP (quad_perm, row mirrors, row_shr) inside 16-lane rows plus readlanes across rows.
+// bc() (ds_bpermute) remains for lane-varying sources.
 template <class T>
 __device__ inline T bc(T x, int src) { return __shfl(x, src, W); }
+__device__ inline int bcu(int x, int src) { return __builtin_amdgcn_readlane(x, src); }
+__device__ inline double bcu(double x, int src) {
+    const long long b = __double_as_longlong(x);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)b, src);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(b >> 32), src);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+__device__ inline uint64_t bcu(uint64_t x, int src) {
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)x, src);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(x >> 32), src);
+    return ((uint64_t)hi << 32) | lo;
+}
+constexpr int kDppXor1 = 0xB1;        // quad_perm [1,0,3,2]
+constexpr int kDppXor2 = 0x4E;        // quad_perm [2,3,0,1]
+constexpr int kDppHalfMirror = 0x141; // row_half_mirror
+constexpr int kDppMirror = 0x140;     // row_mirror
+template <int CTRL>
+__device__ inline int dppi(int x) { return __builtin_amdgcn_mov_dpp(x, CTRL, 0xf, 0xf, false); }
+template <int CTRL>
+__device__ inline double dppd(double x) {
+    const long long b = __double_as_longlong(x);
+    const unsigned lo = (unsigned)__builtin_amdgcn_mov_dpp((int)b, CTRL, 0xf, 0xf, false);
+    const unsigned hi = (unsigned)__builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xf, 0xf, false);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+// row_shr:k with zero fill of the lanes without a source
+template <int K>
+__device__ inline double dpp_shr0(double x) {
+    const long long b = __double_as_longlong(x);
+    const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)b, 0x110 + K, 0xf, 0xf, true);
+    const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x110 + K, 0xf, 0xf, true);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+// sum over the wave, identical in every lane
+__device__ inline double wsum(double x) {
+    x += dppd<kDppXor1>(x);
+    x += dppd<kDppXor2>(x);
+    x += dppd<kDppHalfMirror>(x);
+    x += dppd<kDppMirror>(x);
+    return (bcu(x, 0) + bcu(x, 16)) + (bcu(x, 32) + bcu(x, 48));
+}
+__device__ inline int wor(int x) { return __ballot(x != 0) != 0ull ? 1 : 0; }
+__device__ inline double wmax(double x) {
+    x = fmax(x, dppd<kDppXor1>(x));
+    x = fmax(x, dppd<kDppXor2>(x));
+    x = fmax(x, dppd<kDppHalfMirror>(x));
+    x = fmax(x, dppd<kDppMirror>(x));
+    return fmax(fmax(bcu(x, 0), bcu(x, 16)), fmax(bcu(x, 32), bcu(x, 48)));
+}
+// inclusive prefix sum over the wave (row-local Hillis-Steele, then the row carries)
 __device__ inline double wscan(double x) {
     const int t = lane();
-#pragma unroll
-    for (int d = 1; d < W; d <<= 1) {
-        const double o = __shfl_up(x, d, W);
-        if (t >= d) x += o;
-    }
-    return x;
+    x += dpp_shr0<1>(x);
+    x += dpp_shr0<2>(x);
+    x += dpp_shr0<4>(x);
+    x += dpp_shr0<8>(x);
+    const double r0 = bcu(x, 15), r1 = bcu(x, 31), r2 = bcu(x, 47);
+    const int row = t >> 4;
+    return x + (row == 0 ? 0.0 : (row == 1 ? r0 : (row == 2 ? r0 + r1 : (r0 + r1) + r2)));
 }
+// x of lane t - 1 (lane 0: 0)
+__device__ inline double shift_up1(double x) {
+    const int t = lane();
+    const double y = dpp_shr0<1>(x);
+    const double c15 = bcu(x, 15), c31 = bcu(x, 31), c47 = bcu(x, 47);
+    return t == 16 ? c15 : (t == 32 ? c31 : (t == 48 ? c47 : y));
+}
+// (key, who) minimum with ties to the lower index, identical in every lane
 __device__ inline void wargmin(double& key, int& who) {
+    auto step = [&](double ok, int ow) {
+        if (ok < key || (ok == key && ow < who)) {
+            key = ok;
+            who = ow;
+        }
+    };
+    step(dppd<kDppXor1>(key), dppi<kDppXor1>(who));
+    step(dppd<kDppXor2>(key), dppi<kDppXor2>(who));
+    step(dppd<kDppHalfMirror>(key), dppi<kDppHalfMirror>(who));
+    step(dppd<kDppMirror>(key), dppi<kDppMirror>(who));
+    double bk = bcu(key, 0);
+    int bw = bcu(who, 0);
 #pragma unroll
-    for (int d = W / 2; d > 0; d >>= 1) {
-        const double ok = __shfl_xor(key, d, W);
-        const int ow = __shfl_xor(who, d, W);
-        if (ok < key || (ok == key && ow < who)) { key = ok; who = ow; }
+    for (int r = 16; r < W; r += 16) {
+        const double k2 = bcu(key, r);
+        const int w2 = bcu(who, r);
+        if (k2 < bk || (k2 == bk && w2 < bw)) {
+            bk = k2;
+            bw = w2;
+        }
     }
+    key = bk;
+    who = bw;
 }
 
 // HVP_CENT_DEBUG >= 3: shader-clock cycles per phase of the wave QP, summed over the launch
 // (0 setup, 1 Cholesky, 2 minimiser + J, 3 most-violated search, 4 dv / z, 5 r back-substitution,
 // 6 step lengths, 7 add, 8 drop, 9 direct cost, 10 QPs, 11 iterations)
 __device__ unsigned long long g_cent_prof[16];
+#ifdef HVP_CENT_PROF
 struct Prof {
     bool on;
     long long last;
@@ -108,11 +181,22 @@ struct Prof {
         acc[k] += (unsigned long long)(now - last);
         last = now;
     }
+    __device__ void count(int k) {
+        if (on) acc[k] += 1;
+    }
     __device__ void flush() {
         if (!on || (threadIdx.x & 63) != 0) return;
         for (int k = 0; k < 12; ++k) atomicAdd(&g_cent_prof[k], acc[k]);
     }
 };
+#else  // profiling compiled out (make PROF=1 builds it in)
+struct Prof {
+    __device__ void start(bool) {}
+    __device__ void mark(int) {}
+    __device__ void count(int) {}
+    __device__ void flush() {}
+};
+#endif
 
 // One platoon instance: n vehicles, horizon N, leader index / spacing flag, per-vehicle systems.
 struct Inst {
@@ -405,30 +489,29 @@ __device__ inline int solve(Lane& L, const Lds& Sg, const Consts& C, const Inst&
         wsync();
         const double d = R[j * LD + j];
         if (!(d > 0.0)) return GI_FAIL_CHOL;
+        const double dinv = 1.0 / d;
         if (t > j && t < V) {
             double v = J[t * LD + j];
             for (int k = 0; k < j; ++k) v -= R[t * LD + k] * R[j * LD + k];
-            R[t * LD + j] = v / d;
+            R[t * LD + j] = v * dinv;
         }
         wsync();
     }
     pf.mark(1);
-    // ---- unconstrained minimiser
+    // ---- unconstrained minimiser (lane t holds 1 / L_tt: the substitution chains are a multiply
+    // and a readlane per step)
+    const double ldinv = t < V ? 1.0 / R[t * LD + t] : 0.0;
     {
         double acc = -L.f, w = 0.0;
         for (int i = 0; i < V; ++i) {
-            double wi = 0.0;
-            if (t == i) wi = acc / R[i * LD + i];
-            wi = bc(wi, i);
+            const double wi = bcu(acc * ldinv, i);
             if (t == i) w = wi;
             if (t > i && t < V) acc -= R[t * LD + i] * wi;
         }
         double acc2 = w;
         L.y = 0.0;
         for (int i = V - 1; i >= 0; --i) {
-            double yi = 0.0;
-            if (t == i) yi = acc2 / R[i * LD + i];
-            yi = bc(yi, i);
+            const double yi = bcu(acc2 * ldinv, i);
             if (t == i) L.y = yi;
             if (t < i) acc2 -= R[i * LD + t] * yi;
         }
@@ -439,7 +522,7 @@ __device__ inline int solve(Lane& L, const Lds& Sg, const Consts& C, const Inst&
         for (int i = 0; i < V; ++i) {
             double v = i == t ? 1.0 : 0.0;
             for (int k = 0; k < i; ++k) v -= R[i * LD + k] * J[t * LD + k];
-            J[t * LD + i] = v / R[i * LD + i];
+            J[t * LD + i] = v * bcu(ldinv, i);
         }
     }
     wsync();
@@ -447,6 +530,7 @@ __device__ inline int solve(Lane& L, const Lds& Sg, const Consts& C, const Inst&
         for (int c = 0; c < V; ++c) R[t * LD + c] = 0.0;
     wsync();
     double u = 0.0;
+    double rinv = 0.0;  // 1 / R[t][t] of active position t (the back substitution's divisions)
     int id = -1;
     int nact = 0;
     unsigned act = 0, sat = 0;
@@ -457,7 +541,7 @@ __device__ inline int solve(Lane& L, const Lds& Sg, const Consts& C, const Inst&
         pf.mark(2);
         // ---------------- most violated row
         const double yv = t < V ? L.y : 0.0;
-        double yprev = __shfl_up(yv, 1, W);
+        double yprev = shift_up1(yv);
         if (L.a == 0) yprev = L.v0;
         const double cum = vehicle_prefix(yv, N);
         const double p = L.P1 + L.ts * cum;  // p_{i,a+1}
@@ -469,7 +553,7 @@ __device__ inline int solve(Lane& L, const Lds& Sg, const Consts& C, const Inst&
         int who = t;
         wargmin(key, who);
         if (!(key < 0.0)) break;
-        const int pr = bc(bid, who);
+        const int pr = bcu(bid, who);
         const int base = pr & (REV - 1);
         const bool rev = (pr & REV) != 0;
         const int owner = base / ROWS, rr = base % ROWS;
@@ -483,7 +567,7 @@ __device__ inline int solve(Lane& L, const Lds& Sg, const Consts& C, const Inst&
             if (rr < 6) {
                 const int pair = rr / 2;
                 const double sgn = (rr & 1) ? 1.0 : -1.0;
-                const double ra = bc(pair == 1 ? L.am : (pair == 2 ? 1.0 : 0.0), owner);
+                const double ra = bcu(pair == 1 ? L.am : (pair == 2 ? 1.0 : 0.0), owner);
                 cf1 = flip * sgn;
                 n2 = oa >= 1 && pair != 0 ? 1 : 0;
                 cf2 = -flip * sgn * ra;
@@ -508,7 +592,7 @@ __device__ inline int solve(Lane& L, const Lds& Sg, const Consts& C, const Inst&
                 s1 = owner - oa;
                 n1 = oa;
                 cf1 = flip * L.ts;
-                const int ksf = bc(L.sf, owner);
+                const int ksf = bcu(L.sf, owner);
                 if (ksf == 1) {
                     s2 = owner - oa - N;
                     n2 = oa;
@@ -518,7 +602,7 @@ __device__ inline int solve(Lane& L, const Lds& Sg, const Consts& C, const Inst&
                 }
                 if (t == owner) dloc = L.sfd;
             }
-            dloc = bc(dloc, owner);
+            dloc = bcu(dloc, owner);
             if (rev) dloc = -dloc;
         }
         auto coef = [&](int j) -> double {
@@ -548,9 +632,7 @@ __device__ inline int solve(Lane& L, const Lds& Sg, const Consts& C, const Inst&
             {
                 double accr = t < nact ? dv : 0.0;
                 for (int j = nact - 1; j >= 0; --j) {
-                    double rj_ = 0.0;
-                    if (t == j) rj_ = accr / R[j * LD + j];
-                    rj_ = bc(rj_, j);
+                    const double rj_ = bcu(accr * rinv, j);
                     if (t == j) r = rj_;
                     if (t < j) accr -= R[t * LD + j] * rj_;
                 }
@@ -560,9 +642,7 @@ __device__ inline int solve(Lane& L, const Lds& Sg, const Consts& C, const Inst&
             pf.mark(5);
             // blocking multipliers: r_j above the rounding level of r (a noise-level r_j > 0 with a
             // rounding-level u_j < 0 would give a huge NEGATIVE step), u clamped at 0
-            double rmax = t < nact ? fabs(r) : 0.0;
-#pragma unroll
-            for (int o = W / 2; o > 0; o >>= 1) rmax = fmax(rmax, __shfl_xor(rmax, o, W));
+            const double rmax = wmax(t < nact ? fabs(r) : 0.0);
             if (t < nact && r > 1e-13 * rmax) k1key = fmax(u, 0.0) / r;
             wargmin(k1key, k1);
             const double t1 = k1key;
@@ -583,15 +663,15 @@ __device__ inline int solve(Lane& L, const Lds& Sg, const Consts& C, const Inst&
             const double t2 = zstep && zn > 0.0 ? fmax(-sp_now, 0.0) / zn : 1e300;
             const double tstep = fmin(t1, fmin(t2, t3));
             if (!(tstep < 1e299)) {
-                if (I.debug && t == 0)
+                if (I.debug && I.debug < 3 && t == 0)
                     printf("[cent] GI_FAIL_DUAL iter %d nact %d row %d (owner %d rr %d rev %d) d2n %.3e dn %.3e "
                            "sp %.6e\n", iter, nact, pr, owner, rr, (int)rev, d2n, dn, sp_now);
-                if (I.debug && t < nact) printf("[cent]   act %d: id %d u %.6e r %.6e dv %.6e\n", t, id, u, r, dv);
-                if (I.debug && t < V) printf("[cent]   y %d = %.6e np %.3e\n", t, L.y, np_t);
+                if (I.debug == 1 && t < nact) printf("[cent]   act %d: id %d u %.6e r %.6e dv %.6e\n", t, id, u, r, dv);
+                if (I.debug == 1 && t < V) printf("[cent]   y %d = %.6e np %.3e\n", t, L.y, np_t);
                 iters = iter;
                 return GI_FAIL_DUAL;
             }
-            if (I.debug > 1 && t == 0)
+            if (I.debug == 2 && t == 0)
                 printf("[cent] it %d row %d nact %d t1 %.4e(k%d) t2 %.4e t3 %.4e d2n/dn %.3e sp %.4e\n", iter, pr, nact,
                        t1, k1, t2, t3, dn > 0 ? d2n / dn : 0.0, sp_now);
             if (t2 < 1e299 && t < V) L.y += tstep * z;
@@ -599,7 +679,7 @@ __device__ inline int solve(Lane& L, const Lds& Sg, const Consts& C, const Inst&
             unew += tstep;
             if (t2 <= t1 && t2 <= t3) {
                 pf.mark(6);
-                pf.acc[11] += 1;
+                pf.count(11);
                 // ---- add p: one Householder reflection H of J's trailing columns maps
                 // d2 = dv[nact..V) onto alpha e_nact (J <- J diag(I, H), R gets the column
                 // (dv[0..nact), alpha)).  Every lane updates its own row of J: no serial
@@ -618,7 +698,10 @@ __device__ inline int solve(Lane& L, const Lds& Sg, const Consts& C, const Inst&
                     }
                 }
                 if (t < nact) R[t * LD + nact] = dv;
-                if (t == nact) R[t * LD + nact] = alpha;
+                if (t == nact) {
+                    R[t * LD + nact] = alpha;
+                    rinv = 1.0 / alpha;
+                }
                 if (t == nact) { u = unew; id = pr; }
                 if (t == owner) act |= 1u << rr;
                 ++nact;
@@ -627,7 +710,7 @@ __device__ inline int solve(Lane& L, const Lds& Sg, const Consts& C, const Inst&
                 break;
             }
             pf.mark(6);
-            pf.acc[11] += 1;
+            pf.count(11);
             int drop;
             const bool by_sat = t3 <= t1;
             if (by_sat) {
@@ -641,7 +724,7 @@ __device__ inline int solve(Lane& L, const Lds& Sg, const Consts& C, const Inst&
             } else {
                 drop = k1;
             }
-            const int dropped = bc(id, drop);
+            const int dropped = bcu(id, drop);
             {
                 const int ob = (dropped & (REV - 1)) / ROWS, brr = (dropped & (REV - 1)) % ROWS;
                 if (t == ob) {
@@ -674,6 +757,7 @@ __device__ inline int solve(Lane& L, const Lds& Sg, const Consts& C, const Inst&
                 }
                 wsync();
             }
+            if (t >= drop && t < nact - 1) rinv = 1.0 / R[t * LD + t];
             --nact;
             pf.mark(8);
         }
@@ -695,7 +779,7 @@ __device__ inline double direct_cost(const Lane& L, const Consts& C, const Inst&
     const int t = lane();
     const int N = I.N;
     const double yv = L.on ? L.y : 0.0;
-    double vp = __shfl_up(yv, 1, W);
+    double vp = shift_up1(yv);
     if (L.a == 0) vp = L.v0;
     const double cum = vehicle_prefix(yv, N);
     const double pn = L.P1 + L.ts * cum, vn = yv;        // state a + 1
@@ -726,7 +810,7 @@ __device__ inline double direct_cost(const Lane& L, const Consts& C, const Inst&
         if (L.a < Ki) Jt += C.Qu * u * u;
         if (L.a == 0) Jt += state_terms(0, p0, v0, p0m, v0m);
     }
-    const double uprev = __shfl_up(u, 1, W);
+    const double uprev = shift_up1(u);
     if (L.on && L.a >= 1 && L.a < Ki) Jt += C.Qdu * (u - uprev) * (u - uprev);
     if (u_lane) *u_lane = u;
     return wsum(Jt);

@@ -158,6 +158,7 @@ int hvp_cent_solve_batch(hvp_handle* h, int P, int n, int leader_index, int real
                        h->cent_ties, u_out, x_out, region_out, gear_out, cost_out, status_out, nodes_out, iters_out,
                        h->g_counter);
     HIP_TRY(hipGetLastError());
+#ifdef HVP_CENT_PROF
     if (debug >= 3) {  // phase profile of the wave QP (hvp_cent.h Prof), summed over all platoons
         unsigned long long prof[16];
         HIP_TRY(hipStreamSynchronize(st));
@@ -173,6 +174,7 @@ int hvp_cent_solve_batch(hvp_handle* h, int P, int n, int leader_index, int real
         const unsigned long long zero[16] = {};
         HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(hvp::cent::g_cent_prof), zero, sizeof(zero)));
     }
+#endif
     HIP_TRY(hipEventRecord(h->evq1, st));
     HIP_TRY(hipEventRecord(h->ev1, st));
     h->last_stream = st;

@@ -66,7 +66,7 @@ __device__ inline int platoon_qp(Lane& L, const Lds& S, const Consts& C, const I
     iters = 0;
     wsync();
     pf.mark(10);
-    pf.acc[10] += 1;
+    pf.count(10);
     if (!setup(L, S, C, I, ci, Ki)) return QP_INFEASIBLE;
     pf.mark(0);
     const int r = solve(L, S, C, I, max_iter, it, pf);
@@ -88,7 +88,7 @@ __device__ inline bool joint_less(uint64_t a_code, uint64_t b_code, int n, int N
     const unsigned long long diff = __ballot(t < D && ra != rb);
     if (!diff) return false;
     const int first = __ffsll((long long)diff) - 1;
-    return bc(ra, first) < bc(rb, first);
+    return bcu(ra, first) < bcu(rb, first);
 }
 
 // One child record, read with lane-dependent addresses (vector loads: the slice is rewritten
@@ -98,10 +98,10 @@ __device__ inline Child load_child(const Child* c) {
     const double* w = reinterpret_cast<const double*>(c);
     const double v = t < 4 ? w[t] : 0.0;
     Child ch;
-    ch.lb = bc(v, 0);
-    ch.lo = bc(v, 1);
-    ch.hi = bc(v, 2);
-    ch.r = (int32_t)(__double_as_longlong(bc(v, 3)) & 0xffffffffll);
+    ch.lb = bcu(v, 0);
+    ch.lo = bcu(v, 1);
+    ch.hi = bcu(v, 2);
+    ch.r = (int32_t)(__double_as_longlong(bcu(v, 3)) & 0xffffffffll);
     ch.pad = 0;
     return ch;
 }
@@ -141,7 +141,7 @@ __device__ inline void bnb_platoon(Lane& L, const Lds& S, const Consts& C, const
     auto begin_expand = [&](int dd) {
         const int k = dd / n, i = dd % n;
         const hvp_system& Si = I.systems[I.vsys[i]];
-        const double lo = bc(st.vlo, i), hi = bc(st.vhi, i);
+        const double lo = bcu(st.vlo, i), hi = bcu(st.vhi, i);
         ex_ok = false;
         ex_nlo = ex_nhi = 0.0;
         if (t < Si.n_regions) ex_ok = bnb_child(Si, C, k, lo, hi, t, &ex_nlo, &ex_nhi);
@@ -161,7 +161,7 @@ __device__ inline void bnb_platoon(Lane& L, const Lds& S, const Consts& C, const
         const hvp_system& Si = I.systems[I.vsys[dd % n]];
         int rank = 0;
         for (int c = 0; c < Si.n_regions; ++c) {
-            const double lc = bc(ex_lb, c);
+            const double lc = bcu(ex_lb, c);
             if (((ex_mask >> c) & 1ull) && (lc < ex_lb || (lc == ex_lb && c < t))) ++rank;
         }
         if (ex_ok) {
@@ -183,7 +183,7 @@ __device__ inline void bnb_platoon(Lane& L, const Lds& S, const Consts& C, const
             const double tol = 1e-9 * fmax(1.0, fabs(inc));
             int w = 0;  // drop entries beyond the new window (rows only move down: serial copy)
             for (int j = 0; j < ntie; ++j) {
-                const double cj = bc(st.tie_c, j);
+                const double cj = bcu(st.tie_c, j);
                 if (!(cj <= inc + tol)) continue;
                 if (w != j) {
                     if (t < n) tie_codes[(size_t)w * n + t] = tie_codes[(size_t)j * n + t];
@@ -233,7 +233,7 @@ __device__ inline void bnb_platoon(Lane& L, const Lds& S, const Consts& C, const
                 int win = -1;
                 uint64_t wcode = 0;
                 for (int j = 0; j < ntie; ++j) {
-                    const double cj = bc(st.tie_c, j);
+                    const double cj = bcu(st.tie_c, j);
                     if (!(cj <= inc + tol)) continue;
                     const uint64_t cj_code = t < n ? tie_codes[(size_t)j * n + t] : 0;
                     if (win < 0 || joint_less(cj_code, wcode, n, N)) {
@@ -245,10 +245,10 @@ __device__ inline void bnb_platoon(Lane& L, const Lds& S, const Consts& C, const
                 phase = FINAL;
                 dfix = D;  // re-solve the winner for its trajectory (not counted)
             } else {
-                const int nch = bc(st.f_n, d), cur = bc(st.f_cur, d);
+                const int nch = bcu(st.f_n, d), cur = bcu(st.f_cur, d);
                 const int i = d % n, k = d / n;
                 if (cur >= nch) {  // frame done: vehicle i's interval back to the parent's
-                    const double slo = bc(st.f_slo, d), shi = bc(st.f_shi, d);
+                    const double slo = bcu(st.f_slo, d), shi = bcu(st.f_shi, d);
                     if (t == i) {
                         st.vlo = slo;
                         st.vhi = shi;
@@ -281,7 +281,7 @@ __device__ inline void bnb_platoon(Lane& L, const Lds& S, const Consts& C, const
         ++nodes;
         const int q = platoon_qp(L, S, C, I, st.vcode, dfix, max_iter, c, it, pf);
         iters += it;
-        if (I.debug && q != QP_OK) {
+        if (I.debug && I.debug < 3 && q != QP_OK) {
             const uint64_t c0 = bc(st.vcode, 0), c1 = bc(st.vcode, 1 < n ? 1 : 0), c2 = bc(st.vcode, 2 < n ? 2 : 0);
             if (t == 0)
                 printf("[cent] platoon %d QP %d dfix %d phase %d -> %d (codes v0 %llx v1 %llx v2 %llx)\n",
@@ -297,7 +297,7 @@ __device__ inline void bnb_platoon(Lane& L, const Lds& S, const Consts& C, const
             if (q == QP_OK) {
                 record(c);
             } else if (q == QP_FAILED) {
-                const double plb = D >= 2 ? bc(st.f_lb, D - 2) : -INF;
+                const double plb = D >= 2 ? bcu(st.f_lb, D - 2) : -INF;
                 fail_lb = fmin(fail_lb, plb);
             }
         } else {  // FINAL
