@@ -124,6 +124,8 @@ EXPORTS = {
     "hvp_gadmm_switch": ([_P] + [ctypes.c_int] * 4 + [_P] * 5, ctypes.c_int),
     "hvp_cent_solve_batch": ([_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P, _P, _P, ctypes.c_int]
                              + [_P] * 9, ctypes.c_int),
+    "hvp_env_step_batch": ([_P, ctypes.c_int, ctypes.c_int] + [_P] * 6 + [ctypes.c_int, ctypes.c_int, ctypes.c_double]
+                           + [_P] * 4, ctypes.c_int),
     "hvp_sync": ([_P, _P], ctypes.c_int),
     "hvp_get_stats": ([_P, ctypes.POINTER(HvpStats)], ctypes.c_int),
     "hvp_destroy": ([_P], None),

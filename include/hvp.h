@@ -265,6 +265,20 @@ int hvp_cent_solve_batch(hvp_handle* h, int P, int n, int leader_index, int real
                          double* u_out, double* x_out, int8_t* region_out, int8_t* gear_out,
                          double* cost_out, int32_t* status_out, int32_t* nodes_out, int32_t* iters_out,
                          void* stream);
+/* ---- Plant step (the caller side of the hot path, env.py PlatoonEnv.step + get_stage_cost,
+ * models.py Platoon.step_platoon) for P platoons of n vehicles (device pointers, async):
+ *   x [P][2n] (p, v per vehicle) advanced IN PLACE by ts with 10 explicit Euler sub-steps of the
+ *   nonlinear vehicle model (models.py:114-125, 236-257); masses [P][n]; u [P][n] the throttle;
+ *   gear [P][n] int8 from the action, or NULL / entries <= 0: the PWA-gear model's gear of the
+ *   current velocity (env.py:198-204, models.py:494-515); u_prev [P][n] the previous action
+ *   (= u on the first step, env.py:127-128); leader_x [P][2] the leader state of this step.
+ * Outputs: cost [P] the stage cost of (x, u) before the step (env.py:126-180, quadratic, with the
+ * handle's weights / spacing / d_safe), viol [P] 100 when a gap is below d_safe (else 0),
+ * status [P] 0 ok, 1 a velocity left the traction curve (the reference raises RuntimeError). */
+int hvp_env_step_batch(hvp_handle* h, int P, int n, const double* masses, double* x, const double* u,
+                       const int8_t* gear, const double* u_prev, const double* leader_x, int leader_index,
+                       int real_vehicle_as_reference, double ts, double* cost_out, int32_t* viol_out,
+                       int32_t* status_out, void* stream);
 int hvp_sync(hvp_handle* h, void* stream);
 int hvp_get_stats(hvp_handle* h, hvp_stats* out); /* synchronises the handle's last stream */
 void hvp_destroy(hvp_handle* h);
