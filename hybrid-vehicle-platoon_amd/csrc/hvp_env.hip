@@ -41,8 +41,9 @@ __device__ inline bool traction(double v, int j, double* f) {
     const double v0 = kTracV[j - 1][0], v1 = kTracV[j - 1][1], v2 = kTracV[j - 1][2], v3 = kTracV[j - 1][3];
     const double flo = kTracT[j - 1][0], ftop = kTracT[j - 1][1], fend = kTracT[j - 1][2];
     if (v <= v0 || v >= v3) return false;
-    if (v < v1) *f = flo + (ftop - flo) * (v - v0) / (v1 - v0);
-    else if (v > v2) *f = ftop - (ftop - fend) * (v - v2) / (v3 - v2);
+    // the reference's operation order (models.py:41-48)
+    if (v < v1) *f = ((v - v0) / (v1 - v0)) * (ftop - flo) + flo;
+    else if (v > v2) *f = ftop - ((v - v2) / (v3 - v2)) * (ftop - fend);
     else *f = ftop;
     return true;
 }
@@ -108,7 +109,8 @@ __global__ __launch_bounds__(64) void k_env_step(int P, int n, const double* __r
                 break;
             }
             const double dp = vv;
-            const double dv = -(kCFric * vv * vv) / m - kMu * kGrav + f / m * ui;
+            // x + dt (A(x) + B(x, j) u), models.py:99-125
+            const double dv = (-(kCFric * (vv * vv)) / m - kMu * kGrav) + (f / m) * ui;
             pp = pp + dt * dp;
             vv = vv + dt * dv;
         }

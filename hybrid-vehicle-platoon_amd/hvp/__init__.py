@@ -4,4 +4,4 @@ Product path: PWA vehicle tables (models, tables) -> libhvpsolve.so (HIP, gfx950
 C ABI of include/hvp.h (solver) -> the reference's call surface (mpc, agent, decent).
 """
 
-__all__ = ["models", "params", "env", "tables", "solver", "batched", "mpc", "agent", "decent", "admm", "gadmm", "cent"]
+__all__ = ["models", "params", "env", "tables", "solver", "batched", "mpc", "agent", "decent", "admm", "gadmm", "cent", "envdev"]

@@ -783,3 +783,72 @@ def solve_cent(systems: list[dict], cfg: Cfg, N: int, x0, leader_x, leader_index
     if rc != 0:
         raise RuntimeError(f"oracle_solve_cent failed ({rc})")
     return CentResult(x_out, u_out, sig, float(info[0]), int(info[1]), int(info[2]))
+
+
+# ------------------------------------------------------------------ plant step (env.py / models.py)
+_TRAC_T = ((253.54, 4056.7, 3042.0), (184.0, 2944.75, 2208.55), (132.22, 2115.6, 1586.7),
+           (100 / 415, 1605.0, 1205.0), (72.88, 1166.0, 874.7), (52.4, 838.0, 628.3))   # models.py:13-20
+_TRAC_V = ((2.0706, 4.12158, 9.29, 12.38), (2.85, 5.675, 12.7956, 17.06), (3.9705, 7.90316, 17.8105, 23.7474),
+           (5.228, 10.42, 23.454, 31.2704), (7.203, 14.335, 32.31, 43.0802),
+           (10.027, 19.956, 44.978, 59.9715))                                            # models.py:21-28
+
+
+def _traction(v: float, j: int) -> float:
+    """GearTransimission.get_traction (models.py:30-50), same operation order."""
+    if not 1 <= j <= 6 or v < 2.0706 or v > 59.9715:
+        raise RuntimeError("out of range")
+    (v0, v1, v2, v3), (t0, t1, t2) = _TRAC_V[j - 1], _TRAC_T[j - 1]
+    if v <= v0 or v >= v3:
+        raise RuntimeError("out of range for gear")
+    if v < v1:
+        return ((v - v0) / (v1 - v0)) * (t1 - t0) + t0
+    if v > v2:
+        return t1 - ((v - v2) / (v3 - v2)) * (t1 - t2)
+    return t1
+
+
+def _gear_pwa(v: float) -> int:
+    """PwaGearVehicle.get_gear_from_velocity (models.py:494-515) with v_gear_lim (:401-403)."""
+    lim = [(_VH[i] - _VL[i]) / 2 + _VL[i] for i in range(1, 6)]
+    for i in range(4):
+        if lim[i] <= v < lim[i + 1]:
+            return i + 2
+    return 1 if v < lim[0] else 6
+
+
+def env_step(x, u, masses, leader_state, u_prev=None, gears=None, leader_index: int = 0,
+             real_vehicle_as_reference: bool = False, cfg: Cfg | None = None, ts: float = 1.0):
+    """PlatoonEnv.step for one platoon (env.py:126-212 with the quadratic cost; models.py:99-125,
+    236-257): returns (x_next (2n,), stage cost, violation 0/100, ok).  gears None: the PWA-gear
+    model's gear of each velocity (env.py:198-204)."""
+    cfg = cfg or Cfg()
+    x = np.asarray(x, dtype=float).reshape(-1).copy()
+    u = np.asarray(u, dtype=float).reshape(-1)
+    n = len(u)
+    up = u if u_prev is None else np.asarray(u_prev, dtype=float).reshape(-1)
+    Q = np.array(cfg.Qx, dtype=float).reshape(2, 2)
+    sp = lambda xi: np.array([-cfg.d0 - cfg.t0 * xi[1], 0.0])  # noqa: E731  spacing_policy.spacing
+    xs = [x[2 * i:2 * i + 2] for i in range(n)]
+    ref = np.asarray(leader_state, dtype=float).reshape(2)
+    e = xs[0] - ref - sp(xs[0]) if real_vehicle_as_reference else xs[leader_index] - ref
+    cost = float(e @ Q @ e)
+    for i in range(1, n):
+        e = xs[i] - xs[i - 1] - sp(xs[i])
+        cost += float(e @ Q @ e)
+    cost += sum(cfg.Qu * u[i] ** 2 for i in range(n)) + sum(cfg.Qdu * (u[i] - up[i]) ** 2 for i in range(n))
+    close = any(xs[i][0] - xs[i + 1][0] < cfg.d_safe for i in range(n - 1))
+    if real_vehicle_as_reference and ref[0] - xs[0][0] < cfg.d_safe:
+        close = True
+    j = [int(g) for g in gears] if gears is not None else [_gear_pwa(xs[i][1]) for i in range(n)]
+    dt = ts / 10
+    ok = True
+    try:
+        for _ in range(10):
+            for i in range(n):
+                p, v = x[2 * i], x[2 * i + 1]
+                a0, a1 = v, -(0.5 * v ** 2) / masses[i] - 0.01 * 9.8
+                b1 = _traction(v, j[i]) / masses[i]
+                x[2 * i], x[2 * i + 1] = p + dt * (a0 + 0.0 * u[i]), v + dt * (a1 + b1 * u[i])
+    except RuntimeError:
+        ok = False
+    return x, cost, 100 if close else 0, ok
