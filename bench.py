@@ -361,6 +361,95 @@ def cpu_baseline_gadmm(n: int, N: int, iters: int, max_rounds: int, budget_s: fl
                       f"oracle, {t_run:.1f} s"}
 
 
+def bench_closed_loop(args, world: int, rank: int, local: int, dist) -> None:
+    """fleet_decent_mld closed loop on the device: one step = observe_states (neighbour
+    predictions, hvp_decent_params_batch) + the n local MIQPs of every platoon (hvp_solve_batch)
+    + PlatoonEnv.step (hvp_env_step_batch: 10 Euler sub-steps of the nonlinear plant, stage cost,
+    violations).  The platoons move: step t uses the states produced by step t - 1."""
+    import torch
+
+    from hvp import tables
+    from hvp.env import derive_env_seed, initial_platoon_state
+    from hvp.envdev import DeviceEnv
+    from hvp.models import PwaGearVehicle
+    from hvp.solver import BatchSolver
+
+    n, N, S = args.n, args.N, args.platoons
+    veh = PwaGearVehicle(800)
+    system = tables.system_from_dict(veh.get_discrete_system(1), tables.gears_of(veh))
+    solver = BatchSolver(tables.problem(N), [system], device=local)
+    dev = torch.device("cuda", local)
+    x0 = np.stack([initial_platoon_state(n, derive_env_seed(int(s))).reshape(-1).astype(np.float64)
+                   for s in range(rank * S, (rank + 1) * S)])
+    T = args.warmup + args.steps + N + 2
+    lx = np.stack([3000.0 + 20.0 * np.arange(T), np.full(T, 20.0)])
+    wins = torch.from_numpy(np.ascontiguousarray(np.stack([np.broadcast_to(lx[:, t:t + N + 1], (S, 2, N + 1))
+                                                           for t in range(args.warmup + args.steps)]))).to(dev)
+    lead = torch.from_numpy(np.ascontiguousarray(np.stack([np.broadcast_to(lx[:, t], (S, 2))
+                                                           for t in range(args.warmup + args.steps)]))).to(dev)
+    B = S * n
+    solver.reserve(B)
+    env = DeviceEnv(solver, torch.full((S, n), 800.0, dtype=torch.float64, device=dev))
+    x = torch.from_numpy(x0).to(dev)
+    t_sys = torch.zeros(B, dtype=torch.int32, device=dev)
+    out = solver.alloc_outputs(B, dev)
+    params = torch.empty((B, solver.params_stride), dtype=torch.float64, device=dev)
+    roles = torch.empty(B, dtype=torch.int32, device=dev)
+    u = torch.empty((S, n), dtype=torch.float64, device=dev)
+    u_prev = [None]
+    viol = torch.zeros(S, dtype=torch.int64, device=dev)
+    bad = torch.zeros(S, dtype=torch.int64, device=dev)
+    notopt = torch.zeros((), dtype=torch.int64, device=dev)
+
+    def step(t):
+        solver.decent_params_device(x, wins[t], params=params, roles=roles)
+        solver.solve_device(t_sys, roles, params, out)
+        u.copy_(out["u"][:, 0].view(S, n))
+        st = env.step(x, u, lead[t], u_prev=u_prev[0])
+        u_prev[0] = u.clone()
+        viol.add_(st["viol"])
+        bad.add_(st["status"])
+        notopt.add_((out["status"] != 0).sum())
+
+    for t in range(args.warmup):
+        step(t)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for t in range(args.warmup, args.warmup + args.steps):
+        step(t)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist:
+        tt = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    s = solver.stats()
+    value = S * world * args.steps / dt
+    result = {
+        "metric": f"MPC timesteps/sec (whole platoon) at n={n} N={N} decent_mld closed loop",
+        "value": value, "unit": "platoon-timesteps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic: env.reset random-init platoon states (seeded), constant-velocity leader; the platoons "
+                "move under the nonlinear plant, every step from the previous step's states",
+        "config": {"workload": f"fleet_decent_mld n={n} N={N} pwa_gear closed loop (observe_states + local MIQPs + "
+                               "PlatoonEnv.step on the device)", "n_vehicles": n, "horizon": N,
+                   "platoons_per_gpu": S, "parallelism": f"seeds-sharded x{world}"},
+        "qp_kernel_ms_last_step": s.qp_ms, "solve_ms_last_step": s.last_ms,
+        "not_optimal_total": int(notopt.item()), "plant_failures_total": int(bad.sum().item()),
+        "violation_steps_total": int((viol // 100).sum().item()),
+    }
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
 def cent_qp_bytes(n: int, N: int) -> int:
     """SURVEY.md 8(d) dense bytes of one centralised fixed-sequence QP (condensed like the local
     QP: u (nN) and slacks (n(N+1)) free, m = 13N + 3 rows per vehicle), 8 (n_w^2 + m n_w + m + n_w)."""
@@ -495,6 +584,8 @@ def main() -> None:
                     help="decent: fleet_decent_mld (configs[1]); admm: fleet_naive_admm (configs[2]); "
                          "gadmm: fleet_g_admm (configs[3]); cent: fleet_cent_mld (MpcMldCent)")
     ap.add_argument("--max-nodes", type=int, default=200000, help="cent: QPs per platoon cap")
+    ap.add_argument("--closed-loop", action="store_true",
+                    help="decent: every step = neighbour predictions + local MIQPs + plant step, all on the device")
     ap.add_argument("--admm-iters", type=int, default=None, help="default 20 (admm) / 100 (gadmm)")
     ap.add_argument("--max-rounds", type=int, default=10, help="gadmm: switching rounds cap")
     ap.add_argument("--gadmm-layout", choices=["replicas", "vehicles"], default="replicas")
@@ -524,6 +615,8 @@ def main() -> None:
         return bench_gadmm(args, world, rank, local, dist)
     if args.controller == "cent":
         return bench_cent(args, world, rank, local, dist)
+    if args.closed_loop:
+        return bench_closed_loop(args, world, rank, local, dist)
     n, N, S = args.n, args.N, args.platoons
     veh = PwaGearVehicle(800)
     system = tables.system_from_dict(veh.get_discrete_system(1), tables.gears_of(veh))

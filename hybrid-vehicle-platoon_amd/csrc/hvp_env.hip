@@ -125,9 +125,78 @@ __global__ __launch_bounds__(64) void k_env_step(int P, int n, const double* __r
     }
 }
 
+// TrackingDecentMldCoordinator.observe_states (fleet_decent_mld.py:348-455) for P platoons: one
+// thread per (platoon, vehicle) writes the vehicle's local-MPC parameter block (include/hvp.h
+// layout: x0 | x_front | x_back | leader_x) and role bits.  est: 0 constant velocity (:421-428),
+// 1 two-point (:430-440), 2 saturated two-point (:442-455); x_prev feeds the estimators.
+__global__ __launch_bounds__(256) void k_decent_params(int P, int n, int N, const double* __restrict__ x,
+                                                       const double* __restrict__ x_prev,
+                                                       const double* __restrict__ leader_x, int leader, int rvar,
+                                                       int est, double ts, double* __restrict__ params,
+                                                       int32_t* __restrict__ roles) {
+    const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= (long long)P * n) return;
+    const int p = (int)(g / n), i = (int)(g % n);
+    const double* xp = x + (size_t)p * 2 * n;
+    const double* xq = x_prev ? x_prev + (size_t)p * 2 * n : xp;
+    const int K = N + 1;
+    double* out = params + (size_t)g * (2 + 6 * K);
+    out[0] = xp[2 * i];
+    out[1] = xp[2 * i + 1];
+    auto predict = [&](int j, double* dst) {  // extrapolate vehicle j's state into dst (2, N+1)
+        double pp = xp[2 * j], vv = xp[2 * j + 1];
+        const double dv = est ? vv - xq[2 * j + 1] : 0.0;
+        dst[0] = pp;
+        dst[K] = vv;
+        for (int k = 0; k < N; ++k) {
+            pp = pp + ts * vv;
+            vv = vv + (est == 0 || (est == 2 && k >= N / 2) ? 0.0 : dv);
+            dst[k + 1] = pp;
+            dst[K + k + 1] = vv;
+        }
+    };
+    double* xf = out + 2;
+    double* xb = out + 2 + 2 * K;
+    double* xl = out + 2 + 4 * K;
+    if (i > 0) predict(i - 1, xf);
+    else
+        for (int k = 0; k < 2 * K; ++k) xf[k] = 0.0;
+    if (i < n - 1) predict(i + 1, xb);
+    else
+        for (int k = 0; k < 2 * K; ++k) xb[k] = 0.0;
+    const double* lw = leader_x + (size_t)p * 2 * K;
+    for (int k = 0; k < 2 * K; ++k) xl[k] = i == leader ? lw[k] : 0.0;
+    int r = 0;  // tables.role_bits (fleet_decent_mld.py:100-153, 191-208)
+    if (i != 0) r |= HVP_ROLE_SAFE_FRONT;
+    if (i != n - 1) r |= HVP_ROLE_SAFE_BACK;
+    if (i != 0 && i != leader) r |= HVP_ROLE_TRACK_FRONT;
+    if (i != n - 1 && i != leader) r |= HVP_ROLE_TRACK_BACK;
+    if (i == leader) r |= HVP_ROLE_TRACK_LEADER | (rvar ? HVP_ROLE_LEADER_SPACING : 0);
+    roles[g] = r;
+}
+
 }  // namespace
 
 extern "C" {
+
+int hvp_decent_params_batch(hvp_handle* h, int P, int n, const double* x, const double* x_prev,
+                            const double* leader_x, int leader_index, int real_vehicle_as_reference, int estimator,
+                            double* params, int32_t* roles, void* stream) {
+    if (!h) return fail(HVP_E_ARG, "hvp_decent_params_batch: null handle");
+    if (h->prob.formulation != HVP_FORM_DECENT)
+        return fail(HVP_E_ARG, "hvp_decent_params_batch: the handle is not an HVP_FORM_DECENT problem");
+    if (P < 0 || n < 1 || leader_index < 0 || leader_index >= n || estimator < 0 || estimator > 2)
+        return fail(HVP_E_ARG, "hvp_decent_params_batch: bad layout / estimator");
+    if (P == 0) return 0;
+    if (!x || !leader_x || !params || !roles) return fail(HVP_E_ARG, "hvp_decent_params_batch: bad argument");
+    HIP_TRY(hipSetDevice(h->device));
+    const long long total = (long long)P * n;
+    hipLaunchKernelGGL(k_decent_params, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, P, n,
+                       h->prob.N, x, x_prev, leader_x, leader_index, real_vehicle_as_reference ? 1 : 0, estimator,
+                       h->prob.ts_acc, params, roles);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
 
 int hvp_env_step_batch(hvp_handle* h, int P, int n, const double* masses, double* x, const double* u,
                        const int8_t* gear, const double* u_prev, const double* leader_x, int leader_index,

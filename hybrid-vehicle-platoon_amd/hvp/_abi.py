@@ -126,6 +126,8 @@ EXPORTS = {
                              + [_P] * 9, ctypes.c_int),
     "hvp_env_step_batch": ([_P, ctypes.c_int, ctypes.c_int] + [_P] * 6 + [ctypes.c_int, ctypes.c_int, ctypes.c_double]
                            + [_P] * 4, ctypes.c_int),
+    "hvp_decent_params_batch": ([_P, ctypes.c_int, ctypes.c_int, _P, _P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                 _P, _P, _P], ctypes.c_int),
     "hvp_sync": ([_P, _P], ctypes.c_int),
     "hvp_get_stats": ([_P, ctypes.POINTER(HvpStats)], ctypes.c_int),
     "hvp_destroy": ([_P], None),

@@ -175,6 +175,35 @@ class BatchSolver:
         _abi.check(rc, "hvp_solve_batch")
         return out
 
+    # -------------------------------------------------------------- neighbour predictions
+    def decent_params_device(self, x, leader_window, x_prev=None, leader_index: int = 0,
+                             real_vehicle_as_reference: bool = False, estimator: str = "none",
+                             params=None, roles=None, stream=None):
+        """hvp_decent_params_batch: the local-MPC parameter blocks and roles of P platoons from
+        their measured states x (P, 2n) on the device (observe_states, fleet_decent_mld.py:348-455).
+        leader_window (P, 2, N+1).  Returns (params (P*n, stride), roles (P*n,))."""
+        import torch
+
+        P, n2 = int(x.shape[0]), int(x.shape[1])
+        n = n2 // 2
+        est = {"none": 0, "two_point": 1, "sat": 2}[estimator]
+        dev = x.device
+        for name, t, shape in (("x", x, (P, n2)), ("leader_window", leader_window, (P, 2, self.N + 1))):
+            if not t.is_cuda or t.dtype != torch.float64 or not t.is_contiguous() or tuple(t.shape) != shape:
+                raise ValueError(f"{name} must be a contiguous CUDA float64 {shape} tensor")
+        if params is None:
+            params = torch.empty((P * n, self.params_stride), dtype=torch.float64, device=dev)
+        if roles is None:
+            roles = torch.empty(P * n, dtype=torch.int32, device=dev)
+        if stream is None:
+            stream = torch.cuda.current_stream(dev)
+        ptr = lambda t: ctypes.c_void_p(t.data_ptr() if t is not None else 0)  # noqa: E731
+        rc = self._lib.hvp_decent_params_batch(self._h, P, n, ptr(x), ptr(x_prev), ptr(leader_window),
+                                               int(leader_index), 1 if real_vehicle_as_reference else 0, est,
+                                               ptr(params), ptr(roles), ctypes.c_void_p(stream.cuda_stream))
+        _abi.check(rc, "hvp_decent_params_batch")
+        return params, roles
+
     # -------------------------------------------------------------- fixed-control evaluation
     def evaluate_device(self, sys_idx, roles, params, gears, u, stream=None) -> dict:
         """Cost of fixed controls u (B, N) and gear labels (B, N) on the device (hvp_evaluate_batch:

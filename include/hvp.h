@@ -279,6 +279,15 @@ int hvp_env_step_batch(hvp_handle* h, int P, int n, const double* masses, double
                        const int8_t* gear, const double* u_prev, const double* leader_x, int leader_index,
                        int real_vehicle_as_reference, double ts, double* cost_out, int32_t* viol_out,
                        int32_t* status_out, void* stream);
+/* Neighbour predictions of TrackingDecentMldCoordinator.observe_states (fleet_decent_mld.py:348-455)
+ * for P platoons (device pointers, async): x [P][2n] the measured states, x_prev [P][2n] the
+ * previous ones (NULL: x; read by the two-point estimators), leader_x [P][2][N+1] the leader
+ * window; estimator 0 constant velocity (:421-428), 1 two_point (:430-440), 2 sat (:442-455).
+ * Writes params [P*n][hvp_params_stride(N)] and roles [P*n] (instance p*n + i), the input of
+ * hvp_solve_batch.  HVP_FORM_DECENT handles (their N and ts). */
+int hvp_decent_params_batch(hvp_handle* h, int P, int n, const double* x, const double* x_prev,
+                            const double* leader_x, int leader_index, int real_vehicle_as_reference, int estimator,
+                            double* params, int32_t* roles, void* stream);
 int hvp_sync(hvp_handle* h, void* stream);
 int hvp_get_stats(hvp_handle* h, hvp_stats* out); /* synchronises the handle's last stream */
 void hvp_destroy(hvp_handle* h);

@@ -71,3 +71,79 @@ def test_device_step_matches_oracle(gpu_available, rvar):
         assert abs(float(out["cost"][p]) - c) <= 1e-12 * max(1.0, abs(c)), p
         if ok:
             assert np.allclose(xd[p], xo, rtol=1e-9, atol=1e-9), (p, np.abs(xd[p] - xo).max())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("estimator", ["none", "two_point", "sat"])
+def test_device_params_match_host(gpu_available, estimator):
+    import torch
+
+    from hvp import tables
+    from hvp.batched import decent_params_from_states
+    from hvp.models import PwaGearVehicle
+    from hvp.solver import BatchSolver
+
+    P, n, N = 16, 10, 5
+    X, _, _, _, _ = _platoons(P, n)
+    Xp = X + np.random.default_rng(3).uniform(-2, 2, X.shape)
+    lead = np.stack([np.stack([3000.0 + 20.0 * (np.arange(N + 1) + p), np.full(N + 1, 20.0)]) for p in range(P)])
+    veh = PwaGearVehicle(800)
+    s = BatchSolver(tables.problem(N), [tables.system_from_dict(veh.get_discrete_system(1), tables.gears_of(veh))])
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    params, roles = s.decent_params_device(t(X), t(lead), x_prev=t(Xp), estimator=estimator, leader_index=2)
+    hp, hr = decent_params_from_states(X, N, lead, leader_index=2, prev_states=Xp, velocity_estimator=estimator)
+    assert np.array_equal(roles.cpu().numpy(), hr)
+    assert np.array_equal(params.cpu().numpy(), hp)
+
+
+@pytest.mark.gpu
+def test_device_closed_loop_matches_host_loop(gpu_available):
+    """Three closed-loop steps fully on the device (params -> solve -> plant step) against the
+    host coordinator + env (hvp.decent.TrackingDecentMldCoordinator, hvp.env.PlatoonEnv)."""
+    import torch
+
+    from hvp import tables
+    from hvp.decent import TrackingDecentMldCoordinator
+    from hvp.env import PlatoonEnv
+    from hvp.envdev import DeviceEnv
+    from hvp.models import Platoon
+    from hvp.mpc import LocalMpcMld
+    from hvp.params import ConstantVelocityLeaderTrajectory
+
+    n, N, steps = 4, 5, 3
+    lt = ConstantVelocityLeaderTrajectory(3000, 20, 60, 1)
+    lx = lt.get_leader_trajectory()
+    pl = Platoon(n, vehicle_type="pwa_gear")
+    systems = pl.get_vehicle_system_dicts(1)
+    gears = [tables.gears_of(v) for v in pl.get_vehicles()]
+    mpcs = [LocalMpcMld(N, systems[i], is_front=i == 0, is_leader=i == 0, is_trailer=i == n - 1, gears=gears[i])
+            for i in range(n)]
+    coord = TrackingDecentMldCoordinator(mpcs, ep_len=steps, N=N, leader_x=lx, ts=1.0)
+    env = PlatoonEnv(n=n, platoon=pl, ep_len=steps, leader_trajectory=lt)
+    x, _ = env.reset(seed=7)
+    coord.on_episode_start(env, 0, x)
+    host_x, host_r = [], []
+    for t in range(steps):
+        u, _ = coord.get_control(x)
+        x, r, *_ = env.step(u)
+        coord.on_timestep_end(env, 0, t + 1)
+        host_x.append(np.asarray(x, float).reshape(-1))
+        host_r.append(r)
+    # device loop
+    s = coord._solver
+    dev = torch.device("cuda", 0)
+    tx = torch.from_numpy(np.asarray(env.reset(seed=7)[0], float).reshape(1, -1)).to(dev)
+    denv = DeviceEnv(s, torch.full((1, n), 800.0, dtype=torch.float64, device=dev))
+    sys_idx = torch.arange(n, dtype=torch.int32, device=dev)
+    prev_u = None
+    for t in range(steps):
+        win = torch.from_numpy(np.ascontiguousarray(lx[:, t:t + N + 1])[None]).to(dev)
+        params, roles = s.decent_params_device(tx, win)
+        out = s.solve_device(sys_idx, roles, params)
+        u = out["u"][:, 0].reshape(1, n).contiguous()
+        st = denv.step(tx, u, torch.from_numpy(lx[:, t].copy()[None]).to(dev), u_prev=prev_u)
+        prev_u = u
+        torch.cuda.synchronize()
+        assert int(st["status"][0]) == 0
+        assert np.allclose(tx.cpu().numpy().reshape(-1), host_x[t], rtol=1e-9, atol=1e-8), t
+        assert abs(float(st["cost"][0]) - host_r[t]) <= 1e-8 * abs(host_r[t]), t
