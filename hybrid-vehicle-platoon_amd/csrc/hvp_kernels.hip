@@ -322,11 +322,20 @@ __device__ inline double key_cost(unsigned long long k) {
 }
 __device__ inline double inc_of(const Workspace& ws, int inst) { return key_cost(ws.inc[inst]); }
 
-template <int N, int BS>
+// Occupancy target of the lane B&B kernels (waves per SIMD).  Measured at C2: 2 waves/SIMD forces
+// 800 B/lane of spills and runs 2.7x slower than 1 wave/SIMD with the register file to itself
+#ifndef HVP_LANE_WAVES
+#define HVP_LANE_WAVES 1
+#endif
+#define HVP_LANE_OCC __attribute__((amdgpu_waves_per_eu(HVP_LANE_WAVES)))
+
+// ADMM: the formulation is a template parameter so that each kernel instantiation holds ONE
+// QP path (both paths in one kernel pushed the lane kernels to 256 VGPRs + scratch spills)
+template <int N, int BS, bool ADMM>
 __device__ inline int bnb_qp(hvp::LaneQp<N, LdsMem<N, BS>>& q, const hvp_system& S, const hvp::Consts& C, int rl,
                              const double* prm, uint64_t code, int K, double& cost) {
     int it = 0, st;
-    if (C.form == HVP_FORM_ADMM) {
+    if constexpr (ADMM) {
         st = hvp::solve_admm_lane<N>(q, S, C, rl, prm, code, K, kGiMaxIter<N>, it);
         cost = st == hvp::GI_OK ? hvp::admm_direct_cost<N>(q, S, C, rl, prm, code, K) : 0.0;
     } else {
@@ -337,8 +346,8 @@ __device__ inline int bnb_qp(hvp::LaneQp<N, LdsMem<N, BS>>& q, const hvp_system&
     return st == hvp::GI_OK ? it : -1 - it;
 }
 
-template <int N>
-__global__ __launch_bounds__(kBnbBlock<N>) void k_bnb_root(int B, const hvp_system* __restrict__ systems,
+template <int N, bool ADMM>
+__global__ __launch_bounds__(kBnbBlock<N>) HVP_LANE_OCC void k_bnb_root(int B, const hvp_system* __restrict__ systems,
                                                            const int32_t* __restrict__ sys,
                                                            const int32_t* __restrict__ role,
                                                            const double* __restrict__ params, hvp::Consts C,
@@ -365,7 +374,7 @@ __global__ __launch_bounds__(kBnbBlock<N>) void k_bnb_root(int B, const hvp_syst
         hvp::LaneQp<N, LdsMem<N, BS>> q;
         q.mem.lane = threadIdx.x;
         double c0;
-        int it = bnb_qp<N, BS>(q, S, C, rl, prm, 0, 0, c0);
+        int it = bnb_qp<N, BS, ADMM>(q, S, C, rl, prm, 0, 0, c0);
         ++nodes;
         iters += it >= 0 ? it : -1 - it;
         if (it >= 0) {
@@ -376,7 +385,7 @@ __global__ __launch_bounds__(kBnbBlock<N>) void k_bnb_root(int B, const hvp_syst
             uint64_t code;
             if (hvp::bnb_dive<N>(S, C, v0, ystar, &code)) {
                 double c1;
-                it = bnb_qp<N, BS>(q, S, C, rl, prm, code, N, c1);
+                it = bnb_qp<N, BS, ADMM>(q, S, C, rl, prm, code, N, c1);
                 ++nodes;
                 iters += it >= 0 ? it : -1 - it;
                 if (it >= 0) inc = c1;
@@ -566,8 +575,8 @@ __global__ __launch_bounds__(kBlock) void k_bnb_expand(int k, int quota, const h
 }
 
 // one lane per level-k node: bound (k < N) or exact leaf QP (k = N)
-template <int N>
-__global__ __launch_bounds__(kBnbBlock<N>) void k_bnb_bound(int k, const hvp_system* __restrict__ systems,
+template <int N, bool ADMM>
+__global__ __launch_bounds__(kBnbBlock<N>) HVP_LANE_OCC void k_bnb_bound(int k, const hvp_system* __restrict__ systems,
                                                             const int32_t* __restrict__ sys,
                                                             const int32_t* __restrict__ role,
                                                             const double* __restrict__ params, hvp::Consts C,
@@ -591,7 +600,7 @@ __global__ __launch_bounds__(kBnbBlock<N>) void k_bnb_bound(int k, const hvp_sys
         hvp::LaneQp<N, LdsMem<N, BS>> q;
         q.mem.lane = threadIdx.x;
         double c;
-        const int it = bnb_qp<N, BS>(q, S, C, rl, prm, code, k, c);
+        const int it = bnb_qp<N, BS, ADMM>(q, S, C, rl, prm, code, k, c);
         const bool ok = it >= 0;
         const int its = ok ? it : -1 - it;
         iter_sum += (unsigned long long)its;
@@ -1217,8 +1226,12 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
         hipLaunchKernelGGL(k_bnb_root_coop<N>, dim3((B + kCoopGroups - 1) / kCoopGroups), dim3(kCoopBlock), 0, st, B,
                            h->d_sys, sys, role, params, h->C, ws);
     } else {
-        hipLaunchKernelGGL(k_bnb_root<N>, dim3((B + BS - 1) / BS), dim3(BS), lds, st, B, h->d_sys, sys, role, params,
-                           h->C, ws);
+        if (h->C.form == HVP_FORM_ADMM)
+            hipLaunchKernelGGL((k_bnb_root<N, true>), dim3((B + BS - 1) / BS), dim3(BS), lds, st, B, h->d_sys, sys,
+                               role, params, h->C, ws);
+        else
+            hipLaunchKernelGGL((k_bnb_root<N, false>), dim3((B + BS - 1) / BS), dim3(BS), lds, st, B, h->d_sys, sys,
+                               role, params, h->C, ws);
     }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(h->evb[1], st));
@@ -1236,8 +1249,12 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
             hipLaunchKernelGGL(k_bnb_bound_coop<N>, dim3(g_coop), dim3(kCoopBlock), 0, st, k, h->d_sys, sys, role,
                                params, h->C, ws);
         } else {
-            hipLaunchKernelGGL(k_bnb_bound<N>, dim3(g_qp), dim3(BS), lds, st, k, h->d_sys, sys, role, params, h->C,
-                               ws);
+            if (h->C.form == HVP_FORM_ADMM)
+                hipLaunchKernelGGL((k_bnb_bound<N, true>), dim3(g_qp), dim3(BS), lds, st, k, h->d_sys, sys, role,
+                                   params, h->C, ws);
+            else
+                hipLaunchKernelGGL((k_bnb_bound<N, false>), dim3(g_qp), dim3(BS), lds, st, k, h->d_sys, sys, role,
+                                   params, h->C, ws);
         }
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(h->evb[2 * k + 1], st));
