@@ -44,17 +44,6 @@ HVP_HD inline uint64_t bnb_lexkey(uint64_t code, int N) {
     return key;
 }
 
-// Child of a node at depth k (prefix of k steps, v_k in [lo, hi]) taking region r at step k:
-// false if r is not reachable (band disjoint from [lo, hi] or no admissible input / accel).
-HVP_HD inline bool bnb_child(const hvp_system& S, const Consts& C, int k, double lo, double hi, int r, double* nlo,
-                             double* nhi) {
-    const double tol = 1e-9 * (1.0 + fabs(fmin(hi, S.vhi[r])));
-    double ilo = fmax(lo, S.vlo[r]), ihi = fmin(hi, S.vhi[r]);
-    if (ilo > ihi + tol) return false;
-    if (ilo > ihi) ilo = ihi = 0.5 * (ilo + ihi);
-    return reach_step(ilo, ihi, S.a[r], S.b[r], S.c[r], S.umin, S.umax, C.dec[k], C.acc[k], S.vmin, S.vmax, nlo, nhi);
-}
-
 // Greedy dive from the root: at step k take the reachable region whose band is closest to the
 // relaxed velocity target (v0 at k = 0, ystar[k-1] after), ties to the lower index.  Returns
 // false when it runs into a dead end (no backtracking: the tree search stays exact without an

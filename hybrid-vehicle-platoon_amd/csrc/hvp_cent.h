@@ -24,6 +24,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include "hvp_bnb.h"
 #include "hvp_gi.h"
 #include "hvp_ipm.h"
 
@@ -214,6 +215,8 @@ struct Lane {
     bool on;
     double v0, P1, ts, pmin, pmax;
     double am, vlo, vhi, ulo, uhi, dec, acc;
+    double ub, uc;  // input map of step a: u = (v_{a+1} - am v_a - uc) / ub
+    bool ucost;     // step a carries its input cost (fixed, or relaxed in a virtual region)
     int sf;       // 0 none, 1 pair row with vehicle i-1, 2 leader row w.r.t. x_ref
     double sfd;   // SF row: s_i(y) <= sfd with s = p_{i,a+1} (- p_{i-1,a+1})  (constants folded)
     double y, f;
@@ -283,9 +286,11 @@ __device__ inline void lin(const Consts& C, const Inst& I, int i, int k, double&
 }
 
 // Lane data and Hessian row t (into LDS J) for the assignment ci (region code of the lane's
-// vehicle) with Ki fixed steps of that vehicle.  Returns false if a constant row is violated
-// (p_1 outside the position box).
-__device__ inline bool setup(Lane& L, const Lds& S_lds, const Consts& C, const Inst& I, uint64_t ci, int Ki) {
+// vehicle) with Ki fixed steps of that vehicle; [lo, hi] is the exact interval of v_{Ki} of the
+// lane's vehicle, from which the undecided steps are relaxed (hvp_ipm.h:relax_step, the oracle's
+// relax_tail).  Returns false if a constant row is violated (p_1 outside the position box).
+__device__ inline bool setup(Lane& L, const Lds& S_lds, const Consts& C, const Inst& I, uint64_t ci, int Ki,
+                             double lo, double hi) {
     const int t = lane();
     const int N = I.N, V = I.V, LD = S_lds.LD;
     L.on = t < V;
@@ -300,24 +305,55 @@ __device__ inline bool setup(Lane& L, const Lds& S_lds, const Consts& C, const I
     L.P1 = p0 + ts * v0;
     L.pmin = S.pmin;
     L.pmax = S.pmax;
+    // relaxed steps a, a + 1 of the lane: virtual regions and the interval of v_{a+1}
+    int virt0 = -1, virt1 = -1;
+    double bm0 = 1.0, bm1 = 1.0, rlo = S.vmin, rhi = S.vmax;
+    if (L.on && a + 1 >= Ki) {
+        const int kend = a + 1 < N ? a + 1 : N - 1;
+        for (int k = Ki; k <= kend; ++k) {
+            double nlo, nhi, bm;
+            bool dead;
+            const int vr = relax_step(S, C, k, lo, hi, nlo, nhi, bm, dead);
+            if (dead) break;
+            if (k == a) {
+                virt0 = vr;
+                bm0 = bm;
+                rlo = nlo;
+                rhi = nhi;
+            } else {
+                virt1 = vr;
+                bm1 = bm;
+            }
+            lo = nlo;
+            hi = nhi;
+        }
+    }
     auto dyn = [&](int k, double& aa, double& bb, double& cc) {
-        const int r = code_region(ci, k);
+        const int vr = k == a ? virt0 : virt1;  // k is a or a + 1
         const bool fx = k < Ki;
-        aa = fx ? S.a[r] : 1.0;
-        bb = fx ? S.b[r] : 1.0;
-        cc = fx ? S.c[r] : 0.0;
+        const int r = fx ? code_region(ci, k) : (vr >= 0 ? vr : 0);
+        const bool on = fx || vr >= 0;
+        aa = on ? S.a[r] : 1.0;
+        bb = fx ? S.b[r] : (vr >= 0 ? (k == a ? bm0 : bm1) : 1.0);
+        cc = on ? S.c[r] : 0.0;
     };
     {
         double aa, bb, cc;
         dyn(a, aa, bb, cc);
-        const bool fx = a < Ki;
+        const bool on = a < Ki || virt0 >= 0;
         L.am = aa;
-        L.ulo = fx ? cc + bb * S.umin : -1e30;
-        L.uhi = fx ? cc + bb * S.umax : 1e30;
+        L.ub = bb;
+        L.uc = cc;
+        L.ucost = on;
+        L.ulo = on ? cc + bb * S.umin : -1e30;
+        L.uhi = on ? cc + bb * S.umax : 1e30;
         if (a + 1 < Ki) {
             const int r1 = code_region(ci, a + 1);
             L.vlo = fmax(S.vmin, S.vlo[r1]);
             L.vhi = fmin(S.vmax, S.vhi[r1]);
+        } else if (a >= Ki) {  // relaxed v_{a+1}: its reachable interval (v_{Ki}'s is implied)
+            L.vlo = fmax(S.vmin, rlo);
+            L.vhi = fmin(S.vmax, rhi);
         } else {
             L.vlo = S.vmin;
             L.vhi = S.vmax;
@@ -387,12 +423,12 @@ __device__ inline bool setup(Lane& L, const Lds& S_lds, const Consts& C, const I
     if (L.on) {
         double ub, gk, gkm;
         ucoef(a, ub, gk, gkm);
-        if (a < Ki) {
+        if (L.ucost) {
             Hrow[t] += w2 * gk * gk;
             f += w2 * ub * gk;
             if (a >= 1) Hrow[t - 1] += w2 * gk * gkm;
         }
-        if (a + 1 < N && a + 1 < Ki) {
+        if (a + 1 < N && (a + 1 < Ki || virt1 >= 0)) {
             double ub1, gk1, gkm1;
             ucoef(a + 1, ub1, gk1, gkm1);
             Hrow[t] += w2 * gkm1 * gkm1;
@@ -803,11 +839,9 @@ __device__ inline double direct_cost(const Lane& L, const Consts& C, const Inst&
     };
     double Jt = 0.0, u = 0.0;
     if (L.on) {
-        const hvp_system& S = I.systems[I.vsys[L.i]];
         Jt += state_terms(L.a + 1, pn, vn, pnm, vnm);
-        const int r = code_region(ci, L.a);
-        u = (vn - S.a[r] * vp - S.c[r]) / S.b[r];
-        if (L.a < Ki) Jt += C.Qu * u * u;
+        u = (vn - L.am * vp - L.uc) / L.ub;
+        if (L.ucost) Jt += C.Qu * u * u;
         if (L.a == 0) Jt += state_terms(0, p0, v0, p0m, v0m);
     }
     const double uprev = shift_up1(u);

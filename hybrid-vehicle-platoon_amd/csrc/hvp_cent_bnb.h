@@ -55,19 +55,21 @@ struct Search {
 // fixed steps of vehicle i once the first d decisions (time-major) are taken
 __device__ inline int fixed_steps(int d, int n, int i) { return d / n + (i < d % n ? 1 : 0); }
 
-// Platoon QP with the first `d` decisions fixed.  QP_OK with the cost and the lanes' y.
-__device__ inline int platoon_qp(Lane& L, const Lds& S, const Consts& C, const Inst& I, uint64_t vcode, int d,
-                                 int max_iter, double& cost, int& iters, Prof& pf) {
+// Platoon QP with the first `d` decisions fixed; lane j < n holds vehicle j's code and the exact
+// interval [vlo, vhi] of its first undecided velocity.  QP_OK with the cost and the lanes' y.
+__device__ inline int platoon_qp(Lane& L, const Lds& S, const Consts& C, const Inst& I, uint64_t vcode, double vlo,
+                                 double vhi, int d, int max_iter, double& cost, int& iters, Prof& pf) {
     const int t = lane();
     const int i = t < I.V ? t / I.N : 0;
     const uint64_t ci = bc(vcode, i);
+    const double lo = bc(vlo, i), hi = bc(vhi, i);
     const int Ki = fixed_steps(d, I.n, i);
     int it = 0;
     iters = 0;
     wsync();
     pf.mark(10);
     pf.count(10);
-    if (!setup(L, S, C, I, ci, Ki)) return QP_INFEASIBLE;
+    if (!setup(L, S, C, I, ci, Ki, lo, hi)) return QP_INFEASIBLE;
     pf.mark(0);
     const int r = solve(L, S, C, I, max_iter, it, pf);
     iters = it;
@@ -279,7 +281,16 @@ __device__ inline void bnb_platoon(Lane& L, const Lds& S, const Consts& C, const
         double c = 0.0;
         int it = 0;
         ++nodes;
-        const int q = platoon_qp(L, S, C, I, st.vcode, dfix, max_iter, c, it, pf);
+        // vehicle intervals of the QP: in EXPAND vehicle d % n takes the child's
+        double qlo = st.vlo, qhi = st.vhi;
+        if (phase == EXPAND) {
+            const double clo = bcu(ex_nlo, ex_r), chi = bcu(ex_nhi, ex_r);
+            if (t == d % n) {
+                qlo = clo;
+                qhi = chi;
+            }
+        }
+        const int q = platoon_qp(L, S, C, I, st.vcode, qlo, qhi, dfix, max_iter, c, it, pf);
         iters += it;
         if (I.debug && I.debug < 3 && q != QP_OK) {
             const uint64_t c0 = bc(st.vcode, 0), c1 = bc(st.vcode, 1 < n ? 1 : 0), c2 = bc(st.vcode, 2 < n ? 2 : 0);

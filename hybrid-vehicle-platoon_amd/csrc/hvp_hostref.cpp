@@ -161,7 +161,7 @@ void solve_one_bnb(const hvp_system& S, const hvp::Consts& C, int role, const do
         double y[N];
     };
     int nq = 0, nit = 0;
-    auto qp = [&](uint64_t code, int K, double& c, double* y) {
+    auto qp = [&](uint64_t code, int K, double lo, double hi, double& c, double* y) {
         hvp::LaneQp<N> q;
         int it = 0;
         if (C.form == HVP_FORM_ADMM) {
@@ -174,14 +174,14 @@ void solve_one_bnb(const hvp_system& S, const hvp::Consts& C, int role, const do
                 for (int i = 0; i < N; ++i) y[i] = q.y[i];
             return true;
         }
-        hvp::setup_lane<N>(q, S, C, role, prm, code, K);
+        hvp::setup_lane<N>(q, S, C, role, prm, code, K, lo, hi);
         const int r = hvp::solve_gi<N>(q, C, 8 * hvp::GiConstraintSet<N>::NC, it);
         ++nq;
         nit += it;
         if (r != hvp::GI_OK) {
             // leaves get the interior-point fallback (K_bnb_ipm on the device)
             if (K < N || N > HVP_MAX_N_ENUM) return false;
-            hvp::setup_lane<N>(q, S, C, role, prm, code, K);
+            hvp::setup_lane<N>(q, S, C, role, prm, code, K, lo, hi);
             const hvp::QpOut o = hvp::Solver<N, true>::solve(q, C);
             nit += o.iters;
             if (o.status != 0) return false;
@@ -202,11 +202,11 @@ void solve_one_bnb(const hvp_system& S, const hvp::Consts& C, int role, const do
         root.lo = root.hi = v0;
         root.lb = -1e300;
         double c0;
-        if (qp(0, 0, c0, root.y)) {
+        if (qp(0, 0, v0, v0, c0, root.y)) {
             root.lb = c0;
             uint64_t code;
             double c1;
-            if (hvp::bnb_dive<N>(S, C, v0, root.y, &code) && qp(code, N, c1, nullptr)) inc = c1;
+            if (hvp::bnb_dive<N>(S, C, v0, root.y, &code) && qp(code, N, 0.0, -1.0, c1, nullptr)) inc = c1;
         }
         lvl.push_back(root);
     }
@@ -224,7 +224,7 @@ void solve_one_bnb(const hvp_system& S, const hvp::Consts& C, int role, const do
         if (k == N) nleaves += (int)nxt.size();
         for (Node& c : nxt) {
             double lb;
-            const bool good = qp(c.code, k, lb, c.y);
+            const bool good = qp(c.code, k, c.lo, c.hi, lb, c.y);
             c.stat = good ? 0 : HVP_MAXITER;
             c.lb = good ? lb : (k < N ? -1e300 : 1e300);
             if (k == N && good) inc = fmin(inc, lb);

@@ -768,12 +768,16 @@ HVP_HD inline bool pbox_ok(const LaneQp<N, M>& q) {
     return true;
 }
 
+// tail relaxation of one undecided step (defined below with reach_step)
+HVP_HD inline int relax_step(const hvp_system& S, const Consts& C, int k, double lo, double hi, double& nlo,
+                             double& nhi, double& bmax, bool& dead);
+
 // ------------------------------------------------------------------ problem setup
 // Builds the lane QP for instance params (x0, x_front, x_back, leader_x) and region code.
 // Returns false when a sigma-independent constant row (p_1 box) is violated.
 template <int N, class M>
 HVP_HD inline bool setup_lane(LaneQp<N, M>& q, const hvp_system& S, const Consts& C, int role, const double* prm,
-                              uint64_t code, int K = N) {
+                              uint64_t code, int K = N, double rlo = 0.0, double rhi = -1.0) {
     const double p0 = prm[0], v0 = prm[1];
     const double* xf = prm + 2;
     const double* xb = prm + 2 + 2 * (N + 1);
@@ -787,24 +791,43 @@ HVP_HD inline bool setup_lane(LaneQp<N, M>& q, const hvp_system& S, const Consts
     q.has_sf = (role & HVP_ROLE_SAFE_FRONT) != 0;
     q.has_sb = (role & HVP_ROLE_SAFE_BACK) != 0;
     double a[N], b[N], c[N];
+    unsigned ucost = 0;      // steps carrying their input cost
+    bool relax = rlo <= rhi;  // [rlo, rhi] = exact interval of v_K (branch and bound)
 #pragma unroll
     for (int k = 0; k < N; ++k) {
-        // steps k >= K are RELAXED (branch-and-bound bound problem): their region is free, so
-        // the input rows are dropped (inert bounds) and so is their input cost (>= 0) below;
-        // what remains is a valid lower bound of every completion of the fixed prefix.
-        const int r = code_region(code, k);
+        // steps k >= K are RELAXED (branch-and-bound bound problem, hvp_ipm.h:relax_step): v_{k+1}
+        // keeps the interval reachable from v_K and, when the regions step k may take share
+        // (a, c), the step takes the virtual region (a, b_max, c) with its input rows and cost;
+        // otherwise the input rows and input cost are dropped.  What remains is a valid lower
+        // bound of every completion of the fixed prefix.
         const bool fixed = k < K;
-        a[k] = fixed ? S.a[r] : 1.0;
-        b[k] = fixed ? S.b[r] : 1.0;
-        c[k] = fixed ? S.c[r] : 0.0;
+        int vr = -1;
+        double bm = 1.0, nlo = S.vmin, nhi = S.vmax;
+        if (!fixed && relax) {
+            bool dead;
+            vr = relax_step(S, C, k, rlo, rhi, nlo, nhi, bm, dead);
+            relax = !dead;
+            rlo = nlo;
+            rhi = nhi;
+        }
+        const bool on = fixed || vr >= 0;
+        const int r = fixed ? code_region(code, k) : (vr >= 0 ? vr : 0);
+        a[k] = on ? S.a[r] : 1.0;
+        b[k] = fixed ? S.b[r] : (vr >= 0 ? bm : 1.0);
+        c[k] = on ? S.c[r] : 0.0;
+        ucost |= on ? 1u << k : 0u;
         q.mem.set(F_AM, k, a[k]);
-        q.mem.set(F_ULO, k, fixed ? c[k] + b[k] * S.umin : -1e30);
-        q.mem.set(F_UHI, k, fixed ? c[k] + b[k] * S.umax : 1e30);
-        // bounds on v_{k+1}: region sigma_{k+1} (if fixed) intersected with the state box
+        q.mem.set(F_ULO, k, on ? c[k] + b[k] * S.umin : -1e30);
+        q.mem.set(F_UHI, k, on ? c[k] + b[k] * S.umax : 1e30);
+        // bounds on v_{k+1}: region sigma_{k+1} (if fixed) intersected with the state box; a
+        // relaxed v_{k+1} its reachable interval (v_K's own is implied by the prefix)
         if (k + 1 < K) {
             const int r1 = code_region(code, k + 1);
             q.mem.set(F_VLO, k, fmax(S.vmin, S.vlo[r1]));
             q.mem.set(F_VHI, k, fmin(S.vmax, S.vhi[r1]));
+        } else if (!fixed && relax) {
+            q.mem.set(F_VLO, k, fmax(S.vmin, nlo));
+            q.mem.set(F_VHI, k, fmin(S.vmax, nhi));
         } else {
             q.mem.set(F_VLO, k, S.vmin);
             q.mem.set(F_VHI, k, S.vmax);
@@ -887,7 +910,8 @@ HVP_HD inline bool setup_lane(LaneQp<N, M>& q, const hvp_system& S, const Consts
         ubar[k] = k == 0 ? -(a[0] * v0 + c[0]) * ib : -c[k] * ib;
         gk[k] = ib;
         gkm[k] = k == 0 ? 0.0 : -a[k] * ib;
-        const double w2 = k < K ? 2.0 * C.Qu : 0.0;
+        const bool uk = (ucost >> k) & 1u;
+        const double w2 = uk ? 2.0 * C.Qu : 0.0;
         q.H[tri(k, k)] += w2 * gk[k] * gk[k];
         q.f[k] += w2 * ubar[k] * gk[k];
         if (k >= 1) {
@@ -895,7 +919,7 @@ HVP_HD inline bool setup_lane(LaneQp<N, M>& q, const hvp_system& S, const Consts
             q.H[tri(k, k - 1)] += w2 * gk[k] * gkm[k];
             q.f[k - 1] += w2 * ubar[k] * gkm[k];
         }
-        C0 += k < K ? C.Qu * ubar[k] * ubar[k] : 0.0;
+        C0 += uk ? C.Qu * ubar[k] * ubar[k] : 0.0;
     }
     if (C.Qdu != 0.0) {
 #pragma unroll
@@ -962,8 +986,15 @@ HVP_HD inline double direct_cost(const LaneQp<N, M>& q, const hvp_system& S_in, 
         if (k < N) {
             const int r = code_region(code, k);
             const double vn = q.y[k];
-            const double u = (vn - S.a[r] * v - S.c[r]) / S.b[r];
-            if (k < K) J += C.Qu * u * u;  // relaxed steps carry no input cost
+            double u = (vn - S.a[r] * v - S.c[r]) / S.b[r];
+            if (k < K) {
+                J += C.Qu * u * u;
+            } else if (q.ulo(k) > -1e29) {  // relaxed step in a virtual region (setup_lane)
+                const double bv = (q.mem.get(F_UHI, k) - q.ulo(k)) / (S.umax - S.umin);
+                const double cv = q.ulo(k) - bv * S.umin;
+                const double uv = (vn - q.am(k) * v - cv) / bv;
+                J += C.Qu * uv * uv;
+            }
             if (k >= 1 && k < K) J += C.Qdu * (u - uprev) * (u - uprev);
             uprev = u;
             p = p + S.ts * v;
@@ -1007,6 +1038,45 @@ HVP_HD inline bool reach_step(double lo, double hi, double a, double b, double c
     *nhi = U;
     return true;
 }
+
+// Child of a node at depth k (prefix of k steps, v_k in [lo, hi]) taking region r at step k:
+// false if r is not reachable (band disjoint from [lo, hi] or no admissible input / accel).
+HVP_HD inline bool bnb_child(const hvp_system& S, const Consts& C, int k, double lo, double hi, int r, double* nlo,
+                             double* nhi) {
+    const double tol = 1e-9 * (1.0 + fabs(fmin(hi, S.vhi[r])));
+    double ilo = fmax(lo, S.vlo[r]), ihi = fmin(hi, S.vhi[r]);
+    if (ilo > ihi + tol) return false;
+    if (ilo > ihi) ilo = ihi = 0.5 * (ilo + ihi);
+    return reach_step(ilo, ihi, S.a[r], S.b[r], S.c[r], S.umin, S.umax, C.dec[k], C.acc[k], S.vmin, S.vmax, nlo, nhi);
+}
+
+// Tail relaxation, one undecided step k (oracle: hvp_oracle.c:relax_tail).  From the interval
+// [lo, hi] of v_k: the hull [nlo, nhi] of v_{k+1} over every region step k may still take and,
+// when all of them share the velocity dynamics (a, c) with b > 0 (and umin <= 0 <= umax), the
+// VIRTUAL region of the step: dynamics (a, bmax, c) with the input box and cost on
+// s = u b_r / bmax, a valid relaxation of every region's input (|s| <= |u|).  Returns the first
+// such region (virt) or -1; dead = no region is reachable (the relaxation stops there).
+HVP_HD inline int relax_step(const hvp_system& S, const Consts& C, int k, double lo, double hi, double& nlo,
+                             double& nhi, double& bmax, bool& dead) {
+    nlo = 1e300;
+    nhi = -1e300;
+    bmax = 0.0;
+    int first = -1;
+    bool shared = S.umin <= 0.0 && S.umax >= 0.0 && S.umax > S.umin;
+    for (int r = 0; r < S.n_regions; ++r) {
+        double a, b;
+        if (!bnb_child(S, C, k, lo, hi, r, &a, &b)) continue;
+        nlo = fmin(nlo, a);
+        nhi = fmax(nhi, b);
+        if (first < 0) first = r;
+        else if (S.a[r] != S.a[first] || S.c[r] != S.c[first]) shared = false;
+        if (!(S.b[r] > 0.0)) shared = false;
+        bmax = fmax(bmax, S.b[r]);
+    }
+    dead = first < 0;
+    return shared && !dead ? first : -1;
+}
+
 
 // Depth-first enumeration of every feasible region sequence in lexicographic order.
 // visit(code) is called for each; returns the count.  Iterative (explicit stack).

@@ -333,13 +333,13 @@ __device__ inline double inc_of(const Workspace& ws, int inst) { return key_cost
 // QP path (both paths in one kernel pushed the lane kernels to 256 VGPRs + scratch spills)
 template <int N, int BS, bool ADMM>
 __device__ inline int bnb_qp(hvp::LaneQp<N, LdsMem<N, BS>>& q, const hvp_system& S, const hvp::Consts& C, int rl,
-                             const double* prm, uint64_t code, int K, double& cost) {
+                             const double* prm, uint64_t code, int K, double lo, double hi, double& cost) {
     int it = 0, st;
     if constexpr (ADMM) {
         st = hvp::solve_admm_lane<N>(q, S, C, rl, prm, code, K, kGiMaxIter<N>, it);
         cost = st == hvp::GI_OK ? hvp::admm_direct_cost<N>(q, S, C, rl, prm, code, K) : 0.0;
     } else {
-        hvp::setup_lane<N>(q, S, C, rl, prm, code, K);
+        hvp::setup_lane<N>(q, S, C, rl, prm, code, K, lo, hi);  // tail relaxed from v_K in [lo, hi]
         st = hvp::solve_gi<N>(q, C, kGiMaxIter<N>, it);
         cost = st == hvp::GI_OK ? hvp::direct_cost<N>(q, S, C, rl, prm, code, K) : 0.0;
     }
@@ -374,7 +374,7 @@ __global__ __launch_bounds__(kBnbBlock<N>) HVP_LANE_OCC void k_bnb_root(int B, c
         hvp::LaneQp<N, LdsMem<N, BS>> q;
         q.mem.lane = threadIdx.x;
         double c0;
-        int it = bnb_qp<N, BS, ADMM>(q, S, C, rl, prm, 0, 0, c0);
+        int it = bnb_qp<N, BS, ADMM>(q, S, C, rl, prm, 0, 0, v0, v0, c0);
         ++nodes;
         iters += it >= 0 ? it : -1 - it;
         if (it >= 0) {
@@ -385,7 +385,7 @@ __global__ __launch_bounds__(kBnbBlock<N>) HVP_LANE_OCC void k_bnb_root(int B, c
             uint64_t code;
             if (hvp::bnb_dive<N>(S, C, v0, ystar, &code)) {
                 double c1;
-                it = bnb_qp<N, BS, ADMM>(q, S, C, rl, prm, code, N, c1);
+                it = bnb_qp<N, BS, ADMM>(q, S, C, rl, prm, code, N, 0.0, -1.0, c1);
                 ++nodes;
                 iters += it >= 0 ? it : -1 - it;
                 if (it >= 0) inc = c1;
@@ -600,7 +600,7 @@ __global__ __launch_bounds__(kBnbBlock<N>) HVP_LANE_OCC void k_bnb_bound(int k, 
         hvp::LaneQp<N, LdsMem<N, BS>> q;
         q.mem.lane = threadIdx.x;
         double c;
-        const int it = bnb_qp<N, BS, ADMM>(q, S, C, rl, prm, code, k, c);
+        const int it = bnb_qp<N, BS, ADMM>(q, S, C, rl, prm, code, k, ws.nd_lo[dst][t], ws.nd_hi[dst][t], c);
         const bool ok = it >= 0;
         const int its = ok ? it : -1 - it;
         iter_sum += (unsigned long long)its;

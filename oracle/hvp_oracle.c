@@ -870,6 +870,59 @@ static int make_vmodel(const or_model* md, or_vmodel* vm) {
     return 0;
 }
 
+/* Tail relaxation of one vehicle's undecided steps k >= K (centralised branch and bound):
+ *  - v_k stays in the interval reachable from [lo, hi] = the exact interval of v_K, propagated as
+ *    the hull over the regions step k may still take (the regions whose band meets the interval);
+ *  - when all those regions share the velocity dynamics (a, c) and b > 0, with ul <= 0 <= uh, the
+ *    step takes the VIRTUAL region (a, b_max, c): every completion's input u (region r) maps to
+ *    s = u b_r / b_max, which meets v' = a v + b_max s + c and the input box, with Qu s^2 <= Qu u^2;
+ *    otherwise the velocity dynamics, input rows and input cost of the step are dropped.
+ * Both keep the QP of the prefix a lower bound of every completion. */
+typedef struct {
+    double vlo[OR_MAX_N + 1], vhi[OR_MAX_N + 1]; /* interval of v_k, k = K..N */
+    int virt[OR_MAX_N];                          /* region index carrying (a, c), or -1 */
+    double bmax[OR_MAX_N];
+    double blo, bhi; /* state box of v */
+} or_relax;
+
+static int g_cent_relax = 1;
+void oracle_set_cent_relax(int on) { g_cent_relax = on; }
+
+static void relax_tail(const or_vmodel* vm, int nreg, const or_cfg* cf, int K, double lo, double hi, or_relax* X) {
+    const int N = cf->N;
+    for (int k = 0; k < N; ++k) X->virt[k] = -1;
+    X->blo = vm->blo; X->bhi = vm->bhi;
+    for (int k = 0; k <= N; ++k) { X->vlo[k] = vm->blo; X->vhi[k] = vm->bhi; }
+    if (!g_cent_relax) return;
+    X->vlo[K] = lo; X->vhi[K] = hi;
+    for (int k = K; k < N; ++k) {
+        const double dec = cf->a_dec * cf->ts + k * cf->tight, acc = cf->a_acc * cf->ts - k * cf->tight;
+        double nlo = OR_BIG, nhi = -OR_BIG, bmax = 0.0;
+        int first = -1, shared = vm->ul <= 0.0 && vm->uh >= 0.0 && vm->uh > vm->ul;
+        for (int r = 0; r < nreg; ++r) {
+            if (!vm->rok[r]) continue;
+            double ilo = fmax(X->vlo[k], vm->rlo[r]), ihi = fmin(X->vhi[k], vm->rhi[r]);
+            if (ilo > ihi + 1e-9 * (1.0 + fabs(ihi))) continue;
+            if (ilo > ihi) ilo = ihi = 0.5 * (ilo + ihi);
+            double a, b;
+            if (!next_interval(ilo, ihi, vm->a[r], vm->b[r], vm->c[r], vm->ul, vm->uh, dec, acc, vm->blo, vm->bhi, &a,
+                               &b))
+                continue;
+            nlo = fmin(nlo, a); nhi = fmax(nhi, b);
+            if (first < 0) first = r;
+            else if (vm->a[r] != vm->a[first] || vm->c[r] != vm->c[first]) shared = 0;
+            if (!(vm->b[r] > 0.0)) shared = 0;
+            bmax = fmax(bmax, vm->b[r]);
+        }
+        if (first < 0) { /* no completion: keep the plain relaxation from here on */
+            for (int j = k + 1; j <= N; ++j) { X->vlo[j] = vm->blo; X->vhi[j] = vm->bhi; }
+            return;
+        }
+        if (shared) { X->virt[k] = first; X->bmax[k] = bmax; }
+        X->vlo[k + 1] = nlo; X->vhi[k + 1] = nhi;
+    }
+}
+
 typedef void (*or_visit)(const int* sigma, void* ctx);
 
 static void dfs(const or_vmodel* vm, int nreg, const or_cfg* cf, int k, double lo, double hi, int* sigma,
@@ -1429,7 +1482,7 @@ static lin CX(const or_cent_layout* CL, const double* x0, int N, int i, int k, i
 }
 
 static int build_cent_qp(or_qp* qp, const or_model* md, const or_cfg* cf, or_cent_layout* CL, const int* sigma,
-                         const int* K, const double* x0, const double* xl) {
+                         const int* K, const or_relax* RX, const double* x0, const double* xl) {
     const int N = cf->N, n = CL->n;
     int nz = 0;
     for (int i = 0; i < n; ++i) {
@@ -1447,13 +1500,14 @@ static int build_cent_qp(or_qp* qp, const or_model* md, const or_cfg* cf, or_cen
         const or_model* m = &md[i];
         const int* sg = sigma + i * N;
         for (int k = 0; k < N; ++k) {
-            int r = k < K[i] ? sg[k] : 0;
-            for (int c = 0; c < (k < K[i] ? 2 : 1); ++c) {
+            const int virt = k < K[i] ? -1 : RX[i].virt[k]; /* relaxed step in its virtual region */
+            int r = k < K[i] ? sg[k] : (virt >= 0 ? virt : 0);
+            for (int c = 0; c < (k < K[i] || virt >= 0 ? 2 : 1); ++c) {
                 lin e = CX(CL, x0, N, i, k + 1, c);
                 for (int j = 0; j < 2; ++j) { lin xj = CX(CL, x0, N, i, k, j); e = lin_axpy(-m->A[r][c][j], &xj, &e); }
                 lin uk = lin_const(0.0);
                 lin_add(&uk, CL->uo[i] + k, 1.0);
-                e = lin_axpy(-m->B[r][c], &uk, &e);
+                e = lin_axpy(-(virt >= 0 && c == 1 ? RX[i].bmax[k] : m->B[r][c]), &uk, &e);
                 if (qp->neq >= OR_MAX_EQ) return 0;
                 qp_add_eq(qp, &e, m->c[r][c]);
             }
@@ -1468,6 +1522,12 @@ static int build_cent_qp(or_qp* qp, const or_model* md, const or_cfg* cf, or_cen
                 e = lin_axpy(m->R[r][row], &uk, &e);
                 qp_add_le(qp, &e, m->T[r][row]);
             }
+        }
+        for (int k = K[i] + 1; k <= N; ++k) { /* reachable interval of relaxed v_k (v_K's is implied) */
+            lin v = CX(CL, x0, N, i, k, 1);
+            if (RX[i].vhi[k] < RX[i].bhi) qp_add_le(qp, &v, RX[i].vhi[k]);
+            lin nv = lin_axpy(-1.0, &v, &(lin){.n = 0, .cst = 0.0});
+            if (RX[i].vlo[k] > RX[i].blo) qp_add_le(qp, &nv, -RX[i].vlo[k]);
         }
         for (int k = 1; k <= N; ++k)
             for (int row = 0; row < m->nd; ++row) {
@@ -1531,7 +1591,8 @@ static int build_cent_qp(or_qp* qp, const or_model* md, const or_cfg* cf, or_cen
     }
     double Qu[2][2] = {{cf->Qu, 0}, {0, 0}}, Qdu[2][2] = {{cf->Qdu, 0}, {0, 0}};
     for (int i = 0; i < n; ++i) {
-        for (int k = 0; k < K[i]; ++k) {
+        for (int k = 0; k < N; ++k) {
+            if (k >= K[i] && RX[i].virt[k] < 0) continue;
             lin e[2]; e[0] = lin_const(0.0); lin_add(&e[0], CL->uo[i] + k, 1.0); e[1] = lin_const(0.0);
             add_norm(qp, NULL, cf, e, Qu, 1);
         }
@@ -1549,8 +1610,8 @@ static int build_cent_qp(or_qp* qp, const or_model* md, const or_cfg* cf, or_cen
 }
 
 /* direct objective of a centralised solution z (relaxed steps without input cost) */
-static double cent_objective(const or_cfg* cf, const or_cent_layout* CL, const int* K, const double* x0,
-                             const double* xl, const double* z) {
+static double cent_objective(const or_cfg* cf, const or_cent_layout* CL, const int* K, const or_relax* RX,
+                             const double* x0, const double* xl, const double* z) {
     const int N = cf->N, n = CL->n;
     double J = 0.0;
     for (int k = 0; k <= N; ++k)
@@ -1574,7 +1635,8 @@ static double cent_objective(const or_cfg* cf, const or_cent_layout* CL, const i
             }
         }
     for (int i = 0; i < n; ++i)
-        for (int k = 0; k < K[i]; ++k) {
+        for (int k = 0; k < N; ++k) {
+            if (k >= K[i] && RX[i].virt[k] < 0) continue;
             double u = z[CL->uo[i] + k];
             J += cf->Qu * u * u;
             if (k + 1 < K[i]) { double du = z[CL->uo[i] + k + 1] - u; J += cf->Qdu * du * du; }
@@ -1599,14 +1661,17 @@ typedef struct {
     int* leaf_sig;
 } or_cent;
 
-static double cent_qp(or_cent* C, const int* sigma, const int* K, int leaf) {
+/* lo, hi: per vehicle the exact interval of v_{K[i]} (the tail relaxation starts from it) */
+static double cent_qp(or_cent* C, const int* sigma, const int* K, const double* lo, const double* hi, int leaf) {
     C->n_qp++;
-    if (build_cent_qp(C->qp, C->md, C->cf, &C->CL, sigma, K, C->x0, C->xl) <= 0 || C->qp->infeasible_const)
+    or_relax RX[OR_MAX_VEH];
+    for (int i = 0; i < C->n; ++i) relax_tail(&C->vm[i], C->md[i].nreg, C->cf, K[i], lo[i], hi[i], &RX[i]);
+    if (build_cent_qp(C->qp, C->md, C->cf, &C->CL, sigma, K, RX, C->x0, C->xl) <= 0 || C->qp->infeasible_const)
         return INFINITY;
     or_result r = ipm_solve(C->qp, C->w, C->maxit);
     C->iters += r.iters;
     if (!r.converged) return leaf ? INFINITY : -INFINITY;
-    return cent_objective(C->cf, &C->CL, K, C->x0, C->xl, C->w->z);
+    return cent_objective(C->cf, &C->CL, K, RX, C->x0, C->xl, C->w->z);
 }
 
 /* time-major decision order d -> (k = d / n, i = d % n); lexicographic key in that order */
@@ -1617,8 +1682,8 @@ static int cent_less(const int* a, const int* b, int n, int N) {
     return 0;
 }
 
-static void cent_leaf(or_cent* C, const int* sigma, const int* K) {
-    double obj = cent_qp(C, sigma, K, 1);
+static void cent_leaf(or_cent* C, const int* sigma, const int* K, const double* lo, const double* hi) {
+    double obj = cent_qp(C, sigma, K, lo, hi, 1);
     if (!isfinite(obj)) return;
     const int nN = C->n * C->N;
     if (C->nleaf == C->capleaf) {
@@ -1650,7 +1715,7 @@ void oracle_set_cent_cap(long cap) { g_cent_cap = cap; }
 static void cent_dfs(or_cent* C, int d, int* sigma, int* K, double* lo, double* hi) {
     const int n = C->n, N = C->N;
     if (g_cent_cap > 0 && C->n_qp >= g_cent_cap) return;
-    if (d == n * N) { cent_leaf(C, sigma, K); return; }
+    if (d == n * N) { cent_leaf(C, sigma, K, lo, hi); return; }
     const int k = d / n, i = d % n;
     const or_vmodel* vm = &C->vm[i];
     const or_cfg* cf = C->cf;
@@ -1668,7 +1733,10 @@ static void cent_dfs(or_cent* C, int d, int* sigma, int* K, double* lo, double* 
             continue;
         sigma[i * N + k] = r;
         K[i] = k + 1;
-        lb[nch] = (d + 1 == n * N || C->exhaustive) ? 0.0 : cent_qp(C, sigma, K, 0);
+        const double slo = lo[i], shi = hi[i];
+        lo[i] = nlo; hi[i] = nhi;
+        lb[nch] = (d + 1 == n * N || C->exhaustive) ? 0.0 : cent_qp(C, sigma, K, lo, hi, 0);
+        lo[i] = slo; hi[i] = shi;
         K[i] = k;
         child[nch] = r; clo[nch] = nlo; chi[nch] = nhi;
         nch++;
@@ -1748,7 +1816,7 @@ int oracle_solve_cent(int n, int N, int nreg, int nsr, const double* S, const do
             for (int k = 0; k < N; ++k) sigma_out[i * N + k] = C->best[i * N + k];
         }
         /* re-evaluate the winner for its exact objective and trajectory */
-        double obj = cent_qp(C, C->best, K, 1);
+        double obj = cent_qp(C, C->best, K, lo, hi, 1);
         info_out[0] = obj;
         for (int i = 0; i < n; ++i) {
             x_out[i * 2 * (N + 1)] = x0[2 * i];

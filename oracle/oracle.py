@@ -252,6 +252,8 @@ def lib():
         L.oracle_set_cent_gap.restype = None
         L.oracle_set_cent_cap.argtypes = [ctypes.c_long]
         L.oracle_set_cent_cap.restype = None
+        L.oracle_set_cent_relax.argtypes = [ctypes.c_int]
+        L.oracle_set_cent_relax.restype = None
         L.oracle_set_method.argtypes = [c_int]
         L.oracle_set_method.restype = None
         _lib = L
@@ -759,6 +761,12 @@ def set_cent_gap(gap: float) -> None:
 def set_cent_cap(cap: int) -> None:
     """QP budget per solve_cent call (0 = none; a capped search is a timing sample, not a result)."""
     lib().oracle_set_cent_cap(int(cap))
+
+
+def set_cent_relax(on: bool) -> None:
+    """Tail relaxation of the centralised search: True (default) = reachable intervals + virtual
+    region (hvp_oracle.c:relax_tail), False = undecided steps without velocity dynamics / inputs."""
+    lib().oracle_set_cent_relax(int(bool(on)))
 
 
 def solve_cent(systems: list[dict], cfg: Cfg, N: int, x0, leader_x, leader_index: int = 0,
