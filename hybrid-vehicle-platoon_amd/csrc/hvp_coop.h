@@ -103,6 +103,8 @@ struct Lane {
     bool has_sf, has_sb;
     // step t = lane (valid if t < N)
     double am, vlo, vhi, ulo, uhi, dec, acc;
+    double ub, uc;  // input map of step t: u = (v_{t+1} - am v_t - uc) / ub
+    bool ucost;     // step t carries its input cost (fixed, or relaxed in a virtual region)
     double hf, hb;  // prefix rows of m = t - 1 (t >= 1)
     double y;       // y_t
     double f;       // linear term f_t
@@ -176,10 +178,13 @@ __device__ inline StepForm admm_form(const Consts& C, int role, const double* pr
     return StepForm{Wpp, Wpv, Wvv, lp, lv};
 }
 
-// Lane data + this lane's Hessian row (into LDS J area, row t) for region code / relaxation K.
+// Lane data + this lane's Hessian row (into LDS J area, row t) for region code / relaxation K;
+// [lo, hi] (lo <= hi) = exact interval of v_K: the decentralised tail relaxation of
+// hvp_ipm.h:relax_step (as setup_lane), each lane propagating it up to its own step.
 template <int N>
 __device__ inline bool setup(Lane<N>& L, GroupLds& S_lds, const hvp_system& S, const Consts& C, int role,
-                             const double* prm, uint64_t code, int K, uint64_t hs) {
+                             const double* prm, uint64_t code, int K, uint64_t hs, double lo = 0.0,
+                             double hi = -1.0) {
     const int t = lane16();
     const bool admm = C.form == HVP_FORM_ADMM || C.form == HVP_FORM_GADMM;
     const double p0 = prm[0], v0 = prm[1], ts = S.ts;
@@ -190,26 +195,58 @@ __device__ inline bool setup(Lane<N>& L, GroupLds& S_lds, const hvp_system& S, c
     L.pmax = S.pmax;
     L.has_sf = !admm && (role & HVP_ROLE_SAFE_FRONT) != 0;
     L.has_sb = !admm && (role & HVP_ROLE_SAFE_BACK) != 0;
-    // dynamics of step k (relaxed beyond K)
-    auto dyn = [&](int k, double& a, double& b, double& c) {
-        const int r = code_region(code, k);
-        const bool fx = k < K;
-        a = fx ? S.a[r] : 1.0;
-        b = fx ? S.b[r] : 1.0;
-        c = fx ? S.c[r] : 0.0;
-    };
     const int tt = t < N ? t : N - 1;
+    // relaxed steps tt, tt + 1: virtual regions and the reachable interval of v_{tt+1}
+    const bool relax = !admm && lo <= hi;
+    int virt0 = -1, virt1 = -1;
+    double bm0 = 1.0, bm1 = 1.0, rlo = S.vmin, rhi = S.vmax;
+    if (relax && tt + 1 >= K) {
+        const int kend = tt + 1 < N ? tt + 1 : N - 1;
+        for (int k = K; k <= kend; ++k) {
+            double nlo, nhi, bm;
+            bool dead;
+            const int vr = relax_step(S, C, k, lo, hi, nlo, nhi, bm, dead);
+            if (dead) break;
+            if (k == tt) {
+                virt0 = vr;
+                bm0 = bm;
+                rlo = nlo;
+                rhi = nhi;
+            } else {
+                virt1 = vr;
+                bm1 = bm;
+            }
+            lo = nlo;
+            hi = nhi;
+        }
+    }
+    // dynamics of step k in {tt, tt + 1} (t - 1 .. t + 1 when fixed; relaxed beyond K)
+    auto dyn = [&](int k, double& a, double& b, double& c) {
+        const int vr = k == tt ? virt0 : (k == tt + 1 ? virt1 : -1);
+        const bool fx = k < K;
+        const int r = fx ? code_region(code, k) : (vr >= 0 ? vr : 0);
+        const bool on = fx || vr >= 0;
+        a = on ? S.a[r] : 1.0;
+        b = fx ? S.b[r] : (vr >= 0 ? (k == tt ? bm0 : bm1) : 1.0);
+        c = on ? S.c[r] : 0.0;
+    };
     {
         double a, b, c;
         dyn(tt, a, b, c);
-        const bool fx = tt < K;
+        const bool on = tt < K || virt0 >= 0;
         L.am = a;
-        L.ulo = fx ? c + b * S.umin : -1e30;
-        L.uhi = fx ? c + b * S.umax : 1e30;
+        L.ub = b;
+        L.uc = c;
+        L.ucost = on;
+        L.ulo = on ? c + b * S.umin : -1e30;
+        L.uhi = on ? c + b * S.umax : 1e30;
         if (tt + 1 < K) {
             const int r1 = code_region(code, tt + 1);
             L.vlo = fmax(S.vmin, S.vlo[r1]);
             L.vhi = fmin(S.vmax, S.vhi[r1]);
+        } else if (relax && tt >= K) {  // relaxed v_{tt+1}: its reachable interval
+            L.vlo = fmax(S.vmin, rlo);
+            L.vhi = fmin(S.vmax, rhi);
         } else {
             L.vlo = S.vmin;
             L.vhi = S.vmax;
@@ -266,12 +303,12 @@ __device__ inline bool setup(Lane<N>& L, GroupLds& S_lds, const hvp_system& S, c
     if (t < N) {
         double ub, gk, gkm;
         ucoef(t, ub, gk, gkm);
-        if (t < K) {
+        if (L.ucost) {
             Hrow[t] += w2 * gk * gk;
             f += w2 * ub * gk;
             if (t >= 1) Hrow[t - 1] += w2 * gk * gkm;
         }
-        if (t + 1 < N && t + 1 < K) {
+        if (t + 1 < N && (t + 1 < K || virt1 >= 0)) {
             double ub1, gk1, gkm1;
             ucoef(t + 1, ub1, gk1, gkm1);
             Hrow[t] += w2 * gkm1 * gkm1;
@@ -715,9 +752,8 @@ __device__ inline double direct_cost_decent(const Lane<N>& L, const hvp_system& 
     double J = 0.0, u = 0.0;
     if (t < N) {
         J += state_terms(t + 1, pn, vn);
-        const int r = code_region(code, t);
-        u = (vn - S.a[r] * vprev - S.c[r]) / S.b[r];
-        if (t < K) J += C.Qu * u * u;
+        u = (vn - L.am * vprev - L.uc) / L.ub;
+        if (L.ucost) J += C.Qu * u * u;
     }
     const double uprev = __shfl_up(u, 1, G);
     if (t >= 1 && t < N && t < K) J += C.Qdu * (u - uprev) * (u - uprev);
@@ -817,7 +853,7 @@ __device__ inline uint64_t admm_initial_states(Lane<N>& L, const Consts& C, int 
 template <int N>
 __device__ inline int solve_qp(Lane<N>& L, GroupLds& Sg, const hvp_system& S, const Consts& C, int role,
                                const double* prm, uint64_t code, int K, int max_iter, int& iters, double* cost,
-                               unsigned* edge = nullptr) {
+                               unsigned* edge = nullptr, double lo = 0.0, double hi = -1.0) {
     iters = 0;
     if (C.form == HVP_FORM_ADMM || C.form == HVP_FORM_GADMM) {
         uint64_t hs;
@@ -844,7 +880,7 @@ __device__ inline int solve_qp(Lane<N>& L, GroupLds& Sg, const hvp_system& S, co
         return GI_FAIL_ITER;
     }
     gsync();
-    setup<N>(L, Sg, S, C, role, prm, code, K, 0);
+    setup<N>(L, Sg, S, C, role, prm, code, K, 0, lo, hi);
     const int st = solve<N>(L, Sg, C, max_iter, iters);
     if (st != GI_OK) return st;
     *cost = direct_cost_decent<N>(L, S, C, role, prm, code, K);

@@ -429,7 +429,7 @@ __global__ __launch_bounds__(kCoopBlock) void k_bnb_root_coop(int B, const hvp_s
         hvp::coop::Lane<N> L;
         double c0 = 0.0;
         int it = 0;
-        int st = hvp::coop::solve_qp<N>(L, lds[g], S, C, rl, prm, 0, 0, kGiMaxIter<N>, it, &c0);
+        int st = hvp::coop::solve_qp<N>(L, lds[g], S, C, rl, prm, 0, 0, kGiMaxIter<N>, it, &c0, nullptr, prm[1], prm[1]);
         ++nodes;
         iters += it;
         if (st == hvp::GI_OK) {
@@ -500,7 +500,8 @@ __global__ __launch_bounds__(kCoopBlock) void k_bnb_bound_coop(int k, const hvp_
         hvp::coop::Lane<N> L;
         double c = 0.0;
         int it = 0;
-        const int st = hvp::coop::solve_qp<N>(L, lds[g], S, C, rl, prm, code, k, kGiMaxIter<N>, it, &c);
+        const int st = hvp::coop::solve_qp<N>(L, lds[g], S, C, rl, prm, code, k, kGiMaxIter<N>, it, &c, nullptr,
+                                              ws.nd_lo[dst][q], ws.nd_hi[dst][q]);
         const bool ok = st == hvp::GI_OK;
         if (k == N && t < N) ws.task_y[q * N + t] = L.y;
         if (t == 0) {
