@@ -773,23 +773,118 @@ HVP_HD inline int relax_step(const hvp_system& S, const Consts& C, int k, double
                              double& nhi, double& bmax, bool& dead);
 
 // ------------------------------------------------------------------ problem setup
-// Builds the lane QP for instance params (x0, x_front, x_back, leader_x) and region code.
-// Returns false when a sigma-independent constant row (p_1 box) is violated.
-template <int N, class M>
-HVP_HD inline bool setup_lane(LaneQp<N, M>& q, const hvp_system& S, const Consts& C, int role, const double* prm,
-                              uint64_t code, int K = N, double rlo = 0.0, double rhi = -1.0) {
+// The lane QP of (instance params (x0, x_front, x_back, leader_x), region code) is assembled in
+// two parts:
+//   setup_track  sigma-independent: the tracking terms (H, f, C0), the safe-distance bounds
+//                (hf, hb) and the constant k = 0, 1 slacks -- the same for every node of an
+//                instance, so the branch-and-bound kernels compute it once per instance
+//                (hvp_lane.h: K_inst_prep) and the node kernels only load it;
+//   setup_input  per region sequence / node: dynamics a, b, c of every step (tail relaxed from
+//                v_K in [rlo, rhi] for branch-and-bound bounds), the input and accel bounds, the
+//                velocity bounds, and the input cost Q_u u^2 + Q_du du^2 added to (H, f, C0).
+// setup_lane = both, in this order (H and f accumulate exactly as one pass would).
+
+// tracking part: H (packed lower, NT), f (N), C0, hf / hb (N - 1): bounds of the safe rows of
+// steps 2..N (an absent neighbour gets an INERT row: its bound lies beyond any position
+// reachable under the velocity box, so the row can never be active and every lane runs the same
+// branch-free code).  Returns P1 = p_0 + ts v_0.
+template <int N>
+HVP_HD inline double setup_track(const hvp_system& S, const Consts& C, int role, const double* prm, double* H,
+                                 double* f, double& C0_out, double* hf, double* hb) {
     const double p0 = prm[0], v0 = prm[1];
     const double* xf = prm + 2;
     const double* xb = prm + 2 + 2 * (N + 1);
     const double* xl = prm + 2 + 4 * (N + 1);
     const double ts = S.ts;
+    const double P1 = p0 + ts * v0;
+    const bool has_sf = (role & HVP_ROLE_SAFE_FRONT) != 0, has_sb = (role & HVP_ROLE_SAFE_BACK) != 0;
+#pragma unroll
+    for (int j = 0; j < N - 1; ++j) {
+        const double reach = ts * (j + 1);
+        hf[j] = has_sf ? xf[j + 2] - C.d_safe : P1 + reach * S.vmax + 100.0;
+        hb[j] = has_sb ? xb[j + 2] + C.d_safe : P1 + reach * S.vmin - 100.0;
+    }
+#pragma unroll
+    for (int i = 0; i < N * (N + 1) / 2; ++i) H[i] = 0.0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) f[i] = 0.0;
+    double C0 = 0.0;
+    // quadratic form  x'Wx + 2 l'x + c0  of the tracking terms at step k, x = (p, v)
+    const bool tf = (role & HVP_ROLE_TRACK_FRONT) != 0, tb = (role & HVP_ROLE_TRACK_BACK) != 0;
+    const bool tl = (role & HVP_ROLE_TRACK_LEADER) != 0, lsp = (role & HVP_ROLE_LEADER_SPACING) != 0;
+    const double Qpp = C.Qpp, Qpv = C.Qpv, Qvv = C.Qvv, t0 = C.t0, d0 = C.d0;
+#pragma unroll
+    for (int k = 0; k <= N; ++k) {
+        double Wpp = 0, Wpv = 0, Wvv = 0, lp = 0, lv = 0, cc = 0;
+        // e = M x + r ; adds M'QM, M'Q r, r'Q r
+        auto add = [&](double m00, double m01, double m11, double r0, double r1) {
+            // M = [[m00, m01], [0, m11]]
+            const double qa = Qpp * m00;                                           // (QM)[0][0]
+            const double qc = Qpp * m01 + Qpv * m11, qd = Qpv * m01 + Qvv * m11;  // (QM)[0][1], (QM)[1][1]
+            Wpp += m00 * qa;
+            Wpv += m00 * qc;
+            Wvv += m01 * qc + m11 * qd;
+            const double Qr0 = Qpp * r0 + Qpv * r1, Qr1 = Qpv * r0 + Qvv * r1;
+            lp += m00 * Qr0;
+            lv += m01 * Qr0 + m11 * Qr1;
+            cc += r0 * Qr0 + r1 * Qr1;
+        };
+        const int K1 = N + 1;
+        if (tf) add(1.0, t0, 1.0, d0 - xf[k], -xf[K1 + k]);
+        if (tb) add(-1.0, 0.0, -1.0, xb[k] + t0 * xb[K1 + k] + d0, xb[K1 + k]);
+        if (tl) {
+            if (lsp) add(1.0, t0, 1.0, d0 - xl[k], -xl[K1 + k]);
+            else add(1.0, 0.0, 1.0, -xl[k], -xl[K1 + k]);
+        }
+        // x_k = xbar + Gamma y : p = pbar + ts*prefix(0..k-2), v = vbar + e_{k-1}
+        const double pbar = k == 0 ? p0 : P1;
+        const double vbar = k == 0 ? v0 : 0.0;
+        // gradient of the quadratic form at xbar
+        const double gp = 2.0 * (Wpp * pbar + Wpv * vbar + lp);
+        const double gv = 2.0 * (Wpv * pbar + Wvv * vbar + lv);
+        C0 += Wpp * pbar * pbar + 2.0 * Wpv * pbar * vbar + Wvv * vbar * vbar + 2.0 * (lp * pbar + lv * vbar) + cc;
+        if (k >= 1) {
+            const int jv = k - 1;  // v_k = y[jv]
+            H[tri(jv, jv)] += 2.0 * Wvv;
+            f[jv] += gv;
+            // prefix part (indices 0..k-2) with weight ts
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                if (i > k - 2) break;
+                f[i] += ts * gp;
+#pragma unroll
+                for (int i2 = 0; i2 <= i; ++i2) H[tri(i, i2)] += 2.0 * Wpp * ts * ts;
+                // cross p-v: 2 * Wpv * (ts e_i)(e_jv)' symmetric ; jv > i always
+                H[tri(jv, i)] += 2.0 * Wpv * ts;
+            }
+        }
+    }
+    // constant slacks of k = 0, 1 (p_0, p_1 fixed)
+    if (has_sf) C0 += C.w * (fmax(0.0, p0 - xf[0] + C.d_safe) + fmax(0.0, P1 - xf[1] + C.d_safe));
+    if (has_sb) C0 += C.w * (fmax(0.0, xb[0] + C.d_safe - p0) + fmax(0.0, xb[1] + C.d_safe - P1));
+    C0_out = C0;
+    return P1;
+}
+
+// lane scalars of the instance (the p_1 row is sigma-independent).  Returns false when the
+// constant row p_1 in [pmin, pmax] is violated.
+template <int N, class M>
+HVP_HD inline bool setup_scalars(LaneQp<N, M>& q, const hvp_system& S, int role, double p0, double v0) {
     q.v0 = v0;
-    q.ts = ts;
-    q.P1 = p0 + ts * v0;
+    q.ts = S.ts;
+    q.P1 = p0 + S.ts * v0;
     q.pmin = S.pmin;
     q.pmax = S.pmax;
     q.has_sf = (role & HVP_ROLE_SAFE_FRONT) != 0;
     q.has_sb = (role & HVP_ROLE_SAFE_BACK) != 0;
+    return q.P1 >= S.pmin - 1e-9 * (1.0 + fabs(S.pmin)) && q.P1 <= S.pmax + 1e-9 * (1.0 + fabs(S.pmax));
+}
+
+// per-node part (see above); q.H, q.f, q.C0 hold the tracking part on entry
+template <int N, class M>
+HVP_HD inline void setup_input(LaneQp<N, M>& q, const hvp_system& S, const Consts& C, uint64_t code, int K = N,
+                               double rlo = 0.0, double rhi = -1.0) {
+    const double v0 = q.v0;
     double a[N], b[N], c[N];
     unsigned ucost = 0;      // steps carrying their input cost
     bool relax = rlo <= rhi;  // [rlo, rhi] = exact interval of v_K (branch and bound)
@@ -833,77 +928,10 @@ HVP_HD inline bool setup_lane(LaneQp<N, M>& q, const hvp_system& S, const Consts
             q.mem.set(F_VHI, k, S.vmax);
         }
     }
-    // step-1 rows carry the constant v0 on the left: U: v1 - a0 v0, A: v1 - v0 (handled in for_rows)
-    // An absent neighbour (front / trailer vehicle) gets an INERT safe row instead of none: its
-    // bound lies beyond any position reachable under the velocity box, so the row can never be
-    // active and the optimum is unchanged, while every lane runs the same branch-free code.
-#pragma unroll
-    for (int j = 0; j < N - 1; ++j) {
-        const double reach = ts * (j + 1);
-        q.mem.set(F_HF, j, q.has_sf ? xf[j + 2] - C.d_safe : q.P1 + reach * S.vmax + 100.0);
-        q.mem.set(F_HB, j, q.has_sb ? xb[j + 2] + C.d_safe : q.P1 + reach * S.vmin - 100.0);
-    }
-
-    // ---- cost: 1/2 y'Hy + f'y + C0
-#pragma unroll
-    for (int i = 0; i < LaneQp<N, M>::NT; ++i) q.H[i] = 0.0;
-#pragma unroll
-    for (int i = 0; i < N; ++i) q.f[i] = 0.0;
-    double C0 = 0.0;
-    // quadratic form  x'Wx + 2 l'x + c0  of the tracking terms at step k, x = (p, v)
-    const bool tf = (role & HVP_ROLE_TRACK_FRONT) != 0, tb = (role & HVP_ROLE_TRACK_BACK) != 0;
-    const bool tl = (role & HVP_ROLE_TRACK_LEADER) != 0, lsp = (role & HVP_ROLE_LEADER_SPACING) != 0;
-    const double Qpp = C.Qpp, Qpv = C.Qpv, Qvv = C.Qvv, t0 = C.t0, d0 = C.d0;
-#pragma unroll
-    for (int k = 0; k <= N; ++k) {
-        double Wpp = 0, Wpv = 0, Wvv = 0, lp = 0, lv = 0, cc = 0;
-        // e = M x + r ; adds M'QM, M'Q r, r'Q r
-        auto add = [&](double m00, double m01, double m11, double r0, double r1) {
-            // M = [[m00, m01], [0, m11]]
-            const double qa = Qpp * m00, qb = Qpv * m00;               // (QM)[0][0], (QM)[1][0]
-            const double qc = Qpp * m01 + Qpv * m11, qd = Qpv * m01 + Qvv * m11;  // (QM)[0][1], (QM)[1][1]
-            Wpp += m00 * qa;
-            Wpv += m00 * qc;
-            Wvv += m01 * qc + m11 * qd;
-            const double Qr0 = Qpp * r0 + Qpv * r1, Qr1 = Qpv * r0 + Qvv * r1;
-            lp += m00 * Qr0;
-            lv += m01 * Qr0 + m11 * Qr1;
-            cc += r0 * Qr0 + r1 * Qr1;
-            (void)qb;
-        };
-        const int K1 = N + 1;
-        if (tf) add(1.0, t0, 1.0, d0 - xf[k], -xf[K1 + k]);
-        if (tb) add(-1.0, 0.0, -1.0, xb[k] + t0 * xb[K1 + k] + d0, xb[K1 + k]);
-        if (tl) {
-            if (lsp) add(1.0, t0, 1.0, d0 - xl[k], -xl[K1 + k]);
-            else add(1.0, 0.0, 1.0, -xl[k], -xl[K1 + k]);
-        }
-        // x_k = xbar + Gamma y : p = pbar + ts*prefix(0..k-2), v = vbar + e_{k-1}
-        const double pbar = k == 0 ? p0 : q.P1;
-        const double vbar = k == 0 ? v0 : 0.0;
-        // gradient of the quadratic form at xbar
-        const double gp = 2.0 * (Wpp * pbar + Wpv * vbar + lp);
-        const double gv = 2.0 * (Wpv * pbar + Wvv * vbar + lv);
-        C0 += Wpp * pbar * pbar + 2.0 * Wpv * pbar * vbar + Wvv * vbar * vbar + 2.0 * (lp * pbar + lv * vbar) + cc;
-        if (k >= 1) {
-            const int jv = k - 1;  // v_k = y[jv]
-            q.H[tri(jv, jv)] += 2.0 * Wvv;
-            q.f[jv] += gv;
-            // prefix part (indices 0..k-2) with weight ts
-#pragma unroll
-            for (int i = 0; i < N; ++i) {
-                if (i > k - 2) break;
-                q.f[i] += ts * gp;
-#pragma unroll
-                for (int i2 = 0; i2 <= i; ++i2) q.H[tri(i, i2)] += 2.0 * Wpp * ts * ts;
-                // cross p-v: 2 * Wpv * (ts e_i)(e_jv)' symmetric ; jv > i always
-                q.H[tri(jv, i)] += 2.0 * Wpv * ts;
-            }
-        }
-    }
     // control effort  Qu u_k^2 and variation Qdu (u_{k+1} - u_k)^2, u_k = ubar_k + gu_k . y
     // gu_k has entries at k (1/b_k) and k-1 (-a_k/b_k)
     double ubar[N], gk[N], gkm[N];
+    double C0 = q.C0;
 #pragma unroll
     for (int k = 0; k < N; ++k) {
         const double ib = 1.0 / b[k];
@@ -942,11 +970,24 @@ HVP_HD inline bool setup_lane(LaneQp<N, M>& q, const hvp_system& S, const Consts
             C0 += k + 1 < K ? C.Qdu * eb * eb : 0.0;
         }
     }
-    // constant slacks of k = 0, 1 (p_0, p_1 fixed)
-    if (q.has_sf) C0 += C.w * (fmax(0.0, p0 - xf[0] + C.d_safe) + fmax(0.0, q.P1 - xf[1] + C.d_safe));
-    if (q.has_sb) C0 += C.w * (fmax(0.0, xb[0] + C.d_safe - p0) + fmax(0.0, xb[1] + C.d_safe - q.P1));
     q.C0 = C0;
-    return q.P1 >= S.pmin - 1e-9 * (1.0 + fabs(S.pmin)) && q.P1 <= S.pmax + 1e-9 * (1.0 + fabs(S.pmax));
+}
+
+// Builds the lane QP for instance params (x0, x_front, x_back, leader_x) and region code.
+// Returns false when a sigma-independent constant row (p_1 box) is violated.
+template <int N, class M>
+HVP_HD inline bool setup_lane(LaneQp<N, M>& q, const hvp_system& S, const Consts& C, int role, const double* prm,
+                              uint64_t code, int K = N, double rlo = 0.0, double rhi = -1.0) {
+    const bool ok = setup_scalars<N>(q, S, role, prm[0], prm[1]);
+    double hf[N > 1 ? N - 1 : 1], hb[N > 1 ? N - 1 : 1];
+    setup_track<N>(S, C, role, prm, q.H, q.f, q.C0, hf, hb);
+#pragma unroll
+    for (int j = 0; j < N - 1; ++j) {
+        q.mem.set(F_HF, j, hf[j]);
+        q.mem.set(F_HB, j, hb[j]);
+    }
+    setup_input<N>(q, S, C, code, K, rlo, rhi);
+    return ok;
 }
 
 // Objective of the lane's solution evaluated term by term on the trajectory, as the reference

@@ -1,0 +1,1414 @@
+// hvp_lane.h -- kernel templates of the decentralised / ADMM / switching-ADMM lane paths and
+// their launchers (internal).  hvp_lane_inst.hip instantiates the launchers of ONE horizon N
+// per object file (the Makefile builds N = 2..16 in parallel); hvp_kernels.hip holds the C ABI
+// and dispatches to them.  Kernel design: see the comments below and DESIGN.md section 4.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#ifndef HVP_HD
+#define HVP_HD __host__ __device__
+#endif
+#include "hvp.h"
+#include "hvp_internal.h"
+#include "hvp_admm.h"
+#include "hvp_bnb.h"
+#include "hvp_coop.h"
+#include "hvp_gi.h"
+#include "hvp_ipm.h"
+
+namespace hvp_k {
+
+using hvp_detail::fail;
+using hvp_detail::Workspace;
+
+constexpr int kBlock = 256;
+// HVP_METHOD_AUTO: exhaustive enumeration up to this horizon, branch and bound beyond
+constexpr int kAutoEnumMaxN = 0;  // measured: B&B beats enumeration already at N = 5 (profiles/)
+// active-set iteration cap (then the interior-point fallback takes the candidate)
+template <int N>
+constexpr int kGiMaxIter = 8 * hvp::GiConstraintSet<N>::NC;
+
+// ------------------------------------------------------------------ K_enum
+template <int N>
+__global__ __launch_bounds__(kBlock) void k_enum(int B, const hvp_system* __restrict__ systems,
+                                                 const int32_t* __restrict__ sys, const int32_t* __restrict__ role,
+                                                 const double* __restrict__ params, hvp::Consts C, Workspace ws) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B) return;
+    const hvp_system& S = systems[sys[i]];
+    const double* prm = params + (size_t)i * (2 + 6 * (N + 1));
+    const double p0 = prm[0], v0 = prm[1];
+    const double P1 = p0 + S.ts * v0;
+    // sigma-independent constant row: p_1 = p_0 + ts v_0 inside the position box
+    const bool ok = P1 >= S.pmin - 1e-9 * (1.0 + fabs(S.pmin)) && P1 <= S.pmax + 1e-9 * (1.0 + fabs(S.pmax));
+    int cnt = 0;
+    if (ok) cnt = hvp::enumerate_sequences(S, C, v0, [](uint32_t, int) {});
+    ws.inst_cnt[i] = cnt;
+    ws.inst_flag[i] = ok ? 0 : 1;
+    int off = -1;
+    if (cnt > 0) {
+        const unsigned long long o = atomicAdd(&ws.counter[0], (unsigned long long)cnt);
+        if ((long long)o + cnt <= ws.cap) {
+            off = (int)o;
+        } else {
+            // overflow: the part of the reserved range below the capacity is still swept by
+            // K_qp / K_cost (they run over min(reserved, cap)): mark those slots dead
+            for (long long t = (long long)o; t < ws.cap && t < (long long)o + cnt; ++t) ws.task_inst[t] = -1;
+        }
+    }
+    ws.inst_off[i] = off;
+    if (off < 0) return;
+    hvp::enumerate_sequences(S, C, v0, [&](uint32_t code, int j) {
+        ws.task_inst[off + j] = i;
+        ws.task_code[off + j] = code;
+    });
+    (void)role;
+}
+
+// ------------------------------------------------------------------ K_qp
+// Per-lane constant rows in LDS: field f, step j of lane l at s_rows[(f * N + j) * kBlock + l]
+// (consecutive lanes -> consecutive 8-byte words: conflict-free ds_read_b64).  refresh() makes
+// the lane offset opaque at the start of every IPM sweep so the compiler re-reads the rows from
+// LDS instead of hoisting them into VGPRs for the whole solve.
+extern __shared__ double s_rows[];
+
+template <int N, int BS = kBlock>
+struct LdsMem {
+    unsigned lane;
+    __device__ double get(int f, int j) const { return s_rows[(f * N + j) * BS + lane]; }
+    __device__ void set(int f, int j, double x) { s_rows[(f * N + j) * BS + lane] = x; }
+    __device__ void refresh() { asm volatile("" : "+v"(lane)); }
+};
+
+// K_qp: every candidate by the Goldfarb-Idnani active-set method (hvp_gi.h).  A lane whose
+// result fails the KKT verification (or hits the iteration cap) is queued on the fallback list.
+template <int N>
+__global__ __launch_bounds__(kBlock) void k_qp_gi(const hvp_system* __restrict__ systems,
+                                                  const int32_t* __restrict__ sys, const int32_t* __restrict__ role,
+                                                  const double* __restrict__ params, hvp::Consts C, Workspace ws) {
+    const unsigned long long reserved = ws.counter[0];
+    const long long total = (long long)(reserved < (unsigned long long)ws.cap ? reserved : ws.cap);
+    unsigned long long iter_sum = 0;
+    for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (long long)gridDim.x * blockDim.x) {
+        const int inst = ws.task_inst[t];
+        if (inst < 0) continue;  // dead slot of an overflowed instance
+        const uint32_t code = ws.task_code[t];
+        const hvp_system& S = systems[sys[inst]];
+        const int rl = role[inst];
+        const double* prm = params + (size_t)inst * (2 + 6 * (N + 1));
+        hvp::LaneQp<N, LdsMem<N>> q;
+        q.mem.lane = threadIdx.x;
+        hvp::setup_lane<N>(q, S, C, rl, prm, code);
+        int iters = 0;
+        int status = hvp::solve_gi<N>(q, C, kGiMaxIter<N>, iters);
+        if (status != hvp::GI_OK) {
+            const unsigned long long r = atomicAdd(&ws.counter[2], 1ull);
+            ws.redo[r] = (int32_t)t;
+            status = 4;  // pending: the fallback kernel overwrites it
+        }
+        ws.task_stat[t] = status | (iters << 8);
+#pragma unroll
+        for (int k = 0; k < N; ++k) ws.task_y[t * N + k] = q.y[k];
+        iter_sum += (unsigned long long)iters;
+    }
+    // one atomic per wave for the iteration statistics
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) iter_sum += __shfl_down(iter_sum, off, 64);
+    if ((threadIdx.x & 63) == 0 && iter_sum) atomicAdd(&ws.counter[1], iter_sum);
+}
+
+// K_qp_ipm: the fallback list only (normally empty: the launch reads a zero count and exits),
+// full row set by the Mehrotra interior-point method (hvp_ipm.h).
+template <int N>
+__global__ __launch_bounds__(kBlock) void k_qp_ipm(const hvp_system* __restrict__ systems,
+                                                   const int32_t* __restrict__ sys, const int32_t* __restrict__ role,
+                                                   const double* __restrict__ params, hvp::Consts C, Workspace ws) {
+    const unsigned long long reserved = ws.counter[2];
+    const long long total = (long long)(reserved < (unsigned long long)ws.cap ? reserved : ws.cap);
+    unsigned long long iter_sum = 0;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (long long)gridDim.x * blockDim.x) {
+        const long long t = (long long)ws.redo[i];
+        const int inst = ws.task_inst[t];
+        const uint32_t code = ws.task_code[t];
+        const hvp_system& S = systems[sys[inst]];
+        const int rl = role[inst];
+        const double* prm = params + (size_t)inst * (2 + 6 * (N + 1));
+        hvp::LaneQp<N, LdsMem<N>> q;
+        q.mem.lane = threadIdx.x;
+        hvp::setup_lane<N>(q, S, C, rl, prm, code);
+        const hvp::QpOut o = hvp::Solver<N, true, LdsMem<N>>::solve(q, C);
+        ws.task_stat[t] = o.status | ((o.iters + (ws.task_stat[t] >> 8)) << 8);
+#pragma unroll
+        for (int k = 0; k < N; ++k) ws.task_y[t * N + k] = q.y[k];
+        iter_sum += (unsigned long long)o.iters;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) iter_sum += __shfl_down(iter_sum, off, 64);
+    if ((threadIdx.x & 63) == 0 && iter_sum) atomicAdd(&ws.counter[1], iter_sum);
+}
+
+// ------------------------------------------------------------------ K_cost
+// Objective of every converged candidate, evaluated term by term on its trajectory (separate
+// launch: fused into K_qp its reference loads stay live across the IPM and spill).
+template <int N>
+__global__ __launch_bounds__(kBlock) void k_cost(const hvp_system* __restrict__ systems,
+                                                 const int32_t* __restrict__ sys, const int32_t* __restrict__ role,
+                                                 const double* __restrict__ params, hvp::Consts C, Workspace ws) {
+    const unsigned long long reserved = ws.counter[0];
+    const long long total = (long long)(reserved < (unsigned long long)ws.cap ? reserved : ws.cap);
+    for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (long long)gridDim.x * blockDim.x) {
+        const int inst = ws.task_inst[t];
+        double cost = 1e300;
+        if (inst >= 0 && (ws.task_stat[t] & 0xff) == 0) {
+            const hvp_system& S = systems[sys[inst]];
+            const double* prm = params + (size_t)inst * (2 + 6 * (N + 1));
+            hvp::LaneQp<N> q;
+            const int rl = role[inst];
+            q.has_sf = (rl & HVP_ROLE_SAFE_FRONT) != 0;
+            q.has_sb = (rl & HVP_ROLE_SAFE_BACK) != 0;
+#pragma unroll
+            for (int k = 0; k < N; ++k) q.y[k] = ws.task_y[t * N + k];
+            cost = hvp::direct_cost<N>(q, S, C, rl, prm, ws.task_code[t]);
+        }
+        ws.task_cost[t] = cost;
+    }
+}
+
+// ------------------------------------------------------------------ K_select
+template <int N>
+__global__ __launch_bounds__(kBlock) void k_select(int B, const hvp_system* __restrict__ systems,
+                                                   const int32_t* __restrict__ sys, const double* __restrict__ params,
+                                                   Workspace ws, double* __restrict__ u_out, double* __restrict__ x_out,
+                                                   int8_t* __restrict__ region_out, int8_t* __restrict__ gear_out,
+                                                   double* __restrict__ cost_out, int32_t* __restrict__ status_out,
+                                                   int32_t* __restrict__ nodes_out, int32_t* __restrict__ iters_out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B) return;
+    const int cnt = ws.inst_cnt[i], off = ws.inst_off[i];
+    const hvp_system& S = systems[sys[i]];
+    const double* prm = params + (size_t)i * (2 + 6 * (N + 1));
+    int status;
+    int win = -1;
+    int iters = 0;
+    if (ws.inst_flag[i] != 0 || cnt == 0) {
+        status = HVP_INFEASIBLE;
+    } else if (off < 0) {
+        status = HVP_OVERFLOW;
+    } else {
+        double best = 1e300;
+        for (int j = 0; j < cnt; ++j) {
+            const int st = ws.task_stat[off + j];
+            iters += st >> 8;
+            if ((st & 0xff) == 0) best = fmin(best, ws.task_cost[off + j]);
+        }
+        if (best < 1e300) {
+            const double tol = 1e-9 * fmax(1.0, fabs(best));
+            for (int j = 0; j < cnt; ++j)
+                if ((ws.task_stat[off + j] & 0xff) == 0 && ws.task_cost[off + j] <= best + tol) {
+                    win = off + j;
+                    break;
+                }
+        }
+        status = win >= 0 ? HVP_OPTIMAL : HVP_MAXITER;
+    }
+    if (status_out) status_out[i] = status;
+    if (nodes_out) nodes_out[i] = cnt;
+    if (iters_out) iters_out[i] = iters;
+    if (cost_out) cost_out[i] = win >= 0 ? ws.task_cost[win] : 1e300;
+    const uint32_t code = win >= 0 ? ws.task_code[win] : 0u;
+    double p = prm[0], v = prm[1];
+    if (x_out) {
+        x_out[(size_t)i * 2 * (N + 1)] = p;
+        x_out[(size_t)i * 2 * (N + 1) + N + 1] = v;
+    }
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        const int r = hvp::code_region(code, k);
+        const double vn = win >= 0 ? ws.task_y[(size_t)win * N + k] : v;
+        const double u = win >= 0 ? (vn - S.a[r] * v - S.c[r]) / S.b[r] : 0.0;
+        p = p + S.ts * v;
+        v = vn;
+        if (u_out) u_out[(size_t)i * N + k] = u;
+        if (x_out) {
+            x_out[(size_t)i * 2 * (N + 1) + k + 1] = p;
+            x_out[(size_t)i * 2 * (N + 1) + N + 1 + k + 1] = v;
+        }
+        if (region_out) region_out[(size_t)i * N + k] = (int8_t)(win >= 0 ? r : -1);
+        if (gear_out) gear_out[(size_t)i * N + k] = (int8_t)(win >= 0 ? S.gear[r] : 0);
+    }
+}
+
+// ================================================================== branch and bound
+// Level-synchronous over the whole batch (hvp_bnb.h): K_root (relaxed root QP + greedy dive ->
+// incumbent), then for every depth k = 1..N  K_expand (children of the unpruned parents, one
+// atomicAdd per parent) and K_bound (one lane per child: QP with the tail relaxed after k steps;
+// exact QP at k = N), then K_key / K_write / K_finish (argmin + tie rule over the leaves).
+// Every kernel grid-strides over a count that lives on the device: no host round trip.
+template <int N>
+constexpr int kBnbBlock = N <= 8 ? 256 : 64;  // LDS rows: 7 N doubles per lane
+
+// The incumbent is kept as an order-preserving 64-bit key of the double so that atomicMin on the
+// key is a min on the cost -- for negative costs too (the ADMM objective carries y'(c - z)).
+__device__ inline unsigned long long cost_key(double c) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(c);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+__device__ inline double key_cost(unsigned long long k) {
+    return __longlong_as_double((long long)((k >> 63) ? (k & 0x7fffffffffffffffull) : ~k));
+}
+__device__ inline double inc_of(const Workspace& ws, int inst) { return key_cost(ws.inc[inst]); }
+
+// Occupancy target of the lane B&B kernels (waves per SIMD).  Measured at C2: 2 waves/SIMD forces
+// 800 B/lane of spills and runs 2.7x slower than 1 wave/SIMD with the register file to itself
+#ifndef HVP_LANE_WAVES
+#define HVP_LANE_WAVES 1
+#endif
+#define HVP_LANE_OCC __attribute__((amdgpu_waves_per_eu(HVP_LANE_WAVES)))
+
+// ADMM: the formulation is a template parameter so that each kernel instantiation holds ONE
+// QP path (both paths in one kernel pushed the lane kernels to 256 VGPRs + scratch spills)
+template <int N, int BS, bool ADMM>
+__device__ inline int bnb_qp(hvp::LaneQp<N, LdsMem<N, BS>>& q, const hvp_system& S, const hvp::Consts& C, int rl,
+                             const double* prm, uint64_t code, int K, double lo, double hi, double& cost) {
+    int it = 0, st;
+    if constexpr (ADMM) {
+        st = hvp::solve_admm_lane<N>(q, S, C, rl, prm, code, K, kGiMaxIter<N>, it);
+        cost = st == hvp::GI_OK ? hvp::admm_direct_cost<N>(q, S, C, rl, prm, code, K) : 0.0;
+    } else {
+        hvp::setup_lane<N>(q, S, C, rl, prm, code, K, lo, hi);  // tail relaxed from v_K in [lo, hi]
+        st = hvp::solve_gi<N>(q, C, kGiMaxIter<N>, it);
+        cost = st == hvp::GI_OK ? hvp::direct_cost<N>(q, S, C, rl, prm, code, K) : 0.0;
+    }
+    return st == hvp::GI_OK ? it : -1 - it;
+}
+
+template <int N, bool ADMM>
+__global__ __launch_bounds__(kBnbBlock<N>) HVP_LANE_OCC void k_bnb_root(int B, const hvp_system* __restrict__ systems,
+                                                           const int32_t* __restrict__ sys,
+                                                           const int32_t* __restrict__ role,
+                                                           const double* __restrict__ params, hvp::Consts C,
+                                                           Workspace ws) {
+    constexpr int BS = kBnbBlock<N>;
+    const int i = blockIdx.x * BS + threadIdx.x;
+    if (i == 0) ws.lvl[0] = (unsigned long long)B;
+    if (i >= B) return;
+    const hvp_system& S = systems[sys[i]];
+    const int rl = role[i];
+    const double* prm = params + (size_t)i * C.stride;
+    const double v0 = prm[1], P1 = prm[0] + S.ts * v0;
+    const bool ok = P1 >= S.pmin - 1e-9 * (1.0 + fabs(S.pmin)) && P1 <= S.pmax + 1e-9 * (1.0 + fabs(S.pmax));
+    ws.key[i] = ~0ull;
+    ws.inst_flag[i] = ok ? 0 : 1;
+    ws.nd_inst[0][i] = ok ? i : -1;
+    ws.nd_code[0][i] = 0;
+    ws.nd_lo[0][i] = v0;
+    ws.nd_hi[0][i] = v0;
+    double inc = __longlong_as_double(0x7ff0000000000000ll);  // +inf: no incumbent
+    double lb = -1e300;
+    int nodes = 0, iters = 0;
+    if (ok) {
+        hvp::LaneQp<N, LdsMem<N, BS>> q;
+        q.mem.lane = threadIdx.x;
+        double c0;
+        int it = bnb_qp<N, BS, ADMM>(q, S, C, rl, prm, 0, 0, v0, v0, c0);
+        ++nodes;
+        iters += it >= 0 ? it : -1 - it;
+        if (it >= 0) {
+            lb = c0;
+            double ystar[N];
+#pragma unroll
+            for (int k = 0; k < N; ++k) ystar[k] = q.y[k];
+            uint64_t code;
+            if (hvp::bnb_dive<N>(S, C, v0, ystar, &code)) {
+                double c1;
+                it = bnb_qp<N, BS, ADMM>(q, S, C, rl, prm, code, N, 0.0, -1.0, c1);
+                ++nodes;
+                iters += it >= 0 ? it : -1 - it;
+                if (it >= 0) inc = c1;
+            }
+        }
+    }
+    ws.nd_lb[0][i] = lb;
+    ws.inc[i] = cost_key(inc);
+    ws.nodes[i] = nodes;
+    ws.iters[i] = iters;
+    atomicAdd(&ws.counter[3], (unsigned long long)nodes);
+    atomicAdd(&ws.counter[1], (unsigned long long)iters);
+}
+
+// ---- long horizons: one QP per 16-lane group (hvp_coop.h), 4 groups per 64-lane block
+template <int N>
+constexpr bool kCoop = N > HVP_MAX_N_ENUM;
+constexpr int kCoopBlock = 64;
+constexpr int kCoopGroups = kCoopBlock / hvp::coop::G;
+
+template <int N>
+__global__ __launch_bounds__(kCoopBlock) void k_bnb_root_coop(int B, const hvp_system* __restrict__ systems,
+                                                              const int32_t* __restrict__ sys,
+                                                              const int32_t* __restrict__ role,
+                                                              const double* __restrict__ params, hvp::Consts C,
+                                                              Workspace ws) {
+    __shared__ hvp::coop::GroupLds lds[kCoopGroups];
+    const int g = threadIdx.x / hvp::coop::G, t = threadIdx.x % hvp::coop::G;
+    const int i = blockIdx.x * kCoopGroups + g;
+    if (blockIdx.x == 0 && threadIdx.x == 0) ws.lvl[0] = (unsigned long long)B;
+    if (i >= B) return;  // group-uniform
+    const hvp_system& S = systems[sys[i]];
+    const int rl = role[i];
+    const double* prm = params + (size_t)i * C.stride;
+    const double v0 = prm[1], P1 = prm[0] + S.ts * v0;
+    const bool ok = P1 >= S.pmin - 1e-9 * (1.0 + fabs(S.pmin)) && P1 <= S.pmax + 1e-9 * (1.0 + fabs(S.pmax));
+    double inc = __longlong_as_double(0x7ff0000000000000ll);
+    double lb = -1e300;
+    int nodes = 0, iters = 0;
+    if (ok) {
+        hvp::coop::Lane<N> L;
+        double c0 = 0.0;
+        int it = 0;
+        int st = hvp::coop::solve_qp<N>(L, lds[g], S, C, rl, prm, 0, 0, kGiMaxIter<N>, it, &c0, nullptr, prm[1], prm[1]);
+        ++nodes;
+        iters += it;
+        if (st == hvp::GI_OK) {
+            lb = c0;
+            lds[g].v[t] = t < N ? L.y : 0.0;
+            hvp::coop::gsync();
+            unsigned long long code = 0;
+            int dive_ok = 0;
+            if (t == 0) {
+                double ystar[N];
+#pragma unroll
+                for (int k = 0; k < N; ++k) ystar[k] = lds[g].v[k];
+                uint64_t c64;
+                dive_ok = hvp::bnb_dive<N>(S, C, v0, ystar, &c64) ? 1 : 0;
+                code = c64;
+            }
+            dive_ok = hvp::coop::bcast(dive_ok, 0);
+            code = hvp::coop::bcast(code, 0);
+            if (dive_ok) {
+                double c1 = 0.0;
+                st = hvp::coop::solve_qp<N>(L, lds[g], S, C, rl, prm, code, N, kGiMaxIter<N>, it, &c1);
+                ++nodes;
+                iters += it;
+                if (st == hvp::GI_OK) inc = c1;
+            }
+        }
+    }
+    if (t == 0) {
+        ws.key[i] = ~0ull;
+        ws.inst_flag[i] = ok ? 0 : 1;
+        ws.nd_inst[0][i] = ok ? i : -1;
+        ws.nd_code[0][i] = 0;
+        ws.nd_lo[0][i] = v0;
+        ws.nd_hi[0][i] = v0;
+        ws.nd_lb[0][i] = lb;
+        ws.inc[i] = cost_key(inc);
+        ws.nodes[i] = nodes;
+        ws.iters[i] = iters;
+        atomicAdd(&ws.counter[3], (unsigned long long)nodes);
+        atomicAdd(&ws.counter[1], (unsigned long long)iters);
+    }
+}
+
+template <int N>
+__global__ __launch_bounds__(kCoopBlock) void k_bnb_bound_coop(int k, const hvp_system* __restrict__ systems,
+                                                               const int32_t* __restrict__ sys,
+                                                               const int32_t* __restrict__ role,
+                                                               const double* __restrict__ params, hvp::Consts C,
+                                                               Workspace ws) {
+    __shared__ hvp::coop::GroupLds lds[kCoopGroups];
+    const int g = threadIdx.x / hvp::coop::G, t = threadIdx.x % hvp::coop::G;
+    const int dst = k & 1;
+    const unsigned long long nn = ws.lvl[k];
+    const long long total = (long long)(nn < (unsigned long long)ws.cap ? nn : ws.cap);
+    for (long long q = (long long)blockIdx.x * kCoopGroups + g; q < total; q += (long long)gridDim.x * kCoopGroups) {
+        const int inst = ws.nd_inst[dst][q];
+        if (inst < 0) {
+            if (t == 0) {
+                if (k == N) ws.leaf_stat[q] = HVP_OVERFLOW;
+                else ws.nd_lb[dst][q] = 1e300;
+            }
+            continue;
+        }
+        const uint64_t code = ws.nd_code[dst][q];
+        const hvp_system& S = systems[sys[inst]];
+        const int rl = role[inst];
+        const double* prm = params + (size_t)inst * C.stride;
+        hvp::coop::Lane<N> L;
+        double c = 0.0;
+        int it = 0;
+        const int st = hvp::coop::solve_qp<N>(L, lds[g], S, C, rl, prm, code, k, kGiMaxIter<N>, it, &c, nullptr,
+                                              ws.nd_lo[dst][q], ws.nd_hi[dst][q]);
+        const bool ok = st == hvp::GI_OK;
+        if (k == N && t < N) ws.task_y[q * N + t] = L.y;
+        if (t == 0) {
+            atomicAdd(&ws.nodes[inst], 1);
+            atomicAdd(&ws.iters[inst], it);
+            atomicAdd(&ws.counter[1], (unsigned long long)it);
+            if (k < N) {
+                ws.nd_lb[dst][q] = ok ? c : -1e300;
+                if (!ok) atomicAdd(&ws.counter[4], 1ull);
+            } else {
+                if (ok) ws.nd_lb[dst][q] = c;
+                ws.leaf_stat[q] = ok ? 0 : HVP_MAXITER;
+                if (ok) atomicMin(&ws.inc[inst], cost_key(c));
+                else atomicOr(&ws.inst_flag[inst], 8);
+            }
+        }
+    }
+}
+
+// children of the level-(k-1) nodes that survive the incumbent test
+// Every instance may hold at most `quota` = capacity / B nodes per level: an instance whose
+// tree outgrows its share (the heavy tail at long horizons, e.g. trajectories riding a region
+// boundary) is cut off deterministically and reported HVP_OVERFLOW, so it can never crowd the
+// other instances out of the pooled list.  The host path re-solves it alone (quota = capacity).
+template <int N>
+__global__ __launch_bounds__(kBlock) void k_bnb_expand(int k, int quota, const hvp_system* __restrict__ systems,
+                                                       const int32_t* __restrict__ sys, hvp::Consts C, Workspace ws) {
+    const int src = (k - 1) & 1, dst = k & 1;
+    const unsigned long long np = ws.lvl[k - 1];
+    const long long total = (long long)(np < (unsigned long long)ws.cap ? np : ws.cap);
+    for (long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x; p < total;
+         p += (long long)gridDim.x * blockDim.x) {
+        const int inst = ws.nd_inst[src][p];
+        if (inst < 0 || (ws.inst_flag[inst] & 2)) continue;
+        const double plb = ws.nd_lb[src][p];
+        if (hvp::bnb_pruned(plb, inc_of(ws, inst))) continue;
+        const hvp_system& S = systems[sys[inst]];
+        const double lo = ws.nd_lo[src][p], hi = ws.nd_hi[src][p];
+        const uint64_t code = ws.nd_code[src][p];
+        unsigned mask = 0;
+        for (int r = 0; r < S.n_regions; ++r) {
+            double a, b;
+            if (hvp::bnb_child(S, C, k - 1, lo, hi, r, &a, &b)) mask |= 1u << r;
+        }
+        const int nc = __popc(mask);
+        if (!nc) continue;
+        if (atomicAdd(&ws.inst_lvl[inst], nc) + nc > quota) {
+            atomicOr(&ws.inst_flag[inst], 2);
+            continue;
+        }
+        const unsigned long long off = atomicAdd(&ws.lvl[k], (unsigned long long)nc);
+        if (off + nc > (unsigned long long)ws.cap) {
+            atomicOr(&ws.inst_flag[inst], 2);  // overflow: reported, never truncated silently
+            // the slots of this reservation below the capacity are swept by the next kernels
+            for (unsigned long long t = off; t < (unsigned long long)ws.cap && t < off + nc; ++t)
+                ws.nd_inst[dst][t] = -1;
+            continue;
+        }
+        int j = 0;
+        for (int r = 0; r < S.n_regions; ++r) {
+            if (!((mask >> r) & 1u)) continue;
+            double a, b;
+            hvp::bnb_child(S, C, k - 1, lo, hi, r, &a, &b);
+            ws.nd_inst[dst][off + j] = inst;
+            ws.nd_code[dst][off + j] = hvp::code_with(code, k - 1, r);
+            ws.nd_lo[dst][off + j] = a;
+            ws.nd_hi[dst][off + j] = b;
+            ws.nd_lb[dst][off + j] = plb;  // inherited: kept by a leaf whose QP fails
+            ++j;
+        }
+    }
+}
+
+// one lane per level-k node: bound (k < N) or exact leaf QP (k = N)
+template <int N, bool ADMM>
+__global__ __launch_bounds__(kBnbBlock<N>) HVP_LANE_OCC void k_bnb_bound(int k, const hvp_system* __restrict__ systems,
+                                                            const int32_t* __restrict__ sys,
+                                                            const int32_t* __restrict__ role,
+                                                            const double* __restrict__ params, hvp::Consts C,
+                                                            Workspace ws) {
+    constexpr int BS = kBnbBlock<N>;
+    const int dst = k & 1;
+    const unsigned long long nn = ws.lvl[k];
+    const long long total = (long long)(nn < (unsigned long long)ws.cap ? nn : ws.cap);
+    unsigned long long iter_sum = 0, fails = 0;
+    for (long long t = (long long)blockIdx.x * BS + threadIdx.x; t < total; t += (long long)gridDim.x * BS) {
+        const int inst = ws.nd_inst[dst][t];
+        if (inst < 0) {  // dead slot of an overflowed reservation
+            if (k == N) ws.leaf_stat[t] = HVP_OVERFLOW;
+            else ws.nd_lb[dst][t] = 1e300;
+            continue;
+        }
+        const uint64_t code = ws.nd_code[dst][t];
+        const hvp_system& S = systems[sys[inst]];
+        const int rl = role[inst];
+        const double* prm = params + (size_t)inst * C.stride;
+        hvp::LaneQp<N, LdsMem<N, BS>> q;
+        q.mem.lane = threadIdx.x;
+        double c;
+        const int it = bnb_qp<N, BS, ADMM>(q, S, C, rl, prm, code, k, ws.nd_lo[dst][t], ws.nd_hi[dst][t], c);
+        const bool ok = it >= 0;
+        const int its = ok ? it : -1 - it;
+        iter_sum += (unsigned long long)its;
+        atomicAdd(&ws.nodes[inst], 1);
+        atomicAdd(&ws.iters[inst], its);
+        if (k < N) {
+            // a failed bound QP prunes nothing
+            ws.nd_lb[dst][t] = ok ? c : -1e300;
+            if (!ok) atomicAdd(&ws.counter[4], 1ull);
+        } else {
+            // a failed leaf keeps its parent's bound (K_key: MAXITER if it stays in contention
+            // and no fallback exists)
+            if (ok) ws.nd_lb[dst][t] = c;
+            ws.leaf_stat[t] = ok ? 0 : HVP_MAXITER;
+#pragma unroll
+            for (int j = 0; j < N; ++j) ws.task_y[t * N + j] = q.y[j];
+            if (ok) {
+                atomicMin(&ws.inc[inst], cost_key(c));
+            } else {
+                ++fails;
+                atomicOr(&ws.inst_flag[inst], 8);  // a velocity-feasible sequence exists
+                if (N <= HVP_MAX_N_ENUM && C.form == HVP_FORM_DECENT) {  // K_bnb_ipm re-solves it
+                    const unsigned long long r = atomicAdd(&ws.counter[2], 1ull);
+                    if (r < (unsigned long long)ws.cap) ws.redo[r] = (int32_t)t;
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) iter_sum += __shfl_down(iter_sum, off, 64);
+    if ((threadIdx.x & 63) == 0 && iter_sum) atomicAdd(&ws.counter[1], iter_sum);
+    (void)fails;
+}
+
+// ---- the same bound / leaf QPs, persistent waves (decentralised form, N <= 8)
+// Every wave loops over { one active-set trip per busy lane (scan if due, one step) } and, when
+// at least kRefillMin lanes are free, an EVENT: the lanes whose QP finished write their results
+// together, then every free lane takes a node (one atomic per wave for the batch) and builds
+// its QP together.  A lane's solver state (hvp_gi.h GiLane: J, packed R, multipliers) stays in
+// registers across trips; the sigma-independent part of every node's QP (tracking terms,
+// safe-row bounds) is computed once per instance by K_inst_prep.  2 waves per SIMD (the solver
+// fits 256 VGPRs with a little spill around the event code; 2 x 72 KB of per-lane rows in LDS
+// per CU).  kRefillMin trades idle lanes against events run by few lanes -- measured at C2
+// (profiles/r02e_*): 8 -> 3.52M, 16 -> 3.95M, 32 -> 4.41M, 48 -> 4.69M, 64 -> 4.86M
+// platoon-steps/s: the setup and write code run at full width beats refilling lanes early, so
+// the default refills a wave when ALL its lanes are free (generations of 64 nodes).
+// Same results per node as k_bnb_bound (the node -> lane mapping does not matter).
+#ifndef HVP_REFILL_WAVES
+#define HVP_REFILL_WAVES 2
+#endif
+#ifndef HVP_REFILL_MIN
+#define HVP_REFILL_MIN 64
+#endif
+constexpr int kRefillMin = HVP_REFILL_MIN;
+constexpr int kRefillBlocksPerCu = HVP_REFILL_WAVES;
+
+// per-instance sigma-independent QP part (SoA: field f of instance i at iq[f * max_batch + i])
+template <int N>
+constexpr int kIqFields = N * (N + 1) / 2 + N + 2 * (N - 1);  // H, f, hf, hb
+
+template <int N>
+__global__ __launch_bounds__(kBlock) void k_inst_prep(int B, const hvp_system* __restrict__ systems,
+                                                      const int32_t* __restrict__ sys,
+                                                      const int32_t* __restrict__ role,
+                                                      const double* __restrict__ params, hvp::Consts C, Workspace ws) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B) return;
+    constexpr int NT = N * (N + 1) / 2;
+    double H[NT], f[N], C0, hf[N - 1], hb[N - 1];
+    hvp::setup_track<N>(systems[sys[i]], C, role[i], params + (size_t)i * C.stride, H, f, C0, hf, hb);
+    const size_t mb = (size_t)ws.max_batch;
+    double* o = ws.iq + i;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) o[j * mb] = H[j];
+#pragma unroll
+    for (int j = 0; j < N; ++j) o[(NT + j) * mb] = f[j];
+#pragma unroll
+    for (int j = 0; j < N - 1; ++j) {
+        o[(NT + N + j) * mb] = hf[j];
+        o[(NT + 2 * N - 1 + j) * mb] = hb[j];
+    }
+}
+
+// the node QP of instance inst from the per-instance part + the node's regions / relaxation
+template <int N, class Q>
+__device__ inline bool setup_node(Q& q, const hvp_system& S, const hvp::Consts& C, const Workspace& ws, int inst,
+                                  int rl, const double* prm, uint64_t code, int K, double rlo, double rhi) {
+    constexpr int NT = N * (N + 1) / 2;
+    const size_t mb = (size_t)ws.max_batch;
+    const double* o = ws.iq + inst;
+    const bool ok = hvp::setup_scalars<N>(q, S, rl, prm[0], prm[1]);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) q.H[j] = o[j * mb];
+#pragma unroll
+    for (int j = 0; j < N; ++j) q.f[j] = o[(NT + j) * mb];
+#pragma unroll
+    for (int j = 0; j < N - 1; ++j) {
+        q.mem.set(hvp::F_HF, j, o[(NT + N + j) * mb]);
+        q.mem.set(hvp::F_HB, j, o[(NT + 2 * N - 1 + j) * mb]);
+    }
+    q.C0 = 0.0;  // not used by the active-set path (costs come from direct_cost)
+    hvp::setup_input<N>(q, S, C, code, K, rlo, rhi);
+    return ok;
+}
+
+template <int N>
+__device__ inline void bnb_node_done(int k, long long t, int inst, bool ok, int its, double c, const double* y,
+                                     const hvp::Consts& C, Workspace& ws) {
+    const int dst = k & 1;
+    atomicAdd(&ws.nodes[inst], 1);
+    atomicAdd(&ws.iters[inst], its);
+    if (k < N) {
+        ws.nd_lb[dst][t] = ok ? c : -1e300;  // a failed bound QP prunes nothing
+        if (!ok) atomicAdd(&ws.counter[4], 1ull);
+    } else {
+        if (ok) ws.nd_lb[dst][t] = c;  // a failed leaf keeps its parent's bound
+        ws.leaf_stat[t] = ok ? 0 : HVP_MAXITER;
+#pragma unroll
+        for (int j = 0; j < N; ++j) ws.task_y[t * N + j] = y[j];
+        if (ok) {
+            atomicMin(&ws.inc[inst], cost_key(c));
+        } else {
+            atomicOr(&ws.inst_flag[inst], 8);  // a velocity-feasible sequence exists
+            if (C.form == HVP_FORM_DECENT) {   // K_bnb_ipm re-solves it
+                const unsigned long long r = atomicAdd(&ws.counter[2], 1ull);
+                if (r < (unsigned long long)ws.cap) ws.redo[r] = (int32_t)t;
+            }
+        }
+    }
+}
+
+// wave-level claim of `nfree` consecutive work items from *claim (one atomic per wave): returns
+// the first item; the free lanes take base + their rank among the free lanes (wave_rank)
+__device__ inline unsigned long long wave_claim(unsigned long long* claim, unsigned long long free, int nfree,
+                                                int lane) {
+    const int leader = __ffsll((long long)free) - 1;
+    unsigned long long base = 0;
+    if (lane == leader) base = atomicAdd(claim, (unsigned long long)nfree);
+    return ((unsigned long long)(unsigned)__shfl((int)(base >> 32), leader, 64) << 32) |
+           (unsigned)__shfl((int)(base & 0xffffffffu), leader, 64);
+}
+__device__ inline int wave_rank(unsigned long long mask) {
+    return __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
+}
+
+// lane stages of the refill kernels
+enum { RS_IDLE = 0, RS_SCAN = 1, RS_STEP = 2, RS_FAIL = 3, RS_OPT = 4 };
+
+// one active-set trip of a busy lane (RS_SCAN / RS_STEP); finished lanes end in RS_FAIL / RS_OPT
+template <int N, class Q>
+__device__ inline void gi_trip(Q& q, hvp::GiLane<N>& g, const hvp::Consts& C, int& stage, int& fail) {
+    q.mem.refresh();
+    g.fence(q);
+    if (stage == RS_SCAN) stage = g.scan(q, C) ? RS_STEP : RS_OPT;
+    if (stage == RS_STEP) {
+        const int r = g.step(q, C, kGiMaxIter<N>);
+        if (r == hvp::GI_STEP_NEXT) stage = RS_SCAN;
+        else if (r != hvp::GI_STEP_MORE) stage = RS_FAIL, fail = r;
+    }
+}
+
+template <int N>
+__global__ __launch_bounds__(kBnbBlock<N>) __attribute__((amdgpu_waves_per_eu(HVP_REFILL_WAVES)))
+void k_bnb_bound_refill(int k, const hvp_system* __restrict__ systems, const int32_t* __restrict__ sys,
+                        const int32_t* __restrict__ role, const double* __restrict__ params, hvp::Consts C,
+                        Workspace ws) {
+    constexpr int BS = kBnbBlock<N>;
+    static_assert(N <= HVP_MAX_N_ENUM, "lane refill is the N <= 8 path");
+    const int dst = k & 1;
+    const unsigned long long nn = ws.lvl[k];
+    const long long total = (long long)(nn < (unsigned long long)ws.cap ? nn : ws.cap);
+    unsigned long long* claim = ws.lvl + (HVP_MAX_N + 1) + k;
+    const int lane = threadIdx.x & 63;
+    hvp::LaneQp<N, LdsMem<N, BS>> q;
+    q.mem.lane = threadIdx.x;
+    hvp::GiLane<N> g;
+    long long t = -1;  // node of the lane
+    int inst = 0, stage = RS_IDLE, fail = 0;
+    uint64_t code = 0;
+    bool exhausted = false;
+    unsigned long long iter_sum = 0;
+    for (;;) {
+        const bool done = stage >= RS_FAIL;
+        const unsigned long long free = __ballot(stage == RS_IDLE || done);
+        const int nfree = __popcll(free);
+        if (nfree >= kRefillMin || nfree == 64) {
+            // ---- event: write the finished lanes' results, then refill every free lane
+            if (done) {
+                const int st = stage == RS_OPT ? g.verify(C, nullptr) : fail;
+                const bool ok = st == hvp::GI_OK;
+                const double c = ok ? hvp::direct_cost<N>(q, systems[sys[inst]], C, role[inst],
+                                                          params + (size_t)inst * C.stride, code, k)
+                                    : 0.0;
+                iter_sum += (unsigned long long)g.iter;
+                bnb_node_done<N>(k, t, inst, ok, g.iter, c, q.y, C, ws);
+                stage = RS_IDLE;
+            }
+            if (exhausted && nfree == 64) break;
+            if (!exhausted) {
+                const unsigned long long base = wave_claim(claim, free, nfree, lane);
+                if (base + nfree >= (unsigned long long)total) exhausted = true;
+                const long long mine = (long long)base + wave_rank(free);
+                if (stage == RS_IDLE && mine < total) {
+                    inst = ws.nd_inst[dst][mine];
+                    if (inst < 0) {  // dead slot of an overflowed reservation
+                        if (k == N) ws.leaf_stat[mine] = HVP_OVERFLOW;
+                        else ws.nd_lb[dst][mine] = 1e300;
+                    } else {
+                        t = mine;
+                        code = ws.nd_code[dst][mine];
+                        setup_node<N>(q, systems[sys[inst]], C, ws, inst, role[inst], params + (size_t)inst * C.stride,
+                                      code, k, ws.nd_lo[dst][mine], ws.nd_hi[dst][mine]);
+                        stage = g.init(q) == hvp::GI_OK ? RS_SCAN : RS_FAIL;
+                        fail = hvp::GI_FAIL_CHOL;
+                    }
+                }
+            }
+        }
+        if (stage == RS_SCAN || stage == RS_STEP) gi_trip<N>(q, g, C, stage, fail);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) iter_sum += __shfl_down(iter_sum, off, 64);
+    if (lane == 0 && iter_sum) atomicAdd(&ws.counter[1], iter_sum);
+}
+
+// Leaves whose active-set solve failed its verification (degenerate vertices, e.g. the
+// position box at p_max): re-solved by the interior-point method on the full row set
+// (hvp_ipm.h), as K_qp_ipm does for the enumeration path.  Normally an empty list.
+template <int N>
+__global__ __launch_bounds__(kBnbBlock<N>) void k_bnb_ipm(const hvp_system* __restrict__ systems,
+                                                          const int32_t* __restrict__ sys,
+                                                          const int32_t* __restrict__ role,
+                                                          const double* __restrict__ params, hvp::Consts C,
+                                                          Workspace ws) {
+    constexpr int BS = kBnbBlock<N>;
+    const int src = N & 1;
+    const unsigned long long nr = ws.counter[2];
+    const long long total = (long long)(nr < (unsigned long long)ws.cap ? nr : ws.cap);
+    for (long long i = (long long)blockIdx.x * BS + threadIdx.x; i < total; i += (long long)gridDim.x * BS) {
+        const long long t = ws.redo[i];
+        const int inst = ws.nd_inst[src][t];
+        const uint64_t code = ws.nd_code[src][t];
+        const hvp_system& S = systems[sys[inst]];
+        const int rl = role[inst];
+        const double* prm = params + (size_t)inst * C.stride;
+        hvp::LaneQp<N, LdsMem<N, BS>> q;
+        q.mem.lane = threadIdx.x;
+        hvp::setup_lane<N>(q, S, C, rl, prm, code);
+        const hvp::QpOut o = hvp::Solver<N, true, LdsMem<N, BS>>::solve(q, C);
+        atomicAdd(&ws.iters[inst], o.iters);
+        if (o.status != 0) continue;  // stays HVP_MAXITER with its parent's bound (K_key flags it)
+        const double c = hvp::direct_cost<N>(q, S, C, rl, prm, code);
+#pragma unroll
+        for (int j = 0; j < N; ++j) ws.task_y[t * N + j] = q.y[j];
+        ws.nd_lb[src][t] = c;
+        ws.leaf_stat[t] = 0;
+        atomicMin(&ws.inc[inst], cost_key(c));
+    }
+}
+
+// tie rule: the lexicographically first leaf within 1e-9 relative of the minimum
+template <int N>
+__global__ __launch_bounds__(kBlock) void k_bnb_key(Workspace ws, int form) {
+    const int src = N & 1;
+    const unsigned long long nn = ws.lvl[N];
+    const long long total = (long long)(nn < (unsigned long long)ws.cap ? nn : ws.cap);
+    for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (long long)gridDim.x * blockDim.x) {
+        const int inst = ws.nd_inst[src][t];
+        if (inst < 0) continue;
+        const double best = inc_of(ws, inst);
+        if (ws.leaf_stat[t] != 0) {
+            // Up to HVP_MAX_N_ENUM a leaf that fails the active-set method AND the interior-point
+            // fallback is an infeasible QP (position box), excluded exactly as the enumeration
+            // path and the oracle exclude it.  Beyond, there is no fallback: a failed leaf still
+            // in contention makes the instance MAXITER rather than a possibly wrong answer.
+            if ((N > HVP_MAX_N_ENUM || form != HVP_FORM_DECENT) && !hvp::bnb_pruned(ws.nd_lb[src][t], best))
+                atomicOr(&ws.inst_flag[inst], 4);
+            continue;
+        }
+        if (ws.nd_lb[src][t] <= best + 1e-9 * fmax(1.0, fabs(best)))
+            atomicMin(&ws.key[inst], (unsigned long long)hvp::bnb_lexkey(ws.nd_code[src][t], N));
+    }
+}
+
+template <int N>
+__device__ inline void write_solution(int i, const hvp_system& S, const double* prm, bool win, uint64_t code,
+                                      const double* y, double* u_out, double* x_out, int8_t* region_out,
+                                      int8_t* gear_out) {
+    double p = prm[0], v = prm[1];
+    if (x_out) {
+        x_out[(size_t)i * 2 * (N + 1)] = p;
+        x_out[(size_t)i * 2 * (N + 1) + N + 1] = v;
+    }
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        const int r = hvp::code_region(code, k);
+        const double vn = win ? y[k] : v;
+        const double u = win ? (vn - S.a[r] * v - S.c[r]) / S.b[r] : 0.0;
+        p = p + S.ts * v;
+        v = vn;
+        if (u_out) u_out[(size_t)i * N + k] = u;
+        if (x_out) {
+            x_out[(size_t)i * 2 * (N + 1) + k + 1] = p;
+            x_out[(size_t)i * 2 * (N + 1) + N + 1 + k + 1] = v;
+        }
+        if (region_out) region_out[(size_t)i * N + k] = (int8_t)(win ? r : -1);
+        if (gear_out) gear_out[(size_t)i * N + k] = (int8_t)(win ? S.gear[r] : 0);
+    }
+}
+
+// optimal neighbour copies of an ADMM solution (fleet_naive_admm.py: mpc.x_front.X / x_back.X)
+template <int N>
+__device__ inline void write_copies(int i, const hvp_system& S, const hvp::Consts& C, int rl, const double* prm,
+                                    bool win, const double* y, double* xf_out, double* xb_out) {
+    const bool side_on[2] = {(rl & HVP_ROLE_SAFE_FRONT) != 0, (rl & HVP_ROLE_SAFE_BACK) != 0};
+    const bool track[2] = {(rl & HVP_ROLE_TRACK_FRONT) != 0, (rl & HVP_ROLE_TRACK_BACK) != 0};
+    double* outs[2] = {xf_out, xb_out};
+    const int K1 = N + 1;
+    for (int side = 0; side < 2; ++side) {
+        double* o = outs[side];
+        if (!o) continue;
+        o += (size_t)i * 2 * K1;
+        double p = prm[0], v = prm[1];
+        for (int k = 0; k <= N; ++k) {
+            double e = 0.0, g = 0.0;
+            if (win && side_on[side])
+                hvp::admm_copy_value(C, track[side], side, hvp::admm_y(prm, side, N)[k],
+                                     hvp::admm_y(prm, side, N)[K1 + k], hvp::admm_z(prm, side, N)[k],
+                                     hvp::admm_z(prm, side, N)[K1 + k], p, v, &e, &g);
+            o[k] = e;
+            o[K1 + k] = g;
+            if (k < N) {
+                p = p + S.ts * v;
+                v = win ? y[k] : v;
+            }
+        }
+    }
+}
+
+template <int N>
+__global__ __launch_bounds__(kBlock) void k_bnb_write(const hvp_system* __restrict__ systems,
+                                                      const int32_t* __restrict__ sys,
+                                                      const int32_t* __restrict__ role,
+                                                      const double* __restrict__ params, hvp::Consts C, Workspace ws,
+                                                      double* __restrict__ u_out, double* __restrict__ x_out,
+                                                      int8_t* __restrict__ region_out, int8_t* __restrict__ gear_out,
+                                                      double* __restrict__ cost_out, double* __restrict__ xf_out,
+                                                      double* __restrict__ xb_out) {
+    const int src = N & 1;
+    const unsigned long long nn = ws.lvl[N];
+    const long long total = (long long)(nn < (unsigned long long)ws.cap ? nn : ws.cap);
+    for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (long long)gridDim.x * blockDim.x) {
+        if (ws.leaf_stat[t] != 0) continue;
+        const int inst = ws.nd_inst[src][t];
+        if (inst < 0) continue;
+        const uint64_t code = ws.nd_code[src][t];
+        if (hvp::bnb_lexkey(code, N) != ws.key[inst]) continue;
+        const hvp_system& S = systems[sys[inst]];
+        double y[N];
+#pragma unroll
+        for (int j = 0; j < N; ++j) y[j] = ws.task_y[t * N + j];
+        const double* prm = params + (size_t)inst * C.stride;
+        write_solution<N>(inst, S, prm, true, code, y, u_out, x_out, region_out, gear_out);
+        if (C.form == HVP_FORM_ADMM) write_copies<N>(inst, S, C, role[inst], prm, true, y, xf_out, xb_out);
+        if (cost_out) cost_out[inst] = ws.nd_lb[src][t];
+    }
+}
+
+template <int N>
+__global__ __launch_bounds__(kBlock) void k_bnb_finish(int B, const hvp_system* __restrict__ systems,
+                                                       const int32_t* __restrict__ sys,
+                                                       const int32_t* __restrict__ role,
+                                                       const double* __restrict__ params, hvp::Consts C, Workspace ws,
+                                                       double* __restrict__ u_out, double* __restrict__ x_out,
+                                                       int8_t* __restrict__ region_out, int8_t* __restrict__ gear_out,
+                                                       double* __restrict__ cost_out, int32_t* __restrict__ status_out,
+                                                       int32_t* __restrict__ nodes_out,
+                                                       int32_t* __restrict__ iters_out,
+                                                       double* __restrict__ xf_out, double* __restrict__ xb_out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B) return;
+    const int flag = ws.inst_flag[i];
+    const bool win = ws.key[i] != ~0ull;
+    int status;
+    if (flag & 1) status = HVP_INFEASIBLE;
+    else if (flag & 2) status = HVP_OVERFLOW;
+    else if (flag & 4) status = HVP_MAXITER;  // a leaf in contention whose QP did not converge
+    else if (win) status = HVP_OPTIMAL;
+    else status = (flag & 8) ? HVP_MAXITER : HVP_INFEASIBLE;  // sequences exist but no QP converged
+    if (status_out) status_out[i] = status;
+    if (nodes_out) nodes_out[i] = ws.nodes[i];
+    if (iters_out) iters_out[i] = ws.iters[i];
+    if (!win || status != HVP_OPTIMAL) {
+        if (cost_out) cost_out[i] = 1e300;
+        const double* prm = params + (size_t)i * C.stride;
+        write_solution<N>(i, systems[sys[i]], prm, false, 0, nullptr, u_out, x_out, region_out, gear_out);
+        if (C.form == HVP_FORM_ADMM) write_copies<N>(i, systems[sys[i]], C, role[i], prm, false, nullptr, xf_out, xb_out);
+    }
+}
+
+// ================================================================== fixed-control evaluation
+// MpcGear.evaluate_cost (mpcs/mpc_gear.py:137-170): with u (u_g for the gear model) and the
+// gear of every step fixed, the MIQP has no free decision left but the slacks: the trajectory
+// follows from the dynamics of the mode (gear label, region band containing v_k -- at a shared
+// band edge the PWA dynamics coincide), the slacks take max(0, .), and the objective is the
+// direct cost of that trajectory.  Status HVP_INFEASIBLE when a row of the MLD model fails.
+template <int N>
+__global__ __launch_bounds__(kBlock) void k_evaluate(int B, const hvp_system* __restrict__ systems,
+                                                     const int32_t* __restrict__ sys, const int32_t* __restrict__ role,
+                                                     const double* __restrict__ params, hvp::Consts C,
+                                                     const int8_t* __restrict__ gear_in, const double* __restrict__ u_in,
+                                                     double* __restrict__ cost_out, int32_t* __restrict__ status_out,
+                                                     double* __restrict__ x_out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B) return;
+    const hvp_system& S = systems[sys[i]];
+    const int rl = role[i];
+    const double* prm = params + (size_t)i * (2 + 6 * (N + 1));
+    hvp::LaneQp<N> q;
+    q.has_sf = (rl & HVP_ROLE_SAFE_FRONT) != 0;
+    q.has_sb = (rl & HVP_ROLE_SAFE_BACK) != 0;
+    double p = prm[0], v = prm[1];
+    uint64_t code = 0;
+    bool ok = true;
+    if (x_out) {
+        x_out[(size_t)i * 2 * (N + 1)] = p;
+        x_out[(size_t)i * 2 * (N + 1) + N + 1] = v;
+    }
+    for (int k = 0; k < N; ++k) {
+        const int g = gear_in[(size_t)i * N + k];
+        const double u = u_in[(size_t)i * N + k];
+        int r = -1;
+        for (int m = 0; m < S.n_regions && r < 0; ++m) {
+            const double tol = 1e-9 * (1.0 + fabs(v));
+            if (S.gear[m] == g && v >= S.vlo[m] - tol && v <= S.vhi[m] + tol) r = m;
+        }
+        if (r < 0) { ok = false; r = 0; }
+        const double vn = S.a[r] * v + S.b[r] * u + S.c[r];
+        const double tolu = 1e-9 * (1.0 + fabs(u));
+        if (u < S.umin - tolu || u > S.umax + tolu) ok = false;
+        const double dv = vn - v, tola = 1e-9 * (1.0 + fabs(dv));
+        if (dv < C.dec[k] - tola || dv > C.acc[k] + tola) ok = false;
+        p = p + S.ts * v;
+        v = vn;
+        const double tolv = 1e-9 * (1.0 + fabs(v)), tolp = 1e-9 * (1.0 + fabs(p));
+        if (v < S.vmin - tolv || v > S.vmax + tolv || p < S.pmin - tolp || p > S.pmax + tolp) ok = false;
+        q.y[k] = v;
+        code = hvp::code_with(code, k, r);
+        if (x_out) {
+            x_out[(size_t)i * 2 * (N + 1) + k + 1] = p;
+            x_out[(size_t)i * 2 * (N + 1) + N + 1 + k + 1] = v;
+        }
+    }
+    const double cost = hvp::direct_cost<N>(q, S, C, rl, prm, code);
+    cost_out[i] = ok ? cost : 1e300;
+    status_out[i] = ok ? HVP_OPTIMAL : HVP_INFEASIBLE;
+}
+
+// ================================================================== switching ADMM (HVP_FORM_GADMM)
+// TrackingGAdmmCoordinator / GAdmmCoordinator (fleet_g_admm.py:208-301, dmpcpwa [EXT]) for P
+// platoons: rollout of the warm start, per ADMM iteration one local-QP launch + one consensus
+// launch, sequence switching per round (include/hvp.h "Switching ADMM").  Instance b holds
+// vehicle i = lo + b % m of platoon p = b / m; trajectories live in full-platoon slots p n + i.
+__device__ inline int gadmm_slot(int b, int n, int lo, int m) { return (b / m) * n + lo + b % m; }
+
+__device__ inline void gadmm_fail(int32_t* state, int p) {
+    atomicOr(&state[p], 2);
+    atomicAnd(&state[p], ~1);
+}
+
+// first region whose closed velocity band holds v (buf widens the lower edge: the [0, 1e-4]
+// buffer of PwaGearVehicle.find_region used by get_u_for_constant_vel, models.py:519-540)
+__device__ inline int gadmm_region(const hvp_system& S, double v, double buf) {
+    for (int r = 0; r < S.n_regions; ++r)
+        if (v >= S.vlo[r] - buf && v <= S.vhi[r]) return r;
+    return -1;
+}
+
+template <int N>
+__global__ __launch_bounds__(kBlock) void k_gadmm_rollout(int P, int n, int lo, int m,
+                                                          const hvp_system* __restrict__ systems,
+                                                          const int32_t* __restrict__ sys,
+                                                          const double* __restrict__ params, int stride, int mode,
+                                                          const double* __restrict__ u_prev, double* __restrict__ x,
+                                                          int8_t* __restrict__ seq, double* __restrict__ u_ws,
+                                                          int32_t* __restrict__ state) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= P * m) return;
+    const int p = b / m;
+    const hvp_system& S = systems[sys[b]];
+    const double* prm = params + (size_t)b * stride;
+    double pk = prm[0], vk = prm[1];
+    double* xs = x + (size_t)gadmm_slot(b, n, lo, m) * 2 * (N + 1);
+    bool ok = true;
+    double ucv = 0.0;
+    if (mode == 0) {
+        const int r = gadmm_region(S, vk, 1e-4);
+        if (r < 0) ok = false;
+        else ucv = ((1.0 - S.a[r]) * vk - S.c[r]) / S.b[r];
+    }
+    xs[0] = pk;
+    xs[N + 1] = vk;
+    for (int k = 0; k < N; ++k) {
+        const double u = mode == 0 ? ucv : u_prev[(size_t)b * N + (k + 1 < N ? k + 1 : N - 1)];
+        int r = gadmm_region(S, vk, 0.0);
+        if (r < 0) { ok = false; r = 0; }
+        seq[(size_t)b * N + k] = (int8_t)r;
+        if (u_ws) u_ws[(size_t)b * N + k] = u;
+        const double vn = S.a[r] * vk + S.b[r] * u + S.c[r];
+        pk = pk + S.ts * vk;
+        vk = vn;
+        xs[k + 1] = pk;
+        xs[N + 1 + k + 1] = vk;
+    }
+    if (!ok) gadmm_fail(state, p);
+}
+
+// edge bits of the switching rule: active V rows at a region edge strictly inside the state box
+template <int N>
+__device__ inline uint32_t gadmm_edges(const hvp_system& S, uint64_t code, uint32_t raw) {
+    uint32_t out = 0;
+#pragma unroll
+    for (int j = 0; j + 1 < N; ++j) {
+        const int r = hvp::code_region(code, j + 1);
+        const double lo = S.vlo[r], hi = S.vhi[r];
+        if (((raw >> (2 * j)) & 1u) && lo > S.vmin + 1e-9 * (1.0 + fabs(lo))) out |= 1u << (2 * j);
+        if (((raw >> (2 * j + 1)) & 1u) && hi < S.vmax - 1e-9 * (1.0 + fabs(hi))) out |= 1u << (2 * j + 1);
+    }
+    return out;
+}
+
+// outputs of one solved local problem: u, trajectory slot, copies (front: closed-form optimum of
+// its hinge problem, back: z_b - y_b / rho)
+template <int N>
+__device__ inline void gadmm_write(int b, int slot, const hvp_system& S, const hvp::Consts& C, int rl,
+                                   const double* prm, uint64_t code, const double* y, double* u_out, double* x,
+                                   double* xf, double* xb) {
+    const int K1 = N + 1;
+    double* xs = x + (size_t)slot * 2 * K1;
+    double* fs = xf + (size_t)slot * 2 * K1;
+    double* bs = xb + (size_t)slot * 2 * K1;
+    const bool front = (rl & HVP_ROLE_SAFE_FRONT) != 0, back = (rl & HVP_ROLE_BACK_COPY) != 0;
+    const bool tf = (rl & HVP_ROLE_TRACK_FRONT) != 0;
+    const double* yb = hvp::admm_y(prm, 1, N);
+    const double* zb = hvp::admm_z(prm, 1, N);
+    double p = prm[0], v = prm[1];
+    for (int k = 0; k <= N; ++k) {
+        xs[k] = p;
+        xs[K1 + k] = v;
+        double e = 0.0, g = 0.0;
+        if (front)
+            hvp::admm_copy_value(C, tf, 0, hvp::admm_y(prm, 0, N)[k], hvp::admm_y(prm, 0, N)[K1 + k],
+                                 hvp::admm_z(prm, 0, N)[k], hvp::admm_z(prm, 0, N)[K1 + k], p, v, &e, &g);
+        fs[k] = e;
+        fs[K1 + k] = g;
+        bs[k] = back ? zb[k] - yb[k] / C.rho : 0.0;
+        bs[K1 + k] = back ? zb[K1 + k] - yb[K1 + k] / C.rho : 0.0;
+        if (k < N) {
+            const int r = hvp::code_region(code, k);
+            const double vn = y[k];
+            u_out[(size_t)b * N + k] = (vn - S.a[r] * v - S.c[r]) / S.b[r];
+            p = p + S.ts * v;
+            v = vn;
+        }
+    }
+}
+
+template <int N>
+__device__ inline uint64_t gadmm_code(const int8_t* seq, int b) {
+    uint64_t code = 0;
+#pragma unroll
+    for (int k = 0; k < N; ++k) code = hvp::code_with(code, k, seq[(size_t)b * N + k]);
+    return code;
+}
+
+// x-update, one lane per local QP (N <= 8)
+template <int N>
+__global__ __launch_bounds__(kBnbBlock<N>) void k_gadmm_qp(int P, int n, int lo, int m,
+                                                           const hvp_system* __restrict__ systems,
+                                                           const int32_t* __restrict__ sys,
+                                                           const int32_t* __restrict__ role,
+                                                           const double* __restrict__ params, hvp::Consts C,
+                                                           const int8_t* __restrict__ seq,
+                                                           int32_t* __restrict__ state, double* __restrict__ u_out,
+                                                           double* __restrict__ x, double* __restrict__ xf,
+                                                           double* __restrict__ xb, double* __restrict__ cost_out,
+                                                           int32_t* __restrict__ status_out,
+                                                           uint32_t* __restrict__ edge_out,
+                                                           int32_t* __restrict__ iters_out,
+                                                           unsigned long long* __restrict__ counter) {
+    constexpr int BS = kBnbBlock<N>;
+    const int b = blockIdx.x * BS + threadIdx.x;
+    if (b >= P * m) return;
+    const int p = b / m;
+    if (!(state[p] & 1)) return;
+    const hvp_system& S = systems[sys[b]];
+    const int rl = role[b];
+    const double* prm = params + (size_t)b * C.stride;
+    const uint64_t code = gadmm_code<N>(seq, b);
+    hvp::LaneQp<N, LdsMem<N, BS>> q;
+    q.mem.lane = threadIdx.x;
+    int it = 0;
+    uint32_t raw = 0;
+    const int st = hvp::solve_admm_lane<N>(q, S, C, rl, prm, code, N, kGiMaxIter<N>, it, &raw);
+    if (iters_out) iters_out[b] = it;
+    atomicAdd(&counter[1], (unsigned long long)it);
+    if (st == hvp::GI_OK) {
+        cost_out[b] = hvp::admm_direct_cost<N>(q, S, C, rl, prm, code, N);
+        status_out[b] = HVP_OPTIMAL;
+        edge_out[b] = gadmm_edges<N>(S, code, raw);
+        gadmm_write<N>(b, gadmm_slot(b, n, lo, m), S, C, rl, prm, code, q.y, u_out, x, xf, xb);
+    } else {
+        cost_out[b] = 1e300;
+        status_out[b] = st == hvp::GI_FAIL_DUAL ? HVP_INFEASIBLE : HVP_MAXITER;
+        edge_out[b] = 0;
+        gadmm_fail(state, p);
+    }
+}
+
+// x-update, one 16-lane group per local QP (long horizons, hvp_coop.h)
+template <int N>
+__global__ __launch_bounds__(kCoopBlock) void k_gadmm_qp_coop(int P, int n, int lo, int m,
+                                                              const hvp_system* __restrict__ systems,
+                                                              const int32_t* __restrict__ sys,
+                                                              const int32_t* __restrict__ role,
+                                                              const double* __restrict__ params, hvp::Consts C,
+                                                              const int8_t* __restrict__ seq,
+                                                              int32_t* __restrict__ state, double* __restrict__ u_out,
+                                                              double* __restrict__ x, double* __restrict__ xf,
+                                                              double* __restrict__ xb, double* __restrict__ cost_out,
+                                                              int32_t* __restrict__ status_out,
+                                                              uint32_t* __restrict__ edge_out,
+                                                              int32_t* __restrict__ iters_out,
+                                                              unsigned long long* __restrict__ counter) {
+    __shared__ hvp::coop::GroupLds lds[kCoopGroups];
+    const int g = threadIdx.x / hvp::coop::G, t = threadIdx.x % hvp::coop::G;
+    const int b = blockIdx.x * kCoopGroups + g;
+    if (b >= P * m) return;  // group-uniform
+    const int p = b / m;
+    if (!(state[p] & 1)) return;
+    const hvp_system& S = systems[sys[b]];
+    const int rl = role[b];
+    const double* prm = params + (size_t)b * C.stride;
+    const uint64_t code = gadmm_code<N>(seq, b);
+    hvp::coop::Lane<N> L;
+    double cost = 0.0;
+    int it = 0;
+    unsigned raw = 0;
+    const int st = hvp::coop::solve_qp<N>(L, lds[g], S, C, rl, prm, code, N, kGiMaxIter<N>, it, &cost, &raw);
+    if (st == hvp::GI_OK) {
+        lds[g].v[t] = t < N ? L.y : 0.0;
+        hvp::coop::gsync();
+    }
+    if (t != 0) return;
+    if (iters_out) iters_out[b] = it;
+    atomicAdd(&counter[1], (unsigned long long)it);
+    if (st == hvp::GI_OK) {
+        double y[N];
+#pragma unroll
+        for (int k = 0; k < N; ++k) y[k] = lds[g].v[k];
+        cost_out[b] = cost;
+        status_out[b] = HVP_OPTIMAL;
+        edge_out[b] = gadmm_edges<N>(S, code, raw);
+        gadmm_write<N>(b, gadmm_slot(b, n, lo, m), S, C, rl, prm, code, y, u_out, x, xf, xb);
+    } else {
+        cost_out[b] = 1e300;
+        status_out[b] = st == hvp::GI_FAIL_DUAL ? HVP_INFEASIBLE : HVP_MAXITER;
+        edge_out[b] = 0;
+        gadmm_fail(state, p);
+    }
+}
+
+inline int grid_for(long long n) { return (int)std::max<long long>(1, (n + kBlock - 1) / kBlock); }
+
+template <int N>
+int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, const double* params, double* u_out,
+               double* x_out, int8_t* region_out, int8_t* gear_out, double* cost_out, int32_t* status_out,
+               int32_t* nodes_out, int32_t* iters_out, hipStream_t st, double* xf_out = nullptr,
+               double* xb_out = nullptr) {
+    Workspace ws = h->ws;
+    constexpr int BS = kBnbBlock<N>;
+    HIP_TRY(hipMemsetAsync(ws.counter, 0, 8 * sizeof(unsigned long long), st));
+    HIP_TRY(hipMemsetAsync(ws.lvl, 0, 2 * (HVP_MAX_N + 1) * sizeof(unsigned long long), st));  // + claims
+    HIP_TRY(hipEventRecord(h->ev0, st));
+    HIP_TRY(hipEventRecord(h->evq0, st));
+    const size_t lds = sizeof(double) * hvp::F_COUNT * N * BS;
+    HIP_TRY(hipEventRecord(h->evb[0], st));
+    if constexpr (kCoop<N>) {
+        hipLaunchKernelGGL(k_bnb_root_coop<N>, dim3((B + kCoopGroups - 1) / kCoopGroups), dim3(kCoopBlock), 0, st, B,
+                           h->d_sys, sys, role, params, h->C, ws);
+    } else {
+        if (h->C.form == HVP_FORM_ADMM) {
+            hipLaunchKernelGGL((k_bnb_root<N, true>), dim3((B + BS - 1) / BS), dim3(BS), lds, st, B, h->d_sys, sys,
+                               role, params, h->C, ws);
+        } else {
+            // sigma-independent QP part once per instance, then the root kernel
+            hipLaunchKernelGGL(k_inst_prep<N>, dim3(grid_for(B)), dim3(kBlock), 0, st, B, h->d_sys, sys, role, params,
+                               h->C, ws);
+            HIP_TRY(hipGetLastError());
+            // (a refilling root kernel -- root QP, dive, leaf QP per lane -- measured 1.9x slower than
+            // one lane per instance: its events carry the dive and a second setup)
+            hipLaunchKernelGGL((k_bnb_root<N, false>), dim3((B + BS - 1) / BS), dim3(BS), lds, st, B, h->d_sys, sys,
+                               role, params, h->C, ws);
+        }
+    }
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(h->evb[1], st));
+    const int g_small = (int)std::min<long long>(grid_for(h->ws.cap), (long long)h->n_cu * 8);
+    const int g_qp = (int)std::min<long long>((h->ws.cap + BS - 1) / BS, (long long)h->n_cu * 8 * (kBlock / BS));
+    const int quota = (int)std::min<int64_t>(h->ws.cap / B, 1 << 30);
+    for (int k = 1; k <= N; ++k) {
+        HIP_TRY(hipMemsetAsync(ws.inst_lvl, 0, sizeof(int32_t) * B, st));
+        hipLaunchKernelGGL(k_bnb_expand<N>, dim3(g_small), dim3(kBlock), 0, st, k, quota, h->d_sys, sys, h->C, ws);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(h->evb[2 * k], st));
+        if constexpr (kCoop<N>) {
+            const int g_coop = (int)std::min<long long>((h->ws.cap + kCoopGroups - 1) / kCoopGroups,
+                                                        (long long)h->n_cu * 32);
+            hipLaunchKernelGGL(k_bnb_bound_coop<N>, dim3(g_coop), dim3(kCoopBlock), 0, st, k, h->d_sys, sys, role,
+                               params, h->C, ws);
+        } else {
+            if (h->C.form == HVP_FORM_ADMM) {
+                hipLaunchKernelGGL((k_bnb_bound<N, true>), dim3(g_qp), dim3(BS), lds, st, k, h->d_sys, sys, role,
+                                   params, h->C, ws);
+            } else {
+                // persistent waves: 2 blocks per CU, every wave refills its lanes until the level is done
+                const int g_refill = (int)std::min<long long>((h->ws.cap + BS - 1) / BS,
+                                                              (long long)h->n_cu * kRefillBlocksPerCu);
+                hipLaunchKernelGGL(k_bnb_bound_refill<N>, dim3(g_refill), dim3(BS), lds, st, k, h->d_sys, sys, role,
+                                   params, h->C, ws);
+            }
+        }
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(h->evb[2 * k + 1], st));
+    }
+    HIP_TRY(hipEventRecord(h->evq1, st));
+    if constexpr (N <= HVP_MAX_N_ENUM) {
+        if (h->C.form == HVP_FORM_DECENT)
+        hipLaunchKernelGGL(k_bnb_ipm<N>, dim3(std::max(1, h->n_cu)), dim3(BS), lds, st, h->d_sys, sys, role, params,
+                           h->C, ws);
+        HIP_TRY(hipGetLastError());
+    }
+    hipLaunchKernelGGL(k_bnb_key<N>, dim3(g_small), dim3(kBlock), 0, st, ws, h->C.form);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_bnb_write<N>, dim3(g_small), dim3(kBlock), 0, st, h->d_sys, sys, role, params, h->C, ws,
+                       u_out, x_out, region_out, gear_out, cost_out, xf_out, xb_out);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_bnb_finish<N>, dim3(grid_for(B)), dim3(kBlock), 0, st, B, h->d_sys, sys, role, params, h->C,
+                       ws, u_out, x_out, region_out, gear_out, cost_out, status_out, nodes_out, iters_out, xf_out,
+                       xb_out);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(h->ev1, st));
+    h->last_stream = st;
+    h->last_B = B;
+    h->last_bnb = true;
+    return 0;
+}
+
+template <int N>
+int launch_all(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, const double* params, double* u_out,
+               double* x_out, int8_t* region_out, int8_t* gear_out, double* cost_out, int32_t* status_out,
+               int32_t* nodes_out, int32_t* iters_out, hipStream_t st) {
+    Workspace ws = h->ws;
+    HIP_TRY(hipMemsetAsync(ws.counter, 0, 8 * sizeof(unsigned long long), st));
+    HIP_TRY(hipEventRecord(h->ev0, st));
+    hipLaunchKernelGGL(k_enum<N>, dim3(grid_for(B)), dim3(kBlock), 0, st, B, h->d_sys, sys, role, params, h->C, ws);
+    HIP_TRY(hipGetLastError());
+    // the candidate count is only known on the device: size the grid for the capacity bound
+    // (≈ every CU x 8 blocks) and let the kernel grid-stride over the real count
+    const long long want = std::min<long long>(grid_for(h->ws.cap), (long long)h->n_cu * 8);
+    HIP_TRY(hipEventRecord(h->evq0, st));
+    const size_t lds = sizeof(double) * hvp::F_COUNT * N * kBlock;
+    hipLaunchKernelGGL(k_qp_gi<N>, dim3((int)want), dim3(kBlock), lds, st, h->d_sys, sys, role, params, h->C, ws);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(h->evq1, st));
+    // fallback list (normally empty: the launch reads a zero count and exits)
+    hipLaunchKernelGGL(k_qp_ipm<N>, dim3(std::max(1, h->n_cu)), dim3(kBlock), lds, st, h->d_sys, sys, role,
+                       params, h->C, ws);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_cost<N>, dim3((int)want), dim3(kBlock), 0, st, h->d_sys, sys, role, params, h->C, ws);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_select<N>, dim3(grid_for(B)), dim3(kBlock), 0, st, B, h->d_sys, sys, params, ws, u_out,
+                       x_out, region_out, gear_out, cost_out, status_out, nodes_out, iters_out);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(h->ev1, st));
+    h->last_stream = st;
+    h->last_B = B;
+    h->last_bnb = false;
+    return 0;
+}
+
+template <int N>
+int launch_gadmm_qp(hvp_handle* h, int P, int n, int lo, int m, const int32_t* sys, const int32_t* role,
+                           const double* params, const int8_t* seq, int32_t* state, double* u_out, double* x,
+                           double* xf, double* xb, double* cost_out, int32_t* status_out, uint32_t* edge_out,
+                           int32_t* iters_out, hipStream_t st) {
+    const int B = P * m;
+    HIP_TRY(hipEventRecord(h->evq0, st));
+    if constexpr (kCoop<N>) {
+        hipLaunchKernelGGL(k_gadmm_qp_coop<N>, dim3((B + kCoopGroups - 1) / kCoopGroups), dim3(kCoopBlock), 0, st, P, n,
+                           lo, m, h->d_sys, sys, role, params, h->C, seq, state, u_out, x, xf, xb, cost_out,
+                           status_out, edge_out, iters_out, h->g_counter);
+    } else {
+        constexpr int BS = kBnbBlock<N>;
+        const size_t lds = sizeof(double) * hvp::F_COUNT * N * BS;
+        hipLaunchKernelGGL(k_gadmm_qp<N>, dim3((B + BS - 1) / BS), dim3(BS), lds, st, P, n, lo, m, h->d_sys, sys, role,
+                           params, h->C, seq, state, u_out, x, xf, xb, cost_out, status_out, edge_out, iters_out,
+                           h->g_counter);
+    }
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(h->evq1, st));
+    h->last_stream = st;
+    h->last_B = B;
+    h->last_bnb = false;
+    return 0;
+}
+
+template <int N>
+int launch_evaluate(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, const double* params,
+                    const int8_t* gear_in, const double* u_in, double* cost_out, int32_t* status_out, double* x_out,
+                    hipStream_t st) {
+    hipLaunchKernelGGL(k_evaluate<N>, dim3(grid_for(B)), dim3(kBlock), 0, st, B, h->d_sys, sys, role, params, h->C,
+                       gear_in, u_in, cost_out, status_out, x_out);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+template <int N>
+int launch_gadmm_rollout(hvp_handle* h, int P, int n, int lo, int m, const int32_t* sys, const double* params,
+                         int mode, const double* u_prev, double* x, int8_t* seq, double* u_ws, int32_t* state,
+                         hipStream_t st) {
+    const int B = P * m;
+    hipLaunchKernelGGL(k_gadmm_rollout<N>, dim3(grid_for(B)), dim3(kBlock), 0, st, P, n, lo, m, h->d_sys, sys,
+                       params, h->C.stride, mode, u_prev, x, seq, u_ws, state);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+// One object file per horizon: every other translation unit sees only these declarations.
+#define HVP_LANE_LAUNCHERS(EXT, n)                                                                                  \
+    EXT template int launch_bnb<n>(hvp_handle*, int, const int32_t*, const int32_t*, const double*, double*, double*, \
+                                   int8_t*, int8_t*, double*, int32_t*, int32_t*, int32_t*, hipStream_t, double*,   \
+                                   double*);                                                                          \
+    EXT template int launch_evaluate<n>(hvp_handle*, int, const int32_t*, const int32_t*, const double*,             \
+                                        const int8_t*, const double*, double*, int32_t*, double*, hipStream_t);      \
+    EXT template int launch_gadmm_rollout<n>(hvp_handle*, int, int, int, int, const int32_t*, const double*, int,    \
+                                             const double*, double*, int8_t*, double*, int32_t*, hipStream_t);       \
+    EXT template int launch_gadmm_qp<n>(hvp_handle*, int, int, int, int, const int32_t*, const int32_t*,             \
+                                        const double*, const int8_t*, int32_t*, double*, double*, double*, double*,  \
+                                        double*, int32_t*, uint32_t*, int32_t*, hipStream_t);
+#define HVP_ENUM_LAUNCHER(EXT, n)                                                                                    \
+    EXT template int launch_all<n>(hvp_handle*, int, const int32_t*, const int32_t*, const double*, double*, double*, \
+                                   int8_t*, int8_t*, double*, int32_t*, int32_t*, int32_t*, hipStream_t);
+#define HVP_FOR_LANE_N(X, EXT) X(EXT, 2) X(EXT, 3) X(EXT, 4) X(EXT, 5) X(EXT, 6) X(EXT, 7) X(EXT, 8) X(EXT, 9) \
+    X(EXT, 10) X(EXT, 11) X(EXT, 12) X(EXT, 13) X(EXT, 14) X(EXT, 15) X(EXT, 16)
+#define HVP_FOR_ENUM_N(X, EXT) X(EXT, 2) X(EXT, 3) X(EXT, 4) X(EXT, 5) X(EXT, 6) X(EXT, 7) X(EXT, 8)
+
+#ifndef HVP_LANE_INST
+HVP_FOR_LANE_N(HVP_LANE_LAUNCHERS, extern)
+HVP_FOR_ENUM_N(HVP_ENUM_LAUNCHER, extern)
+#endif
+
+}  // namespace hvp_k

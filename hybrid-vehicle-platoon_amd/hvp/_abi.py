@@ -97,7 +97,8 @@ def params_stride(N: int, formulation: int = 0) -> int:
 
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_DIR = os.path.join(_PKG_ROOT, "lib")
-LIB_PATH = os.path.join(LIB_DIR, "libhvpsolve.so")
+# HVP_LIB: an alternative build of the same library (A/B kernel variants); default the in-tree build
+LIB_PATH = os.environ.get("HVP_LIB") or os.path.join(LIB_DIR, "libhvpsolve.so")
 HOSTREF_PATH = os.path.join(LIB_DIR, "libhvp_hostref.so")
 
 _lib = None

@@ -23,6 +23,7 @@ and the run repeats until no sequence changes (at most ``max_rounds``).
 
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import pickle
 import time
@@ -240,9 +241,21 @@ class GAdmmEngine:
         if self.exchange is not None:
             self.exchange(self.x, self.xf, self.xb)
 
+    def _on(self, stream):
+        """Make `stream` torch's current stream for the duration: the halo exchange, the flag
+        reductions and the torch ops between launches then run in launch order with the kernels
+        (a caller stream other than the current one would otherwise race with them)."""
+        import torch
+
+        return torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
+
     def run(self, mode: int, stream=None) -> dict:
         """One GAdmmCoordinator.g_admm_control(state, warm_start) for every platoon: returns
         cost (P,) (inf where the run failed), rounds and QP launches."""
+        with self._on(stream):
+            return self._run(mode, None)
+
+    def _run(self, mode: int, stream=None) -> dict:
         import torch
 
         st = self.state
@@ -281,6 +294,10 @@ class GAdmmEngine:
         """TrackingGAdmmCoordinator.g_admm_control (:255-301) for every platoon.  states: (P, 2n)
         measured platoon states.  Returns u (B, N) of the best warm start, its cost (P,) (inf:
         no warm start succeeded -> the reference raises) and per-run details."""
+        with self._on(stream):
+            return self._control(states)
+
+    def _control(self, states, stream=None) -> dict:
         import torch
 
         st = torch.as_tensor(states, dtype=torch.float64).to(self.dev).reshape(self.P, self.n, 2)
@@ -292,7 +309,7 @@ class GAdmmEngine:
         modes = [0] if self.prev_u is None else [0, 1]
         new_prev = self.prev_u.clone() if self.prev_u is not None else torch.zeros_like(self.u)
         for w, mode in enumerate(modes):
-            r = self.run(mode, stream)
+            r = self._run(mode, stream)
             runs.append(r)
             okB = (~r["failed"]).repeat_interleave(self.m)[:, None]
             better = r["cost"] < best_cost  # ties keep the earlier warm start (:290)

@@ -11,6 +11,11 @@ profiles/<round>_summary.json with, per kernel:
                          FETCH_SIZE tallies half the bytes of wide reads; WRITE_SIZE is exact)
   f64_wave_instrs        SQ_INSTS_VALU_{FMA,MUL,ADD,TRANS}_F64 per launch (wave instructions)
   f64_flop               64 lanes * (2 FMA + MUL + ADD + TRANS): an upper bound (masked lanes count)
+  lane_util              SQ_THREAD_CYCLES_VALU / (64 SQ_ACTIVE_INST_VALU): active lanes per VALU issue
+  f64_flop_active        f64_flop * lane_util (masked lanes removed, assuming the F64 share is uniform)
+  valu_issue_frac        SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES (share of wave lifetime issuing VALU)
+  wait_frac, stall_frac  SQ_WAIT_ANY, SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES (parked on waitcnt / issue-stalled)
+  waves_per_cu           mean resident waves per CU: 4 SQ_WAVE_CYCLES (quad-cycles) / (GRBM_GUI_ACTIVE / 8 XCDs) / 256 CUs
 bench.py reads hbm_bytes of its dominant kernel from here as roofline.traffic.
 """
 
@@ -61,7 +66,7 @@ def main() -> None:
         with open(p) as f:
             extra[name] = {short(r["Name"]): {"avg_ms": float(r["AverageNs"]) / 1e6, "calls": int(r["Calls"])}
                            for r in csv.DictReader(f)}
-    for sub in ("fetch", "write", "f64"):
+    for sub in ("fetch", "write", "f64", "occ"):
         p = os.path.join(src, sub, "run_counter_collection.csv")
         if not os.path.exists(p):
             continue
@@ -81,7 +86,22 @@ def main() -> None:
             d["f64_flop"] = 64.0 * (2 * f64[0] + f64[1] + f64[2] + f64[3])
             if d.get("avg_ms"):
                 d["f64_tflops"] = d["f64_flop"] / (d["avg_ms"] * 1e-3) / 1e12
+        if d.get("SQ_ACTIVE_INST_VALU") and d.get("SQ_THREAD_CYCLES_VALU") is not None:
+            d["lane_util"] = d["SQ_THREAD_CYCLES_VALU"] / (64.0 * d["SQ_ACTIVE_INST_VALU"])
+            if "f64_flop" in d:
+                d["f64_flop_active"] = d["f64_flop"] * d["lane_util"]
+                if d.get("avg_ms"):
+                    d["f64_tflops_active"] = d["f64_flop_active"] / (d["avg_ms"] * 1e-3) / 1e12
+        wc = d.get("SQ_WAVE_CYCLES")
+        if wc:
+            for key, c in (("valu_issue_frac", "SQ_ACTIVE_INST_VALU"), ("wait_frac", "SQ_WAIT_ANY"),
+                           ("stall_frac", "SQ_WAIT_INST_ANY"), ("active_frac", "SQ_ACTIVE_INST_ANY")):
+                if d.get(c) is not None:
+                    d[key] = d[c] / wc
+            if d.get("GRBM_GUI_ACTIVE"):
+                d["waves_per_cu"] = 4.0 * wc / (d["GRBM_GUI_ACTIVE"] / 8.0) / 256.0
     meta = {"round": rnd, "source": "profiles/run_profiles.sh (rocprofv3 kernel trace + separate PMC passes)",
+            "workload": open(os.path.join(src, "cmd.txt")).read().strip() if os.path.exists(os.path.join(src, "cmd.txt")) else None,
             "kernels": out, "workloads": extra}
     with open(os.path.join(here, f"{rnd}_summary.json"), "w") as f:
         json.dump(meta, f, indent=1, sort_keys=True)
