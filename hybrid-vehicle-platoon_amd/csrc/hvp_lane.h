@@ -1248,8 +1248,9 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
             hipLaunchKernelGGL(k_inst_prep<N>, dim3(grid_for(B)), dim3(kBlock), 0, st, B, h->d_sys, sys, role, params,
                                h->C, ws);
             HIP_TRY(hipGetLastError());
-            // (a refilling root kernel -- root QP, dive, leaf QP per lane -- measured 1.9x slower than
-            // one lane per instance: its events carry the dive and a second setup)
+            // (one lane per instance, 1 wave per SIMD: a persistent 2-wave root kernel -- root QP,
+            // dive, leaf QP per lane, generations of 64 -- spilled inside its active-set loop and
+            // measured 17 % slower on the whole step, profiles/r02f_*)
             hipLaunchKernelGGL((k_bnb_root<N, false>), dim3((B + BS - 1) / BS), dim3(BS), lds, st, B, h->d_sys, sys,
                                role, params, h->C, ws);
         }
