@@ -42,17 +42,62 @@ def instance_io_bytes(N: int) -> int:
     return 8 * (2 + 6 * (N + 1) + N + 2 * (N + 1) + 1) + N
 
 
-def profiled(kernel: str):
-    """Per-launch PMC figures of `kernel` from the newest committed profiles/r*_summary.json
-    (profiles/run_profiles.sh runs this bench at its default workload under rocprofv3)."""
+def profiled(kernel: str, tag: str):
+    """Per-launch PMC figures of `kernel` from the newest committed profiles/r*_<tag>_summary.json
+    (profiles/run_profiles.sh runs this bench's workload `tag` under rocprofv3)."""
     import glob
 
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_summary.json")), reverse=True):
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{tag}_summary.json")), reverse=True):
         with open(path) as f:
             d = json.load(f)["kernels"].get(kernel)
         if d:
             return d, os.path.relpath(path, ROOT)
     return None, None
+
+
+def qp_roofline(qp_step_ms: float, kernels: list, notional_bytes: float, tag: str) -> dict:
+    """Roofline of the QP kernels of one step, from the live HIP-event time of their launches
+    (qp_step_ms) and the per-launch PMC figures of profiles/ (the same bench workload):
+
+      bound "fp64"   the kernels are FP64-VALU / latency bound (dense fixed-sequence QPs built
+                     in registers): achieved = PMC FP64 FLOPs of the step's
+                     QP launches, masked lanes removed (f64_flop_active = 64-lane FLOP count x
+                     SQ_THREAD_CYCLES_VALU / (64 SQ_ACTIVE_INST_VALU)), / qp_step_ms; peak 78.6.
+      traffic        PMC HBM bytes of the same launches (2 FETCH_SIZE + WRITE_SIZE) per step;
+                     "hbm" reports traffic / qp_step_ms against 8 TB/s.
+      survey_8d      SURVEY 8(d)'s notional dense-QP bytes (never moved by these kernels), as a
+                     labelled side figure only.
+    kernels: [(name, launches per step)]; tag: the profiled workload (profiles/r*_<tag>_summary.json)."""
+    flop = flop_all = traffic = 0.0
+    srcs, prof_ms = set(), {}
+    for name, count in kernels:
+        d, src = profiled(name, tag)
+        if not d or "f64_flop_active" not in d or "hbm_bytes" not in d:
+            flop = None
+            break
+        flop += d["f64_flop_active"] * count
+        flop_all += d["f64_flop"] * count
+        traffic += d["hbm_bytes"] * count
+        srcs.add(src)
+        prof_ms[name] = d.get("avg_ms")
+    t = qp_step_ms * 1e-3
+    out = {"bound": "fp64", "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "kernel": "+".join(k for k, _ in kernels),
+           "launches_per_step": sum(c for _, c in kernels), "qp_ms_per_step": qp_step_ms,
+           "kernel_avg_ms": qp_step_ms / max(1, sum(c for _, c in kernels)),
+           "survey_8d": {"note": "notional dense-QP bytes of SURVEY 8(d), not moved by the kernels",
+                         "bytes_per_step": notional_bytes, "GB_per_s": notional_bytes / t / 1e9}}
+    if flop is None:
+        out.update({"achieved": None, "frac": None, "traffic": None,
+                    "note": "no committed PMC profile of this workload (profiles/run_profiles.sh)"})
+        return out
+    achieved = flop / t / 1e12
+    out.update({"achieved": achieved, "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
+                "flop_per_step": flop, "flop_per_step_all_lanes": flop_all,
+                "frac_all_lanes": flop_all / t / 1e12 / FP64_PEAK_TFLOPS,
+                "hbm": {"achieved": traffic / t / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": traffic / t / 1e9 / HBM_PEAK_GBS},
+                "profile": sorted(srcs), "profile_avg_ms": prof_ms})
+    return out
 
 
 def make_inputs(seeds, n: int, N: int):
@@ -119,14 +164,31 @@ def hostref_baseline(n: int, N: int, budget_s: float, threads: int, method: int 
             "sample": f"{done} platoons, same lane algorithm built with g++ -O2 -fopenmp"}
 
 
+def leader_windows(T: int, N: int, S: int, dev):
+    """Constant-velocity leader (p = 3000 + 20 t, v = 20): per step t its window (S, 2, N+1)
+    and state (S, 2), resident on the device."""
+    import torch
+
+    lx = np.stack([3000.0 + 20.0 * np.arange(T + N + 1), np.full(T + N + 1, 20.0)])
+    wins = torch.from_numpy(np.ascontiguousarray(np.stack([np.broadcast_to(lx[:, t:t + N + 1], (S, 2, N + 1))
+                                                           for t in range(T)]))).to(dev)
+    lead = torch.from_numpy(np.ascontiguousarray(np.stack([np.broadcast_to(lx[:, t], (S, 2)) for t in range(T)]))).to(dev)
+    return wins, lead
+
+
 def bench_admm(args, world: int, rank: int, local: int, dist) -> None:
-    """configs[2]: fleet_naive_admm, one step = admm_iters x (n local MIQPs per platoon + the
-    z/y update) for every platoon of the rank's seed range, all on the device."""
+    """configs[2]: fleet_naive_admm in closed loop on the device.  One step = one platoon
+    timestep of ADMMCoordinator.get_control (fleet_naive_admm.py:379-477: warm start from the
+    shifted previous solutions, y carried across steps as the reference never resets it
+    (:357-359), admm_iters x (n local MIQPs per platoon + the z/y update)) followed by
+    PlatoonEnv.step on the device (hvp_env_step_batch); the next step starts from the new states
+    and the moved leader window."""
     import torch
 
     from hvp import tables
     from hvp.admm import AdmmEngine, admm_problem
     from hvp.env import derive_env_seed, initial_platoon_state
+    from hvp.envdev import DeviceEnv
     from hvp.models import PwaGearVehicle
 
     n, N, S, iters = args.n, args.N, args.platoons, args.admm_iters
@@ -137,33 +199,41 @@ def bench_admm(args, world: int, rank: int, local: int, dist) -> None:
                        for s in seeds])
     roles = [tables.role_bits(i == 0, i == n - 1, i == 0) for i in range(n)] * S
     eng = AdmmEngine(admm_problem(N, 0.5), [system], np.zeros(n * S, np.int32), roles, n, S, device=local)
-    eng.set_leader(np.stack([3000.0 + 20.0 * np.arange(N + 1), np.full(N + 1, 20.0)]))
-    t_states = torch.from_numpy(states).to(eng.dev)
+    dev = eng.dev
+    T = args.warmup + args.steps + 1
+    wins, lead = leader_windows(T, N, S, dev)
+    env = DeviceEnv(eng.solver, torch.full((S, n), 800.0, dtype=torch.float64, device=dev))
+    x = torch.from_numpy(states).to(dev)
+    u = torch.empty((S, n), dtype=torch.float64, device=dev)
+    u_prev = [None]
+    notopt = torch.zeros((), dtype=torch.int64, device=dev)
+    bad = torch.zeros((), dtype=torch.int64, device=dev)
 
-    def fresh():  # every timed step starts from the same coordinator state (y = z = 0, no warm start)
-        eng.params.zero_()
-        eng.y_front.zero_()
-        eng.y_back.zero_()
-        eng.x_prev = None
-        eng.set_leader(np.stack([3000.0 + 20.0 * np.arange(N + 1), np.full(N + 1, 20.0)]))
+    def step(t, on_solve=None):
+        eng.set_leader_device(wins[t])
+        o = eng.step(x, iters, on_solve=on_solve)
+        u.copy_(o["u"][:, 0].view(S, n))
+        notopt.add_((o["status"] != 0).sum())
+        r = env.step(x, u, lead[t], u_prev=u_prev[0])
+        bad.add_(r["status"].sum())
+        u_prev[0] = u.clone()
+        return o
 
-    for _ in range(args.warmup):
-        fresh()
-        eng.step(t_states, iters)
+    for t in range(args.warmup):
+        step(t)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        fresh()
-        eng.step(t_states, iters)
+    for t in range(args.warmup, args.warmup + args.steps):
+        step(t)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     dt = time.perf_counter() - t0
     if dist:
-        tt = torch.tensor([dt], device=eng.dev, dtype=torch.float64)
+        tt = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     # QP-launch timing and work counters of one more step (stats synchronise per iteration)
@@ -175,29 +245,24 @@ def bench_admm(args, world: int, rank: int, local: int, dist) -> None:
         acc["qps"] += st.n_candidates
         acc["it"] += st.qp_iterations
 
-    fresh()
-    o = eng.step(t_states, iters, on_solve=on_solve)
-    ok = bool((o["status"] == 0).all().item())
+    step(args.warmup + args.steps, on_solve=on_solve)
     value = S * world * args.steps / dt
-    alg_bytes = acc["qps"] * dense_qp_bytes(N) + iters * n * S * instance_io_bytes(N)
-    achieved = alg_bytes / (acc["qp_ms"] * 1e-3) / 1e9
+    notional = acc["qps"] * dense_qp_bytes(N) + iters * n * S * instance_io_bytes(N)
+    qk = ([("k_bnb_root_coop", iters), ("k_bnb_bound_coop", iters * N)] if N > 8
+          else [("k_bnb_root", iters), ("k_bnb_bound", iters * N)])
     result = {
         "metric": f"MPC timesteps/sec (whole platoon) at n={n} N={N} naive_admm ({iters} ADMM iterations)",
         "value": value, "unit": "platoon-timesteps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic: env.reset random-init platoon states (seeded), constant-velocity leader, "
-                "coordinator state reset each step (first-time-step ADMM: y = z = 0)",
-        "config": {"workload": f"fleet_naive_admm n={n} N={N} pwa_gear (configs[2])", "n_vehicles": n, "horizon": N,
-                   "admm_iters": iters, "rho": 0.5, "platoons_per_gpu": S,
+        "data": "synthetic: env.reset random-init platoon states (seeded), constant-velocity leader; closed loop "
+                "on the device (ADMM control + plant step), y and the warm starts carried across steps",
+        "config": {"workload": f"fleet_naive_admm n={n} N={N} pwa_gear closed loop (configs[2])", "n_vehicles": n,
+                   "horizon": N, "admm_iters": iters, "rho": 0.5, "platoons_per_gpu": S,
                    "local_miqps_per_step": iters * n * S * world, "parallelism": f"seeds-sharded x{world}"},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "k_bnb_root+k_bnb_bound", "qp_ms_per_step": acc["qp_ms"],
-                     "kernel_avg_ms": acc["qp_ms"] / (iters * (N + 1)),
-                     "algorithmic_bytes_per_step": alg_bytes,
-                     "note": "SURVEY 8(d) dense-QP bytes per local QP solved / HIP-event time of the QP launches"},
-        "qps_per_step": acc["qps"], "qp_iters_per_qp": acc["it"] / max(acc["qps"], 1), "all_optimal": ok,
+        "roofline": qp_roofline(acc["qp_ms"], qk, notional, f"admm_n{n}_N{N}"),
+        "qps_per_step": acc["qps"], "qp_iters_per_qp": acc["it"] / max(acc["qps"], 1),
+        "not_optimal_total": int(notopt.item()), "plant_failures_total": int(bad.item()),
     }
     if rank == 0 and not args.no_cpu and args.cpu_budget > 0 and world == 1:
         result["cpu_baseline"] = cpu_baseline_admm(n, N, iters, min(args.cpu_budget, 20.0))
@@ -302,8 +367,7 @@ def bench_gadmm(args, world: int, rank: int, local: int, dist) -> None:
     n_qp_launch = len(qp_ms)
     qp_avg = float(np.mean(qp_ms))
     live_qps = S * eng.m  # upper bound: platoons that stopped switching skip their lanes
-    alg_bytes = live_qps * (gadmm_qp_bytes(N) + 8 * (2 + 14 * (N + 1)))
-    achieved = alg_bytes / (qp_avg * 1e-3) / 1e9
+    notional = live_qps * n_qp_launch * (gadmm_qp_bytes(N) + 8 * (2 + 14 * (N + 1)))
     platoons_total = S * (1 if sharded else world)
     value = platoons_total * args.steps / dt
     result = {
@@ -317,11 +381,8 @@ def bench_gadmm(args, world: int, rank: int, local: int, dist) -> None:
                    "admm_iters": iters, "max_rounds": args.max_rounds, "rho": 0.5, "platoons_per_gpu": S,
                    "parallelism": (f"vehicles-sharded x{world} (RCCL halo send/recv per ADMM iteration)" if sharded
                                    else f"seeds-sharded x{world} (replicas, no collective)")},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "k_gadmm_qp_coop" if N > 8
-                     else "k_gadmm_qp", "kernel_avg_ms": qp_avg, "launches_measured": n_qp_launch,
-                     "note": "SURVEY 8(d) dense bytes of the local QP (n_w = 6N+5, m = 14N+4) + its parameter "
-                             "block, for every held vehicle of every platoon, / HIP-event time per QP launch"},
+        "roofline": qp_roofline(qp_avg * n_qp_launch, [("k_gadmm_qp_coop" if N > 8 else "k_gadmm_qp", n_qp_launch)],
+                                notional, f"gadmm_n{n}_N{N}"),
         "admm_rounds_per_step": rounds / args.steps, "qp_launches_per_step": launches / args.steps,
         "all_feasible": ok,
     }
@@ -507,25 +568,20 @@ def bench_cent(args, world: int, rank: int, local: int, dist) -> None:
     st = solver.stats()
     kernel_ms = st.last_ms
     qps = int(nodes.sum())
-    alg_bytes = qps * cent_qp_bytes(n, N) + S * 8 * (2 * n + 2 * (N + 1) + n * (3 * N + 2) + 1)
-    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+    notional = qps * cent_qp_bytes(n, N) + S * 8 * (2 * n + 2 * (N + 1) + n * (3 * N + 2) + 1)
+    n_opt = int((status == 0).sum())
     value = S * world * args.steps / dt
     q = np.percentile(nodes, [50, 90, 99, 100])
     result = {
-        "metric": f"MPC timesteps/sec (whole platoon) at n={n} N={N} cent_mld",
+        "metric": f"MPC timesteps/sec (whole platoon) at n={n} N={N} cent_mld (QP cap {args.max_nodes} per platoon)",
         "value": value, "unit": "platoon-timesteps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic: env.reset random-init platoon states (seeded), constant-velocity leader",
         "config": {"workload": f"fleet_cent_mld n={n} N={N} pwa_gear (MpcMldCent)", "n_vehicles": n, "horizon": N,
                    "platoons_per_gpu": S, "max_nodes": args.max_nodes, "parallelism": f"seeds-sharded x{world}"},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "k_cent_bnb",
-                     "kernel_avg_ms": kernel_ms, "launches_per_step": 1,
-                     "note": "SURVEY 8(d) notional dense bytes of every platoon QP solved (n_w = n(2N+1), "
-                             "m = n(13N+3)) + platoon I/O / the HIP-event time of the search kernel. The wave "
-                             "builds each QP in LDS from the platoon block: the kernel is FP64-latency bound "
-                             "(one wavefront per platoon, sequential active-set steps)"},
+        "value_optimal_only": n_opt * world * args.steps / dt,
+        "roofline": qp_roofline(kernel_ms, [("k_cent_bnb", 1)], notional, f"cent_n{n}_N{N}"),
         "qps_per_step": qps, "qp_iters_per_qp": float(iters.sum()) / max(qps, 1),
         "nodes_per_platoon": {"p50": float(q[0]), "p90": float(q[1]), "p99": float(q[2]), "max": float(q[3])},
         "status_counts": {"optimal": int((status == 0).sum()), "infeasible": int((status == 1).sum()),
@@ -670,31 +726,17 @@ def main() -> None:
     steps_total = S * world * args.steps
     value = steps_total / dt
     bnb = method != 1
-    # QP time per step: K_qp_gi (enumeration) or K_bnb_root + the N K_bnb_bound launches (B&B),
+    # QP time per step: the root kernel + the N bound launches (B&B) or K_qp_gi (enumeration),
     # each bracketed by HIP events the library records on the solve stream
     qp_step_ms = float(np.mean(qp_ms))
-    launches = (N + 1) if bnb else 1
-    qp_avg_ms = qp_step_ms / launches
     cand_per_step = cand / args.steps
-    alg_bytes = cand_per_step * dense_qp_bytes(N) + B * instance_io_bytes(N)
-    achieved = alg_bytes / (qp_step_ms * 1e-3) / 1e9
-    traffic, flop, fp64, prof_src = None, None, None, None
-    if (n, N) == (10, 5):  # the committed PMC summary (profiles/) is of the default workload
-        if bnb:
-            pb, prof_src = profiled("k_bnb_bound")
-            pr, _ = profiled("k_bnb_root")
-            if pb and pr and "hbm_bytes" in pb and "hbm_bytes" in pr:
-                traffic = pb["hbm_bytes"] * N + pr["hbm_bytes"]
-                if pb.get("f64_flop") and pr.get("f64_flop"):
-                    flop = pb["f64_flop"] * N + pr["f64_flop"]
-        else:
-            prof, prof_src = profiled("k_qp_gi")
-            if prof:
-                traffic, flop = prof.get("hbm_bytes"), prof.get("f64_flop")
-    if traffic is not None and flop:
-        tf = flop / (qp_step_ms * 1e-3) / 1e12
-        fp64 = {"achieved": tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tf / FP64_PEAK_TFLOPS,
-                "flop_per_step": flop, "source": prof_src}
+    notional = cand_per_step * dense_qp_bytes(N) + B * instance_io_bytes(N)
+    if bnb:
+        qk = [("k_bnb_root_coop", 1), ("k_bnb_bound_coop", N)] if N > 8 else [("k_bnb_root", 1),
+                                                                              ("k_bnb_bound_refill", N)]
+    else:
+        qk = [("k_qp_gi", 1)]
+    roofline = qp_roofline(qp_step_ms, qk, notional, f"decent_n{n}_N{N}" + ("" if bnb else "_enum"))
 
     result = {
         "metric": f"MPC timesteps/sec (whole platoon) at n={n} N={N} decent_mld",
@@ -714,29 +756,22 @@ def main() -> None:
                                 + (" (configs[1])" if (n, N) == (10, 5) else " (configs[4] sweep point)")),
                    "n_vehicles": n, "horizon": N, "search": "branch-and-bound" if bnb else "enumeration",
                    "platoons_per_gpu": S, "local_miqps_per_step": B * world, "parallelism": f"seeds-sharded x{world}"},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "k_bnb_root+k_bnb_bound" if bnb else "k_qp_gi", "kernel_avg_ms": qp_avg_ms,
-                     "launches_per_step": launches, "qp_ms_per_step": qp_step_ms,
-                     "algorithmic_bytes_per_step": alg_bytes, "traffic_source": prof_src,
-                     "note": "achieved = SURVEY 8(d) notional dense-QP bytes (8(n_w^2+m n_w+m+n_w) per QP solved) "
-                             "+ instance I/O, per step / the HIP-event time of the QP launches of the step "
-                             "(per-launch average = kernel_avg_ms). The kernels never materialise those "
-                             "matrices (QPs are built in registers from the instance block), so frac can "
-                             "exceed 1; traffic = measured HBM bytes of the same launches per step "
-                             "(2*FETCH_SIZE + WRITE_SIZE, profiles/). See DESIGN.md 'Roofline'."},
-        "fp64": fp64,
+        "roofline": roofline,
         "qps_per_step": cand_per_step,
         "qp_iters_per_candidate": iters / max(cand, 1),
         "ipm_fallbacks_per_step": fallback / args.steps,
         "all_optimal": ok,
     }
     if rank == 0 and not args.no_cpu and args.cpu_budget > 0 and world == 1:
-        threads = min(len(os.sched_getaffinity(0)), 16)
+        # every core this job may use: the pool gives each GPU a 16-core share (OMP_NUM_THREADS=16
+        # on the box; nproc shows the whole machine), plus a 1-core run
+        threads = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16")), 16)
         result["cpu_baseline"] = cpu_baseline(n, N, args.cpu_budget, threads)
+        result["cpu_baseline_1core"] = cpu_baseline(n, N, args.cpu_budget * 0.5, 1)
         hr = hostref_baseline(n, N, min(args.cpu_budget, 10.0), threads, method)
         if hr:
             result["cpu_same_algorithm"] = hr
+            result["cpu_same_algorithm_1core"] = hostref_baseline(n, N, min(args.cpu_budget, 10.0) * 0.5, 1, method)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist:

@@ -77,16 +77,18 @@ __global__ __launch_bounds__(64) void k_env_step(int P, int n, const double* __r
     // ---- stage cost of (x, u) (env.py:126-180)
     const double pm = __shfl(pos, i > 0 ? i - 1 : 0, 64), vm = __shfl(vel, i > 0 ? i - 1 : 0, 64);
     const double pn = __shfl(pos, i + 1 < n ? i + 1 : i, 64);
-    auto quad = [&](double ep, double ev) {
-        return C.Qpp * ep * ep + 2.0 * C.Qpv * ep * ev + C.Qvv * ev * ev;
-    };
+    // PlatoonEnv's own weights (env.py:16-18: Q_x = diag(1, 0.1), Q_u = 1, Q_du = 0), not the
+    // controller's: the env prices every controller's actions alike
+    constexpr double kQpp = 1.0, kQvv = 0.1, kQu = 1.0;
+    auto quad = [&](double ep, double ev) { return kQpp * ep * ep + kQvv * ev * ev; };
     double c = 0.0;
     int close = 0;
     if (on) {
         const double rp = leader_x[(size_t)p * 2], rv = leader_x[(size_t)p * 2 + 1];
         if (rvar ? i == 0 : i == leader) c += quad(pos - rp + (rvar ? C.d0 + C.t0 * vel : 0.0), vel - rv);
         if (i >= 1) c += quad(pos - pm + C.d0 + C.t0 * vel, vel - vm);
-        c += C.Qu * ui * ui + C.Qdu * (ui - upi) * (ui - upi);
+        c += kQu * ui * ui;  // + Q_du (u - u_prev)^2 with Q_du = 0
+        (void)upi;
         if (i + 1 < n && pos - pn < C.d_safe) close = 1;
         if (rvar && i == 0 && rp - pos < C.d_safe) close = 1;
     }

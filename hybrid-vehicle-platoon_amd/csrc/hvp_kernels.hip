@@ -213,11 +213,13 @@ void free_ws(Workspace& w) {
     w = Workspace{};
 }
 
-int64_t default_capacity(int N, int B, bool bnb) {
+int64_t default_capacity(int N, int B, bool bnb, int form) {
     if (bnb) {
         // nodes of ONE tree level, pooled over the batch (C2..C5 means: 3 leaves at N = 5, 4 at
-        // N = 10, 30 at N = 15; the widest level a few times that)
-        const int64_t per = N <= 8 ? 64 : (N <= 12 ? 256 : 1024);
+        // N = 10, 30 at N = 15; the widest level a few times that; the naive-ADMM local trees,
+        // with their hinge states, ~8 per level at C3, a heavy tail far beyond -- 4x room)
+        int64_t per = N <= 8 ? 64 : (N <= 12 ? 256 : 1024);
+        if (form == HVP_FORM_ADMM) per *= 4;
         return per * (int64_t)std::max(B, 1);
     }
     // per-instance average budget: 7^N capped (N = 5: mean ~30, max ~85 region sequences)
@@ -315,7 +317,7 @@ int hvp_create(hvp_handle** out, const hvp_problem* problem, const hvp_system* s
 
 int hvp_reserve(hvp_handle* h, int max_batch, int64_t cap) {
     if (!h || max_batch <= 0) return fail(HVP_E_ARG, "hvp_reserve: bad argument");
-    if (cap <= 0) cap = default_capacity(h->prob.N, max_batch, h->bnb);
+    if (cap <= 0) cap = default_capacity(h->prob.N, max_batch, h->bnb, h->prob.formulation);
     if (max_batch <= h->ws.max_batch && cap <= h->ws.cap) return 0;
     HIP_TRY(hipSetDevice(h->device));
     HIP_TRY(hipDeviceSynchronize());
@@ -395,7 +397,7 @@ static int solve_impl(hvp_handle* h, int B, const int32_t* sys, const int32_t* r
         return fail(HVP_E_ARG, "hvp_solve_batch: HVP_FORM_CENT handles are solved by hvp_cent_solve_batch");
     if (B == 0) return 0;
     if (B > h->ws.max_batch) {
-        int rc = hvp_reserve(h, B, default_capacity(h->prob.N, B, h->bnb));
+        int rc = hvp_reserve(h, B, default_capacity(h->prob.N, B, h->bnb, h->prob.formulation));
         if (rc) return rc;
     }
     HIP_TRY(hipSetDevice(h->device));

@@ -467,10 +467,13 @@ __global__ __launch_bounds__(kCoopBlock) void k_bnb_bound_coop(int k, const hvp_
 }
 
 // children of the level-(k-1) nodes that survive the incumbent test
-// Every instance may hold at most `quota` = capacity / B nodes per level: an instance whose
-// tree outgrows its share (the heavy tail at long horizons, e.g. trajectories riding a region
-// boundary) is cut off deterministically and reported HVP_OVERFLOW, so it can never crowd the
-// other instances out of the pooled list.  The host path re-solves it alone (quota = capacity).
+// Every instance may hold at most `quota` nodes per level; an instance whose children do not fit
+// (its quota, or the pooled capacity) is reported HVP_OVERFLOW, never truncated silently, and
+// is re-solved alone by the caller (solve_device(retry_overflow)).  The launcher passes the
+// whole capacity as the quota: the pooled list is sized at 64-1024 x the batch per level while
+// the widest level of the batch averages a few nodes per instance, so a heavy tree (trajectories
+// riding a region boundary, naive-ADMM hinge states) simply uses the room the light ones leave
+// -- a per-instance share of capacity / B made 68 of 80 naive-ADMM solves at C3 re-run.
 template <int N>
 __global__ __launch_bounds__(kBlock) void k_bnb_expand(int k, int quota, const hvp_system* __restrict__ systems,
                                                        const int32_t* __restrict__ sys, hvp::Consts C, Workspace ws) {
@@ -1259,7 +1262,7 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
     HIP_TRY(hipEventRecord(h->evb[1], st));
     const int g_small = (int)std::min<long long>(grid_for(h->ws.cap), (long long)h->n_cu * 8);
     const int g_qp = (int)std::min<long long>((h->ws.cap + BS - 1) / BS, (long long)h->n_cu * 8 * (kBlock / BS));
-    const int quota = (int)std::min<int64_t>(h->ws.cap / B, 1 << 30);
+    const int quota = (int)std::min<int64_t>(h->ws.cap, 1 << 30);
     for (int k = 1; k <= N; ++k) {
         HIP_TRY(hipMemsetAsync(ws.inst_lvl, 0, sizeof(int32_t) * B, st));
         hipLaunchKernelGGL(k_bnb_expand<N>, dim3(g_small), dim3(kBlock), 0, st, k, quota, h->d_sys, sys, h->C, ws);

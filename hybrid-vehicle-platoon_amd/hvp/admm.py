@@ -168,10 +168,19 @@ class AdmmEngine:
         rows = torch.arange(self.P, device=self.dev) * self.n + self.leader_index
         self.params[rows, 2 + 4 * self.E:] = lx
 
+    def set_leader_device(self, leader_x) -> None:
+        """set_leader from a (P, 2, N+1) CUDA tensor (no host round trip)."""
+        import torch
+
+        rows = torch.arange(self.P, device=self.dev) * self.n + self.leader_index
+        self.params[rows, 2 + 4 * self.E:] = leader_x.reshape(self.P, self.E)
+
     def step(self, states, admm_iters: int, stream=None, on_solve=None) -> dict:
         """One platoon time step (:379-468): warm start, admm_iters x (local solves + update).
         states: (P, 2n) tensor/array of the measured platoon states.  Returns the output dict of
-        the last iteration's local solves (u, x, x_front, x_back, status, ...)."""
+        the last iteration's local solves (u, x, x_front, x_back, status, ...).  A local search
+        that outgrows the workspace (HVP_OVERFLOW, rare) is re-solved alone inside its iteration
+        (one host read of the status per iteration)."""
         import torch
 
         n, E, N = self.n, self.E, self.N

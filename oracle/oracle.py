@@ -834,7 +834,7 @@ def env_step(x, u, masses, leader_state, u_prev=None, gears=None, leader_index: 
     u = np.asarray(u, dtype=float).reshape(-1)
     n = len(u)
     up = u if u_prev is None else np.asarray(u_prev, dtype=float).reshape(-1)
-    Q = np.array(cfg.Qx, dtype=float).reshape(2, 2)
+    Q = np.diag([1.0, 0.1])  # PlatoonEnv.Q_x (env.py:16); Q_u = 1, Q_du = 0 (env.py:17-18)
     sp = lambda xi: np.array([-cfg.d0 - cfg.t0 * xi[1], 0.0])  # noqa: E731  spacing_policy.spacing
     xs = [x[2 * i:2 * i + 2] for i in range(n)]
     ref = np.asarray(leader_state, dtype=float).reshape(2)
@@ -843,7 +843,7 @@ def env_step(x, u, masses, leader_state, u_prev=None, gears=None, leader_index: 
     for i in range(1, n):
         e = xs[i] - xs[i - 1] - sp(xs[i])
         cost += float(e @ Q @ e)
-    cost += sum(cfg.Qu * u[i] ** 2 for i in range(n)) + sum(cfg.Qdu * (u[i] - up[i]) ** 2 for i in range(n))
+    cost += sum(1.0 * u[i] ** 2 for i in range(n)) + sum(0.0 * (u[i] - up[i]) ** 2 for i in range(n))
     close = any(xs[i][0] - xs[i + 1][0] < cfg.d_safe for i in range(n - 1))
     if real_vehicle_as_reference and ref[0] - xs[0][0] < cfg.d_safe:
         close = True

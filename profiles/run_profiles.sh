@@ -7,7 +7,8 @@
 #      f64           : FP64 instruction mix + VALU / SALU / LDS instruction counts
 #      occ           : occupancy and issue utilisation (waves, wave / busy cycles, VALU active and
 #                      thread cycles = lane utilisation, issue and wait stalls) + GRBM_GUI_ACTIVE
-# profiles/summarize.py OUT <round> condenses the passes into profiles/<round>_summary.json.
+# profiles/summarize.py OUT <round> <tag> condenses the passes into profiles/<round>_<tag>_summary.json
+# (profiles/profile_all.sh runs the four bench workloads bench.py looks up by tag).
 set -euo pipefail
 export TMPDIR=/tmp
 OUT=${1:-gpurun_out/prof}

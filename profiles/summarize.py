@@ -1,10 +1,11 @@
 #!/usr/bin/env python3
 """Condense a profiles/run_profiles.sh output directory into a committed per-round summary.
 
-    python profiles/summarize.py gpurun_out/prof r01
+    python profiles/summarize.py gpurun_out/prof r01 [tag]
 
-writes profiles/<round>_kernel_stats.csv (rocprofv3 --kernel-trace --stats, as produced) and
-profiles/<round>_summary.json with, per kernel:
+writes profiles/<round>[_<tag>]_kernel_stats.csv (rocprofv3 --kernel-trace --stats, as produced) and
+profiles/<round>[_<tag>]_summary.json with, per kernel (tag: the bench workload, e.g. decent_n10_N5,
+which bench.py looks up for its roofline):
   avg_ms                 average duration from the kernel-trace pass
   fetch_kb, write_kb     FETCH_SIZE / WRITE_SIZE per launch (separate PMC passes)
   hbm_bytes              2 * FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md, HBM section: on gfx950
@@ -38,7 +39,8 @@ def per_kernel(path: str) -> dict:
 
 
 def short(name: str) -> str:
-    for k in ("k_qp_gi", "k_qp_ipm", "k_enum", "k_cost", "k_select", "k_bnb_root", "k_bnb_expand", "k_bnb_bound",
+    for k in ("k_qp_gi", "k_qp_ipm", "k_enum", "k_cost", "k_select", "k_inst_prep", "k_bnb_root_coop", "k_bnb_root",
+              "k_bnb_expand", "k_bnb_bound_refill", "k_bnb_bound_coop", "k_bnb_bound",
               "k_bnb_key", "k_bnb_write", "k_bnb_finish", "k_gadmm_qp_coop", "k_gadmm_qp", "k_gadmm_update",
               "k_gadmm_rollout", "k_gadmm_switch", "k_admm_update"):
         if k in name:
@@ -48,6 +50,9 @@ def short(name: str) -> str:
 
 def main() -> None:
     src, rnd = sys.argv[1], sys.argv[2]
+    tag = sys.argv[3] if len(sys.argv) > 3 else None
+    if tag:
+        rnd = f"{rnd}_{tag}"
     here = os.path.dirname(os.path.abspath(__file__))
     out = {}
     with open(os.path.join(src, "trace", "run_kernel_stats.csv")) as f:
@@ -100,7 +105,7 @@ def main() -> None:
                     d[key] = d[c] / wc
             if d.get("GRBM_GUI_ACTIVE"):
                 d["waves_per_cu"] = 4.0 * wc / (d["GRBM_GUI_ACTIVE"] / 8.0) / 256.0
-    meta = {"round": rnd, "source": "profiles/run_profiles.sh (rocprofv3 kernel trace + separate PMC passes)",
+    meta = {"round": rnd, "tag": tag, "source": "profiles/run_profiles.sh (rocprofv3 kernel trace + separate PMC passes)",
             "workload": open(os.path.join(src, "cmd.txt")).read().strip() if os.path.exists(os.path.join(src, "cmd.txt")) else None,
             "kernels": out, "workloads": extra}
     with open(os.path.join(here, f"{rnd}_summary.json"), "w") as f:
