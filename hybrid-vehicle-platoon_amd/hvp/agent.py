@@ -65,7 +65,7 @@ class MldAgent:
             while not done:
                 action, _ = self.get_control(state)
                 state, r, term, trunc, _ = env.step(action)
-                returns[ep] += r
+                returns[ep] += float(np.asarray(r).sum())
                 done = term or trunc
                 t += 1
                 self.on_timestep_end(env, ep, t)

@@ -117,12 +117,15 @@ class PlatoonEnv:
         self.viol_counter.append(np.zeros(self.ep_len))
         return self.x, {}
 
-    def _cost(self, e: np.ndarray, Q: np.ndarray) -> float:
+    def _cost(self, e: np.ndarray, Q: np.ndarray):
+        """quad_cost / lin_cost (env.py:118-124): x'Qx is a (1, 1) array as in the reference, so
+        the stage cost -- and the rewards the results files store -- keep its shape
+        (results_analysis/perf_n.py reads sum(R)[0, 0])."""
         if self.quadratic_cost:
-            return (e.T @ Q @ e).item()
-        return float(np.linalg.norm(Q @ e, ord=1))
+            return e.T @ Q @ e
+        return np.linalg.norm(Q @ e, ord=1)
 
-    def get_stage_cost(self, state: np.ndarray, action: np.ndarray) -> float:
+    def get_stage_cost(self, state: np.ndarray, action: np.ndarray):
         if self.previous_action is None:
             self.previous_action = action
         xs = np.split(np.asarray(state, dtype=float), self.n, axis=0)

@@ -11,7 +11,8 @@ the reference the checker needs as inputs:
 * ``friction_pwa_system(m, ts)`` <- models.py:272-332
 * ``env_initial_state(n, seed)`` <- env.py:79-101 with the mpcrl seed derivation
                                   (SeedSequence(seed).generate_state(1)[0], model_validation.py:76)
-* ``constant_velocity_prediction`` <- fleet_decent_mld.py:421-428
+* ``constant_velocity_prediction`` <- fleet_decent_mld.py:421-428, ``two_point_prediction`` <-
+  :430-455 (two-point and saturated estimators), ``observe_states`` <- :348-419
 
 Parity status: pinned to the reference's constants through the known answers listed in
 SURVEY.md 8(c) (discretised tables, seed derivation, env init at seed 0) and, for the MIQP
@@ -158,12 +159,57 @@ def env_initial_state(n: int, seed: int) -> np.ndarray:
 
 
 def constant_velocity_prediction(p: float, v: float, N: int, ts: float = 1.0) -> np.ndarray:
+    """extrapolate_position_constant_vel (fleet_decent_mld.py:421-428)."""
     out = np.zeros((2, N + 1))
     out[:, 0] = (p, v)
     for k in range(N):
         out[0, k + 1] = out[0, k] + ts * out[1, k]
         out[1, k + 1] = out[1, k]
     return out
+
+
+def two_point_prediction(p: float, v: float, v_prev: float, N: int, ts: float = 1.0,
+                         saturated: bool = False) -> np.ndarray:
+    """extrapolate_position_two_point_estimator (fleet_decent_mld.py:430-440): the velocity keeps
+    changing by dv = v - v_prev every step; saturated (:442-455): only for the first floor(N/2)
+    steps, constant after."""
+    out = np.zeros((2, N + 1))
+    out[:, 0] = (p, v)
+    dv = v - v_prev
+    steps = int(np.floor(N / 2)) if saturated else N
+    for k in range(N):
+        out[0, k + 1] = out[0, k] + ts * out[1, k]
+        out[1, k + 1] = out[1, k] + (dv if k < steps else 0.0)
+    return out
+
+
+def observe_states(x, x_prev, N: int, leader_window, leader_index: int = 0, real_vehicle_as_reference: bool = False,
+                   velocity_estimator: str = "none", ts: float = 1.0):
+    """TrackingDecentMldCoordinator.observe_states (fleet_decent_mld.py:348-419) + the leader
+    window of on_episode_start / on_timestep_end (:329-346) for ONE platoon, as the local-MPC
+    parameter blocks [x0 | x_front | x_back | leader_x] and roles.  The first vehicle has no
+    front prediction, the last no back prediction (zeros: those roles carry no such rows); the
+    estimator is 'none' (constant velocity), 'two_point' or 'sat' (from x_prev's velocities)."""
+    x = np.asarray(x, dtype=float).reshape(-1)
+    n = len(x) // 2
+    xp = x if x_prev is None else np.asarray(x_prev, dtype=float).reshape(-1)
+
+    def pred(j):
+        if velocity_estimator == "two_point":
+            return two_point_prediction(x[2 * j], x[2 * j + 1], xp[2 * j + 1], N, ts)
+        if velocity_estimator == "sat":
+            return two_point_prediction(x[2 * j], x[2 * j + 1], xp[2 * j + 1], N, ts, saturated=True)
+        return constant_velocity_prediction(x[2 * j], x[2 * j + 1], N, ts)
+
+    params, roles = [], []
+    zero = np.zeros((2, N + 1))
+    for i in range(n):
+        xf = pred(i - 1) if i > 0 else zero
+        xb = pred(i + 1) if i < n - 1 else zero
+        xl = np.asarray(leader_window, dtype=float).reshape(2, N + 1) if i == leader_index else zero
+        params.append(np.concatenate([x[2 * i:2 * i + 2], xf.ravel(), xb.ravel(), xl.ravel()]))
+        roles.append(role_bits(i, n, leader_index, real_vehicle_as_reference))
+    return np.array(params), np.array(roles, dtype=np.int32)
 
 
 # ------------------------------------------------------------------ controller constants

@@ -41,9 +41,20 @@ def test_oracle_step_matches_host_env():
         prev = u
 
 
+class _OtherWeights:
+    """Controller weights that differ from PlatoonEnv's (env.py:16-18): the env must keep its own."""
+
+    from hvp.params import Params as _P
+
+    Q_x = np.diag([2.0, 0.5])
+    Q_u = 3 * np.eye(1)
+    Q_du = 0.7 * np.eye(1)
+    w, a_acc, a_dec, ts, d_safe = _P.w, _P.a_acc, _P.a_dec, _P.ts, _P.d_safe
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("rvar", [False, True])
-def test_device_step_matches_oracle(gpu_available, rvar):
+@pytest.mark.parametrize("rvar,weights", [(False, False), (True, False), (False, True)])
+def test_device_step_matches_oracle(gpu_available, rvar, weights):
     import torch
 
     from hvp import tables
@@ -54,7 +65,8 @@ def test_device_step_matches_oracle(gpu_available, rvar):
     P, n = 64, 10
     X, U, Up, M, L = _platoons(P, n)
     veh = PwaGearVehicle(800)
-    s = BatchSolver(tables.problem(5), [tables.system_from_dict(veh.get_discrete_system(1), tables.gears_of(veh))])
+    prob = tables.problem(5, params=_OtherWeights) if weights else tables.problem(5)
+    s = BatchSolver(prob, [tables.system_from_dict(veh.get_discrete_system(1), tables.gears_of(veh))])
     dev = torch.device("cuda", 0)
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
     env = DeviceEnv(s, t(M), real_vehicle_as_reference=rvar)
@@ -71,6 +83,28 @@ def test_device_step_matches_oracle(gpu_available, rvar):
         assert abs(float(out["cost"][p]) - c) <= 1e-12 * max(1.0, abs(c)), p
         if ok:
             assert np.allclose(xd[p], xo, rtol=1e-9, atol=1e-9), (p, np.abs(xd[p] - xo).max())
+
+
+@pytest.mark.parametrize("estimator", ["none", "two_point", "sat"])
+@pytest.mark.parametrize("N", [5, 6, 10])
+def test_host_params_match_oracle_observe_states(estimator, N):
+    """The product's batched observe_states (hvp.batched) against the oracle's per-vehicle
+    restatement of fleet_decent_mld.py:348-455, the three velocity estimators."""
+    from hvp.batched import decent_params_from_states
+
+    P, n = 8, 6
+    X, _, _, _, _ = _platoons(P, n)
+    Xp = X + np.random.default_rng(5).uniform(-2, 2, X.shape)
+    lead = np.stack([np.stack([3000.0 + 20.0 * (np.arange(N + 1) + p), np.full(N + 1, 20.0)]) for p in range(P)])
+    for li, rvar in ((0, False), (0, True), (2, False)):
+        hp, hr = decent_params_from_states(X, N, lead, leader_index=li, prev_states=Xp, velocity_estimator=estimator,
+                                           real_vehicle_as_reference=rvar)
+        hp, hr = hp.reshape(P, n, -1), hr.reshape(P, n)
+        for p in range(P):
+            op, orl = O.observe_states(X[p], Xp[p], N, lead[p], leader_index=li, real_vehicle_as_reference=rvar,
+                                       velocity_estimator=estimator)
+            assert np.array_equal(hr[p], orl)
+            np.testing.assert_allclose(hp[p], op, rtol=1e-15, atol=1e-12)
 
 
 @pytest.mark.gpu
@@ -94,6 +128,12 @@ def test_device_params_match_host(gpu_available, estimator):
     hp, hr = decent_params_from_states(X, N, lead, leader_index=2, prev_states=Xp, velocity_estimator=estimator)
     assert np.array_equal(roles.cpu().numpy(), hr)
     assert np.array_equal(params.cpu().numpy(), hp)
+    # and against the oracle's restatement of observe_states (fleet_decent_mld.py:348-455)
+    dp, dr = params.cpu().numpy().reshape(P, n, -1), roles.cpu().numpy().reshape(P, n)
+    for p in range(P):
+        op, orl = O.observe_states(X[p], Xp[p], N, lead[p], leader_index=2, velocity_estimator=estimator)
+        assert np.array_equal(dr[p], orl)
+        np.testing.assert_allclose(dp[p], op, rtol=1e-15, atol=1e-12)
 
 
 @pytest.mark.gpu
