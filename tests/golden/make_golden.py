@@ -39,7 +39,7 @@ Files (numpy .npz, no pickles):
                       n = 3 at N = 10, n = 10 at N = 3, variants (real_vehicle_as_reference, leader
                       index, task_2 masses / ConstantTime / stop-and-go, Q_du), mid-rollout states,
                       the gear model (MpcGearCent, model = 1)
-Run:  python tests/golden/make_golden.py [sweep | gear | admm | gadmm | cent [n10]]
+Run:  python tests/golden/make_golden.py [sweep | gear | admm | gadmm | cent [n10] | configs admm|gadmm]
 """
 
 from __future__ import annotations
@@ -244,6 +244,56 @@ def admm_fixtures():
     print("admm_steps_n4_N5.npz written")
 
 
+def config_size_fixtures(which: str):
+    """configs[2] and configs[3] at their own sizes: the oracle coordinators on
+    t = 0 platoon states for two consecutive time steps (the state advances along the solution's
+    x_1; the coordinator state -- naive ADMM's y, switching ADMM's previous solution -- carries
+    over, fleet_naive_admm.py:357-359, fleet_g_admm.py:265-272).
+      admm:  fleet_naive_admm n = 10, N = 10, 20 ADMM iterations, one seed  -> admm_steps_n10_N10.npz
+      gadmm: fleet_g_admm n = 20, N = 10, 100 ADMM iterations, two seeds  -> gadmm_steps_n20_N10.npz"""
+    if which == "admm":
+        n, N, iters = 10, 10, 20
+        sysd = O.gear_pwa_system(800.0)
+        coord = O.AdmmCoordinator(sysd, O.Cfg(), N, n)
+        st = O.env_initial_state(n, 0).astype(float)
+        states, us, xs = [], [], []
+        for t in range(2):
+            coord.set_leader_x(leader_window(N, t))
+            u, hist = coord.step(st, iters)
+            states.append(st.copy()); us.append(np.array([[r.u for r in res] for res in hist]))
+            xs.append(np.array([[r.x for r in res] for res in hist]))
+            st = np.concatenate([r.x[:, 1] for r in hist[-1]])
+            print(f"admm step {t} done", flush=True)
+        np.savez_compressed(os.path.join(HERE, f"admm_steps_n{n}_N{N}.npz"), N=N, n=n, iters=iters, rho=0.5,
+                            states=np.array(states), exp_u=np.array(us), exp_x=np.array(xs))
+        print(f"admm_steps_n{n}_N{N}.npz written")
+        return
+    n, N, iters = 20, 10, 100
+    systems = [O.gear_pwa_system(800.0) for _ in range(n)]
+    co = O.GAdmmCoordinator(systems, O.Cfg(), N, admm_iters=iters)
+    states, exp_u, exp_cost, exp_ws, exp_rounds, exp_seq, exp_runcost = [], [], [], [], [], [], []
+    for seed in range(2):
+        co.prev_u = None
+        st = O.env_initial_state(n, seed).astype(float)
+        for t in range(2):
+            co.set_leader_traj(leader_window(N, t))
+            u, c, runs = co.control(st)
+            ws = next(k for k, r in enumerate(runs) if r is not None and r[1] == c)
+            states.append(st.copy()); exp_u.append(u); exp_cost.append(c); exp_ws.append(ws + 1)
+            exp_rounds.append([r[2]["rounds"] if r else -1 for r in runs] + [-1] * (2 - len(runs)))
+            exp_seq.append([r[2]["sigma"] if r else np.full((n, N), -1) for r in runs] +
+                           [np.full((n, N), -1)] * (2 - len(runs)))
+            exp_runcost.append([r[1] if r else np.inf for r in runs] + [np.nan] * (2 - len(runs)))
+            st = np.concatenate([runs[ws][2]["x"][i][:, 1] for i in range(n)])
+            print(f"gadmm seed {seed} step {t} done", flush=True)
+    name = f"gadmm_steps_n{n}_N{N}.npz"
+    np.savez_compressed(os.path.join(HERE, name), N=N, n=n, iters=iters, rho=0.5, max_rounds=co.max_rounds,
+                        steps=2, states=np.array(states), exp_u=np.array(exp_u), exp_cost=np.array(exp_cost),
+                        exp_warm_start=np.array(exp_ws, np.int32), exp_rounds=np.array(exp_rounds, np.int32),
+                        exp_seq=np.array(exp_seq, np.int32), exp_run_cost=np.array(exp_runcost))
+    print(f"{name}: {len(states)} coordinator calls")
+
+
 def gadmm_fixtures():
     """Switching ADMM (fleet_g_admm.py, configs[3]): the oracle's restated coordinator
     (oracle.py GAdmmCoordinator) on t = 0 platoon states; every local QP it solves is traced and
@@ -370,6 +420,9 @@ def cent_fixtures(big: bool = False):
 def main():
     if len(sys.argv) > 1 and sys.argv[1] == "cent":
         cent_fixtures(big=len(sys.argv) > 2 and sys.argv[2] == "n10")
+        return
+    if len(sys.argv) > 2 and sys.argv[1] == "configs":
+        config_size_fixtures(sys.argv[2])
         return
     if len(sys.argv) > 1 and sys.argv[1] == "gadmm":
         gadmm_fixtures()

@@ -49,6 +49,44 @@ def test_oracle_bnb_equals_exhaustive(n, N, seed):
     assert a.n_qps <= b.n_qps
 
 
+@pytest.mark.parametrize("n,N,seed", [(2, 3, 0), (2, 4, 1), (3, 3, 2)])
+def test_oracle_bnb_equals_exhaustive_gear_friction(n, N, seed):
+    """The gear-friction model (MpcGearCent: b differs per gear inside a friction region, so the
+    virtual-region relaxation is active): branch and bound = exhaustive joint enumeration."""
+    systems = [O.gear_friction_mld_system(800.0)] * n
+    x0 = O.env_initial_state(n, seed).astype(float)
+    a = O.solve_cent(systems, O.Cfg(), N, x0, leader_window(N))
+    b = O.solve_cent(systems, O.Cfg(), N, x0, leader_window(N), exhaustive=True)
+    assert a.status == b.status == 0
+    assert np.array_equal(a.sigma, b.sigma)
+    assert abs(a.cost - b.cost) <= 1e-9 * abs(b.cost)
+    assert a.n_qps <= b.n_qps
+
+
+@pytest.mark.parametrize("name", ["cent_gear_n3_N4.npz", "cent_qdu_n4_N5.npz"])
+def test_tail_relaxation_changes_only_the_search(name):
+    """The tail relaxation (reachable intervals + virtual regions) against the
+    plain relaxation (undecided steps without dynamics or input terms) on the gear-friction and
+    Q_du fixtures: the same regions and cost, and never more QPs."""
+    fx = load(name)
+    N = int(fx["N"])
+    cfg = _cfg(fx["cfg"])
+    for p in range(len(fx["x0"])):
+        args = (_oracle_systems(fx, p), cfg, N, fx["x0"][p].reshape(-1), fx["leader_x"][p], int(fx["leader_index"][p]),
+                bool(fx["lsp"][p]))
+        on = O.solve_cent(*args)
+        O.set_cent_relax(False)
+        try:
+            off = O.solve_cent(*args)
+        finally:
+            O.set_cent_relax(True)
+        assert on.status == off.status
+        if on.status == 0:
+            assert np.array_equal(on.sigma, off.sigma), p
+            assert abs(on.cost - off.cost) <= 1e-9 * max(1.0, abs(off.cost)), p
+            assert on.n_qps <= off.n_qps, (p, on.n_qps, off.n_qps)
+
+
 @pytest.mark.parametrize("name", FAST)
 def test_oracle_reproduces_cent_golden(name):
     fx = load(name)
