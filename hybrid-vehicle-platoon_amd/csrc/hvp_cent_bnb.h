@@ -5,8 +5,13 @@
 // Decision d = k n + i fixes sigma_{i,k} (time-major, the order of oracle/hvp_oracle.c
 // cent_dfs).  A node's children are the regions reachable from the exact velocity interval of
 // v_{i,k} (bnb_child); each child's bound is the platoon QP with the assigned prefix fixed and
-// every later step relaxed (a valid lower bound: the feasible set grows, nonnegative input-cost
-// terms are dropped).  Children are visited in increasing (bound, region) order and pruned when
+// every later step relaxed (hvp_ipm.h relax_step): an undecided step keeps the
+// interval of its next velocity reachable over every region it may still take and, where those
+// regions share the velocity dynamics (a, c), a virtual region (a, b_max, c) whose input rows
+// and input cost are kept on s = u b_r / b_max.  A valid lower bound of every completion: b_r <=
+// b_max and umin <= 0 <= umax make s feasible with Q_u s^2 <= Q_u u^2, the reachable intervals
+// contain every completion's velocities, and Q_du terms of undecided steps (>= 0) are dropped.
+// Children are visited in increasing (bound, region) order and pruned when
 // bound > incumbent + kPruneRel (1 + |incumbent|); leaves (all n N steps fixed) are exact QPs.
 // The answer is the lexicographically first (time-major) joint sequence within 1e-9 relative of
 // the minimum -- the oracle's rule -- and the exploration order, hence the QP count, is the
