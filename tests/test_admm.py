@@ -115,16 +115,18 @@ def test_admm_local_problem_on_gpu(gpu_available, N):
 
 
 @pytest.mark.gpu
-def test_admm_coordinator_steps_match_oracle(gpu_available):
-    """Three closed-loop time steps x 4 ADMM iterations of a 4-vehicle platoon: the device
-    coordinator (batched local solves + hvp_admm_update) reproduces the oracle coordinator's
-    controls at every iteration's end and the local trajectories of the last iteration."""
+@pytest.mark.parametrize("name", ["admm_steps_n4_N5.npz", "admm_steps_n10_N10.npz"])
+def test_admm_coordinator_steps_match_oracle(gpu_available, name):
+    """Closed-loop time steps of the naive-ADMM coordinator: the device coordinator (batched
+    local solves + hvp_admm_update, y carried across steps) reproduces the oracle coordinator's
+    controls and the local trajectories of the last iteration -- 3 steps x 4 iterations at
+    n = 4, N = 5, and configs[2] at its own size (n = 10, N = 10, 20 iterations, 2 steps)."""
     import torch
 
     from hvp.admm import AdmmEngine, admm_problem
     from instances import leader_window
 
-    fx = load("admm_steps_n4_N5.npz")
+    fx = load(name)
     n, N, iters = int(fx["n"]), int(fx["N"]), int(fx["iters"])
     roles = [O.role_bits(i, n) for i in range(n)]
     eng = AdmmEngine(admm_problem(N, float(fx["rho"])), [_system()], np.zeros(n, np.int32), roles, n, 1)

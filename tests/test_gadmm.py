@@ -256,7 +256,7 @@ def _run_steps(fx, engines):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["gadmm_steps_n4_N5.npz", "gadmm_steps_n3_N10.npz"])
+@pytest.mark.parametrize("name", ["gadmm_steps_n4_N5.npz", "gadmm_steps_n3_N10.npz", "gadmm_steps_n20_N10.npz"])
 def test_gadmm_engine_matches_oracle_coordinator(gpu_available, name):
     fx = load(name)
     P = len(fx["states"]) // int(fx["steps"])
@@ -314,13 +314,16 @@ class LocalHalo:
 
 
 @pytest.mark.gpu
-def test_gadmm_vehicle_sharded_engine_matches(gpu_available):
+@pytest.mark.parametrize("name,world", [("gadmm_steps_n4_N5.npz", 2), ("gadmm_steps_n20_N10.npz", 8)])
+def test_gadmm_vehicle_sharded_engine_matches(gpu_available, name, world):
+    """The vehicle-sharded engine (halo exchange per ADMM iteration) against the oracle
+    coordinator: 2 shards at n = 4, and configs[3]'s layout -- n = 20 over 8 shards (blocks of
+    2-3 vehicles) -- as lockstep threads on one GPU."""
     from hvp.gadmm import GAdmmEngine, gadmm_problem, shard_range
 
-    fx = load("gadmm_steps_n4_N5.npz")
+    fx = load(name)
     n, N = int(fx["n"]), int(fx["N"])
     P = len(fx["states"]) // int(fx["steps"])
-    world = 2
     bar = threading.Barrier(world)
     group: list = []
     for r in range(world):
