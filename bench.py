@@ -639,7 +639,7 @@ def main() -> None:
     ap.add_argument("--controller", choices=["decent", "admm", "gadmm", "cent"], default="decent",
                     help="decent: fleet_decent_mld (configs[1]); admm: fleet_naive_admm (configs[2]); "
                          "gadmm: fleet_g_admm (configs[3]); cent: fleet_cent_mld (MpcMldCent)")
-    ap.add_argument("--max-nodes", type=int, default=200000, help="cent: QPs per platoon cap")
+    ap.add_argument("--max-nodes", type=int, default=2000000, help="cent: QPs per platoon cap")
     ap.add_argument("--closed-loop", action="store_true",
                     help="decent: every step = neighbour predictions + local MIQPs + plant step, all on the device")
     ap.add_argument("--admm-iters", type=int, default=None, help="default 20 (admm) / 100 (gadmm)")

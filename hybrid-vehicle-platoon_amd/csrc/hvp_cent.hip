@@ -22,29 +22,33 @@ using hvp_detail::fail;
 // (hvp_cent_bnb.h) runs inside the wave, J / R of its QPs in dynamic LDS (2 V (V+1) doubles,
 // 41 KB at n = 10, N = 5: three platoons per CU).  Then the wave writes the winner: lane
 // t = i N + a stores u_{i,a}, x_{i,a+1}, region and gear.
-__global__ __launch_bounds__(64) void k_cent_bnb(int P, int n, int N, int leader, int lsp,
-                                                 const hvp_system* __restrict__ systems,
-                                                 const int32_t* __restrict__ sys, const double* __restrict__ x0,
-                                                 const double* __restrict__ xl, const hvp::Consts* __restrict__ Cp, int nreg_max,
-                                                 int max_nodes, int exhaustive, int max_iter, int debug,
-                                                 hvp::cent::Child* frames, uint64_t* ties, double* __restrict__ u_out,
-                                                 double* __restrict__ x_out, int8_t* __restrict__ region_out,
-                                                 int8_t* __restrict__ gear_out, double* __restrict__ cost_out,
-                                                 int32_t* __restrict__ status_out, int32_t* __restrict__ nodes_out,
-                                                 int32_t* __restrict__ iters_out,
-                                                 unsigned long long* __restrict__ counter) {
-    using namespace hvp::cent;
-    extern __shared__ double cent_lds[];
-    const hvp::Consts& C = *Cp;  // in global memory: lane-indexed rows (C.dec[a]) stay loads
-    const int p = blockIdx.x;
-    if (p >= P) return;
-    const int t = lane();
-    const int V = n * N;
-    const Lds S = lds_carve(cent_lds, V);
-    Inst I;
+//
+// Heavy platoons (a search past kSplitBudget QPs) split: their open DFS frames become subtree
+// tasks that rounds of k_cent_tasks spread over every wave of the chip (the platoon's incumbent
+// shared through its PlatoonRec), and k_cent_final picks and writes their winners.  A batch's
+// time was set by its few heaviest platoons (one wave each, ~1 ms per QP, up to 1e5 QPs).
+constexpr int kSplitBudget = 1000;  // QPs of a platoon's own search before it splits (p90: ~500)
+constexpr int kTaskBudget = 256;    // QPs of a subtree task before it splits again
+constexpr int kTaskRounds = 4096;   // bound on the rounds of k_cent_tasks (one host read each)
+
+struct Epilogue {
+    double* u_out;
+    double* x_out;
+    int8_t* region_out;
+    int8_t* gear_out;
+    double* cost_out;
+    int32_t* status_out;
+    int32_t* nodes_out;
+    int32_t* iters_out;
+    unsigned long long* counter;
+};
+
+__device__ inline hvp::cent::Inst cent_inst(int p, int n, int N, int leader, int lsp, const hvp_system* systems,
+                                            const int32_t* sys, const double* x0, const double* xl, int debug) {
+    hvp::cent::Inst I;
     I.n = n;
     I.N = N;
-    I.V = V;
+    I.V = n * N;
     I.L = leader;
     I.lsp = lsp != 0;
     I.systems = systems;
@@ -52,11 +56,15 @@ __global__ __launch_bounds__(64) void k_cent_bnb(int P, int n, int N, int leader
     I.x0 = x0 + (size_t)p * 2 * n;
     I.xl = xl + (size_t)p * 2 * (N + 1);
     I.debug = debug;
-    Lane L;
-    Search st;
-    Result res;
-    bnb_platoon(L, S, C, I, st, frames + (size_t)p * V * nreg_max, nreg_max, ties + (size_t)p * kTie * n, max_nodes,
-                exhaustive != 0, max_iter, res);
+    return I;
+}
+
+// the winner's outputs (lanes' L.y and st.vcode hold it when res.status is HVP_OPTIMAL)
+__device__ inline void cent_write(int p, hvp::cent::Lane& L, const hvp::Consts& C, const hvp::cent::Inst& I,
+                                  const hvp::cent::Search& st, const hvp::cent::Result& res, const Epilogue& E) {
+    using namespace hvp::cent;
+    const int t = lane();
+    const int n = I.n, N = I.N, V = I.V;
     const bool win = res.status == HVP_OPTIMAL;
     const int i = t < V ? t / N : 0, a = t < V ? t % N : 0;
     const uint64_t ci = bc(st.vcode, i);
@@ -65,11 +73,11 @@ __global__ __launch_bounds__(64) void k_cent_bnb(int P, int n, int N, int leader
     const double yv = win && t < V ? L.y : 0.0;
     const double cum = vehicle_prefix(yv, N);
     if (t < V) {
-        const hvp_system& Sv = systems[I.vsys[i]];
+        const hvp_system& Sv = I.systems[I.vsys[i]];
         const size_t veh = (size_t)p * n + i;
         const double p0 = I.x0[2 * i], v0 = I.x0[2 * i + 1];
-        if (x_out) {
-            double* xo = x_out + veh * 2 * (N + 1);
+        if (E.x_out) {
+            double* xo = E.x_out + veh * 2 * (N + 1);
             if (a == 0) {
                 xo[0] = p0;
                 xo[N + 1] = v0;
@@ -78,19 +86,193 @@ __global__ __launch_bounds__(64) void k_cent_bnb(int P, int n, int N, int leader
             xo[a + 1] = win ? p0 + Sv.ts * v0 + Sv.ts * cum : p0 + Sv.ts * v0 * (a + 1);
             xo[N + 1 + a + 1] = win ? yv : v0;
         }
-        if (u_out) u_out[veh * N + a] = win ? u : 0.0;
+        if (E.u_out) E.u_out[veh * N + a] = win ? u : 0.0;
         const int r = hvp::code_region(ci, a);
-        if (region_out) region_out[veh * N + a] = (int8_t)(win ? r : -1);
-        if (gear_out) gear_out[veh * N + a] = (int8_t)(win ? Sv.gear[r] : 0);
+        if (E.region_out) E.region_out[veh * N + a] = (int8_t)(win ? r : -1);
+        if (E.gear_out) E.gear_out[veh * N + a] = (int8_t)(win ? Sv.gear[r] : 0);
     }
     if (t == 0) {
-        cost_out[p] = win ? res.cost : 1e300;
-        status_out[p] = res.status;
-        if (nodes_out) nodes_out[p] = res.nodes;
-        if (iters_out) iters_out[p] = res.iters;
-        atomicAdd(&counter[0], (unsigned long long)res.nodes);
-        atomicAdd(&counter[1], (unsigned long long)res.iters);
+        E.cost_out[p] = win ? res.cost : 1e300;
+        E.status_out[p] = res.status;
+        if (E.nodes_out) E.nodes_out[p] = res.nodes;
+        if (E.iters_out) E.iters_out[p] = res.iters;
+        atomicAdd(&E.counter[0], (unsigned long long)res.nodes);
+        atomicAdd(&E.counter[1], (unsigned long long)res.iters);
     }
+}
+
+__global__ __launch_bounds__(64) void k_cent_init(int P, hvp::cent::PlatoonRec* rec) {
+    const int p = blockIdx.x * 64 + threadIdx.x;
+    if (p >= P) return;
+    rec[p].inc_key = ~0ull;
+    rec[p].fail_key = ~0ull;
+    rec[p].nodes = rec[p].iters = 0;
+    rec[p].tie_count = 0;
+    rec[p].flags = 0;
+}
+
+__global__ __launch_bounds__(64) void k_cent_bnb(int P, int n, int N, int leader, int lsp,
+                                                 const hvp_system* __restrict__ systems,
+                                                 const int32_t* __restrict__ sys, const double* __restrict__ x0,
+                                                 const double* __restrict__ xl, const hvp::Consts* __restrict__ Cp, int nreg_max,
+                                                 int max_nodes, int exhaustive, int max_iter, int debug,
+                                                 hvp::cent::Child* frames, uint64_t* ties, hvp::cent::SplitWs ws,
+                                                 Epilogue E) {
+    using namespace hvp::cent;
+    extern __shared__ double cent_lds[];
+    const hvp::Consts& C = *Cp;  // in global memory: lane-indexed rows (C.dec[a]) stay loads
+    const int p = blockIdx.x;
+    if (p >= P) return;
+    const int V = n * N;
+    const Lds S = lds_carve(cent_lds, V);
+    const Inst I = cent_inst(p, n, N, leader, lsp, systems, sys, x0, xl, debug);
+    Lane L;
+    Search st;
+    Result res;
+    SplitArgs sa;
+    const bool split = ws.budget > 0 && !exhaustive;
+    if (split) {
+        sa.mode = 1;
+        sa.budget = ws.budget;
+        sa.p = p;
+        sa.task = nullptr;
+        sa.rec = ws.rec + p;
+        sa.tie_g = ws.tie_g + (size_t)p * kTieG * n;
+        sa.tie_gc = ws.tie_gc + (size_t)p * kTieG;
+        sa.out = ws.out;
+        sa.out_count = ws.out_count;
+        sa.out_cap = ws.out_cap;
+    }
+    bnb_platoon(L, S, C, I, st, frames + (size_t)p * V * nreg_max, nreg_max, ties + (size_t)p * kTie * n, max_nodes,
+                exhaustive != 0, max_iter, res, split ? &sa : nullptr);
+    if (res.status == kSplit) return;  // k_cent_final writes it
+    cent_write(p, L, C, I, st, res, E);
+}
+
+// One round of subtree tasks: persistent waves claim tasks of any split platoon.  Each wave has
+// its own DFS frames and tie slice (frames_w, ties_w at its wave index).
+__global__ __launch_bounds__(64) void k_cent_tasks(int n, int N, int leader, int lsp,
+                                                   const hvp_system* __restrict__ systems,
+                                                   const int32_t* __restrict__ sys, const double* __restrict__ x0,
+                                                   const double* __restrict__ xl, const hvp::Consts* __restrict__ Cp,
+                                                   int nreg_max, int max_nodes, int max_iter, int debug,
+                                                   hvp::cent::Child* frames_w, uint64_t* ties_w, hvp::cent::SplitWs ws) {
+    using namespace hvp::cent;
+    extern __shared__ double cent_lds[];
+    const hvp::Consts& C = *Cp;
+    const int t = lane();
+    const int V = n * N;
+    const Lds S = lds_carve(cent_lds, V);
+    Child* frames = frames_w + (size_t)blockIdx.x * V * nreg_max;
+    uint64_t* ties = ties_w + (size_t)blockIdx.x * kTie * n;
+    for (;;) {
+        uint64_t q = 0;
+        if (t == 0) q = atomicAdd(ws.in_claim, 1ull);
+        q = bcu(q, 0);
+        if (q >= ws.in_count) break;
+        const Task* tk = ws.in + q;
+        const int p = tk->p;
+        PlatoonRec* rec = ws.rec + p;
+        uint64_t done_nodes = 0, ik = 0;
+        if (t == 0) {
+            done_nodes = __atomic_load_n(&rec->nodes, __ATOMIC_RELAXED);
+            ik = __atomic_load_n(&rec->inc_key, __ATOMIC_RELAXED);
+        }
+        done_nodes = bcu(done_nodes, 0);
+        const double incg = kcost(bcu(ik, 0));
+        if (incg < __builtin_inf() && hvp::bnb_pruned(tk->lb, incg)) continue;  // pruned meanwhile
+        if ((long long)done_nodes >= (long long)max_nodes) {  // the platoon's QP cap
+            if (t == 0) atomicOr(&rec->flags, REC_NODE_LIMIT);
+            continue;
+        }
+        const Inst I = cent_inst(p, n, N, leader, lsp, systems, sys, x0, xl, debug);
+        SplitArgs sa;
+        sa.mode = 2;
+        sa.budget = ws.budget;
+        sa.p = p;
+        sa.task = tk;
+        sa.rec = rec;
+        sa.tie_g = ws.tie_g + (size_t)p * kTieG * n;
+        sa.tie_gc = ws.tie_gc + (size_t)p * kTieG;
+        sa.out = ws.out;
+        sa.out_count = ws.out_count;
+        sa.out_cap = ws.out_cap;
+        Lane L;
+        Search st;
+        Result res;
+        const long long c0 = debug ? (long long)wall_clock64() : 0;
+        bnb_platoon(L, S, C, I, st, frames, nreg_max, ties, max_nodes - (int)done_nodes, false, max_iter, res, &sa);
+        const long long dt = debug ? (long long)wall_clock64() - c0 : 0;
+        if (t == 0 && (debug >= 4 || (debug && (dt > 50000000ll || res.iters > 200 * (res.nodes + 1)))))
+            printf("[cent-task] p %d d0 %d lb %.6g inc %.6g nodes %d iters %d ticks %lld\n", p, tk->d0, tk->lb, incg,
+                   res.nodes, res.iters, dt);
+    }
+}
+
+// tasks left when the round bound is reached: their platoons end as HVP_MAXITER (never a
+// possibly wrong answer)
+__global__ __launch_bounds__(64) void k_cent_abandon(const hvp::cent::Task* tasks, unsigned long long count,
+                                                     hvp::cent::PlatoonRec* rec) {
+    const unsigned long long q = (unsigned long long)blockIdx.x * 64 + threadIdx.x;
+    if (q < count) atomicOr(&rec[tasks[q].p].flags, hvp::cent::REC_NODE_LIMIT);
+}
+
+// Winner of every split platoon: the lexicographically first (time-major) merged leaf within
+// 1e-9 relative of the shared incumbent, re-solved for its trajectory (the oracle's rule).
+__global__ __launch_bounds__(64) void k_cent_final(int P, int n, int N, int leader, int lsp,
+                                                   const hvp_system* __restrict__ systems,
+                                                   const int32_t* __restrict__ sys, const double* __restrict__ x0,
+                                                   const double* __restrict__ xl, const hvp::Consts* __restrict__ Cp,
+                                                   int max_iter, int debug, hvp::cent::SplitWs ws, Epilogue E) {
+    using namespace hvp::cent;
+    extern __shared__ double cent_lds[];
+    const hvp::Consts& C = *Cp;
+    const int p = blockIdx.x;
+    if (p >= P) return;
+    const PlatoonRec rec = ws.rec[p];
+    if (!(rec.flags & REC_SPLIT)) return;
+    const int t = lane();
+    const int V = n * N;
+    const Lds S = lds_carve(cent_lds, V);
+    const Inst I = cent_inst(p, n, N, leader, lsp, systems, sys, x0, xl, debug);
+    Lane L;
+    Search st;
+    Result res;
+    res.nodes = (int)rec.nodes;
+    res.iters = (int)rec.iters;
+    res.cost = __builtin_inf();
+    st.vcode = 0;
+    const double inc = kcost(rec.inc_key);
+    const int ntie = rec.tie_count < kTieG ? rec.tie_count : kTieG;
+    const double fail_lb = kcost(rec.fail_key);
+    if (rec.flags & REC_NODE_LIMIT) res.status = HVP_MAXITER;
+    else if (rec.flags & (REC_TIE_OVER | REC_TASK_OVER)) res.status = HVP_OVERFLOW;
+    else if (!(inc < __builtin_inf())) res.status = fail_lb < __builtin_inf() ? HVP_MAXITER : HVP_INFEASIBLE;
+    else res.status = HVP_OPTIMAL;
+    if (res.status == HVP_OPTIMAL) {
+        const double tol = 1e-9 * fmax(1.0, fabs(inc));
+        int win = -1;
+        uint64_t wcode = 0;
+        for (int j = 0; j < ntie; ++j) {
+            const double cj = ws.tie_gc[(size_t)p * kTieG + j];
+            if (!(cj <= inc + tol)) continue;
+            const uint64_t cj_code = t < n ? ws.tie_g[((size_t)p * kTieG + j) * n + t] : 0;
+            if (win < 0 || joint_less(cj_code, wcode, n, N)) {
+                win = j;
+                wcode = cj_code;
+            }
+        }
+        st.vcode = wcode;
+        double c = 0.0;
+        int it = 0;
+        Prof pf;
+        const int q = win < 0 ? QP_FAILED : platoon_qp(L, S, C, I, st.vcode, 0.0, 0.0, V, max_iter, c, it, pf);
+        // a failed leaf whose bound is not above the incumbent could hide the optimum
+        res.status = (fail_lb < __builtin_inf() && !hvp::bnb_pruned(fail_lb, inc)) ? HVP_MAXITER : HVP_OPTIMAL;
+        if (q != QP_OK) res.status = HVP_MAXITER;
+        res.cost = c;
+    }
+    cent_write(p, L, C, I, st, res, E);
 }
 
 
@@ -145,19 +327,104 @@ int hvp_cent_solve_batch(hvp_handle* h, int P, int n, int leader_index, int real
     }
     const size_t lds = hvp::cent::lds_doubles(V) * sizeof(double);
     HIP_TRY(hipFuncSetAttribute((const void*)k_cent_bnb, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    HIP_TRY(hipFuncSetAttribute((const void*)k_cent_tasks, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    HIP_TRY(hipFuncSetAttribute((const void*)k_cent_final, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     HIP_TRY(hipMemsetAsync(h->g_counter, 0, 8 * sizeof(unsigned long long), st));
     const int exhaustive = h->prob.method == HVP_METHOD_ENUMERATE ? 1 : 0;
     const char* dbg = std::getenv("HVP_CENT_DEBUG");  // diagnostics: printf of failing QPs
     const int debug = dbg && dbg[0] ? std::atoi(dbg) : 0;  // 1: failures, 2: + every GI step
-    const int cap = max_nodes > 0 ? max_nodes : 200000;
+    const int cap = max_nodes > 0 ? max_nodes : 2000000;
     const int max_iter = 8 * hvp::cent::ROWS * V;  // active-set iterations per QP
+    // split-search workspace: platoon records, merged tie lists, two task lists (ping-pong),
+    // counters, and per-wave DFS frames / tie slices of the task kernel
+    using hvp::cent::kTie;
+    using hvp::cent::kTieG;
+    const int waves = std::max(1, h->n_cu) * 3;  // LDS: three wave QPs per CU
+    const long long task_cap = std::max<long long>(1 << 16, 64LL * P);
+    auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    const size_t b_rec = al(sizeof(hvp::cent::PlatoonRec) * P), b_tg = al(sizeof(uint64_t) * P * kTieG * n),
+                 b_tgc = al(sizeof(double) * P * kTieG), b_task = al(sizeof(hvp::cent::Task) * task_cap),
+                 b_cnt = al(8 * sizeof(unsigned long long)),
+                 b_wf = al(sizeof(hvp::cent::Child) * (size_t)waves * V * h->nreg_max),
+                 b_wt = al(sizeof(uint64_t) * (size_t)waves * kTie * n);
+    const size_t sb = b_rec + b_tg + b_tgc + 2 * b_task + b_cnt + b_wf + b_wt;
+    if (sb > h->cent_split_bytes) {
+        HIP_TRY(hipDeviceSynchronize());
+        (void)hipFree(h->cent_split);
+        h->cent_split = nullptr;
+        h->cent_split_bytes = 0;
+        if (hipMalloc(&h->cent_split, sb) != hipSuccess)
+            return fail(HVP_E_NOMEM, "hvp_cent_solve_batch: device allocation failed");
+        h->cent_split_bytes = sb;
+    }
+    char* cp = h->cent_split;
+    auto take = [&](size_t b) { char* r = cp; cp += b; return r; };
+    hvp::cent::SplitWs ws{};
+    ws.rec = (hvp::cent::PlatoonRec*)take(b_rec);
+    ws.tie_g = (uint64_t*)take(b_tg);
+    ws.tie_gc = (double*)take(b_tgc);
+    hvp::cent::Task* lists[2] = {(hvp::cent::Task*)take(b_task), (hvp::cent::Task*)take(b_task)};
+    unsigned long long* cnt = (unsigned long long*)take(b_cnt);  // [0], [1] list sizes, [2] claim
+    hvp::cent::Child* frames_w = (hvp::cent::Child*)take(b_wf);
+    uint64_t* ties_w = (uint64_t*)take(b_wt);
+    ws.out_cap = task_cap;
+    ws.budget = exhaustive ? 0 : kSplitBudget;
+    if (const char* b = std::getenv("HVP_CENT_SPLIT")) ws.budget = std::atoi(b);  // 0: never split
+    Epilogue E{u_out, x_out, region_out, gear_out, cost_out, status_out, nodes_out, iters_out, h->g_counter};
+    HIP_TRY(hipMemsetAsync(cnt, 0, 8 * sizeof(unsigned long long), st));
+    hipLaunchKernelGGL(k_cent_init, dim3((P + 63) / 64), dim3(64), 0, st, P, ws.rec);
     HIP_TRY(hipEventRecord(h->ev0, st));
     HIP_TRY(hipEventRecord(h->evq0, st));
+    ws.out = lists[0];
+    ws.out_count = cnt + 0;
     hipLaunchKernelGGL(k_cent_bnb, dim3(P), dim3(64), lds, st, P, n, N, leader_index, real_vehicle_as_reference ? 1 : 0,
                        h->d_sys, sys, x0, leader_x, h->d_consts, h->nreg_max, cap, exhaustive, max_iter, debug, h->cent_frames,
-                       h->cent_ties, u_out, x_out, region_out, gear_out, cost_out, status_out, nodes_out, iters_out,
-                       h->g_counter);
+                       h->cent_ties, ws, E);
     HIP_TRY(hipGetLastError());
+    if (ws.budget > 0) {
+        // rounds of subtree tasks until none is left (one host read of the task count per round)
+        int cur = 0;
+        unsigned long long left = 0;
+        ws.budget = kTaskBudget;
+        if (const char* b = std::getenv("HVP_CENT_TASK_BUDGET")) ws.budget = std::max(1, std::atoi(b));
+        for (int r = 0; r < kTaskRounds; ++r) {
+            HIP_TRY(hipMemcpyAsync(&left, cnt + cur, sizeof(left), hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+            if (debug) {
+                unsigned long long prog[2] = {0, 0};
+                (void)hipMemcpy(prog, h->g_counter, sizeof(prog), hipMemcpyDeviceToHost);
+                std::fprintf(stderr, "[cent] split round %d: %llu tasks (QPs of finished searches so far %llu)\n", r,
+                             left, prog[0]);
+            }
+            if (!left) break;
+            ws.in = lists[cur];
+            ws.in_count = std::min<unsigned long long>(left, (unsigned long long)task_cap);
+            ws.in_claim = cnt + 2;
+            ws.out = lists[cur ^ 1];
+            ws.out_count = cnt + (cur ^ 1);
+            HIP_TRY(hipMemsetAsync(cnt + 2, 0, sizeof(unsigned long long), st));
+            HIP_TRY(hipMemsetAsync(cnt + (cur ^ 1), 0, sizeof(unsigned long long), st));
+            hipLaunchKernelGGL(k_cent_tasks, dim3(waves), dim3(64), lds, st, n, N, leader_index,
+                               real_vehicle_as_reference ? 1 : 0, h->d_sys, sys, x0, leader_x, h->d_consts, h->nreg_max,
+                               cap, max_iter, debug, frames_w, ties_w, ws);
+            HIP_TRY(hipGetLastError());
+            cur ^= 1;
+            left = 0;
+        }
+        if (!left) {
+            HIP_TRY(hipMemcpyAsync(&left, cnt + cur, sizeof(left), hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+        }
+        if (left) {
+            const unsigned long long c = std::min<unsigned long long>(left, (unsigned long long)task_cap);
+            hipLaunchKernelGGL(k_cent_abandon, dim3((unsigned)((c + 63) / 64)), dim3(64), 0, st, lists[cur], c, ws.rec);
+            HIP_TRY(hipGetLastError());
+        }
+        hipLaunchKernelGGL(k_cent_final, dim3(P), dim3(64), lds, st, P, n, N, leader_index,
+                           real_vehicle_as_reference ? 1 : 0, h->d_sys, sys, x0, leader_x, h->d_consts, max_iter, debug,
+                           ws, E);
+        HIP_TRY(hipGetLastError());
+    }
 #ifdef HVP_CENT_PROF
     if (debug >= 3) {  // phase profile of the wave QP (hvp_cent.h Prof), summed over all platoons
         unsigned long long prof[16];

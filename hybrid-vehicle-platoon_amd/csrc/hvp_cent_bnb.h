@@ -28,7 +28,68 @@
 namespace hvp {
 namespace cent {
 
-constexpr int kTie = 16;  // near-optimal leaves kept for the tie rule
+constexpr int kTie = 16;  // near-optimal leaves kept for the tie rule (per search / task)
+constexpr int kTieG = 64; // near-optimal leaves kept per platoon across the tasks of a split search
+
+// ---- split searches (heavy platoons): a search that exceeds its QP budget exports the
+// unexplored children of its open DFS frames as subtree TASKS; rounds of k_cent_tasks run the
+// tasks of all split platoons on every wave of the chip (sharing each platoon's incumbent for
+// pruning), and k_cent_final picks the winner from the platoon's merged near-optimal leaves.
+constexpr int kSplit = 100;     // Result.status: exported as tasks (k_cent_final finishes it)
+constexpr int kTaskDone = 101;  // Result.status of a finished subtree task
+
+struct Task {
+    int32_t p, d0;  // platoon; decisions fixed at the subtree root
+    double lb;      // the root's bound
+    uint64_t code[kMaxVeh];
+    double lo[kMaxVeh], hi[kMaxVeh];  // exact interval of each vehicle's first undecided velocity
+};
+
+// per-platoon record of a split search (global memory, initialised per call)
+struct PlatoonRec {
+    unsigned long long inc_key;   // incumbent (order-preserving key of the cost; ~0: none)
+    unsigned long long fail_key;  // smallest bound of a leaf whose QP failed (~0: none)
+    unsigned long long nodes, iters;
+    int tie_count;                // entries of the merged tie list
+    int flags;                    // 1 split, 2 node limit, 4 tie list overflow, 8 task list overflow
+};
+enum { REC_SPLIT = 1, REC_NODE_LIMIT = 2, REC_TIE_OVER = 4, REC_TASK_OVER = 8 };
+
+__device__ inline unsigned long long ckey(double c) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(c);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+__device__ inline double kcost(unsigned long long k) {
+    if (k == ~0ull) return __builtin_inf();
+    return __longlong_as_double((long long)((k >> 63) ? (k & 0x7fffffffffffffffull) : ~k));
+}
+
+// device pointers of a call's split-search workspace (hvp_cent.hip)
+struct SplitWs {
+    PlatoonRec* rec;          // [P]
+    uint64_t* tie_g;          // [P][kTieG][n]
+    double* tie_gc;           // [P][kTieG]
+    Task* out;                // next round's tasks
+    unsigned long long* out_count;
+    long long out_cap;
+    const Task* in;           // this round's tasks (k_cent_tasks)
+    unsigned long long* in_claim;
+    unsigned long long in_count;
+    int budget;               // QPs per search / task before it splits (0: no splitting)
+};
+
+struct SplitArgs {
+    int mode;                  // 1 whole search that may split, 2 subtree task
+    int budget;                // QPs of this search before it splits
+    int p;                     // platoon
+    const Task* task;          // mode 2: the subtree root
+    PlatoonRec* rec;           // this platoon's record
+    uint64_t* tie_g;           // [kTieG][n] merged near-optimal codes of this platoon
+    double* tie_gc;            // [kTieG] their costs
+    Task* out;                 // tasks for the next round
+    unsigned long long* out_count;
+    long long out_cap;
+};
 
 enum { QP_OK = 0, QP_INFEASIBLE = 1, QP_FAILED = 2 };
 
@@ -117,14 +178,24 @@ __device__ inline Child load_child(const Child* c) {
 // st.vcode hold the winner.  Written as a loop with ONE platoon-QP call site (bound QPs of a
 // node's children, leaf QPs and the final re-solve all go through it), so the large QP body is
 // inlined once and its state stays in registers.
+//
+// sp (split searches, see Task): mode 1 = the whole search of a platoon that exports its open
+// frames as tasks once it has solved sp->budget QPs (then Result.status = kSplit); mode 2 = the
+// subtree of sp->task, merged into the platoon's record when done (kTaskDone; it splits again
+// past its budget).  Both prune against the platoon's shared incumbent.  Without sp the search
+// runs to the end (the exhaustive mode and the searches that fit their budget behave alike:
+// a platoon alone on its record sees only its own incumbent, so its QP count is the oracle's).
 __device__ inline void bnb_platoon(Lane& L, const Lds& S, const Consts& C, const Inst& I, Search& st, Child* frames,
                                    int nreg_max, uint64_t* tie_codes, int max_nodes, bool exhaustive, int max_iter,
-                                   Result& res) {
+                                   Result& res, const SplitArgs* sp = nullptr) {
     const int t = lane();
     const int n = I.n, N = I.N, D = n * N;
     const double INF = __builtin_inf();
-    st.vcode = 0;
-    st.vlo = st.vhi = t < n ? I.x0[2 * t + 1] : 0.0;
+    const bool task = sp && sp->mode == 2;
+    const int d0 = task ? sp->task->d0 : 0;  // the search ends when it backtracks above d0
+    st.vcode = task && t < n ? sp->task->code[t] : 0;
+    st.vlo = t < n ? (task ? sp->task->lo[t] : I.x0[2 * t + 1]) : 0.0;
+    st.vhi = t < n ? (task ? sp->task->hi[t] : I.x0[2 * t + 1]) : 0.0;
     st.f_n = st.f_cur = 0;
     st.f_slo = st.f_shi = st.f_lb = 0.0;
     st.tie_c = INF;
@@ -135,10 +206,17 @@ __device__ inline void bnb_platoon(Lane& L, const Lds& S, const Consts& C, const
     int nodes = 0, iters = 0, searched = 0;
     Prof pf;
     pf.start(I.debug >= 3);
+    // the platoon's shared incumbent (split searches)
+    auto shared_inc = [&]() -> double {
+        if (!sp) return inc;
+        unsigned long long k = 0;
+        if (t == 0) k = __atomic_load_n(&sp->rec->inc_key, __ATOMIC_RELAXED);
+        return fmin(inc, kcost(bcu((uint64_t)k, 0)));
+    };
 
     // expansion of the node with d decisions taken: lane r holds child r's interval and bound
-    enum { EXPAND = 0, VISIT = 1, FINAL = 2 };
-    int phase = EXPAND, d = 0;
+    enum { EXPAND = 0, VISIT = 1, FINAL = 2, LEAF = 3 };
+    int phase = EXPAND, d = d0;
     unsigned long long ex_mask = 0, ex_todo = 0;
     uint64_t ex_save = 0;
     bool ex_ok = false;
@@ -211,9 +289,77 @@ __device__ inline void bnb_platoon(Lane& L, const Lds& S, const Consts& C, const
             }
         }
         have_best = true;
+        if (sp && t == 0) atomicMin(&sp->rec->inc_key, ckey(cost));
+    };
+    // split searches: this search's leaves, counters and flags into the platoon's record
+    auto merge = [&]() {
+        for (int j = 0; j < ntie; ++j) {
+            const double cj = bcu(st.tie_c, j);
+            int slot = 0;
+            if (t == 0) slot = atomicAdd(&sp->rec->tie_count, 1);
+            slot = bcu(slot, 0);
+            if (slot >= kTieG) {
+                tie_over = true;
+                continue;
+            }
+            if (t < n) sp->tie_g[(size_t)slot * n + t] = tie_codes[(size_t)j * n + t];
+            if (t == 0) sp->tie_gc[slot] = cj;
+        }
+        if (t == 0) {
+            atomicAdd(&sp->rec->nodes, (unsigned long long)nodes);
+            atomicAdd(&sp->rec->iters, (unsigned long long)iters);
+            if (fail_lb < INF) atomicMin(&sp->rec->fail_key, ckey(fail_lb));
+            const int fl = (tie_over ? REC_TIE_OVER : 0) | (node_limit ? REC_NODE_LIMIT : 0);
+            if (fl) atomicOr(&sp->rec->flags, fl);
+        }
+    };
+    // split: the unexplored children of the open frames d .. d0 become tasks (deepest first;
+    // each vehicle's interval goes back to its parent's as the DFS backtrack does)
+    auto export_tasks = [&]() {
+        uint64_t vcode_w = st.vcode;
+        double vlo_w = st.vlo, vhi_w = st.vhi;
+        bool over = false;
+        const double incp = shared_inc();
+        for (int j = d; j >= d0; --j) {
+            const int nch = bcu(st.f_n, j), cur = bcu(st.f_cur, j);
+            const int i = j % n, k = j / n;
+            for (int c = cur; c < nch; ++c) {
+                const Child ch = load_child(frames + (size_t)j * nreg_max + c);
+                if (!(ch.lb < INF)) continue;
+                if (incp < INF && bnb_pruned(ch.lb, incp)) continue;
+                uint64_t slot = 0;
+                if (t == 0) slot = atomicAdd(sp->out_count, 1ull);
+                slot = bcu(slot, 0);
+                if ((long long)slot >= sp->out_cap) {
+                    over = true;
+                    continue;
+                }
+                Task* tk = sp->out + slot;
+                if (t < n) {
+                    tk->code[t] = t == i ? code_with(vcode_w, k, ch.r) : vcode_w;
+                    tk->lo[t] = t == i ? ch.lo : vlo_w;
+                    tk->hi[t] = t == i ? ch.hi : vhi_w;
+                }
+                if (t == 0) {
+                    tk->p = sp->p;
+                    tk->d0 = j + 1;
+                    tk->lb = ch.lb;
+                }
+            }
+            const double slo = bcu(st.f_slo, j), shi = bcu(st.f_shi, j);
+            if (t == i) {
+                vlo_w = slo;
+                vhi_w = shi;
+            }
+        }
+        if (t == 0) atomicOr(&sp->rec->flags, REC_SPLIT | (over ? REC_TASK_OVER : 0));
     };
 
-    begin_expand(0);
+    if (task && d0 >= D) {
+        phase = LEAF;  // the task is one leaf
+    } else {
+        begin_expand(d0);
+    }
     for (;;) {
         // ---- decide the next QP (dfix decisions fixed), or move the search without one
         int dfix = -1;
@@ -227,10 +373,29 @@ __device__ inline void bnb_platoon(Lane& L, const Lds& S, const Consts& C, const
             ex_r = __ffsll((long long)ex_todo) - 1;
             if (t == d % n) st.vcode = code_with(ex_save, d / n, ex_r);
             dfix = d + 1;
+        } else if (phase == LEAF) {
+            dfix = D;
         } else if (phase == VISIT) {
             if (nodes >= max_nodes) {
                 node_limit = true;
                 break;
+            }
+            if (task && d < d0) {  // subtree done
+                merge();
+                res.status = kTaskDone;
+                res.nodes = nodes;
+                res.iters = iters;
+                pf.flush();
+                return;
+            }
+            if (sp && d >= d0 && nodes >= sp->budget) {  // past the budget: split
+                export_tasks();
+                merge();
+                res.status = task ? kTaskDone : kSplit;
+                res.nodes = nodes;
+                res.iters = iters;
+                pf.flush();
+                return;
             }
             if (d < 0) {  // search done
                 searched = nodes;
@@ -265,7 +430,8 @@ __device__ inline void bnb_platoon(Lane& L, const Lds& S, const Consts& C, const
                 }
                 if (t == d) st.f_cur = cur + 1;
                 const Child ch = load_child(frames + (size_t)d * nreg_max + cur);
-                if (have_best && bnb_pruned(ch.lb, inc)) continue;
+                const double incp = shared_inc();
+                if ((have_best || incp < INF) && bnb_pruned(ch.lb, incp)) continue;
                 if (!(ch.lb < INF)) continue;
                 if (t == i) {
                     st.vcode = code_with(st.vcode, k, ch.r);
@@ -316,6 +482,11 @@ __device__ inline void bnb_platoon(Lane& L, const Lds& S, const Consts& C, const
                 const double plb = D >= 2 ? bcu(st.f_lb, D - 2) : -INF;
                 fail_lb = fmin(fail_lb, plb);
             }
+        } else if (phase == LEAF) {  // a one-leaf task: its bound is the exported child's
+            if (q == QP_OK) record(c);
+            else if (q == QP_FAILED) fail_lb = fmin(fail_lb, sp->task->lb);
+            phase = VISIT;
+            d = d0 - 1;  // done
         } else {  // FINAL
             // a failed leaf whose bound is not above the incumbent could hide the optimum
             res.status = (fail_lb < INF && !bnb_pruned(fail_lb, inc)) ? HVP_MAXITER : HVP_OPTIMAL;
@@ -326,6 +497,14 @@ __device__ inline void bnb_platoon(Lane& L, const Lds& S, const Consts& C, const
             pf.flush();
             return;
         }
+    }
+    if (task) {  // a subtree stopped by the QP cap
+        merge();
+        res.status = kTaskDone;
+        res.nodes = nodes;
+        res.iters = iters;
+        pf.flush();
+        return;
     }
     res.cost = INF;
     if (node_limit) res.status = HVP_MAXITER;

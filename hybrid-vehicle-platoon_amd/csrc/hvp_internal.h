@@ -87,4 +87,6 @@ struct hvp_handle {
     hvp::cent::Child* cent_frames = nullptr;
     uint64_t* cent_ties = nullptr;
     hvp::Consts* d_consts = nullptr;  // device copy of C (the centralised kernel reads it by pointer)
+    size_t cent_split_bytes = 0;      // split-search workspace of the centralised path (hvp_cent.hip)
+    char* cent_split = nullptr;
 };

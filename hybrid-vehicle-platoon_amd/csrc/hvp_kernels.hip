@@ -648,6 +648,7 @@ void hvp_destroy(hvp_handle* h) {
     if (h->g_counter) (void)hipFree(h->g_counter);
     if (h->cent_frames) (void)hipFree(h->cent_frames);
     if (h->cent_ties) (void)hipFree(h->cent_ties);
+    if (h->cent_split) (void)hipFree(h->cent_split);
     if (h->d_consts) (void)hipFree(h->d_consts);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);

@@ -28,7 +28,7 @@ from .env import EpisodeMonitor, PlatoonEnv
 from .models import Platoon, Vehicle
 from .params import ConstantSpacingPolicy, Params, Sim, SpacingPolicy
 
-DEFAULT_MAX_NODES = 200_000
+DEFAULT_MAX_NODES = 2_000_000
 
 
 def cent_problem(N: int, spacing_policy: SpacingPolicy | None = None, quadratic_cost: bool = True,

@@ -256,10 +256,17 @@ int hvp_gadmm_switch(hvp_handle* h, int P, int n, int lo, int m, const int32_t* 
  * Exact branch and bound over the joint region sequence (time-major), ties to the
  * lexicographically first sequence in that order; hvp_problem.method == HVP_METHOD_ENUMERATE
  * visits every velocity-feasible joint sequence instead (cross-check, tiny instances only).
- * max_nodes (<= 0: 200000) caps the QPs per platoon; a platoon that reaches it is HVP_MAXITER.
+ * max_nodes (<= 0: 2000000) caps the QPs per platoon; a platoon that reaches it is HVP_MAXITER
+ * (a split search, below, checks the cap per subtree task, so it may overshoot by the tasks in
+ * flight).  A platoon whose search passes 1000 QPs is SPLIT: its open DFS frames become subtree
+ * tasks that rounds of one kernel spread over every wave of the device (sharing the platoon's
+ * incumbent); a final kernel applies the tie rule to the merged near-optimal leaves.  The answer
+ * is the same; the QP count of a split platoon is not the sequential search's.  The call then
+ * synchronises the stream once per round (it reads the number of tasks left).
  * Outputs: u [P][n][N], x [P][n][2][N+1] (may be NULL), region / gear [P][n][N] int8 (may be
  * NULL), cost [P], status [P], nodes [P] (QPs solved, Gurobi NodeCount analogue), iters [P] (may
- * be NULL).  Workspace grows on demand (one synchronisation when it does). */
+ * be NULL).  Workspace grows on demand (one synchronisation when it does).  HVP_CENT_SPLIT=0 in
+ * the environment disables the split (HVP_CENT_SPLIT=k: split past k QPs). */
 int hvp_cent_solve_batch(hvp_handle* h, int P, int n, int leader_index, int real_vehicle_as_reference,
                          const int32_t* sys, const double* x0, const double* leader_x, int max_nodes,
                          double* u_out, double* x_out, int8_t* region_out, int8_t* gear_out,

@@ -175,6 +175,32 @@ def test_gpu_matches_cent_golden(gpu_available, name):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("name,split", [("cent_n6_N5.npz", 40), ("cent_n8_N5.npz", 25), ("cent_n3_N10.npz", 30),
+                                        ("cent_gear_n3_N4.npz", 10), ("cent_task2_n5_N5.npz", 20)])
+def test_gpu_split_search_matches_cent_golden(gpu_available, monkeypatch, name, split):
+    """The split search (heavy platoons: open DFS frames exported as subtree tasks run by every
+    wave, shared incumbent, tie rule over the merged leaves) forced on the fixtures by a tiny
+    split budget: the same regions, gears, cost and trajectories as the oracle's sequential
+    search (the QP counts differ: the order of exploration does)."""
+    monkeypatch.setenv("HVP_CENT_SPLIT", str(split))
+    monkeypatch.setenv("HVP_CENT_TASK_BUDGET", "32")
+    fx = load(name)
+    s, sys_idx = _product(fx)
+    for lead_idx, lsp in sorted({(int(a), int(b)) for a, b in zip(fx["leader_index"], fx["lsp"])}):
+        sel = np.flatnonzero((fx["leader_index"] == lead_idx) & (fx["lsp"] == lsp))
+        res = s.solve(sys_idx[sel], fx["x0"][sel], fx["leader_x"][sel], lead_idx, bool(lsp))
+        for j, p in enumerate(sel):
+            assert res.status[j] == fx["exp_status"][p], (name, p, res.status[j])
+            if fx["exp_status"][p] != 0:
+                continue
+            assert np.array_equal(res.region[j], fx["exp_region"][p]), (name, p, res.region[j], fx["exp_region"][p])
+            assert np.array_equal(res.gear[j], fx["exp_gear"][p]), (name, p)
+            assert abs(res.cost[j] - fx["exp_cost"][p]) <= 1e-9 * abs(fx["exp_cost"][p]), (name, p)
+            assert np.abs(res.u[j] - fx["exp_u"][p]).max() <= 1e-6, (name, p)
+            assert np.abs(res.x[j] - fx["exp_x"][p]).max() <= 1e-4, (name, p)
+
+
+@pytest.mark.gpu
 def test_gpu_exhaustive_equals_bnb(gpu_available):
     from hvp import tables
     from hvp.cent import CentSolver, cent_problem
