@@ -596,6 +596,9 @@ __global__ __launch_bounds__(kBnbBlock<N>) HVP_LANE_OCC void k_bnb_bound(int k, 
 // (profiles/r02e_*): 8 -> 3.52M, 16 -> 3.95M, 32 -> 4.41M, 48 -> 4.69M, 64 -> 4.86M
 // platoon-steps/s: the setup and write code run at full width beats refilling lanes early, so
 // the default refills a wave when ALL its lanes are free (generations of 64 nodes).
+// A variant written as explicit generations (claim 64 nodes -> set up -> trips until the wave is
+// done -> write 64 results) ran at 2.73M against this kernel's 4.87M (profiles/r02q_*): with two
+// trip-loop levels the compiler's allocation spills ~3x more scratch traffic inside the trips.
 // Same results per node as k_bnb_bound (the node -> lane mapping does not matter).
 #ifndef HVP_REFILL_WAVES
 #define HVP_REFILL_WAVES 2
