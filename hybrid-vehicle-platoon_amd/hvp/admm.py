@@ -3,6 +3,9 @@
 * :class:`LocalMpcADMM` <- fleet_naive_admm.py:24-258: the local MIQP with neighbour COPIES as
   decision variables (``set_front_vars(y, z)``, ``set_back_vars(y, z)``, ``set_leader_x``;
   after a solve ``x.X``, ``u.X``, ``x_front.X``, ``x_back.X`` as the coordinator reads them).
+* :class:`LocalMpcGear` <- :261-288: the same local problem on the pwa_friction model with gear
+  binaries (MpcGear.setup_gears); the table enumerates (gear, friction region) modes as
+  :class:`hvp.mpc.MpcGear` does, and ``solve_mpc`` returns [u_g0; gear0].
 * :class:`AdmmEngine` -- the batched device form of ``ADMMCoordinator.get_control``
   (:379-468) for P platoons of n vehicles: per ADMM iteration ONE ``hvp_solve_admm_batch``
   over all P*n local MIQPs (they only couple through z, y of the previous iteration), then ONE
@@ -131,6 +134,35 @@ class LocalMpcADMM:
         info = {"x": x, "u": u, "cost": cost, "run_time": run_time, "nodes": int(res.nodes[i]),
                 "bin_vars": self.num_bin_vars, "status": int(res.status[i])}
         return u[:, [0]], info
+
+
+class LocalMpcGear(LocalMpcADMM):
+    """fleet_naive_admm.py:261-288: LocalMpcADMM's cost and copies on the gear MPC
+    (mpcs/mpc_gear.py:30-114): the decision variable is the throttle u_g, bounded by the system's
+    F u_g <= G, and every step picks a (gear, friction region) mode.  ``solve_mpc`` returns
+    [u_g0; gear0] and info["u"] = vstack(u_g, gears), as MpcGear.solve_mpc does (:116-135)."""
+
+    def __init__(self, N: int, system: dict, rho: float, spacing_policy: SpacingPolicy = ConstantSpacingPolicy(50),
+                 quadratic_cost: bool = True, is_front: bool = False, is_leader: bool = False,
+                 is_trailer: bool = False, thread_limit: int | None = None,
+                 accel_cnstr_tightening: float = 0.0) -> None:
+        from .mpc import MpcGear
+
+        super().__init__(N, system, rho, spacing_policy, quadratic_cost, is_front, is_leader, is_trailer,
+                         thread_limit, accel_cnstr_tightening)
+        self.table = tables.gear_system_from_dict(system)
+        MpcGear.setup_gears(self, N, system["F"], system["G"])  # the u_g box on self.table
+        self.num_bin_vars = (len(system["S"]) + len(Vehicle.b)) * N
+        self.gears_pred = None
+
+    def absorb(self, res, i: int, run_time: float, raises: bool, state=None):
+        _, info = super().absorb(res, i, run_time, raises, state)
+        ok = info["status"] == _abi.OPTIMAL
+        u_g = info["u"]
+        gears = res.gear[i].reshape(1, -1).astype(float) if ok else 6 * np.ones((1, self.N))
+        info["u"] = np.vstack((u_g, gears))
+        self.gears_pred = gears
+        return np.vstack((u_g[:, [0]], gears[:, [0]])), info
 
 
 class AdmmEngine:
@@ -267,11 +299,17 @@ class ADMMCoordinator(MldAgent):
                 m.x_back.X = res["x_back"][i]
             a.record({"x": res["x"][i], "u": res["u"][i].reshape(1, -1), "cost": float(res["cost"][i]),
                       "run_time": dt / self.admm_iters, "nodes": int(res["nodes"][i]), "bin_vars": m.num_bin_vars})
-            u.append(res["u"][i][:1].reshape(1, 1))
+            if isinstance(m, LocalMpcGear):
+                m.gears_pred = res["gear"][i].reshape(1, -1).astype(float)
+                u.append(np.array([[res["u"][i][0]], [m.gears_pred[0, 0]]]))
+            else:
+                u.append(res["u"][i][:1].reshape(1, 1))
         # solve-time bookkeeping (:470-477): per iteration the slowest agent; the n agents of an
         # iteration run in one batched launch
         self.temp_solve_time += dt
         self.temp_node_count = max(self.temp_node_count, int(res["nodes"].max()))
+        if u[0].shape[0] > self.nu_l:  # gear MPCs: continuous controls first, then the gears (:557-566)
+            return np.vstack([np.vstack([a[:self.nu_l] for a in u]), np.vstack([a[self.nu_l:] for a in u])]), {}
         return np.vstack(u), {}
 
     def on_timestep_end(self, env, episode: int, timestep: int) -> None:
@@ -290,8 +328,9 @@ def simulate(sim: Sim, admm_iters: int = 20, save: bool = False, plot: bool = Fa
     """Closed-loop run of the naive-ADMM controller (fleet_naive_admm.py:580-692)."""
     n, N, ep_len, ts = sim.n, sim.N, sim.ep_len, Params.ts
     leader_x = sim.leader_trajectory.get_leader_trajectory()
-    if sim.vehicle_model_type != "pwa_gear":
-        raise NotImplementedError("the GPU ADMM path implements the pwa_gear model (LocalMpcADMM)")
+    if sim.vehicle_model_type not in ("pwa_gear", "pwa_friction"):  # :630-637
+        raise NotImplementedError("the GPU ADMM path implements the pwa_gear (LocalMpcADMM) and pwa_friction "
+                                  "(LocalMpcGear) models; the nonlinear model is out of scope (DESIGN.md)")
     platoon = Platoon(n, vehicle_type=sim.vehicle_model_type, masses=sim.masses)
     systems = platoon.get_vehicle_system_dicts(ts)
     env = EpisodeMonitor(
@@ -301,9 +340,14 @@ def simulate(sim: Sim, admm_iters: int = 20, save: bool = False, plot: bool = Fa
         max_episode_steps=ep_len,
     )
     vehicles = platoon.get_vehicles()
-    mpcs = [LocalMpcADMM(N, systems[i], rho=0.5, spacing_policy=sim.spacing_policy, is_front=i == 0,
-                         is_leader=i == leader_index, is_trailer=i == n - 1, thread_limit=thread_limit,
-                         gears=tables.gears_of(vehicles[i])) for i in range(n)]
+    def local(i):
+        kw = dict(rho=0.5, spacing_policy=sim.spacing_policy, is_front=i == 0, is_leader=i == leader_index,
+                  is_trailer=i == n - 1, thread_limit=thread_limit)
+        if sim.vehicle_model_type == "pwa_friction":
+            return LocalMpcGear(N, systems[i], **kw)
+        return LocalMpcADMM(N, systems[i], gears=tables.gears_of(vehicles[i]), **kw)
+
+    mpcs = [local(i) for i in range(n)]
     agent = ADMMCoordinator(leader_index=leader_index, local_mpcs=mpcs, admm_iters=admm_iters, rho=0.5,
                             ep_len=ep_len, N=N, leader_x=leader_x, ts=ts)
     agent.evaluate(env=env, episodes=1, seed=seed)

@@ -1357,6 +1357,55 @@ int oracle_solve_qp(int N, int nreg, int nsr, const double* S, const double* R, 
     return 0;
 }
 
+/* Certificate of a batch of answers (tests only): for every instance the fixed-sigma QP of the
+ * sequence sigma_in[i] (the product's chosen regions) solved and KKT-certified by the IPM above;
+ * out[i*(2+N)] = objective (INFINITY if not converged), out[..+1] = certified, then u (N).
+ * A product answer is certified when its cost equals this objective and its u this u (the QP is
+ * strictly convex in u, so the certified u is THE optimum of that sequence). */
+int oracle_certify_batch(int B, int N, int nsys, int nreg, int nsr, const double* S, const double* R,
+                         const double* T, const double* A, const double* B_, const double* c, int nd,
+                         const double* D, const double* E, int nf, const double* F, const double* G,
+                         const double* cfgp, int quadratic, const int* sys, const int* role, const double* params,
+                         const int* sigma_in, double* out, int nthreads) {
+    const int P = 2 + 6 * (N + 1);
+    int err = 0;
+    (void)nsys;
+    if (N > OR_MAX_N) return -1;
+#pragma omp parallel num_threads(nthreads > 0 ? nthreads : 1) reduction(| : err)
+    {
+        or_qp* qp = (or_qp*)malloc(sizeof(or_qp));
+        or_work* w = (or_work*)malloc(sizeof(or_work));
+        if (!qp || !w) err |= 1;
+#pragma omp for schedule(dynamic, 64)
+        for (int i = 0; i < B; ++i) {
+            if (!qp || !w) continue;
+            const int s = sys[i];
+            const double* p = params + (size_t)i * P;
+            or_model md;
+            or_cfg cf;
+            double* o = out + (size_t)i * (2 + N);
+            if (unpack_model(&md, nreg, nsr, S + (size_t)s * nreg * nsr * 2, R + (size_t)s * nreg * nsr,
+                             T + (size_t)s * nreg * nsr, A + (size_t)s * nreg * 4, B_ + (size_t)s * nreg * 2,
+                             c + (size_t)s * nreg * 2, nd, D + (size_t)s * nd * 2, E + (size_t)s * nd, nf,
+                             F + (size_t)s * nf, G + (size_t)s * nf)) {
+                err |= 1;
+                continue;
+            }
+            unpack_cfg(&cf, N, quadratic, role[i], cfgp);
+            const int nz = build_qp(qp, &md, &cf, sigma_in + (size_t)i * N, p, p + 2, p + 2 + 2 * (N + 1),
+                                    p + 2 + 4 * (N + 1));
+            or_result r = {0, 0, 0, INFINITY};
+            if (nz > 0 && !qp->infeasible_const) r = ipm_solve(qp, w, 200);
+            o[0] = r.converged ? r.obj : INFINITY;
+            o[1] = r.certified;
+            for (int k = 0; k < N; ++k) o[2 + k] = (nz > 0 && r.converged) ? w->z[2 * N + k] : NAN;
+        }
+        free(qp);
+        free(w);
+    }
+    return err ? -1 : 0;
+}
+
 /* Dense export of one fixed-sigma QP (tests only): P[nz*nz], q[nz], Aeq[neq*nz], beq, G[m*nz], h,
  * dims_out = [nz, neq, m, r0, infeasible_const]. Capacity of each buffer given by cap_* . */
 int oracle_export_qp(int N, int nreg, int nsr, const double* S, const double* R, const double* T, const double* A,

@@ -285,6 +285,9 @@ def lib():
         L.oracle_solve_batch.argtypes = [c_int, c_int, c_int, c_int, c_int, dp, dp, dp, dp, dp, dp, c_int, dp, dp,
                                          c_int, dp, dp, dp, c_int, ip, ip, dp, c_int, dp, dp, ip, dp, c_int]
         L.oracle_solve_batch.restype = c_int
+        L.oracle_certify_batch.argtypes = [c_int, c_int, c_int, c_int, c_int, dp, dp, dp, dp, dp, dp, c_int, dp, dp,
+                                           c_int, dp, dp, dp, c_int, ip, ip, dp, ip, dp, c_int]
+        L.oracle_certify_batch.restype = c_int
         L.oracle_solve_admm_miqp.argtypes = model_args + [dp, c_int, ctypes.c_double, dp, c_int, dp, dp, ip, dp,
                                                           dp, dp]
         L.oracle_solve_admm_miqp.restype = c_int
@@ -473,6 +476,30 @@ def solve_batch(systems: list[dict], cfg: Cfg, N: int, sys_idx, roles, params, q
     if rc != 0:
         raise RuntimeError("oracle_solve_batch failed")
     return x_out, u_out, sig, info
+
+
+def certify_batch(systems: list[dict], cfg: Cfg, N: int, sys_idx, roles, params, sigma, quadratic: bool = True,
+                  nthreads: int = 1):
+    """KKT-certified optimum of every instance's fixed-sequence QP for the GIVEN sequences (the
+    product's answers).  Returns (objective (B,), certified (B,) bool, u (B, N))."""
+    L = lib()
+    nreg = np.asarray(systems[0]["S"]).shape[0]
+    nsr = np.asarray(systems[0]["S"]).shape[1]
+    st = {k: np.ascontiguousarray(np.stack([np.asarray(s[k], dtype=np.float64) for s in systems])) for k in
+          "SRTABcDEFG"}
+    B = len(sys_idx)
+    sys_idx = np.ascontiguousarray(np.asarray(sys_idx, dtype=np.int32))
+    roles = np.ascontiguousarray(np.asarray(roles, dtype=np.int32))
+    params = np.ascontiguousarray(np.asarray(params, dtype=np.float64))
+    sig = np.ascontiguousarray(np.asarray(sigma, dtype=np.int32).reshape(B, N))
+    out = np.zeros((B, 2 + N))
+    rc = L.oracle_certify_batch(B, N, len(systems), nreg, nsr, _d(st["S"]), _d(st["R"]), _d(st["T"]), _d(st["A"]),
+                                _d(st["B"]), _d(st["c"]), st["D"].shape[1], _d(st["D"]), _d(st["E"]),
+                                st["F"].shape[1], _d(st["F"]), _d(st["G"]), _d(cfg.vector()), int(quadratic),
+                                _i(sys_idx), _i(roles), _d(params), _i(sig), _d(out), nthreads)
+    if rc != 0:
+        raise RuntimeError("oracle_certify_batch failed")
+    return out[:, 0].copy(), out[:, 1] != 0, out[:, 2:].copy()
 
 
 def export_qp(sysd: dict, cfg: Cfg, N: int, role: int, sigma, x0, xf, xb, xl, quadratic: bool = True):

@@ -29,6 +29,9 @@ Files (numpy .npz, no pickles):
                       (gear, friction region) modes, oracle gear_friction_mld_system
   admm_local_N{5,10}.npz, admm_steps_n4_N5.npz  naive ADMM (configs[2]): local problems with
                       copies, and 3 closed-loop time steps x 4 ADMM iterations (oracle coordinator)
+  admm_gear_local_N5.npz, admm_gear_steps_n4_N5.npz  naive ADMM on the pwa_friction model
+                      (fleet_naive_admm.py:261-288 LocalMpcGear): local problems on the oracle's
+                      gear_friction_mld_system and 3 closed-loop steps x 4 iterations
   gadmm_local_N{5,10}.npz, gadmm_steps_n4_N5.npz, gadmm_steps_n3_N10.npz  switching ADMM
                       (fleet_g_admm.py, configs[3]): every local QP of oracle coordinator runs
                       (sampled), and two time steps of the restated coordinator (warm starts,
@@ -39,7 +42,7 @@ Files (numpy .npz, no pickles):
                       n = 3 at N = 10, n = 10 at N = 3, variants (real_vehicle_as_reference, leader
                       index, task_2 masses / ConstantTime / stop-and-go, Q_du), mid-rollout states,
                       the gear model (MpcGearCent, model = 1)
-Run:  python tests/golden/make_golden.py [sweep | gear | admm | gadmm | cent [n10] | configs admm|gadmm]
+Run:  python tests/golden/make_golden.py [sweep | gear | admm | admm_gear | gadmm | cent [n10] | configs admm|gadmm]
 """
 
 from __future__ import annotations
@@ -244,6 +247,52 @@ def admm_fixtures():
     print("admm_steps_n4_N5.npz written")
 
 
+def admm_gear_fixtures():
+    """Naive ADMM with LocalMpcGear (fleet_naive_admm.py:261-288, selected for pwa_friction at
+    :632-633): the local problem's modes are (gear, friction region) pairs (oracle
+    gear_friction_mld_system, as for the decentralised gear fixtures); the same local-problem and
+    closed-loop sets as admm_fixtures."""
+    rng = np.random.default_rng(11)
+    sysd = O.gear_friction_mld_system(800.0)
+    N = 5
+    P, R, X, U, XF, XB, C, S, REG = [], [], [], [], [], [], [], [], []
+    for seed in range(3):
+        n = 4
+        st = O.env_initial_state(n, seed).astype(float)
+        for i in range(n):
+            pred = lambda j: O.constant_velocity_prediction(st[2 * j], st[2 * j + 1], N)  # noqa: E731
+            zf = pred(i - 1) + rng.normal(0, 3, (2, N + 1)) if i > 0 else np.zeros((2, N + 1))
+            zb = pred(i + 1) + rng.normal(0, 3, (2, N + 1)) if i < n - 1 else np.zeros((2, N + 1))
+            yf = rng.normal(0, 2, (2, N + 1)) if i > 0 else np.zeros((2, N + 1))
+            yb = rng.normal(0, 2, (2, N + 1)) if i < n - 1 else np.zeros((2, N + 1))
+            if seed == 0:
+                yf, zf, yb, zb = (np.zeros((2, N + 1)),) * 4
+            xl = leader_window(N) if i == 0 else np.zeros((2, N + 1))
+            p = O.admm_params(st[2 * i:2 * i + 2], yf, zf, yb, zb, xl)
+            r = O.solve_admm_miqp(sysd, O.Cfg(), N, O.role_bits(i, n), 0.5, p)
+            P.append(p); R.append(O.role_bits(i, n)); X.append(r.x); U.append(r.u); XF.append(r.x_front)
+            XB.append(r.x_back); C.append(r.cost); S.append(r.status); REG.append(r.sigma)
+    np.savez_compressed(os.path.join(HERE, "admm_gear_local_N5.npz"), N=N, rho=0.5, params=np.array(P),
+                        roles=np.array(R, np.int32), exp_x=np.array(X), exp_u=np.array(U), exp_xf=np.array(XF),
+                        exp_xb=np.array(XB), exp_cost=np.array(C), exp_status=np.array(S, np.int32),
+                        exp_region=np.array(REG, np.int32), exp_gear=np.asarray(sysd["gear"])[np.array(REG)])
+    print(f"admm_gear_local_N5.npz: {len(R)} instances")
+    n, iters = 4, 4
+    coord = O.AdmmCoordinator(sysd, O.Cfg(), N, n)
+    st = O.env_initial_state(n, 3).astype(float)
+    states, us, xs, gs = [], [], [], []
+    for t in range(3):
+        coord.set_leader_x(leader_window(N, t))
+        u, hist = coord.step(st, iters)
+        states.append(st.copy()); us.append(np.array([[r.u for r in res] for res in hist]))
+        xs.append(np.array([[r.x for r in res] for res in hist]))
+        gs.append(np.array([np.asarray(sysd["gear"])[r.sigma] for r in hist[-1]]))
+        st = np.concatenate([r.x[:, 1] for r in hist[-1]])
+    np.savez_compressed(os.path.join(HERE, "admm_gear_steps_n4_N5.npz"), N=N, n=n, iters=iters, rho=0.5,
+                        states=np.array(states), exp_u=np.array(us), exp_x=np.array(xs), exp_gear=np.array(gs))
+    print("admm_gear_steps_n4_N5.npz written")
+
+
 def config_size_fixtures(which: str):
     """configs[2] and configs[3] at their own sizes: the oracle coordinators on
     t = 0 platoon states for two consecutive time steps (the state advances along the solution's
@@ -429,6 +478,9 @@ def main():
         return
     if len(sys.argv) > 1 and sys.argv[1] == "admm":
         admm_fixtures()
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == "admm_gear":
+        admm_gear_fixtures()
         return
     if len(sys.argv) > 1 and sys.argv[1] == "sweep":
         sweep()

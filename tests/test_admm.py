@@ -173,3 +173,112 @@ def test_admm_engine_batch_independence(gpu_available):
         assert np.array_equal(c["region"], a["region"][sl])
         assert np.abs(c["u"] - a["u"][sl]).max() <= 1e-9
     del bench
+
+
+# ---------------------------------------------------------------- pwa_friction: LocalMpcGear
+# fleet_naive_admm.py:261-288 (selected for pwa_friction at :632-633): the local problem over
+# (gear, friction region) modes, fixtures from the oracle's gear_friction_mld_system.
+
+
+def _gear_mpc(i=1, n=4):
+    from hvp.admm import LocalMpcGear
+    from hvp.models import PwaFrictionVehicle
+
+    return LocalMpcGear(5, PwaFrictionVehicle(800).get_discrete_system(1), rho=0.5, is_front=i == 0,
+                        is_leader=i == 0, is_trailer=i == n - 1)
+
+
+def test_admm_gear_local_problem_host_build_matches_oracle(hostref):
+    from hvp import _abi
+
+    fx = load("admm_gear_local_N5.npz")
+    m = _gear_mpc()
+    assert m.num_bin_vars == 8 * 5
+    N, B = 5, len(fx["roles"])
+    S = (_abi.HvpSystem * 1)(m.table)
+    u, x, reg = np.zeros((B, N)), np.zeros((B, 2, N + 1)), np.zeros((B, N), np.int8)
+    cost, st, nodes, it = np.zeros(B), np.zeros(B, np.int32), np.zeros(B, np.int32), np.zeros(B, np.int32)
+    xf, xb = np.zeros((B, 2, N + 1)), np.zeros((B, 2, N + 1))
+    f = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    rc = hostref.hvp_hostref_solve_admm_batch(ctypes.byref(m.problem), S, B, f(np.zeros(B, np.int32)),
+                                              f(np.ascontiguousarray(fx["roles"])), f(np.ascontiguousarray(fx["params"])),
+                                              f(u), f(x), f(reg), f(cost), f(st), f(nodes), f(it), f(xf), f(xb), 2)
+    assert rc == 0
+    _check(fx, u, x, reg, cost, st, xf, xb)
+
+
+@pytest.mark.gpu
+def test_admm_gear_local_problem_on_gpu(gpu_available):
+    """LocalMpcGear's batch solve against the oracle: modes (regions), gears, u_g, cost, copies."""
+    from hvp.solver import BatchSolver
+
+    fx = load("admm_gear_local_N5.npz")
+    m = _gear_mpc()
+    s = BatchSolver(m.problem, [m.table])
+    B = len(fx["roles"])
+    res = s.solve_admm(np.zeros(B, np.int32), fx["roles"], fx["params"])
+    _check(fx, res.u, res.x, res.region, res.cost, res.status, res.x_front, res.x_back)
+    assert np.array_equal(res.gear, fx["exp_gear"])
+
+
+@pytest.mark.gpu
+def test_admm_gear_solve_mpc_surface(gpu_available):
+    """LocalMpcGear.solve_mpc returns [u_g0; gear0] and info["u"] = vstack(u_g, gears)
+    (MpcGear.solve_mpc, mpcs/mpc_gear.py:116-135), on the fixture's second vehicle."""
+    fx = load("admm_gear_local_N5.npz")
+    m = _gear_mpc(1, 4)
+    k = 1  # seed 0, vehicle 1 (role of a middle vehicle)
+    prm = fx["params"][k]
+    E = 2 * 6
+    m.set_front_vars(prm[2:2 + E].reshape(2, 6), prm[2 + E:2 + 2 * E].reshape(2, 6))
+    m.set_back_vars(prm[2 + 2 * E:2 + 3 * E].reshape(2, 6), prm[2 + 3 * E:2 + 4 * E].reshape(2, 6))
+    u0, info = m.solve_mpc(prm[:2].reshape(2, 1))
+    assert u0.shape == (2, 1) and info["u"].shape == (2, 5)
+    assert np.abs(info["u"][0] - fx["exp_u"][k]).max() <= 1e-6
+    assert list(info["u"][1].astype(int)) == list(fx["exp_gear"][k])
+    assert abs(info["cost"] - fx["exp_cost"][k]) <= 1e-9 * abs(fx["exp_cost"][k])
+
+
+@pytest.mark.gpu
+def test_admm_gear_coordinator_steps_match_oracle(gpu_available):
+    """Closed-loop naive-ADMM steps on the gear model: device coordinator vs oracle coordinator
+    (3 steps x 4 iterations, n = 4, N = 5): controls, trajectories and gears of the last iteration."""
+    import torch
+
+    from hvp.admm import AdmmEngine
+    from instances import leader_window
+
+    fx = load("admm_gear_steps_n4_N5.npz")
+    n, N, iters = int(fx["n"]), int(fx["N"]), int(fx["iters"])
+    mpcs = [_gear_mpc(i, n) for i in range(n)]
+    eng = AdmmEngine(mpcs[0].problem, [mpcs[0].table], np.zeros(n, np.int32), [O.role_bits(i, n) for i in range(n)],
+                     n, 1)
+    for t in range(len(fx["states"])):
+        eng.set_leader(leader_window(N, t))
+        o = eng.step(fx["states"][t][None], iters)
+        torch.cuda.synchronize()
+        assert (o["status"] == 0).all()
+        assert np.abs(o["u"].cpu().numpy() - fx["exp_u"][t][-1]).max() <= 1e-6, t
+        assert np.abs(o["x"].cpu().numpy() - fx["exp_x"][t][-1]).max() <= 1e-4, t
+        assert np.array_equal(o["gear"].cpu().numpy(), fx["exp_gear"][t]), t
+
+
+@pytest.mark.gpu
+def test_admm_simulate_gear_model(gpu_available):
+    """simulate() with vehicle_model_type = "pwa_friction" (fleet_naive_admm.py:630-637): the
+    coordinator returns [u_g of every vehicle; gears of every vehicle] (:557-566)."""
+    from hvp.admm import LocalMpcGear, simulate
+    from hvp.params import Sim
+
+    class ShortGear(Sim):
+        n = 3
+        N = 5
+        ep_len = 4
+        vehicle_model_type = "pwa_friction"
+
+    X, U, R, agent, env = simulate(ShortGear(), admm_iters=3, seed=3)
+    assert all(isinstance(a.mpc, LocalMpcGear) for a in agent.agents)
+    U = np.asarray(U)
+    assert X.shape == (5, 6) and U.shape == (4, 6)
+    assert set(np.unique(U[:, 3:])) <= {1.0, 2.0, 3.0, 4.0, 5.0, 6.0}
+    assert np.isfinite(np.asarray(R)).all()

@@ -172,6 +172,35 @@ def test_full_size_batch_properties(gpu_available):
         assert np.abs(u[j] - r.u).max() <= 1e-6
 
 
+def test_every_answer_kkt_certified_at_bench_size(gpu_available):
+    """configs[1] at bench size (163,840 local MIQPs): EVERY answer's region sequence re-solved
+    by the oracle's fixed-sequence QP (full (x, u, s) space, Mehrotra IPM, KKT-certified to
+    1e-9): the certified optimum of that sequence equals the GPU's cost (1e-9 relative + 1e-7
+    absolute, the IPM objective's own accuracy) and u (1e-6, the north-star KKT bar).  With test_branch_and_bound_equals_enumeration_at_bench_size
+    (the chosen sequence is the enumeration's) this checks the whole batch, not a sample."""
+    import os
+
+    import torch
+
+    import bench
+
+    n, S = 10, 16384
+    params, roles = bench.make_inputs(range(S), n, N)
+    dev = torch.device("cuda", 0)
+    tp, tr = torch.from_numpy(params).to(dev), torch.from_numpy(roles).to(dev)
+    ts = torch.zeros(len(roles), dtype=torch.int32, device=dev)
+    a = _solver([_gear_system()]).solve_device(ts, tr, tp)
+    torch.cuda.synchronize()
+    assert (a["status"] == 0).all()
+    reg, cost, u = a["region"].cpu().numpy(), a["cost"].cpu().numpy(), a["u"].cpu().numpy()
+    obj, cert, uo = O.certify_batch([O.gear_pwa_system(800.0)], O.Cfg(), N, np.zeros(len(roles), np.int32), roles,
+                                    params, reg, nthreads=min(16, os.cpu_count() or 1))
+    assert cert.all(), int((~cert).sum())
+    err = np.abs(cost - obj) - (1e-9 * np.abs(obj) + 1e-7)
+    assert err.max() <= 0, (int(err.argmax()), cost[err.argmax()], obj[err.argmax()])
+    assert np.abs(u - uo).max() <= 1e-6, int(np.abs(u - uo).max(axis=1).argmax())
+
+
 def test_branch_and_bound_equals_enumeration_at_bench_size(gpu_available):
     """configs[1] at bench size through both searches: the same sequence for every one of the
     163,840 local MIQPs, costs and trajectories equal to rounding."""

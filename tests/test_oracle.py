@@ -43,6 +43,20 @@ def _instance(seed=0, n=4, N=5, i=1):
     return params[i], int(roles[i])
 
 
+def test_certify_batch_reproduces_golden():
+    """oracle_certify_batch (the full-size KKT check of the GPU answers) on the golden sequences:
+    certified, the fixture's cost and u."""
+    fx = load("decent_n10_N5.npz")
+    systems = [O.gear_pwa_system(float(m)) for m in fx["masses"]]
+    obj, cert, u = O.certify_batch(systems, O.Cfg(), int(fx["N"]), fx["sys"], fx["roles"], fx["params"],
+                                   fx["exp_region"], nthreads=4)
+    ok = fx["exp_status"] == 0
+    assert cert[ok].all()
+    # the IPM objective of a fresh solve agrees to ~1e-8 absolute (costs 1 .. 1e5)
+    assert np.all(np.abs(obj[ok] - fx["exp_cost"][ok]) <= 1e-9 * np.abs(fx["exp_cost"][ok]) + 1e-7)
+    assert np.abs(u[ok] - fx["exp_u"][ok]).max() <= 1e-6
+
+
 @pytest.mark.parametrize("seed,veh", [(0, 0), (1, 1), (2, 3), (5, 2)])
 def test_fixed_sequence_qp_vs_scipy(seed, veh):
     from scipy.optimize import LinearConstraint, minimize
