@@ -563,7 +563,7 @@ def bench_cent(args, world: int, rank: int, local: int, dist) -> None:
         tt = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
-    # kernel time: HIP events the library records around k_cent_bnb on the solve stream
+    # kernel time: HIP events the library records around the search kernels on the solve stream
     run()
     st = solver.stats()
     kernel_ms = st.last_ms
@@ -581,7 +581,7 @@ def bench_cent(args, world: int, rank: int, local: int, dist) -> None:
         "config": {"workload": f"fleet_cent_mld n={n} N={N} pwa_gear (MpcMldCent)", "n_vehicles": n, "horizon": N,
                    "platoons_per_gpu": S, "max_nodes": args.max_nodes, "parallelism": f"seeds-sharded x{world}"},
         "value_optimal_only": n_opt * world * args.steps / dt,
-        "roofline": qp_roofline(kernel_ms, [("k_cent_bnb", 1)], notional, f"cent_n{n}_N{N}"),
+        "roofline": qp_roofline(kernel_ms, cent_kernels(f"cent_n{n}_N{N}"), notional, f"cent_n{n}_N{N}"),
         "qps_per_step": qps, "qp_iters_per_qp": float(iters.sum()) / max(qps, 1),
         "nodes_per_platoon": {"p50": float(q[0]), "p90": float(q[1]), "p99": float(q[2]), "max": float(q[3])},
         "status_counts": {"optimal": int((status == 0).sum()), "infeasible": int((status == 1).sum()),
@@ -593,6 +593,19 @@ def bench_cent(args, world: int, rank: int, local: int, dist) -> None:
         print(json.dumps(result), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def cent_kernels(tag: str) -> list:
+    """The search kernels of one centralised solve: k_cent_bnb once, then (split search, heavy
+    platoons) the rounds of k_cent_tasks and k_cent_final.  The number of task rounds per solve
+    is read from the same profile (launches of k_cent_tasks per launch of k_cent_bnb; every solve
+    of the profiled run has the same inputs, so the same rounds)."""
+    out = [("k_cent_bnb", 1)]
+    d_bnb, _ = profiled("k_cent_bnb", tag)
+    d_t, _ = profiled("k_cent_tasks", tag)
+    if d_bnb and d_t and d_bnb.get("calls"):
+        out += [("k_cent_tasks", d_t["calls"] / d_bnb["calls"]), ("k_cent_final", 1)]
+    return out
 
 
 def cpu_baseline_cent(n: int, N: int, budget_s: float, qps_per_platoon: float):
