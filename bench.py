@@ -198,7 +198,8 @@ def bench_admm(args, world: int, rank: int, local: int, dist) -> None:
     states = np.stack([initial_platoon_state(n, derive_env_seed(int(s))).reshape(-1).astype(np.float64)
                        for s in seeds])
     roles = [tables.role_bits(i == 0, i == n - 1, i == 0) for i in range(n)] * S
-    eng = AdmmEngine(admm_problem(N, 0.5), [system], np.zeros(n * S, np.int32), roles, n, S, device=local)
+    eng = AdmmEngine(admm_problem(N, 0.5), [system], np.zeros(n * S, np.int32), roles, n, S, device=local,
+                     warm_incumbent=not args.no_warm_incumbent)
     dev = eng.dev
     T = args.warmup + args.steps + 1
     wins, lead = leader_windows(T, N, S, dev)
@@ -259,7 +260,8 @@ def bench_admm(args, world: int, rank: int, local: int, dist) -> None:
                 "on the device (ADMM control + plant step), y and the warm starts carried across steps",
         "config": {"workload": f"fleet_naive_admm n={n} N={N} pwa_gear closed loop (configs[2])", "n_vehicles": n,
                    "horizon": N, "admm_iters": iters, "rho": 0.5, "platoons_per_gpu": S,
-                   "local_miqps_per_step": iters * n * S * world, "parallelism": f"seeds-sharded x{world}"},
+                   "local_miqps_per_step": iters * n * S * world, "warm_incumbent": not args.no_warm_incumbent,
+                   "parallelism": f"seeds-sharded x{world}"},
         "roofline": qp_roofline(acc["qp_ms"], qk, notional, f"admm_n{n}_N{N}"),
         "qps_per_step": acc["qps"], "qp_iters_per_qp": acc["it"] / max(acc["qps"], 1),
         "not_optimal_total": int(notopt.item()), "plant_failures_total": int(bad.item()),
@@ -657,6 +659,8 @@ def main() -> None:
                     help="decent: every step = neighbour predictions + local MIQPs + plant step, all on the device")
     ap.add_argument("--admm-iters", type=int, default=None, help="default 20 (admm) / 100 (gadmm)")
     ap.add_argument("--max-rounds", type=int, default=10, help="gadmm: switching rounds cap")
+    ap.add_argument("--no-warm-incumbent", action="store_true",
+                    help="admm: do not try the previous iteration's sequences as incumbents (A/B)")
     ap.add_argument("--gadmm-layout", choices=["replicas", "vehicles"], default="replicas")
     args = ap.parse_args()
 

@@ -57,6 +57,8 @@ struct Workspace {
     int32_t* inst_lvl = nullptr;                 // [max_batch] children of the instance at this level
     double* iq = nullptr;                        // [fields][max_batch] sigma-independent QP part per
                                                  // instance (decentralised branch and bound, N <= 8)
+    const int8_t* hint = nullptr;                // [B][N] regions of a previous solve of the same
+                                                 // instances (hvp_set_region_hint; ADMM form only)
 };
 
 
@@ -89,4 +91,5 @@ struct hvp_handle {
     hvp::Consts* d_consts = nullptr;  // device copy of C (the centralised kernel reads it by pointer)
     size_t cent_split_bytes = 0;      // split-search workspace of the centralised path (hvp_cent.hip)
     char* cent_split = nullptr;
+    const int8_t* region_hint = nullptr;  // hvp_set_region_hint (copied into ws.hint per solve)
 };

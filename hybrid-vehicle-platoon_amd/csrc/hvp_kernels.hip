@@ -385,6 +385,12 @@ int hvp_solve_admm_batch(hvp_handle* h, int B, const int32_t* sys, const int32_t
                       iters_out, stream, xf_out, xb_out);
 }
 
+int hvp_set_region_hint(hvp_handle* h, const int8_t* region_hint) {
+    if (!h) return fail(HVP_E_ARG, "hvp_set_region_hint: null handle");
+    h->region_hint = region_hint;
+    return 0;
+}
+
 static int solve_impl(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, const double* params,
                       double* u_out, double* x_out, int8_t* region_out, int8_t* gear_out, double* cost_out,
                       int32_t* status_out, int32_t* nodes_out, int32_t* iters_out, void* stream, double* xf_out,
@@ -402,6 +408,7 @@ static int solve_impl(hvp_handle* h, int B, const int32_t* sys, const int32_t* r
     }
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t st = (hipStream_t)stream;
+    h->ws.hint = h->prob.formulation == HVP_FORM_ADMM ? h->region_hint : nullptr;
     if (h->bnb) {
         switch (h->prob.N) {
 #define HVP_CASE(n) \

@@ -291,6 +291,28 @@ __device__ inline int bnb_qp(hvp::LaneQp<N, LdsMem<N, BS>>& q, const hvp_system&
     return st == hvp::GI_OK ? it : -1 - it;
 }
 
+// The region sequence of hvp_set_region_hint for instance i as a leaf code, if every step is a
+// region of the table reachable from the previous step's interval (a stale or uninitialised hint
+// is simply not used).  Its leaf QP only tightens the initial incumbent: the prune margin
+// (1e-7 relative) is wider than the tie window (1e-9), so every leaf that can win is still
+// reached by the search and the answer does not depend on the hint.
+template <int N>
+__device__ inline bool hint_code(const Workspace& ws, int i, const hvp_system& S, const hvp::Consts& C, double v0,
+                                 uint64_t* code_out) {
+    double lo = v0, hi = v0;
+    uint64_t code = 0;
+    for (int k = 0; k < N; ++k) {
+        const int r = ws.hint[(size_t)i * N + k];
+        double nlo, nhi;
+        if (r < 0 || r >= S.n_regions || !hvp::bnb_child(S, C, k, lo, hi, r, &nlo, &nhi)) return false;
+        code = hvp::code_with(code, k, r);
+        lo = nlo;
+        hi = nhi;
+    }
+    *code_out = code;
+    return true;
+}
+
 template <int N, bool ADMM>
 __global__ __launch_bounds__(kBnbBlock<N>) HVP_LANE_OCC void k_bnb_root(int B, const hvp_system* __restrict__ systems,
                                                            const int32_t* __restrict__ sys,
@@ -334,6 +356,16 @@ __global__ __launch_bounds__(kBnbBlock<N>) HVP_LANE_OCC void k_bnb_root(int B, c
                 ++nodes;
                 iters += it >= 0 ? it : -1 - it;
                 if (it >= 0) inc = c1;
+            }
+            if constexpr (ADMM) {  // the previous ADMM iteration's sequence as a second incumbent
+                uint64_t hc;
+                if (ws.hint && hint_code<N>(ws, i, S, C, v0, &hc)) {
+                    double c2;
+                    it = bnb_qp<N, BS, ADMM>(q, S, C, rl, prm, hc, N, 0.0, -1.0, c2);
+                    ++nodes;
+                    iters += it >= 0 ? it : -1 - it;
+                    if (it >= 0 && !(c2 >= inc)) inc = c2;
+                }
             }
         }
     }
@@ -399,6 +431,24 @@ __global__ __launch_bounds__(kCoopBlock) void k_bnb_root_coop(int B, const hvp_s
                 ++nodes;
                 iters += it;
                 if (st == hvp::GI_OK) inc = c1;
+            }
+            if (ws.hint && C.form == HVP_FORM_ADMM) {  // see hint_code
+                unsigned long long hc = 0;
+                int hok = 0;
+                if (t == 0) {
+                    uint64_t c64;
+                    hok = hint_code<N>(ws, i, S, C, v0, &c64) ? 1 : 0;
+                    hc = c64;
+                }
+                hok = hvp::coop::bcast(hok, 0);
+                hc = hvp::coop::bcast(hc, 0);
+                if (hok) {
+                    double c2 = 0.0;
+                    st = hvp::coop::solve_qp<N>(L, lds[g], S, C, rl, prm, hc, N, kGiMaxIter<N>, it, &c2);
+                    ++nodes;
+                    iters += it;
+                    if (st == hvp::GI_OK && !(c2 >= inc)) inc = c2;
+                }
             }
         }
     }

@@ -241,6 +241,14 @@ class BatchSolver:
         return {k: v.cpu().numpy() for k, v in out.items()}
 
     # -------------------------------------------------------------- ADMM formulation
+    def set_region_hint(self, region) -> None:
+        """hvp_set_region_hint: a (B, N) int8 device tensor of region sequences (e.g. the "region"
+        output the previous ADMM iteration wrote) that later ADMM solves try as a second initial
+        incumbent; None clears it.  Only pruning changes, never the answer."""
+        self._hint = region
+        rc = self._lib.hvp_set_region_hint(self._h, ctypes.c_void_p(region.data_ptr() if region is not None else 0))
+        _abi.check(rc, "hvp_set_region_hint")
+
     def solve_admm_device(self, sys_idx, roles, params, out: dict, stream=None, retry_overflow: bool = False) -> dict:
         """hvp_solve_admm_batch on device tensors; ``out`` also needs "x_front", "x_back".
         ``retry_overflow`` as in :meth:`solve_device`."""
@@ -254,8 +262,13 @@ class BatchSolver:
             if attempt:
                 self.reserve(int(roles.shape[0]), 4 * self.stats().capacity)
             sub = {k: torch.empty_like(v[over]) for k, v in out.items()}
+            hint = getattr(self, "_hint", None)
+            if hint is not None:  # the hint rows are indexed by the full batch: not for the subset
+                self.set_region_hint(None)
             self._launch_admm(sys_idx[over].contiguous(), roles[over].contiguous(), params[over].contiguous(), sub,
                               stream)
+            if hint is not None:
+                self.set_region_hint(hint)
             for k, v in sub.items():
                 out[k][over] = v
         return out

@@ -188,6 +188,14 @@ int hvp_solve_admm_batch(hvp_handle* h, int B, const int32_t* sys, const int32_t
                          int8_t* gear_out, double* cost_out, int32_t* status_out, int32_t* nodes_out,
                          int32_t* iters_out, double* xf_out, double* xb_out, void* stream);
 
+/* Region sequence hint for the HVP_FORM_ADMM solves of this handle: device pointer
+ * region_hint[B][N] (int8, e.g. the region_out of the previous ADMM iteration; NULL clears it),
+ * read at the start of every later hvp_solve_admm_batch.  Instance i's hinted sequence, when it is
+ * velocity-feasible, is solved as a second initial incumbent next to the greedy dive; it only
+ * tightens pruning (prune margin 1e-7 > tie window 1e-9), the answer does not depend on it, and
+ * nodes_out counts its QP.  The pointer must stay valid while solves may read it. */
+int hvp_set_region_hint(hvp_handle* h, const int8_t* region_hint);
+
 /* ADMM z- and y-update of ADMMCoordinator.get_control (fleet_naive_admm.py:421-468) for P
  * platoons of n vehicles (instance p*n + i), device pointers, async on stream:
  *   z_i = mean of x_i, vehicle (i+1)'s front copy and vehicle (i-1)'s back copy;

@@ -282,3 +282,37 @@ def test_admm_simulate_gear_model(gpu_available):
     assert X.shape == (5, 6) and U.shape == (4, 6)
     assert set(np.unique(U[:, 3:])) <= {1.0, 2.0, 3.0, 4.0, 5.0, 6.0}
     assert np.isfinite(np.asarray(R)).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,P", [(5, 256), (10, 128)])
+def test_warm_incumbent_does_not_change_answers(gpu_available, N, P):
+    """hvp_set_region_hint (AdmmEngine warm_incumbent): the previous iteration's sequences tried as
+    incumbents change how much of the tree is pruned, never the answer -- two closed-loop steps
+    with and without it give bit-identical controls, trajectories, copies, regions and costs."""
+    import torch
+
+    from hvp.admm import AdmmEngine, admm_problem
+
+    n = 10
+    states = np.stack([O.env_initial_state(n, s).astype(float) for s in range(P)])
+    roles = [O.role_bits(i, n) for i in range(n)] * P
+    lead = np.stack([3000.0 + 20.0 * np.arange(N + 1), np.full(N + 1, 20.0)])
+    res = []
+    for warm in (True, False):
+        eng = AdmmEngine(admm_problem(N, 0.5), [_system()], np.zeros(P * n, np.int32), roles, n, P,
+                         warm_incumbent=warm)
+        eng.set_leader(lead)
+        outs = []
+        for t in range(2):
+            o = eng.step(states, 6)
+            torch.cuda.synchronize()
+            outs.append({k: v.cpu().numpy().copy() for k, v in o.items()})
+        res.append(outs)
+    for a, b in zip(*res):
+        assert (a["status"] == 0).all()
+        for k in a:
+            if k in ("nodes", "iters"):
+                continue
+            assert np.array_equal(a[k], b[k]), k
+    assert sum(o["nodes"].sum() for o in res[0]) < sum(o["nodes"].sum() for o in res[1])
