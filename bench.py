@@ -199,7 +199,7 @@ def bench_admm(args, world: int, rank: int, local: int, dist) -> None:
                        for s in seeds])
     roles = [tables.role_bits(i == 0, i == n - 1, i == 0) for i in range(n)] * S
     eng = AdmmEngine(admm_problem(N, 0.5), [system], np.zeros(n * S, np.int32), roles, n, S, device=local,
-                     warm_incumbent=not args.no_warm_incumbent)
+                     warm_incumbent=False if args.no_warm_incumbent else None)
     dev = eng.dev
     T = args.warmup + args.steps + 1
     wins, lead = leader_windows(T, N, S, dev)
@@ -260,7 +260,7 @@ def bench_admm(args, world: int, rank: int, local: int, dist) -> None:
                 "on the device (ADMM control + plant step), y and the warm starts carried across steps",
         "config": {"workload": f"fleet_naive_admm n={n} N={N} pwa_gear closed loop (configs[2])", "n_vehicles": n,
                    "horizon": N, "admm_iters": iters, "rho": 0.5, "platoons_per_gpu": S,
-                   "local_miqps_per_step": iters * n * S * world, "warm_incumbent": not args.no_warm_incumbent,
+                   "local_miqps_per_step": iters * n * S * world, "warm_incumbent": N > 8 and not args.no_warm_incumbent,
                    "parallelism": f"seeds-sharded x{world}"},
         "roofline": qp_roofline(acc["qp_ms"], qk, notional, f"admm_n{n}_N{N}"),
         "qps_per_step": acc["qps"], "qp_iters_per_qp": acc["it"] / max(acc["qps"], 1),

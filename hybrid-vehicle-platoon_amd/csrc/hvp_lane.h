@@ -350,7 +350,8 @@ __global__ __launch_bounds__(kBnbBlock<N>) HVP_LANE_OCC void k_bnb_root(int B, c
 #pragma unroll
             for (int k = 0; k < N; ++k) ystar[k] = q.y[k];
             uint64_t code;
-            if (hvp::bnb_dive<N>(S, C, v0, ystar, &code)) {
+            const bool dived = hvp::bnb_dive<N>(S, C, v0, ystar, &code);
+            if (dived) {
                 double c1;
                 it = bnb_qp<N, BS, ADMM>(q, S, C, rl, prm, code, N, 0.0, -1.0, c1);
                 ++nodes;
@@ -359,7 +360,7 @@ __global__ __launch_bounds__(kBnbBlock<N>) HVP_LANE_OCC void k_bnb_root(int B, c
             }
             if constexpr (ADMM) {  // the previous ADMM iteration's sequence as a second incumbent
                 uint64_t hc;
-                if (ws.hint && hint_code<N>(ws, i, S, C, v0, &hc)) {
+                if (ws.hint && hint_code<N>(ws, i, S, C, v0, &hc) && !(dived && hc == code)) {
                     double c2;
                     it = bnb_qp<N, BS, ADMM>(q, S, C, rl, prm, hc, N, 0.0, -1.0, c2);
                     ++nodes;
@@ -437,7 +438,7 @@ __global__ __launch_bounds__(kCoopBlock) void k_bnb_root_coop(int B, const hvp_s
                 int hok = 0;
                 if (t == 0) {
                     uint64_t c64;
-                    hok = hint_code<N>(ws, i, S, C, v0, &c64) ? 1 : 0;
+                    hok = hint_code<N>(ws, i, S, C, v0, &c64) && (!dive_ok || c64 != code) ? 1 : 0;
                     hc = c64;
                 }
                 hok = hvp::coop::bcast(hok, 0);

@@ -169,7 +169,7 @@ class AdmmEngine:
     """ADMMCoordinator.get_control for P platoons of n vehicles, entirely on the device."""
 
     def __init__(self, problem: _abi.HvpProblem, systems: list, sys_idx, roles, n: int, P: int, device: int = 0,
-                 leader_index: int = 0, warm_incumbent: bool = True) -> None:
+                 leader_index: int = 0, warm_incumbent: bool | None = None) -> None:
         import torch
 
         self.N = N = int(problem.N)
@@ -190,8 +190,9 @@ class AdmmEngine:
         self.out["x_front"], self.out["x_back"] = z(B, 2, N + 1), z(B, 2, N + 1)
         # every ADMM solve tries the sequence the previous iteration chose (its region output) as
         # a second initial incumbent; -1 = no previous solution yet
+        # (default: from N > 8, where the trees are deep enough for the extra leaf QP to pay off)
         self.out["region"].fill_(-1)
-        if warm_incumbent:
+        if warm_incumbent if warm_incumbent is not None else N > 8:
             self.solver.set_region_hint(self.out["region"])
         self.z = z(B, 2, N + 1)
         self.x_prev = None  # last step's final local trajectories (warm start)

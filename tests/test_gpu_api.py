@@ -61,7 +61,9 @@ def test_closed_loop_simulate(gpu_available):
         ep_len = 12
 
     X, U, R, agent, env = simulate(Short(), seed=1)
-    assert X.shape == (13, 8) and U.shape == (12, 4) and R.shape == (12,)
+    # the stage cost is a (1, 1) array as PlatoonEnv.get_stage_cost computes it (env.py:126-212;
+    # results_analysis/perf_n.py reads sum(R)[0, 0])
+    assert X.shape == (13, 8) and U.shape == (12, 4) and np.asarray(R).shape == (12, 1, 1)
     assert np.all(np.abs(U) <= 1 + 1e-9)
     assert (agent.solve_times[:12] > 0).all() and (agent.node_counts[:12] >= 1).all()
     # the first action is the batched solution of the t = 0 problems, identical to the oracle
