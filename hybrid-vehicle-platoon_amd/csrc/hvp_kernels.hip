@@ -408,7 +408,11 @@ static int solve_impl(hvp_handle* h, int B, const int32_t* sys, const int32_t* r
     }
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t st = (hipStream_t)stream;
-    h->ws.hint = h->prob.formulation == HVP_FORM_ADMM ? h->region_hint : nullptr;
+    // the region hint: naive-ADMM solves, and decentralised solves on the 16-lane path (N > 8)
+    h->ws.hint = h->prob.formulation == HVP_FORM_ADMM ||
+                         (h->prob.formulation == HVP_FORM_DECENT && h->prob.N > HVP_MAX_N_ENUM)
+                     ? h->region_hint
+                     : nullptr;
     if (h->bnb) {
         switch (h->prob.N) {
 #define HVP_CASE(n) \

@@ -433,7 +433,7 @@ __global__ __launch_bounds__(kCoopBlock) void k_bnb_root_coop(int B, const hvp_s
                 iters += it;
                 if (st == hvp::GI_OK) inc = c1;
             }
-            if (ws.hint && C.form == HVP_FORM_ADMM) {  // see hint_code
+            if (ws.hint) {  // see hint_code (set for the ADMM and decentralised forms only)
                 unsigned long long hc = 0;
                 int hok = 0;
                 if (t == 0) {

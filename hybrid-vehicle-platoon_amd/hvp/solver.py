@@ -148,8 +148,13 @@ class BatchSolver:
                 break
             if attempt:
                 self.reserve(int(roles.shape[0]), 4 * self.stats().capacity)
+            hint = getattr(self, "_hint", None)
+            if hint is not None:  # the hint rows are indexed by the full batch: not for the subset
+                self.set_region_hint(None)
             sub = self._launch(sys_idx[over].contiguous(), roles[over].contiguous(), params[over].contiguous(),
                                None, stream)
+            if hint is not None:
+                self.set_region_hint(hint)
             for k, v in sub.items():
                 out[k][over] = v
         return out
@@ -242,9 +247,10 @@ class BatchSolver:
 
     # -------------------------------------------------------------- ADMM formulation
     def set_region_hint(self, region) -> None:
-        """hvp_set_region_hint: a (B, N) int8 device tensor of region sequences (e.g. the "region"
-        output the previous ADMM iteration wrote) that later ADMM solves try as a second initial
-        incumbent; None clears it.  Only pruning changes, never the answer."""
+        """hvp_set_region_hint: a (B, N) int8 device tensor of region sequences (the "region" output
+        of the previous ADMM iteration, or the previous time step's sequences shifted by one step)
+        that later solves try as a second initial incumbent -- naive-ADMM solves and decentralised
+        solves with N > 8; None clears it.  Only pruning changes, never the answer."""
         self._hint = region
         rc = self._lib.hvp_set_region_hint(self._h, ctypes.c_void_p(region.data_ptr() if region is not None else 0))
         _abi.check(rc, "hvp_set_region_hint")

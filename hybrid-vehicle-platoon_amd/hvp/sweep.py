@@ -44,7 +44,7 @@ def shard(points, n_seeds: int, rank: int, world: int):
 
 
 def run_point(n: int, N: int, seeds, ep_len: int = 150, device: int = 0, out_dir: str | None = None,
-              velocity_estimator: str = "none") -> dict:
+              velocity_estimator: str = "none", warm_incumbent: bool = True) -> dict:
     """Closed-loop episodes of the decentralised controller for `seeds` (one platoon each) at
     (n, N), all on the device.  Returns per-seed X (T+1, 2n), U (T, n), R (T,), violations (T,),
     node_counts (T,), and the step times; writes the reference's results files if out_dir."""
@@ -85,6 +85,11 @@ def run_point(n: int, N: int, seeds, ep_len: int = 150, device: int = 0, out_dir
     x_prev = x.clone()
     u = torch.empty((S, n), dtype=torch.float64, device=dev)
     u_prev = None
+    # the previous step's sequences shifted by one step (last region repeated) as a second initial
+    # incumbent of the next step's local searches (N > 8; pruning only, the answers do not change)
+    hint = torch.full((B, N), -1, dtype=torch.int8, device=dev)
+    if N > 8 and warm_incumbent:
+        solver.set_region_hint(hint)
     step_s = np.zeros(T)
     for t in range(T):
         t0 = time.perf_counter()
@@ -92,6 +97,8 @@ def run_point(n: int, N: int, seeds, ep_len: int = 150, device: int = 0, out_dir
         solver.decent_params_device(x, win, x_prev=x_prev, estimator=velocity_estimator, params=params, roles=roles)
         solver.solve_device(t_sys, roles, params, out, retry_overflow=N > 8)
         u.copy_(out["u"][:, 0].view(S, n))
+        hint[:, :-1] = out["region"][:, 1:]
+        hint[:, -1] = out["region"][:, -1]
         bad.add_((out["status"] != 0).sum())
         NODES[t] = out["nodes"].view(S, n).max(dim=1).values
         x_prev.copy_(x)

@@ -188,9 +188,10 @@ int hvp_solve_admm_batch(hvp_handle* h, int B, const int32_t* sys, const int32_t
                          int8_t* gear_out, double* cost_out, int32_t* status_out, int32_t* nodes_out,
                          int32_t* iters_out, double* xf_out, double* xb_out, void* stream);
 
-/* Region sequence hint for the HVP_FORM_ADMM solves of this handle: device pointer
- * region_hint[B][N] (int8, e.g. the region_out of the previous ADMM iteration; NULL clears it),
- * read at the start of every later hvp_solve_admm_batch.  Instance i's hinted sequence, when it is
+/* Region sequence hint for the HVP_FORM_ADMM solves of this handle and its HVP_FORM_DECENT
+ * solves with N > 8: device pointer region_hint[B][N] (int8, e.g. the region_out of the previous
+ * ADMM iteration, or the previous time step's sequences shifted by one step; NULL clears it),
+ * read at the start of every later solve.  Instance i's hinted sequence, when it is
  * velocity-feasible, is solved as a second initial incumbent next to the greedy dive; it only
  * tightens pruning (prune margin 1e-7 > tie window 1e-9), the answer does not depend on it, and
  * nodes_out counts its QP.  The pointer must stay valid while solves may read it. */

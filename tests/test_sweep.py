@@ -90,3 +90,15 @@ def test_sweep_point_matches_host_simulate(gpu_available, tmp_path):
         X, U, R, solve_times, node_counts, violations, leader_state = (pickle.load(f) for _ in range(7))
     assert np.isfinite(sum(R)[0, 0]) and min(solve_times)[0] > 0 and max(node_counts)[0] >= 1
     assert len(violations) == T and np.asarray(leader_state).shape[0] == 2
+
+
+@pytest.mark.gpu
+def test_sweep_warm_incumbent_keeps_the_episodes(gpu_available):
+    """N > 8: the previous step's sequences (shifted) tried as incumbents of the next step's local
+    searches change the QP counts only -- the closed-loop episodes are bit-identical."""
+    from hvp.sweep import run_point
+
+    a = run_point(5, 10, [0, 1, 2, 3], ep_len=6, warm_incumbent=True)
+    b = run_point(5, 10, [0, 1, 2, 3], ep_len=6, warm_incumbent=False)
+    for k in ("X", "U", "R", "viol"):
+        assert np.array_equal(a[k], b[k]), k
