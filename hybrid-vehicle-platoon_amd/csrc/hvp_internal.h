@@ -54,7 +54,6 @@ struct Workspace {
     int32_t* iters = nullptr;                    // [max_batch] active-set iterations
     unsigned long long* lvl = nullptr;           // [2 (HVP_MAX_N + 1)] nodes per level, then per-level
                                                  // claim counters of the refilling bound kernel
-    int32_t* inst_lvl = nullptr;                 // [max_batch] children of the instance at this level
     double* iq = nullptr;                        // [fields][max_batch] sigma-independent QP part per
                                                  // instance (decentralised branch and bound, N <= 8)
     const int8_t* hint = nullptr;                // [B][N] regions of a previous solve of the same

@@ -208,7 +208,6 @@ void free_ws(Workspace& w) {
     (void)hipFree(w.nodes);
     (void)hipFree(w.iters);
     (void)hipFree(w.lvl);
-    (void)hipFree(w.inst_lvl);
     (void)hipFree(w.iq);
     w = Workspace{};
 }
@@ -348,8 +347,7 @@ int hvp_reserve(hvp_handle* h, int max_batch, int64_t cap) {
              hipMalloc(&w.key, sizeof(unsigned long long) * max_batch) == hipSuccess &&
              hipMalloc(&w.nodes, sizeof(int32_t) * max_batch) == hipSuccess &&
              hipMalloc(&w.iters, sizeof(int32_t) * max_batch) == hipSuccess &&
-             hipMalloc(&w.lvl, sizeof(unsigned long long) * 2 * (HVP_MAX_N + 1)) == hipSuccess &&
-             hipMalloc(&w.inst_lvl, sizeof(int32_t) * max_batch) == hipSuccess;
+             hipMalloc(&w.lvl, sizeof(unsigned long long) * 2 * (HVP_MAX_N + 1)) == hipSuccess;
         // K_inst_prep's per-instance QP part: H (NT) + f (N) + hf, hb (N - 1 each)
         if (ok && N <= HVP_MAX_N_ENUM)
             ok = hipMalloc(&w.iq, sizeof(double) * (size_t)max_batch * (N * (N + 1) / 2 + 3 * N - 2)) == hipSuccess;

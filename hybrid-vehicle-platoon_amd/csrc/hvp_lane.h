@@ -517,41 +517,60 @@ __global__ __launch_bounds__(kCoopBlock) void k_bnb_bound_coop(int k, const hvp_
     }
 }
 
-// children of the level-(k-1) nodes that survive the incumbent test
-// Every instance may hold at most `quota` nodes per level; an instance whose children do not fit
-// (its quota, or the pooled capacity) is reported HVP_OVERFLOW, never truncated silently, and
-// is re-solved alone by the caller (solve_device(retry_overflow)).  The launcher passes the
-// whole capacity as the quota: the pooled list is sized at 64-1024 x the batch per level while
-// the widest level of the batch averages a few nodes per instance, so a heavy tree (trajectories
-// riding a region boundary, naive-ADMM hinge states) simply uses the room the light ones leave
-// -- a per-instance share of capacity / B made 68 of 80 naive-ADMM solves at C3 re-run.
+// children of the level-(k-1) nodes that survive the incumbent test.
+// The level's node list is shared by the whole batch: a heavy tree (trajectories riding a region
+// boundary, naive-ADMM hinge states) uses the room the light ones leave (a per-instance share of
+// capacity / B made 68 of 80 naive-ADMM solves at C3 re-run).  An instance whose children do not
+// fit is reported HVP_OVERFLOW, never truncated silently, and re-solved alone by the caller
+// (solve_device(retry_overflow)).  One thread per parent; the slots are reserved per WAVE (an
+// inclusive scan of the children counts, one atomic by the last lane): a per-thread atomic on the
+// level counter serialised ~1e5 atomics on one address per level (0.076 ms per launch at C2).
 template <int N>
-__global__ __launch_bounds__(kBlock) void k_bnb_expand(int k, int quota, const hvp_system* __restrict__ systems,
+__global__ __launch_bounds__(kBlock) void k_bnb_expand(int k, const hvp_system* __restrict__ systems,
                                                        const int32_t* __restrict__ sys, hvp::Consts C, Workspace ws) {
     const int src = (k - 1) & 1, dst = k & 1;
     const unsigned long long np = ws.lvl[k - 1];
     const long long total = (long long)(np < (unsigned long long)ws.cap ? np : ws.cap);
-    for (long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x; p < total;
-         p += (long long)gridDim.x * blockDim.x) {
-        const int inst = ws.nd_inst[src][p];
-        if (inst < 0 || (ws.inst_flag[inst] & 2)) continue;
-        const double plb = ws.nd_lb[src][p];
-        if (hvp::bnb_pruned(plb, inc_of(ws, inst))) continue;
-        const hvp_system& S = systems[sys[inst]];
-        const double lo = ws.nd_lo[src][p], hi = ws.nd_hi[src][p];
-        const uint64_t code = ws.nd_code[src][p];
+    const int lane = threadIdx.x & 63;
+    const long long wave0 = (long long)blockIdx.x * blockDim.x + (threadIdx.x & ~63);
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long pw = wave0; pw < total; pw += stride) {  // wave-uniform loop
+        const long long p = pw + lane;
+        int inst = -1;
         unsigned mask = 0;
-        for (int r = 0; r < S.n_regions; ++r) {
-            double a, b;
-            if (hvp::bnb_child(S, C, k - 1, lo, hi, r, &a, &b)) mask |= 1u << r;
+        double lo = 0.0, hi = 0.0, plb = 0.0;
+        uint64_t code = 0;
+        if (p < total) {
+            inst = ws.nd_inst[src][p];
+            if (inst >= 0 && !(ws.inst_flag[inst] & 2)) {
+                plb = ws.nd_lb[src][p];
+                if (!hvp::bnb_pruned(plb, inc_of(ws, inst))) {
+                    const hvp_system& S = systems[sys[inst]];
+                    lo = ws.nd_lo[src][p];
+                    hi = ws.nd_hi[src][p];
+                    code = ws.nd_code[src][p];
+                    for (int r = 0; r < S.n_regions; ++r) {
+                        double a, b;
+                        if (hvp::bnb_child(S, C, k - 1, lo, hi, r, &a, &b)) mask |= 1u << r;
+                    }
+                }
+            }
         }
         const int nc = __popc(mask);
-        if (!nc) continue;
-        if (atomicAdd(&ws.inst_lvl[inst], nc) + nc > quota) {
-            atomicOr(&ws.inst_flag[inst], 2);
-            continue;
+        int incl = nc;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int v = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += v;
         }
-        const unsigned long long off = atomicAdd(&ws.lvl[k], (unsigned long long)nc);
+        const int wave_total = __shfl(incl, 63, 64);
+        if (!wave_total) continue;
+        unsigned long long base = 0;
+        if (lane == 63) base = atomicAdd(&ws.lvl[k], (unsigned long long)wave_total);
+        base = ((unsigned long long)(unsigned)__shfl((int)(base >> 32), 63, 64) << 32) |
+               (unsigned)__shfl((int)(base & 0xffffffffu), 63, 64);
+        if (!nc) continue;
+        const unsigned long long off = base + (unsigned long long)(incl - nc);
         if (off + nc > (unsigned long long)ws.cap) {
             atomicOr(&ws.inst_flag[inst], 2);  // overflow: reported, never truncated silently
             // the slots of this reservation below the capacity are swept by the next kernels
@@ -559,6 +578,7 @@ __global__ __launch_bounds__(kBlock) void k_bnb_expand(int k, int quota, const h
                 ws.nd_inst[dst][t] = -1;
             continue;
         }
+        const hvp_system& S = systems[sys[inst]];
         int j = 0;
         for (int r = 0; r < S.n_regions; ++r) {
             if (!((mask >> r) & 1u)) continue;
@@ -1316,10 +1336,8 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
     HIP_TRY(hipEventRecord(h->evb[1], st));
     const int g_small = (int)std::min<long long>(grid_for(h->ws.cap), (long long)h->n_cu * 8);
     const int g_qp = (int)std::min<long long>((h->ws.cap + BS - 1) / BS, (long long)h->n_cu * 8 * (kBlock / BS));
-    const int quota = (int)std::min<int64_t>(h->ws.cap, 1 << 30);
     for (int k = 1; k <= N; ++k) {
-        HIP_TRY(hipMemsetAsync(ws.inst_lvl, 0, sizeof(int32_t) * B, st));
-        hipLaunchKernelGGL(k_bnb_expand<N>, dim3(g_small), dim3(kBlock), 0, st, k, quota, h->d_sys, sys, h->C, ws);
+        hipLaunchKernelGGL(k_bnb_expand<N>, dim3(g_small), dim3(kBlock), 0, st, k, h->d_sys, sys, h->C, ws);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(h->evb[2 * k], st));
         if constexpr (kCoop<N>) {
