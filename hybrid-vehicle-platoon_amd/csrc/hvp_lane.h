@@ -291,6 +291,60 @@ __device__ inline int bnb_qp(hvp::LaneQp<N, LdsMem<N, BS>>& q, const hvp_system&
     return st == hvp::GI_OK ? it : -1 - it;
 }
 
+// regions r the node's next step (`step`, from the interval [lo, hi] of v_step) can take
+__device__ inline unsigned bnb_children(const hvp_system& S, const hvp::Consts& C, int step, double lo, double hi) {
+    unsigned mask = 0;
+    for (int r = 0; r < S.n_regions; ++r) {
+        double a, b;
+        if (hvp::bnb_child(S, C, step, lo, hi, r, &a, &b)) mask |= 1u << r;
+    }
+    return mask;
+}
+
+// writes the children (regions in mask) of a level-(lv-1) node into level lv's list at slots
+// off.. (reserved by the caller); past the capacity the instance is flagged HVP_OVERFLOW
+__device__ inline void bnb_put_children(Workspace& ws, int lv, unsigned long long off, unsigned mask, int inst,
+                                        const hvp_system& S, const hvp::Consts& C, uint64_t code, double lo,
+                                        double hi, double plb) {
+    const int nc = __popc(mask), d = lv & 1;
+    if (off + nc > (unsigned long long)ws.cap) {
+        atomicOr(&ws.inst_flag[inst], 2);  // overflow: reported, never truncated silently
+        // the slots of this reservation below the capacity are swept by the next kernels
+        for (unsigned long long t = off; t < (unsigned long long)ws.cap && t < off + nc; ++t) ws.nd_inst[d][t] = -1;
+        return;
+    }
+    int j = 0;
+    for (int r = 0; r < S.n_regions; ++r) {
+        if (!((mask >> r) & 1u)) continue;
+        double a, b;
+        hvp::bnb_child(S, C, lv - 1, lo, hi, r, &a, &b);
+        ws.nd_inst[d][off + j] = inst;
+        ws.nd_code[d][off + j] = hvp::code_with(code, lv - 1, r);
+        ws.nd_lo[d][off + j] = a;
+        ws.nd_hi[d][off + j] = b;
+        ws.nd_lb[d][off + j] = plb;  // inherited: kept by a leaf whose QP fails
+        ++j;
+    }
+}
+
+// wave-level reservation of nc slots per lane in level lv's list (an inclusive scan, one atomic
+// by the last lane); every lane of the wave must call it.  Returns the lane's first slot.
+__device__ inline unsigned long long wave_reserve(Workspace& ws, int lv, int nc, int lane, bool& any) {
+    int incl = nc;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int v = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += v;
+    }
+    const int wave_total = __shfl(incl, 63, 64);
+    any = wave_total != 0;
+    unsigned long long base = 0;
+    if (lane == 63 && wave_total) base = atomicAdd(&ws.lvl[lv], (unsigned long long)wave_total);
+    base = ((unsigned long long)(unsigned)__shfl((int)(base >> 32), 63, 64) << 32) |
+           (unsigned)__shfl((int)(base & 0xffffffffu), 63, 64);
+    return base + (unsigned long long)(incl - nc);
+}
+
 // The region sequence of hvp_set_region_hint for instance i as a leaf code, if every step is a
 // region of the table reachable from the previous step's interval (a stale or uninitialised hint
 // is simply not used).  Its leaf QP only tightens the initial incumbent: the prune margin
@@ -376,6 +430,17 @@ __global__ __launch_bounds__(kBnbBlock<N>) HVP_LANE_OCC void k_bnb_root(int B, c
     ws.iters[i] = iters;
     atomicAdd(&ws.counter[3], (unsigned long long)nodes);
     atomicAdd(&ws.counter[1], (unsigned long long)iters);
+    if constexpr (!ADMM) {
+        // the level-1 nodes (k_bnb_expand's work, fused): the incumbent only changes at the
+        // leaves (level N), so the pruning test here sees the value the expand kernel would
+        if (ok && !hvp::bnb_pruned(lb, inc)) {
+            const unsigned mask = bnb_children(S, C, 0, v0, v0);
+            if (mask) {
+                const unsigned long long off = atomicAdd(&ws.lvl[1], (unsigned long long)__popc(mask));
+                bnb_put_children(ws, 1, off, mask, i, S, C, 0, v0, v0, lb);
+            }
+        }
+    }
 }
 
 // ---- long horizons: one QP per 16-lane group (hvp_coop.h), 4 groups per 64-lane block
@@ -528,7 +593,7 @@ __global__ __launch_bounds__(kCoopBlock) void k_bnb_bound_coop(int k, const hvp_
 template <int N>
 __global__ __launch_bounds__(kBlock) void k_bnb_expand(int k, const hvp_system* __restrict__ systems,
                                                        const int32_t* __restrict__ sys, hvp::Consts C, Workspace ws) {
-    const int src = (k - 1) & 1, dst = k & 1;
+    const int src = (k - 1) & 1;
     const unsigned long long np = ws.lvl[k - 1];
     const long long total = (long long)(np < (unsigned long long)ws.cap ? np : ws.cap);
     const int lane = threadIdx.x & 63;
@@ -545,52 +610,17 @@ __global__ __launch_bounds__(kBlock) void k_bnb_expand(int k, const hvp_system* 
             if (inst >= 0 && !(ws.inst_flag[inst] & 2)) {
                 plb = ws.nd_lb[src][p];
                 if (!hvp::bnb_pruned(plb, inc_of(ws, inst))) {
-                    const hvp_system& S = systems[sys[inst]];
                     lo = ws.nd_lo[src][p];
                     hi = ws.nd_hi[src][p];
                     code = ws.nd_code[src][p];
-                    for (int r = 0; r < S.n_regions; ++r) {
-                        double a, b;
-                        if (hvp::bnb_child(S, C, k - 1, lo, hi, r, &a, &b)) mask |= 1u << r;
-                    }
+                    mask = bnb_children(systems[sys[inst]], C, k - 1, lo, hi);
                 }
             }
         }
-        const int nc = __popc(mask);
-        int incl = nc;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const int v = __shfl_up(incl, off, 64);
-            if (lane >= off) incl += v;
-        }
-        const int wave_total = __shfl(incl, 63, 64);
-        if (!wave_total) continue;
-        unsigned long long base = 0;
-        if (lane == 63) base = atomicAdd(&ws.lvl[k], (unsigned long long)wave_total);
-        base = ((unsigned long long)(unsigned)__shfl((int)(base >> 32), 63, 64) << 32) |
-               (unsigned)__shfl((int)(base & 0xffffffffu), 63, 64);
-        if (!nc) continue;
-        const unsigned long long off = base + (unsigned long long)(incl - nc);
-        if (off + nc > (unsigned long long)ws.cap) {
-            atomicOr(&ws.inst_flag[inst], 2);  // overflow: reported, never truncated silently
-            // the slots of this reservation below the capacity are swept by the next kernels
-            for (unsigned long long t = off; t < (unsigned long long)ws.cap && t < off + nc; ++t)
-                ws.nd_inst[dst][t] = -1;
-            continue;
-        }
-        const hvp_system& S = systems[sys[inst]];
-        int j = 0;
-        for (int r = 0; r < S.n_regions; ++r) {
-            if (!((mask >> r) & 1u)) continue;
-            double a, b;
-            hvp::bnb_child(S, C, k - 1, lo, hi, r, &a, &b);
-            ws.nd_inst[dst][off + j] = inst;
-            ws.nd_code[dst][off + j] = hvp::code_with(code, k - 1, r);
-            ws.nd_lo[dst][off + j] = a;
-            ws.nd_hi[dst][off + j] = b;
-            ws.nd_lb[dst][off + j] = plb;  // inherited: kept by a leaf whose QP fails
-            ++j;
-        }
+        bool any;
+        const unsigned long long off = wave_reserve(ws, k, __popc(mask), lane, any);
+        if (!any || !mask) continue;
+        bnb_put_children(ws, k, off, mask, inst, systems[sys[inst]], C, code, lo, hi, plb);
     }
 }
 
@@ -811,6 +841,8 @@ void k_bnb_bound_refill(int k, const hvp_system* __restrict__ systems, const int
         const int nfree = __popcll(free);
         if (nfree >= kRefillMin || nfree == 64) {
             // ---- event: write the finished lanes' results, then refill every free lane
+            unsigned cmask = 0;  // children of a finished bound node (k_bnb_expand's work, fused)
+            double clb = 0.0;
             if (done) {
                 const int st = stage == RS_OPT ? g.verify(C, nullptr) : fail;
                 const bool ok = st == hvp::GI_OK;
@@ -820,6 +852,18 @@ void k_bnb_bound_refill(int k, const hvp_system* __restrict__ systems, const int
                 iter_sum += (unsigned long long)g.iter;
                 bnb_node_done<N>(k, t, inst, ok, g.iter, c, q.y, C, ws);
                 stage = RS_IDLE;
+                // the incumbent only changes at the leaves (level N): below N this pruning test
+                // sees the value a separate expand kernel would
+                clb = ok ? c : -1e300;
+                if (k < N && !(ws.inst_flag[inst] & 2) && !hvp::bnb_pruned(clb, inc_of(ws, inst)))
+                    cmask = bnb_children(systems[sys[inst]], C, k, ws.nd_lo[dst][t], ws.nd_hi[dst][t]);
+            }
+            if (k < N) {
+                bool any;
+                const unsigned long long off = wave_reserve(ws, k + 1, __popc(cmask), lane, any);
+                if (cmask)
+                    bnb_put_children(ws, k + 1, off, cmask, inst, systems[sys[inst]], C, code, ws.nd_lo[dst][t],
+                                     ws.nd_hi[dst][t], clb);
             }
             if (exhausted && nfree == 64) break;
             if (!exhausted) {
@@ -1336,8 +1380,12 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
     HIP_TRY(hipEventRecord(h->evb[1], st));
     const int g_small = (int)std::min<long long>(grid_for(h->ws.cap), (long long)h->n_cu * 8);
     const int g_qp = (int)std::min<long long>((h->ws.cap + BS - 1) / BS, (long long)h->n_cu * 8 * (kBlock / BS));
+    // the decentralised lane path generates every level's nodes inside k_bnb_root / the bound
+    // kernel of the level above (fused expand); the other paths run k_bnb_expand per level
+    const bool fused = !kCoop<N> && h->C.form == HVP_FORM_DECENT;
     for (int k = 1; k <= N; ++k) {
-        hipLaunchKernelGGL(k_bnb_expand<N>, dim3(g_small), dim3(kBlock), 0, st, k, h->d_sys, sys, h->C, ws);
+        if (!fused)
+            hipLaunchKernelGGL(k_bnb_expand<N>, dim3(g_small), dim3(kBlock), 0, st, k, h->d_sys, sys, h->C, ws);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(h->evb[2 * k], st));
         if constexpr (kCoop<N>) {
