@@ -659,6 +659,8 @@ def main() -> None:
                     help="decent: every step = neighbour predictions + local MIQPs + plant step, all on the device")
     ap.add_argument("--admm-iters", type=int, default=None, help="default 20 (admm) / 100 (gadmm)")
     ap.add_argument("--max-rounds", type=int, default=10, help="gadmm: switching rounds cap")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="decent: platoons split over this many handles / HIP streams (2: measured best, 3-4 no better)")
     ap.add_argument("--no-warm-incumbent", action="store_true",
                     help="admm: do not try the previous iteration's sequences as incumbents (A/B)")
     ap.add_argument("--gadmm-layout", choices=["replicas", "vehicles"], default="replicas")
@@ -694,22 +696,37 @@ def main() -> None:
     veh = PwaGearVehicle(800)
     system = tables.system_from_dict(veh.get_discrete_system(1), tables.gears_of(veh))
     method = {"auto": 0, "enum": 1, "bnb": 2}[args.method]
-    solver = BatchSolver(tables.problem(N, method=method), [system], device=local)
     # each rank owns a disjoint seed range: platoons are independent (weak scaling)
     params, roles = make_inputs(range(rank * S, (rank + 1) * S), n, N)
     B = len(roles)
-    solver.reserve(B)
     dev = torch.device("cuda", local)
-    t_params = torch.from_numpy(params).to(dev)
-    t_roles = torch.from_numpy(roles).to(dev)
-    t_sys = torch.zeros(B, dtype=torch.int32, device=dev)
-    out = solver.alloc_outputs(B, dev)
+    t_params_all = torch.from_numpy(params).to(dev)
+    t_roles_all = torch.from_numpy(roles).to(dev)
+    # --streams K: the platoons split into K handles on K HIP streams (the levels of one handle's
+    # search are serial; K independent searches let one fill the CUs another's level tail leaves)
+    K = max(1, args.streams)
+    cuts = [(S * j // K) * n for j in range(K + 1)]
+    chunks = []
+    for j in range(K):
+        a, b = cuts[j], cuts[j + 1]
+        sv = BatchSolver(tables.problem(N, method=method), [system], device=local)
+        sv.reserve(b - a)
+        chunks.append((sv, torch.zeros(b - a, dtype=torch.int32, device=dev), t_roles_all[a:b].contiguous(),
+                       t_params_all[a:b].contiguous(), sv.alloc_outputs(b - a, dev),
+                       torch.cuda.current_stream(dev) if K == 1 else torch.cuda.Stream(dev)))
+    solver = chunks[0][0]
 
     # long horizons: a heavy-tailed search can outgrow an instance's workspace share; those
     # instances are re-solved inside the step (one synchronisation), so every step is complete
     retry = N > 8
+
+    def step():
+        for sv, ts, tr, tp, o, stm in chunks:
+            with torch.cuda.stream(stm):
+                sv.solve_device(ts, tr, tp, o, stream=stm, retry_overflow=retry)
+
     for _ in range(args.warmup):
-        solver.solve_device(t_sys, t_roles, t_params, out, retry_overflow=retry)
+        step()
     torch.cuda.synchronize()
 
     if dist:
@@ -717,12 +734,12 @@ def main() -> None:
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        solver.solve_device(t_sys, t_roles, t_params, out, retry_overflow=retry)
+        step()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     dt = time.perf_counter() - t0
-    ok = bool((out["status"] == 0).all().item())  # the timed steps' own results
+    ok = all(bool((c[4]["status"] == 0).all().item()) for c in chunks)  # the timed steps' own results
     if dist:
         tt = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -731,14 +748,18 @@ def main() -> None:
     # per-launch kernel time (HIP events recorded by the library on the solve stream around
     # K_qp_gi) and work counters: a second pass of the same steps, outside the timed region,
     # since reading them synchronises the stream after every step
+    # (with K streams the chunks are timed one after the other here: qp_ms is their sum)
     qp_ms, cand, iters, fallback = [], 0, 0, 0
     for _ in range(args.steps):
-        solver.solve_device(t_sys, t_roles, t_params, out)
-        s = solver.stats()
-        qp_ms.append(s.qp_ms)
-        cand += s.n_candidates
-        iters += s.qp_iterations
-        fallback += s.n_fallback
+        t_qp = 0.0
+        for sv, ts, tr, tp, o, stm in chunks:
+            sv.solve_device(ts, tr, tp, o, stream=stm)
+            s = sv.stats()
+            t_qp += s.qp_ms
+            cand += s.n_candidates
+            iters += s.qp_iterations
+            fallback += s.n_fallback
+        qp_ms.append(t_qp)
 
     steps_total = S * world * args.steps
     value = steps_total / dt
@@ -772,7 +793,8 @@ def main() -> None:
         "config": {"workload": (f"fleet_decent_mld n={n} N={N} pwa_gear"
                                 + (" (configs[1])" if (n, N) == (10, 5) else " (configs[4] sweep point)")),
                    "n_vehicles": n, "horizon": N, "search": "branch-and-bound" if bnb else "enumeration",
-                   "platoons_per_gpu": S, "local_miqps_per_step": B * world, "parallelism": f"seeds-sharded x{world}"},
+                   "platoons_per_gpu": S, "local_miqps_per_step": B * world, "streams_per_gpu": K,
+                   "parallelism": f"seeds-sharded x{world}"},
         "roofline": roofline,
         "qps_per_step": cand_per_step,
         "qp_iters_per_candidate": iters / max(cand, 1),
