@@ -13,7 +13,7 @@ set -euo pipefail
 export TMPDIR=/tmp
 OUT=${1:-gpurun_out/prof}
 shift || true
-if [ $# -gt 0 ]; then BENCH=(python3 bench.py "$@"); else BENCH=(python3 bench.py --platoons 16384 --steps 5 --warmup 1 --no-cpu); fi
+if [ $# -gt 0 ]; then BENCH=(python3 bench.py "$@"); else BENCH=(python3 bench.py --platoons 16384 --steps 5 --warmup 1 --no-cpu --streams 1); fi
 mkdir -p "$OUT"
 echo "${BENCH[*]}" > "$OUT/cmd.txt"
 echo "profiling: ${BENCH[*]}"
