@@ -197,28 +197,63 @@ def bench_admm(args, world: int, rank: int, local: int, dist) -> None:
     seeds = range(rank * S, (rank + 1) * S)
     states = np.stack([initial_platoon_state(n, derive_env_seed(int(s))).reshape(-1).astype(np.float64)
                        for s in seeds])
-    roles = [tables.role_bits(i == 0, i == n - 1, i == 0) for i in range(n)] * S
-    eng = AdmmEngine(admm_problem(N, 0.5), [system], np.zeros(n * S, np.int32), roles, n, S, device=local,
-                     warm_incumbent=False if args.no_warm_incumbent else None)
-    dev = eng.dev
     T = args.warmup + args.steps + 1
+    dev = torch.device("cuda", local)
     wins, lead = leader_windows(T, N, S, dev)
-    env = DeviceEnv(eng.solver, torch.full((S, n), 800.0, dtype=torch.float64, device=dev))
-    x = torch.from_numpy(states).to(dev)
-    u = torch.empty((S, n), dtype=torch.float64, device=dev)
-    u_prev = [None]
     notopt = torch.zeros((), dtype=torch.int64, device=dev)
     bad = torch.zeros((), dtype=torch.int64, device=dev)
+    # --streams K: the platoons split over K engines, each stepped by its own host thread on its
+    # own HIP stream (platoons are independent; one engine's level tails are filled by the other)
+    K = max(1, args.streams)
+    groups = []
+    for j in range(K):
+        a, b = S * j // K, S * (j + 1) // K
+        P = b - a
+        roles = [tables.role_bits(i == 0, i == n - 1, i == 0) for i in range(n)] * P
+        eng = AdmmEngine(admm_problem(N, 0.5), [system], np.zeros(n * P, np.int32), roles, n, P, device=local,
+                         warm_incumbent=False if args.no_warm_incumbent else None)
+        groups.append({"eng": eng, "P": P, "env": DeviceEnv(eng.solver, torch.full((P, n), 800.0, dtype=torch.float64,
+                                                                                  device=dev)),
+                       "x": torch.from_numpy(states[a:b]).to(dev), "u": torch.empty((P, n), dtype=torch.float64,
+                                                                                      device=dev),
+                       "u_prev": None, "wins": [w[a:b].contiguous() for w in wins],
+                       "lead": [ld[a:b].contiguous() for ld in lead],
+                       "notopt": torch.zeros((), dtype=torch.int64, device=dev),
+                       "bad": torch.zeros((), dtype=torch.int64, device=dev),
+                       "stream": torch.cuda.current_stream(dev) if K == 1 else torch.cuda.Stream(dev)})
+
+    def group_step(g, t, on_solve=None):
+        with torch.cuda.stream(g["stream"]):
+            g["eng"].set_leader_device(g["wins"][t])
+            o = g["eng"].step(g["x"], iters, stream=g["stream"], on_solve=on_solve)
+            g["u"].copy_(o["u"][:, 0].view(g["P"], n))
+            g["notopt"].add_((o["status"] != 0).sum())
+            r = g["env"].step(g["x"], g["u"], g["lead"][t], u_prev=g["u_prev"])
+            g["bad"].add_(r["status"].sum())
+            g["u_prev"] = g["u"].clone()
 
     def step(t, on_solve=None):
-        eng.set_leader_device(wins[t])
-        o = eng.step(x, iters, on_solve=on_solve)
-        u.copy_(o["u"][:, 0].view(S, n))
-        notopt.add_((o["status"] != 0).sum())
-        r = env.step(x, u, lead[t], u_prev=u_prev[0])
-        bad.add_(r["status"].sum())
-        u_prev[0] = u.clone()
-        return o
+        if K == 1 or on_solve is not None:
+            for g in groups:
+                group_step(g, t, on_solve)
+            return
+        import threading
+
+        errs = []
+
+        def run(g):
+            try:
+                group_step(g, t)
+            except BaseException as e:  # noqa: BLE001 -- re-raised on the main thread
+                errs.append(e)
+
+        th = [threading.Thread(target=run, args=(g,)) for g in groups]
+        for h in th:
+            h.start()
+        for h in th:
+            h.join()
+        if errs:
+            raise errs[0]
 
     for t in range(args.warmup):
         step(t)
@@ -237,6 +272,9 @@ def bench_admm(args, world: int, rank: int, local: int, dist) -> None:
         tt = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
+    for g in groups:
+        notopt.add_(g["notopt"])
+        bad.add_(g["bad"])
     # QP-launch timing and work counters of one more step (stats synchronise per iteration)
     acc = {"qp_ms": 0.0, "qps": 0, "it": 0}
 
@@ -261,8 +299,8 @@ def bench_admm(args, world: int, rank: int, local: int, dist) -> None:
         "config": {"workload": f"fleet_naive_admm n={n} N={N} pwa_gear closed loop (configs[2])", "n_vehicles": n,
                    "horizon": N, "admm_iters": iters, "rho": 0.5, "platoons_per_gpu": S,
                    "local_miqps_per_step": iters * n * S * world, "warm_incumbent": N > 8 and not args.no_warm_incumbent,
-                   "parallelism": f"seeds-sharded x{world}"},
-        "roofline": qp_roofline(acc["qp_ms"], qk, notional, f"admm_n{n}_N{N}"),
+                   "streams_per_gpu": K, "parallelism": f"seeds-sharded x{world}"},
+        "roofline": qp_roofline(acc["qp_ms"] if K == 1 else dt / args.steps * 1e3, qk, notional, f"admm_n{n}_N{N}"),
         "qps_per_step": acc["qps"], "qp_iters_per_qp": acc["it"] / max(acc["qps"], 1),
         "not_optimal_total": int(notopt.item()), "plant_failures_total": int(bad.item()),
     }
@@ -323,14 +361,50 @@ def bench_gadmm(args, world: int, rank: int, local: int, dist) -> None:
     states = np.stack([initial_platoon_state(n, derive_env_seed(int(s))).reshape(-1).astype(np.float64)
                        for s in range(seed0, seed0 + S)])
     ex = HaloExchange(S, n, N, rank, world) if sharded else None
-    eng = GAdmmEngine(gadmm_problem(N, 0.5), [system] * n, n, S, device=local, admm_iters=iters,
-                      max_rounds=args.max_rounds, exchange=ex)
     lead = np.stack([3000.0 + 20.0 * np.arange(N + 1), np.full(N + 1, 20.0)])
-    eng.set_leader(lead)
-    t_states = torch.from_numpy(states).to(eng.dev)
-    eng.control(t_states)  # t = 0 (one warm start): establishes the previous solution
+    # --streams K (replicas): the platoons split over K engines, each driven by its own host thread
+    # on its own HIP stream (the engine synchronises once per switching round; the other engine's
+    # launches fill the GPU meanwhile)
+    K = 1 if sharded else max(1, args.streams)
+    dev = torch.device("cuda", local)
+    groups = []
+    for j in range(K):
+        a, b = S * j // K, S * (j + 1) // K
+        eng = GAdmmEngine(gadmm_problem(N, 0.5), [system] * n, n, b - a, device=local, admm_iters=iters,
+                          max_rounds=args.max_rounds, exchange=ex)
+        eng.set_leader(lead)
+        groups.append({"eng": eng, "x": torch.from_numpy(states[a:b]).to(dev),
+                       "stream": torch.cuda.current_stream(dev) if K == 1 else torch.cuda.Stream(dev), "out": None})
+
+    def control(g):
+        with torch.cuda.stream(g["stream"]):
+            g["out"] = g["eng"].control(g["x"])
+
+    def step():
+        if K == 1:
+            control(groups[0])
+            return
+        import threading
+
+        errs = []
+
+        def run(g):
+            try:
+                control(g)
+            except BaseException as e:  # noqa: BLE001 -- re-raised on the main thread
+                errs.append(e)
+
+        th = [threading.Thread(target=run, args=(g,)) for g in groups]
+        for h in th:
+            h.start()
+        for h in th:
+            h.join()
+        if errs:
+            raise errs[0]
+
+    step()  # t = 0 (one warm start): establishes the previous solution
     for _ in range(args.warmup):
-        eng.control(t_states)
+        step()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -338,37 +412,41 @@ def bench_gadmm(args, world: int, rank: int, local: int, dist) -> None:
     t0 = time.perf_counter()
     rounds = launches = 0
     for _ in range(args.steps):
-        out = eng.control(t_states)
-        rounds += sum(r["rounds"] for r in out["runs"])
-        launches += sum(r["launches"] for r in out["runs"])
+        step()
+        for g in groups:
+            rounds += sum(r["rounds"] for r in g["out"]["runs"])
+            launches += sum(r["launches"] for r in g["out"]["runs"])
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     dt = time.perf_counter() - t0
-    ok = bool(torch.isfinite(out["cost"]).all().item())
+    ok = all(bool(torch.isfinite(g["out"]["cost"]).all().item()) for g in groups)
     if dist:
-        tt = torch.tensor([dt], device=eng.dev, dtype=torch.float64)
+        tt = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     # per-launch time of the local-QP kernel: HIP events on the launch stream over one more step
+    # (the groups one after the other)
     qp_ev = []
-    solve = eng.solve
+    for g in groups:
+        eng = g["eng"]
+        solve = eng.solve
 
-    def timed_solve(stream=None):
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record()
-        solve(stream)
-        b.record()
-        qp_ev.append((a, b))
+        def timed_solve(stream=None, solve=solve):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            solve(stream)
+            b.record()
+            qp_ev.append((a, b))
 
-    eng.solve = timed_solve
-    out2 = eng.control(t_states)
-    torch.cuda.synchronize()
-    eng.solve = solve
+        eng.solve = timed_solve
+        control(g)
+        torch.cuda.synchronize()
+        eng.solve = solve
     qp_ms = [a.elapsed_time(b) for a, b in qp_ev]
     n_qp_launch = len(qp_ms)
     qp_avg = float(np.mean(qp_ms))
-    live_qps = S * eng.m  # upper bound: platoons that stopped switching skip their lanes
+    live_qps = sum(g["eng"].P * g["eng"].m for g in groups) / K  # upper bound: platoons that stopped switching skip their lanes
     notional = live_qps * n_qp_launch * (gadmm_qp_bytes(N) + 8 * (2 + 14 * (N + 1)))
     platoons_total = S * (1 if sharded else world)
     value = platoons_total * args.steps / dt
@@ -381,9 +459,10 @@ def bench_gadmm(args, world: int, rank: int, local: int, dist) -> None:
                 "step is a g_admm_control with both warm starts (previous solution from the preceding call)",
         "config": {"workload": f"fleet_g_admm n={n} N={N} pwa_gear (configs[3])", "n_vehicles": n, "horizon": N,
                    "admm_iters": iters, "max_rounds": args.max_rounds, "rho": 0.5, "platoons_per_gpu": S,
+                   "streams_per_gpu": K,
                    "parallelism": (f"vehicles-sharded x{world} (RCCL halo send/recv per ADMM iteration)" if sharded
                                    else f"seeds-sharded x{world} (replicas, no collective)")},
-        "roofline": qp_roofline(qp_avg * n_qp_launch, [("k_gadmm_qp_coop" if N > 8 else "k_gadmm_qp", n_qp_launch)],
+        "roofline": qp_roofline(qp_avg * n_qp_launch if K == 1 else dt / args.steps * 1e3, [("k_gadmm_qp_coop" if N > 8 else "k_gadmm_qp", n_qp_launch)],
                                 notional, f"gadmm_n{n}_N{N}"),
         "admm_rounds_per_step": rounds / args.steps, "qp_launches_per_step": launches / args.steps,
         "all_feasible": ok,
