@@ -614,16 +614,50 @@ def bench_cent(args, world: int, rank: int, local: int, dist) -> None:
     n, N, S = args.n, args.N, args.platoons
     veh = PwaGearVehicle(800)
     system = tables.system_from_dict(veh.get_discrete_system(1), tables.gears_of(veh))
-    solver = CentSolver(cent_problem(N), [system], device=local)
     dev = torch.device("cuda", local)
     seeds = range(rank * S, (rank + 1) * S)
     x0 = np.stack([initial_platoon_state(n, derive_env_seed(int(s))).reshape(n, 2).astype(np.float64) for s in seeds])
     lead = np.stack([3000.0 + 20.0 * np.arange(N + 1), np.full(N + 1, 20.0)])
-    t_x0 = torch.from_numpy(x0).to(dev)
-    t_sys = torch.zeros((S, n), dtype=torch.int32, device=dev)
-    t_lead = torch.from_numpy(np.ascontiguousarray(np.broadcast_to(lead, (S, 2, N + 1)))).to(dev)
-    out = solver.alloc_outputs(S, n, dev)
-    run = lambda: solver.solve_device(t_sys, t_x0, t_lead, max_nodes=args.max_nodes, out=out)  # noqa: E731
+    # --streams K: the platoons over K handles, each solved by its own host thread on its own HIP
+    # stream (a solve synchronises once per round of subtree tasks; the other fills the GPU)
+    K = max(1, args.streams)
+    groups = []
+    for j in range(K):
+        a, b = S * j // K, S * (j + 1) // K
+        sv = CentSolver(cent_problem(N), [system], device=local)
+        groups.append((sv, torch.zeros((b - a, n), dtype=torch.int32, device=dev), torch.from_numpy(x0[a:b]).to(dev),
+                       torch.from_numpy(np.ascontiguousarray(np.broadcast_to(lead, (b - a, 2, N + 1)))).to(dev),
+                       sv.alloc_outputs(b - a, n, dev),
+                       torch.cuda.current_stream(dev) if K == 1 else torch.cuda.Stream(dev)))
+    solver = groups[0][0]
+
+    def solve_group(g):
+        sv, ts, tx, tl, o, stm = g
+        with torch.cuda.stream(stm):
+            sv.solve_device(ts, tx, tl, max_nodes=args.max_nodes, out=o, stream=stm)
+
+    def run():
+        if K == 1:
+            solve_group(groups[0])
+            return
+        import threading
+
+        errs = []
+
+        def work(g):
+            try:
+                solve_group(g)
+            except BaseException as e:  # noqa: BLE001 -- re-raised on the main thread
+                errs.append(e)
+
+        th = [threading.Thread(target=work, args=(g,)) for g in groups]
+        for h in th:
+            h.start()
+        for h in th:
+            h.join()
+        if errs:
+            raise errs[0]
+
     for _ in range(args.warmup):
         run()
     torch.cuda.synchronize()
@@ -637,17 +671,20 @@ def bench_cent(args, world: int, rank: int, local: int, dist) -> None:
     if dist:
         dist.barrier()
     dt = time.perf_counter() - t0
-    status = out["status"].cpu().numpy()
-    nodes = out["nodes"].cpu().numpy()
-    iters = out["iters"].cpu().numpy()
+    status = np.concatenate([g[4]["status"].cpu().numpy() for g in groups])
+    nodes = np.concatenate([g[4]["nodes"].cpu().numpy() for g in groups])
+    iters = np.concatenate([g[4]["iters"].cpu().numpy() for g in groups])
     if dist:
         tt = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     # kernel time: HIP events the library records around the search kernels on the solve stream
-    run()
-    st = solver.stats()
-    kernel_ms = st.last_ms
+    # (K streams: their searches overlap, so the step's wall time)
+    if K == 1:
+        run()
+        kernel_ms = solver.stats().last_ms
+    else:
+        kernel_ms = dt / args.steps * 1e3
     qps = int(nodes.sum())
     notional = qps * cent_qp_bytes(n, N) + S * 8 * (2 * n + 2 * (N + 1) + n * (3 * N + 2) + 1)
     n_opt = int((status == 0).sum())
@@ -660,7 +697,8 @@ def bench_cent(args, world: int, rank: int, local: int, dist) -> None:
         "dtype": "f64",
         "data": "synthetic: env.reset random-init platoon states (seeded), constant-velocity leader",
         "config": {"workload": f"fleet_cent_mld n={n} N={N} pwa_gear (MpcMldCent)", "n_vehicles": n, "horizon": N,
-                   "platoons_per_gpu": S, "max_nodes": args.max_nodes, "parallelism": f"seeds-sharded x{world}"},
+                   "platoons_per_gpu": S, "max_nodes": args.max_nodes, "streams_per_gpu": K,
+                   "parallelism": f"seeds-sharded x{world}"},
         "value_optimal_only": n_opt * world * args.steps / dt,
         "roofline": qp_roofline(kernel_ms, cent_kernels(f"cent_n{n}_N{N}"), notional, f"cent_n{n}_N{N}"),
         "qps_per_step": qps, "qp_iters_per_qp": float(iters.sum()) / max(qps, 1),
