@@ -777,7 +777,8 @@ def main() -> None:
     ap.add_argument("--admm-iters", type=int, default=None, help="default 20 (admm) / 100 (gadmm)")
     ap.add_argument("--max-rounds", type=int, default=10, help="gadmm: switching rounds cap")
     ap.add_argument("--streams", type=int, default=2,
-                    help="decent: platoons split over this many handles / HIP streams (2: measured best, 3-4 no better)")
+                    help="platoons split over this many handles / HIP streams (decent: one host thread; admm, "
+                         "gadmm replicas, cent: one host thread each); 2 measured best (DESIGN.md section 4)")
     ap.add_argument("--no-warm-incumbent", action="store_true",
                     help="admm: do not try the previous iteration's sequences as incumbents (A/B)")
     ap.add_argument("--gadmm-layout", choices=["replicas", "vehicles"], default="replicas")
