@@ -102,3 +102,19 @@ def test_sweep_warm_incumbent_keeps_the_episodes(gpu_available):
     b = run_point(5, 10, [0, 1, 2, 3], ep_len=6, warm_incumbent=False)
     for k in ("X", "U", "R", "viol"):
         assert np.array_equal(a[k], b[k]), k
+
+
+@pytest.mark.gpu
+def test_run_points_blocks_equal_one_batch(gpu_available):
+    """run_points (seed blocks on concurrent host threads / streams) gives every seed the same
+    episode as one batch of all seeds: the blocks share nothing (numpy's global generator, which
+    the task_2 masses and env.reset seed, is drawn under a lock)."""
+    from hvp.sweep import run_point, run_points
+
+    seeds = list(range(8))
+    one = run_point(6, 5, seeds, ep_len=5)
+    blocks, _ = run_points(6, 5, seeds, ep_len=5, device=0, out_dir=None, estimator="none", streams=2)
+    X = np.concatenate([b["X"] for b in blocks], axis=1)
+    R = np.concatenate([b["R"] for b in blocks], axis=1)
+    np.testing.assert_array_equal(X, one["X"])
+    np.testing.assert_array_equal(R, one["R"])
