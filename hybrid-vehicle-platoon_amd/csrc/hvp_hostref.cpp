@@ -12,6 +12,7 @@
 #include "hvp_bnb.h"
 #include "hvp_gi.h"
 #include "hvp_ipm.h"
+#include "hvp_l1.h"
 
 namespace {
 
@@ -45,6 +46,7 @@ hvp::Consts make_consts(const hvp_problem& p) {
                : p.formulation == HVP_FORM_GADMM ? hvp_params_stride_gadmm(p.N)
                                                  : hvp_params_stride(p.N);
     C.rho = p.rho;
+    C.l1 = p.quadratic_cost ? 0 : 1;
     return C;
 }
 
@@ -65,6 +67,17 @@ void solve_one(const hvp_system& S, const hvp::Consts& C, int role, const double
     if (ok) {
         n = hvp::enumerate_sequences(S, C, prm[1], [&](uint32_t code, int) {
             hvp::LaneQp<N> q;
+            if (C.l1) {  // min_1_norm: the fixed-sequence LP (hvp_l1.h)
+                hvp::L1Lp<N> lp;
+                hvp::l1_setup<N>(lp, S, C, role, prm, code);
+                Cand c;
+                c.code = code;
+                c.status = hvp::l1_solve<N>(lp, prm[1], hvp::kL1MaxIter, c.iters);
+                c.cost = c.status == 0 ? hvp::l1_direct_cost<N>(lp.y, S, C, role, prm, code) : 1e300;
+                for (int i = 0; i < N; ++i) c.y[i] = lp.y[i];
+                cands.push_back(c);
+                return;
+            }
             hvp::setup_lane<N>(q, S, C, role, prm, code);
             hvp::QpOut o;
             bool gi_done = false;
@@ -293,7 +306,7 @@ void solve_range(const hvp_problem& P, const hvp_system* systems, int B, const i
     const int stride = C.stride;
 #pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1)
     for (int i = 0; i < B; ++i) {
-        const bool bnb = P.method == HVP_METHOD_BNB || (P.method == HVP_METHOD_AUTO && N > kAutoEnumMaxN);
+        const bool bnb = !C.l1 && (P.method == HVP_METHOD_BNB || (P.method == HVP_METHOD_AUTO && N > kAutoEnumMaxN));
         if (bnb || N > HVP_MAX_N_ENUM || C.form == HVP_FORM_ADMM) {
             solve_one_bnb<N>(systems[sys[i]], C, role[i], params + (size_t)i * stride, u + (size_t)i * N,
                              x + (size_t)i * 2 * (N + 1), region + (size_t)i * N, cost + i, status + i, nodes + i,

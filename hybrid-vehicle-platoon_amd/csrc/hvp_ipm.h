@@ -52,6 +52,7 @@ struct Consts {
     int form;      // HVP_FORM_*
     int stride;    // parameter block stride (doubles)
     double rho;    // ADMM penalty
+    int l1;        // 1: min_1_norm cost (hvp_l1.h), 0: min_2_norm
 };
 
 struct QpOut {

@@ -57,6 +57,7 @@ hvp::Consts make_consts(const hvp_problem& p) {
                : p.formulation == HVP_FORM_GADMM ? hvp_params_stride_gadmm(p.N)
                                                  : hvp_params_stride(p.N);
     C.rho = p.rho;
+    C.l1 = p.quadratic_cost ? 0 : 1;
     return C;
 }
 
@@ -285,8 +286,12 @@ int hvp_create(hvp_handle** out, const hvp_problem* problem, const hvp_system* s
         return fail(HVP_E_UNSUPPORTED, "hvp_create: the ADMM formulation is solved by branch and bound only");
     if (problem->formulation == HVP_FORM_ADMM && !(problem->rho > 0))
         return fail(HVP_E_ARG, "hvp_create: the ADMM formulation needs rho > 0");
-    if (problem->quadratic_cost != 1)
-        return fail(HVP_E_UNSUPPORTED, "hvp_create: only the quadratic cost (min_2_norm) runs on the GPU");
+    if (problem->quadratic_cost != 1 && problem->quadratic_cost != 0)
+        return fail(HVP_E_ARG, "hvp_create: quadratic_cost must be 1 (min_2_norm) or 0 (min_1_norm)");
+    if (problem->quadratic_cost == 0 &&
+        (problem->formulation != HVP_FORM_DECENT || problem->N > HVP_MAX_N_ENUM || problem->method == HVP_METHOD_BNB))
+        return fail(HVP_E_UNSUPPORTED, "hvp_create: the min_1_norm cost runs for HVP_FORM_DECENT problems with N <= " +
+                                           std::to_string(HVP_MAX_N_ENUM) + " by enumeration");
     for (int i = 0; i < n_systems; ++i) {
         std::string why;
         if (!valid_system(systems[i], &why)) return fail(HVP_E_ARG, "hvp_create: system " + std::to_string(i) + ": " + why);
@@ -296,7 +301,8 @@ int hvp_create(hvp_handle** out, const hvp_problem* problem, const hvp_system* s
     h->device = device;
     h->prob = *problem;
     h->C = make_consts(*problem);
-    h->bnb = problem->method == HVP_METHOD_BNB || (problem->method == HVP_METHOD_AUTO && problem->N > kAutoEnumMaxN);
+    h->bnb = problem->quadratic_cost == 1 && (problem->method == HVP_METHOD_BNB ||
+                                             (problem->method == HVP_METHOD_AUTO && problem->N > kAutoEnumMaxN));
     h->n_systems = n_systems;
     for (int i = 0; i < n_systems; ++i) h->nreg_max = std::max(h->nreg_max, (int)systems[i].n_regions);
     (void)hipDeviceGetAttribute(&h->n_cu, hipDeviceAttributeMultiprocessorCount, device);
@@ -437,6 +443,7 @@ int hvp_evaluate_batch(hvp_handle* h, int B, const int32_t* sys, const int32_t* 
         return fail(HVP_E_ARG, "hvp_evaluate_batch: bad argument");
     if (h->prob.formulation != HVP_FORM_DECENT)
         return fail(HVP_E_UNSUPPORTED, "hvp_evaluate_batch: HVP_FORM_DECENT problems only");
+    if (h->C.l1) return fail(HVP_E_UNSUPPORTED, "hvp_evaluate_batch: min_2_norm problems only");
     if (B == 0) return 0;
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t st = (hipStream_t)stream;

@@ -1,0 +1,406 @@
+// hvp_l1.h -- fixed-sequence LP of the min_1_norm local MPC (the L1 / MILP variant).
+//
+// LocalMpcMld.setup_cost_and_constraints(quadratic_cost=False) (fleet_decent_mld.py:73-76)
+// prices every term of the objective with min_1_norm [EXT dmpcpwa]: sum_i Q_ii |e_i| of the
+// tracking errors (:110-153), Q_u |u_k| (:155), Q_du |u_{k+1} - u_k| (:157-162), plus the
+// linear slack cost w (s_f + s_b) (:164-169).  With the region sequence sigma fixed the MLD
+// MILP is an LP; its optimum over sigma is the MILP optimum (same search and tie rule as the
+// quadratic path: hvp_lane.h k_enum / k_select).
+//
+// Formulation (velocity space, as hvp_ipm.h): y = (v_1 .. v_N), p_k = P1 + ts (y_0 + .. + y_{k-2}),
+// u_k = (y_k - a_k y_{k-1} - c_k) / b_k.
+//   hard rows  g.y <= h : V (region sigma_{k+1} and the state box), U (input box), A (accel
+//              rows with tightening), P (position box)                       8N - 2 rows
+//   pairs      w |g.y + e0|        (alpha = 1: tracking errors, u, du)   or
+//              w max(0, g.y + e0)  (alpha = 0: the soft safe-distance rows, slack eliminated)
+//              each with its epigraph variable t:  g.y - t <= -e0,  -alpha g.y - t <= alpha e0,
+//              cost w t.
+// Variable-free terms (k = 0, the p_1 errors, the k = 0, 1 slacks) are constants: they enter the
+// cost (l1_direct_cost) but not the LP.
+//
+// Solver: Mehrotra predictor-corrector primal-dual interior point in (y, t), every epigraph
+// variable eliminated analytically from its two rows (Schur complement per pair:
+// D1 D2 (1 + alpha)^2 / (D1 + D2) g g'), so the Newton system is N x N whatever the number of
+// terms.  Rows are stored densely per lane (N <= HVP_MAX_N_ENUM = 8: at most 62 hard rows and
+// 80 pairs); this path runs with exhaustive enumeration only.  The interior point converges to
+// a point of the optimal face; the objective -- what the sequence search compares -- is
+// evaluated term by term on it (l1_direct_cost).
+//
+// No HIP dependency: hvp_lane.h compiles it for gfx950, the test-only host build
+// (hvp_hostref.cpp) with g++.
+#pragma once
+
+#include "hvp_ipm.h"
+
+namespace hvp {
+
+constexpr int kL1MaxIter = 120;
+
+template <int N>
+struct L1Lp {
+    static constexpr int MH = 8 * N - 2;
+    static constexpr int MP = 10 * N;
+    static constexpr int NT = N * (N + 1) / 2;
+    int mh, mp;
+    double gh[MH][N], h[MH];
+    double gp[MP][N], e0[MP], wp[MP], al[MP];
+    // iterate
+    double y[N], t[MP];
+    double sh[MH], lh[MH];
+    double s1[MP], s2[MP], l1[MP], l2[MP];
+    // affine (predictor) directions of s and l, for the corrector's second-order term
+    double dsh[MH], dlh[MH], ds1[MP], dl1[MP], ds2[MP], dl2[MP];
+};
+
+template <int N>
+HVP_HD inline double l1_dot(const double* g, const double* y) {
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) s += g[i] * y[i];
+    return s;
+}
+
+// Rows of the fixed-sequence LP of instance params prm (x0, x_front, x_back, leader_x) and
+// region code.  Returns false when the constant row p_1 in [pmin, pmax] is violated.
+template <int N>
+HVP_HD inline bool l1_setup(L1Lp<N>& L, const hvp_system& S, const Consts& C, int role, const double* prm,
+                            uint64_t code) {
+    const double p0 = prm[0], v0 = prm[1];
+    const double* xf = prm + 2;
+    const double* xb = prm + 2 + 2 * (N + 1);
+    const double* xl = prm + 2 + 4 * (N + 1);
+    const int K1 = N + 1;
+    const double ts = S.ts, P1 = p0 + ts * v0;
+    L.mh = 0;
+    L.mp = 0;
+    auto hard = [&](const double* g, double sgn, double hh) {
+        for (int i = 0; i < N; ++i) L.gh[L.mh][i] = sgn * g[i];
+        L.h[L.mh] = hh;
+        ++L.mh;
+    };
+    auto pair = [&](const double* g, double e0, double w, double alpha) {
+        bool any = false;
+        for (int i = 0; i < N; ++i) any = any || g[i] != 0.0;
+        if (!(w > 0.0) || !any) return;  // zero weight, or a constant term (in the direct cost)
+        for (int i = 0; i < N; ++i) L.gp[L.mp][i] = g[i];
+        L.e0[L.mp] = e0;
+        L.wp[L.mp] = w;
+        L.al[L.mp] = alpha;
+        ++L.mp;
+    };
+    double a[N], b[N], c[N];
+    for (int k = 0; k < N; ++k) {
+        const int r = code_region(code, k);
+        a[k] = S.a[r];
+        b[k] = S.b[r];
+        c[k] = S.c[r];
+    }
+    double g[N];
+    auto zero = [&]() {
+        for (int i = 0; i < N; ++i) g[i] = 0.0;
+    };
+    // ---- hard rows
+    for (int j = 0; j < N; ++j) {
+        // V: v_{j+1} in region sigma_{j+1} (k < N) and the state box
+        double vlo = S.vmin, vhi = S.vmax;
+        if (j + 1 < N) {
+            const int r1 = code_region(code, j + 1);
+            vlo = fmax(vlo, S.vlo[r1]);
+            vhi = fmin(vhi, S.vhi[r1]);
+        }
+        zero();
+        g[j] = 1.0;
+        hard(g, 1.0, vhi);
+        hard(g, -1.0, -vlo);
+        // U: c + b umin <= v_{j+1} - a v_j <= c + b umax   (F u <= G)
+        const double cu = j == 0 ? a[0] * v0 : 0.0;
+        zero();
+        g[j] = 1.0;
+        if (j) g[j - 1] = -a[j];
+        hard(g, 1.0, c[j] + b[j] * S.umax + cu);
+        hard(g, -1.0, -(c[j] + b[j] * S.umin + cu));
+        // A: dec_j <= v_{j+1} - v_j <= acc_j   (fleet_decent_mld.py:172-188)
+        const double ca = j == 0 ? v0 : 0.0;
+        zero();
+        g[j] = 1.0;
+        if (j) g[j - 1] = -1.0;
+        hard(g, 1.0, C.acc[j] + ca);
+        hard(g, -1.0, -(C.dec[j] + ca));
+    }
+    for (int m = 0; m + 2 <= N; ++m) {  // P: pmin <= p_{m+2} <= pmax
+        for (int i = 0; i < N; ++i) g[i] = i <= m ? ts : 0.0;
+        hard(g, 1.0, S.pmax - P1);
+        hard(g, -1.0, P1 - S.pmin);
+    }
+    // ---- L1 terms and soft rows
+    const bool tf = (role & HVP_ROLE_TRACK_FRONT) != 0, tb = (role & HVP_ROLE_TRACK_BACK) != 0;
+    const bool tl = (role & HVP_ROLE_TRACK_LEADER) != 0, lsp = (role & HVP_ROLE_LEADER_SPACING) != 0;
+    const bool sf = (role & HVP_ROLE_SAFE_FRONT) != 0, sb = (role & HVP_ROLE_SAFE_BACK) != 0;
+    const double t0 = C.t0, d0 = C.d0;
+    for (int k = 1; k <= N; ++k) {
+        double gpre[N], gv[N], tmp[N];
+        for (int i = 0; i < N; ++i) {
+            gpre[i] = i <= k - 2 ? ts : 0.0;  // p_k = P1 + gpre.y
+            gv[i] = i == k - 1 ? 1.0 : 0.0;   // v_k = gv.y
+        }
+        if (tf) {  // x_k - xf_k - spacing(x_k)   (:110-121)
+            for (int i = 0; i < N; ++i) tmp[i] = gpre[i] + t0 * gv[i];
+            pair(tmp, P1 + d0 - xf[k], C.Qpp, 1.0);
+            pair(gv, -xf[K1 + k], C.Qvv, 1.0);
+        }
+        if (tb) {  // xb_k - x_k - spacing(xb_k)   (:122-133)
+            for (int i = 0; i < N; ++i) tmp[i] = -gpre[i];
+            pair(tmp, xb[k] + t0 * xb[K1 + k] + d0 - P1, C.Qpp, 1.0);
+            for (int i = 0; i < N; ++i) tmp[i] = -gv[i];
+            pair(tmp, xb[K1 + k], C.Qvv, 1.0);
+        }
+        if (tl) {  // x_k - leader_x_k (- spacing(x_k) with real_vehicle_as_reference)   (:134-153)
+            for (int i = 0; i < N; ++i) tmp[i] = gpre[i] + (lsp ? t0 * gv[i] : 0.0);
+            pair(tmp, P1 - xl[k] + (lsp ? d0 : 0.0), C.Qpp, 1.0);
+            pair(gv, -xl[K1 + k], C.Qvv, 1.0);
+        }
+        if (k >= 2 && sf) pair(gpre, P1 - xf[k] + C.d_safe, C.w, 0.0);  // w max(0, p_k - pf_k + d_safe)
+        if (k >= 2 && sb) {                                                // w max(0, pb_k + d_safe - p_k)
+            for (int i = 0; i < N; ++i) tmp[i] = -gpre[i];
+            pair(tmp, xb[k] + C.d_safe - P1, C.w, 0.0);
+        }
+    }
+    // inputs u_k = ubar_k + gu_k.y ; Q_u |u_k| and Q_du |u_{k+1} - u_k|
+    double gprev[N], uprev = 0.0;
+    for (int k = 0; k < N; ++k) {
+        double gu[N];
+        const double ib = 1.0 / b[k];
+        for (int i = 0; i < N; ++i) gu[i] = i == k ? ib : (i + 1 == k ? -a[k] * ib : 0.0);
+        const double ubar = k == 0 ? -(a[0] * v0 + c[0]) * ib : -c[k] * ib;
+        pair(gu, ubar, C.Qu, 1.0);
+        if (k >= 1) {
+            double gd[N];
+            for (int i = 0; i < N; ++i) gd[i] = gu[i] - gprev[i];
+            pair(gd, ubar - uprev, C.Qdu, 1.0);
+        }
+        for (int i = 0; i < N; ++i) gprev[i] = gu[i];
+        uprev = ubar;
+    }
+    return P1 >= S.pmin - 1e-9 * (1.0 + fabs(S.pmin)) && P1 <= S.pmax + 1e-9 * (1.0 + fabs(S.pmax));
+}
+
+// Newton direction for the complementarity targets rc_i = s_i l_i (predictor) or
+// s_i l_i + ds_i dl_i - sigma mu (corrector, with the predictor's directions held in L); the
+// residuals of the current iterate are recomputed here.  Returns false if the N x N Schur
+// complement is not positive definite.
+template <int N>
+HVP_HD inline bool l1_direction(L1Lp<N>& L, double sigmu, bool corr, double* dy, double* dt, double* dsh, double* dlh,
+                                double* ds1, double* dl1, double* ds2, double* dl2) {
+    const int mh = L.mh, mp = L.mp;
+    double K[L1Lp<N>::NT], rhs[N];
+    for (int i = 0; i < L1Lp<N>::NT; ++i) K[i] = 0.0;
+    for (int i = 0; i < N; ++i) rhs[i] = 0.0;
+    // rd_y = sum_h l g + sum_p (l1 - alpha l2) g   (accumulated into rhs with a minus sign)
+    for (int i = 0; i < mh; ++i) {
+        const double* g = L.gh[i];
+        const double gy = l1_dot<N>(g, L.y);
+        const double rp = gy + L.sh[i] - L.h[i];
+        const double D = L.lh[i] / L.sh[i];
+        const double rc = L.sh[i] * L.lh[i] + (corr ? L.dsh[i] * L.dlh[i] - sigmu : 0.0);
+        const double rho = (L.lh[i] * rp - rc) / L.sh[i];
+        const double coef = -(L.lh[i] + rho);
+        for (int a = 0; a < N; ++a) {
+            rhs[a] += coef * g[a];
+            for (int b = 0; b <= a; ++b) K[tri(a, b)] += D * g[a] * g[b];
+        }
+    }
+    for (int j = 0; j < mp; ++j) {
+        const double* g = L.gp[j];
+        const double al = L.al[j];
+        const double gy = l1_dot<N>(g, L.y);
+        const double rp1 = gy - L.t[j] + L.s1[j] + L.e0[j];
+        const double rp2 = -al * gy - L.t[j] + L.s2[j] - al * L.e0[j];
+        const double D1 = L.l1[j] / L.s1[j], D2 = L.l2[j] / L.s2[j];
+        const double rc1 = L.s1[j] * L.l1[j] + (corr ? L.ds1[j] * L.dl1[j] - sigmu : 0.0);
+        const double rc2 = L.s2[j] * L.l2[j] + (corr ? L.ds2[j] * L.dl2[j] - sigmu : 0.0);
+        const double rho1 = (L.l1[j] * rp1 - rc1) / L.s1[j], rho2 = (L.l2[j] * rp2 - rc2) / L.s2[j];
+        const double rdt = L.wp[j] - L.l1[j] - L.l2[j];
+        const double rhst = -rdt + rho1 + rho2;
+        const double mt = D1 + D2, m = al * D2 - D1;
+        const double ce = D1 * D2 * (1.0 + al) * (1.0 + al) / mt;
+        // rhs_y -= (l1 - al l2) g + (rho1 - al rho2) g + m g rhs_t / Mtt
+        const double coef = -(L.l1[j] - al * L.l2[j]) - (rho1 - al * rho2) - m * rhst / mt;
+        for (int a = 0; a < N; ++a) {
+            rhs[a] += coef * g[a];
+            for (int b = 0; b <= a; ++b) K[tri(a, b)] += ce * g[a] * g[b];
+        }
+    }
+    if (!cholesky<N>(K)) return false;
+    chol_solve<N>(K, rhs, dy);
+    for (int i = 0; i < mh; ++i) {
+        const double* g = L.gh[i];
+        const double gy = l1_dot<N>(g, L.y), gd = l1_dot<N>(g, dy);
+        const double rp = gy + L.sh[i] - L.h[i];
+        const double D = L.lh[i] / L.sh[i];
+        const double rc = L.sh[i] * L.lh[i] + (corr ? L.dsh[i] * L.dlh[i] - sigmu : 0.0);
+        const double rho = (L.lh[i] * rp - rc) / L.sh[i];
+        dsh[i] = -rp - gd;
+        dlh[i] = D * gd + rho;
+    }
+    for (int j = 0; j < mp; ++j) {
+        const double* g = L.gp[j];
+        const double al = L.al[j];
+        const double gy = l1_dot<N>(g, L.y), gd = l1_dot<N>(g, dy);
+        const double rp1 = gy - L.t[j] + L.s1[j] + L.e0[j];
+        const double rp2 = -al * gy - L.t[j] + L.s2[j] - al * L.e0[j];
+        const double D1 = L.l1[j] / L.s1[j], D2 = L.l2[j] / L.s2[j];
+        const double rc1 = L.s1[j] * L.l1[j] + (corr ? L.ds1[j] * L.dl1[j] - sigmu : 0.0);
+        const double rc2 = L.s2[j] * L.l2[j] + (corr ? L.ds2[j] * L.dl2[j] - sigmu : 0.0);
+        const double rho1 = (L.l1[j] * rp1 - rc1) / L.s1[j], rho2 = (L.l2[j] * rp2 - rc2) / L.s2[j];
+        const double rdt = L.wp[j] - L.l1[j] - L.l2[j];
+        const double rhst = -rdt + rho1 + rho2;
+        const double mt = D1 + D2, m = al * D2 - D1;
+        dt[j] = (rhst - m * gd) / mt;
+        const double a1 = gd - dt[j], a2 = -al * gd - dt[j];
+        ds1[j] = -rp1 - a1;
+        dl1[j] = D1 * a1 + rho1;
+        ds2[j] = -rp2 - a2;
+        dl2[j] = D2 * a2 + rho2;
+    }
+    return true;
+}
+
+HVP_HD inline void l1_ratio(double& a, double v, double dv) {
+    if (dv < 0.0) a = fmin(a, -v / dv);
+}
+
+// Interior point on the rows of l1_setup.  Returns 0 (converged) or 2 (not converged /
+// numerical failure); the iterate is left in L.y.
+template <int N>
+HVP_HD inline int l1_solve(L1Lp<N>& L, double v0, int max_iter, int& iters) {
+    const int mh = L.mh, mp = L.mp;
+    const int mtot = mh + 2 * mp;
+    double hscale = 1.0, wmax = 1.0;
+    for (int i = 0; i < N; ++i) L.y[i] = v0;
+    for (int i = 0; i < mh; ++i) {
+        L.sh[i] = fmax(L.h[i] - l1_dot<N>(L.gh[i], L.y), 1.0);
+        L.lh[i] = 1.0;
+        hscale = fmax(hscale, fabs(L.h[i]));
+    }
+    for (int j = 0; j < mp; ++j) {
+        const double e = l1_dot<N>(L.gp[j], L.y) + L.e0[j];
+        L.t[j] = (L.al[j] > 0.0 ? fabs(e) : fmax(e, 0.0)) + 1.0;
+        L.s1[j] = L.t[j] - e;
+        L.s2[j] = L.t[j] + L.al[j] * e;
+        L.l1[j] = 0.5 * L.wp[j];
+        L.l2[j] = 0.5 * L.wp[j];
+        wmax = fmax(wmax, L.wp[j]);
+        hscale = fmax(hscale, fabs(L.e0[j]));
+    }
+    double dy[N], dt[L1Lp<N>::MP];
+    double dsh[L1Lp<N>::MH], dlh[L1Lp<N>::MH], ds1[L1Lp<N>::MP], dl1[L1Lp<N>::MP], ds2[L1Lp<N>::MP],
+        dl2[L1Lp<N>::MP];
+    for (iters = 0; iters < max_iter; ++iters) {
+        // residuals and the duality measure
+        double gap = 0.0, obj = 0.0, rpmax = 0.0, rdmax = 0.0;
+        double rdy[N];
+        for (int a = 0; a < N; ++a) rdy[a] = 0.0;
+        for (int i = 0; i < mh; ++i) {
+            gap += L.sh[i] * L.lh[i];
+            rpmax = fmax(rpmax, fabs(l1_dot<N>(L.gh[i], L.y) + L.sh[i] - L.h[i]));
+            for (int a = 0; a < N; ++a) rdy[a] += L.lh[i] * L.gh[i][a];
+        }
+        for (int j = 0; j < mp; ++j) {
+            const double gy = l1_dot<N>(L.gp[j], L.y), al = L.al[j];
+            gap += L.s1[j] * L.l1[j] + L.s2[j] * L.l2[j];
+            obj += L.wp[j] * L.t[j];
+            rpmax = fmax(rpmax, fabs(gy - L.t[j] + L.s1[j] + L.e0[j]));
+            rpmax = fmax(rpmax, fabs(-al * gy - L.t[j] + L.s2[j] - al * L.e0[j]));
+            rdmax = fmax(rdmax, fabs(L.wp[j] - L.l1[j] - L.l2[j]));
+            for (int a = 0; a < N; ++a) rdy[a] += (L.l1[j] - al * L.l2[j]) * L.gp[j][a];
+        }
+        for (int a = 0; a < N; ++a) rdmax = fmax(rdmax, fabs(rdy[a]));
+        if (rpmax <= 1e-10 * hscale && rdmax <= 1e-10 * wmax && gap <= 1e-12 * fmax(1.0, fabs(obj))) return 0;
+        const double mu = gap / mtot;
+        // predictor
+        if (!l1_direction<N>(L, 0.0, false, dy, dt, L.dsh, L.dlh, L.ds1, L.dl1, L.ds2, L.dl2)) return 2;
+        double ap = 1.0, ad = 1.0;
+        for (int i = 0; i < mh; ++i) {
+            l1_ratio(ap, L.sh[i], L.dsh[i]);
+            l1_ratio(ad, L.lh[i], L.dlh[i]);
+        }
+        for (int j = 0; j < mp; ++j) {
+            l1_ratio(ap, L.s1[j], L.ds1[j]);
+            l1_ratio(ap, L.s2[j], L.ds2[j]);
+            l1_ratio(ad, L.l1[j], L.dl1[j]);
+            l1_ratio(ad, L.l2[j], L.dl2[j]);
+        }
+        double gaff = 0.0;
+        for (int i = 0; i < mh; ++i) gaff += (L.sh[i] + ap * L.dsh[i]) * (L.lh[i] + ad * L.dlh[i]);
+        for (int j = 0; j < mp; ++j)
+            gaff += (L.s1[j] + ap * L.ds1[j]) * (L.l1[j] + ad * L.dl1[j]) +
+                    (L.s2[j] + ap * L.ds2[j]) * (L.l2[j] + ad * L.dl2[j]);
+        const double ratio = gaff / gap;
+        const double sigma = ratio * ratio * ratio;
+        // corrector (centring + second-order term)
+        if (!l1_direction<N>(L, sigma * mu, true, dy, dt, dsh, dlh, ds1, dl1, ds2, dl2)) return 2;
+        ap = 1.0 / 0.995;
+        ad = 1.0 / 0.995;
+        for (int i = 0; i < mh; ++i) {
+            l1_ratio(ap, L.sh[i], dsh[i]);
+            l1_ratio(ad, L.lh[i], dlh[i]);
+        }
+        for (int j = 0; j < mp; ++j) {
+            l1_ratio(ap, L.s1[j], ds1[j]);
+            l1_ratio(ap, L.s2[j], ds2[j]);
+            l1_ratio(ad, L.l1[j], dl1[j]);
+            l1_ratio(ad, L.l2[j], dl2[j]);
+        }
+        ap *= 0.995;
+        ad *= 0.995;
+        for (int a = 0; a < N; ++a) L.y[a] += ap * dy[a];
+        for (int i = 0; i < mh; ++i) {
+            L.sh[i] += ap * dsh[i];
+            L.lh[i] += ad * dlh[i];
+        }
+        for (int j = 0; j < mp; ++j) {
+            L.t[j] += ap * dt[j];
+            L.s1[j] += ap * ds1[j];
+            L.s2[j] += ap * ds2[j];
+            L.l1[j] += ad * dl1[j];
+            L.l2[j] += ad * dl2[j];
+        }
+    }
+    return 2;
+}
+
+// Objective of a trajectory (y = v_1 .. v_N under region code), term by term as the reference
+// writes it with min_1_norm (fleet_decent_mld.py:107-169): Q_ii |e_i| of the tracking errors,
+// Q_u |u|, Q_du |du| and w * max(0, .) slacks, constants included.
+template <int N>
+HVP_HD inline double l1_direct_cost(const double* y, const hvp_system& S, const Consts& C, int role, const double* prm,
+                                    uint64_t code) {
+    const double* xf = prm + 2;
+    const double* xb = prm + 2 + 2 * (N + 1);
+    const double* xl = prm + 2 + 4 * (N + 1);
+    const int K1 = N + 1;
+    const bool tf = (role & HVP_ROLE_TRACK_FRONT) != 0, tb = (role & HVP_ROLE_TRACK_BACK) != 0;
+    const bool tl = (role & HVP_ROLE_TRACK_LEADER) != 0, lsp = (role & HVP_ROLE_LEADER_SPACING) != 0;
+    const bool sf = (role & HVP_ROLE_SAFE_FRONT) != 0, sb = (role & HVP_ROLE_SAFE_BACK) != 0;
+    double J = 0.0, p = prm[0], v = prm[1], uprev = 0.0;
+    for (int k = 0; k <= N; ++k) {
+        auto nrm = [&](double ep, double ev) { return C.Qpp * fabs(ep) + C.Qvv * fabs(ev); };
+        if (tf) J += nrm(p + C.t0 * v + C.d0 - xf[k], v - xf[K1 + k]);
+        if (tb) J += nrm(xb[k] + C.t0 * xb[K1 + k] + C.d0 - p, xb[K1 + k] - v);
+        if (tl) J += nrm(p - xl[k] + (lsp ? C.t0 * v + C.d0 : 0.0), v - xl[K1 + k]);
+        if (sf) J += C.w * fmax(0.0, p - xf[k] + C.d_safe);
+        if (sb) J += C.w * fmax(0.0, xb[k] + C.d_safe - p);
+        if (k < N) {
+            const int r = code_region(code, k);
+            const double u = (y[k] - S.a[r] * v - S.c[r]) / S.b[r];
+            J += C.Qu * fabs(u);
+            if (k >= 1) J += C.Qdu * fabs(u - uprev);
+            uprev = u;
+            p = p + S.ts * v;
+            v = y[k];
+        }
+    }
+    return J;
+}
+
+}  // namespace hvp

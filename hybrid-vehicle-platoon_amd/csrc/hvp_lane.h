@@ -21,6 +21,7 @@
 #include "hvp_coop.h"
 #include "hvp_gi.h"
 #include "hvp_ipm.h"
+#include "hvp_l1.h"
 
 namespace hvp_k {
 
@@ -155,6 +156,38 @@ __global__ __launch_bounds__(kBlock) void k_qp_ipm(const hvp_system* __restrict_
     if ((threadIdx.x & 63) == 0 && iter_sum) atomicAdd(&ws.counter[1], iter_sum);
 }
 
+// K_qp_l1: min_1_norm problems (hvp_l1.h), every candidate's fixed-sequence LP by the
+// interior-point method.  The rows live in the lane's private segment (dense, up to ~19 KB per
+// lane at N = 8), so the kernel runs small blocks over a grid-stride loop; this path is the
+// L1 / MILP variant of the reference, not the quadratic headline path.
+constexpr int kL1Block = 64;
+template <int N>
+__global__ __launch_bounds__(kL1Block) void k_qp_l1(const hvp_system* __restrict__ systems,
+                                                    const int32_t* __restrict__ sys, const int32_t* __restrict__ role,
+                                                    const double* __restrict__ params, hvp::Consts C, Workspace ws) {
+    const unsigned long long reserved = ws.counter[0];
+    const long long total = (long long)(reserved < (unsigned long long)ws.cap ? reserved : ws.cap);
+    unsigned long long iter_sum = 0;
+    for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (long long)gridDim.x * blockDim.x) {
+        const int inst = ws.task_inst[t];
+        if (inst < 0) continue;  // dead slot of an overflowed instance
+        const hvp_system& S = systems[sys[inst]];
+        const double* prm = params + (size_t)inst * (2 + 6 * (N + 1));
+        hvp::L1Lp<N> L;
+        hvp::l1_setup<N>(L, S, C, role[inst], prm, ws.task_code[t]);
+        int iters = 0;
+        const int status = hvp::l1_solve<N>(L, prm[1], hvp::kL1MaxIter, iters);
+        ws.task_stat[t] = status | (iters << 8);
+#pragma unroll
+        for (int k = 0; k < N; ++k) ws.task_y[t * N + k] = L.y[k];
+        iter_sum += (unsigned long long)iters;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) iter_sum += __shfl_down(iter_sum, off, 64);
+    if ((threadIdx.x & 63) == 0 && iter_sum) atomicAdd(&ws.counter[1], iter_sum);
+}
+
 // ------------------------------------------------------------------ K_cost
 // Objective of every converged candidate, evaluated term by term on its trajectory (separate
 // launch: fused into K_qp its reference loads stay live across the IPM and spill).
@@ -177,7 +210,8 @@ __global__ __launch_bounds__(kBlock) void k_cost(const hvp_system* __restrict__ 
             q.has_sb = (rl & HVP_ROLE_SAFE_BACK) != 0;
 #pragma unroll
             for (int k = 0; k < N; ++k) q.y[k] = ws.task_y[t * N + k];
-            cost = hvp::direct_cost<N>(q, S, C, rl, prm, ws.task_code[t]);
+            cost = C.l1 ? hvp::l1_direct_cost<N>(q.y, S, C, rl, prm, ws.task_code[t])
+                        : hvp::direct_cost<N>(q, S, C, rl, prm, ws.task_code[t]);
         }
         ws.task_cost[t] = cost;
     }
@@ -1445,13 +1479,21 @@ int launch_all(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
     const long long want = std::min<long long>(grid_for(h->ws.cap), (long long)h->n_cu * 8);
     HIP_TRY(hipEventRecord(h->evq0, st));
     const size_t lds = sizeof(double) * hvp::F_COUNT * N * kBlock;
-    hipLaunchKernelGGL(k_qp_gi<N>, dim3((int)want), dim3(kBlock), lds, st, h->d_sys, sys, role, params, h->C, ws);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(h->evq1, st));
-    // fallback list (normally empty: the launch reads a zero count and exits)
-    hipLaunchKernelGGL(k_qp_ipm<N>, dim3(std::max(1, h->n_cu)), dim3(kBlock), lds, st, h->d_sys, sys, role,
-                       params, h->C, ws);
-    HIP_TRY(hipGetLastError());
+    if (h->C.l1) {
+        // min_1_norm: the fixed-sequence LPs (4 waves per CU: bounded private-segment footprint)
+        hipLaunchKernelGGL(k_qp_l1<N>, dim3(std::max(1, h->n_cu) * 4), dim3(kL1Block), 0, st, h->d_sys, sys, role,
+                           params, h->C, ws);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(h->evq1, st));
+    } else {
+        hipLaunchKernelGGL(k_qp_gi<N>, dim3((int)want), dim3(kBlock), lds, st, h->d_sys, sys, role, params, h->C, ws);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(h->evq1, st));
+        // fallback list (normally empty: the launch reads a zero count and exits)
+        hipLaunchKernelGGL(k_qp_ipm<N>, dim3(std::max(1, h->n_cu)), dim3(kBlock), lds, st, h->d_sys, sys, role,
+                           params, h->C, ws);
+        HIP_TRY(hipGetLastError());
+    }
     hipLaunchKernelGGL(k_cost<N>, dim3((int)want), dim3(kBlock), 0, st, h->d_sys, sys, role, params, h->C, ws);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_select<N>, dim3(grid_for(B)), dim3(kBlock), 0, st, B, h->d_sys, sys, params, ws, u_out,

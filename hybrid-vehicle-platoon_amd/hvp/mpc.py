@@ -152,8 +152,10 @@ class LocalMpcMld(MpcMld):
     def setup_cost_and_constraints(self, u, spacing_policy=ConstantSpacingPolicy(50), quadratic_cost: bool = True,
                                    is_front: bool = False, is_leader=False, is_trailer=False,
                                    accel_cnstr_tightening: float = 0.0, real_vehicle_as_reference: bool = False):
-        if not quadratic_cost:
-            raise NotImplementedError("the GPU path implements the quadratic cost (min_2_norm) only")
+        # quadratic_cost=False (min_1_norm, fleet_decent_mld.py:73-76): the fixed-sequence LPs of
+        # csrc/hvp_l1.h under exhaustive enumeration (N <= HVP_MAX_N_ENUM; hvp_create refuses longer
+        # horizons with HVP_E_UNSUPPORTED)
+        self.quadratic_cost = quadratic_cost
         self.is_front, self.is_leader, self.is_trailer = is_front, is_leader, is_trailer
         self.spacing_policy = spacing_policy
         self.role = tables.role_bits(is_front, is_trailer, is_leader, real_vehicle_as_reference)

@@ -91,16 +91,16 @@ def solve_set(systems, masses_idx, cfg, N, params, roles, quadratic=True):
     return {k: np.array(v) for k, v in out.items()}
 
 
-def save(name, N, masses, cfg, params, roles, sys_idx, exp, method=0, model=0):
+def save(name, N, masses, cfg, params, roles, sys_idx, exp, method=0, model=0, quadratic=1):
     path = os.path.join(HERE, name)
     np.savez_compressed(path, N=N, masses=np.asarray(masses, float), cfg=cfg.vector(), params=params,
                         roles=roles.astype(np.int32), sys=np.asarray(sys_idx, np.int32), method=method, model=model,
-                        **{f"exp_{k}": v for k, v in exp.items()})
+                        quadratic=quadratic, **{f"exp_{k}": v for k, v in exp.items()})
     cert = exp["certified"][exp["status"] == 0].mean() if (exp["status"] == 0).any() else 0
     print(f"{name}: {len(roles)} instances, optimal {int((exp['status'] == 0).sum())}, certified {cert:.3f}")
 
 
-def decent_seeds(n, N, seeds, mass=800.0, cfg=None, system=None):
+def decent_seeds(n, N, seeds, mass=800.0, cfg=None, system=None, quadratic=True):
     cfg = cfg or O.Cfg()
     P, R = [], []
     for s in seeds:
@@ -110,7 +110,40 @@ def decent_seeds(n, N, seeds, mass=800.0, cfg=None, system=None):
     params, roles = np.concatenate(P), np.concatenate(R)
     sys_idx = np.zeros(len(roles), np.int32)
     system = system or O.gear_pwa_system(mass)
-    return params, roles, sys_idx, solve_set([system], sys_idx, cfg, N, params, roles)
+    return params, roles, sys_idx, solve_set([system], sys_idx, cfg, N, params, roles, quadratic)
+
+
+def l1_fixtures():
+    """min_1_norm (quadratic_cost=False, fleet_decent_mld.py:73-76): the local MILP optima of the
+    oracle, whose L1 path is checked against HiGHS milp on the reference's big-M MLD
+    (tests/test_oracle.py).  Files l1_*.npz carry quadratic = 0."""
+    N = 5
+    params, roles, si, exp = decent_seeds(10, N, range(4), quadratic=False)
+    save("l1_decent_n10_N5.npz", N, [800.0], O.Cfg(), params, roles, si, exp, quadratic=0)
+    cfg = O.Cfg(Qdu=0.5)
+    params, roles, si, exp = decent_seeds(4, N, range(3), cfg=cfg, quadratic=False)
+    save("l1_variant_n4_N5_qdu.npz", N, [800.0], cfg, params, roles, si, exp, quadratic=0)
+    for NN in (3, 7):
+        params, roles, si, exp = decent_seeds(3, NN, range(2), quadratic=False)
+        save(f"l1_variant_n3_N{NN}.npz", NN, [800.0], O.Cfg(), params, roles, si, exp, quadratic=0)
+    P, R = [], []
+    for s in range(2):
+        p, r = decent_instances(O.env_initial_state(5, s), N, leader_window(N), leader_index=2)
+        P.append(p)
+        R.append(r)
+        p, r = decent_instances(O.env_initial_state(5, s + 10), N, leader_window(N, 0, 3100.0),
+                                real_vehicle_as_reference=True)
+        P.append(p)
+        R.append(r)
+    params, roles = np.concatenate(P), np.concatenate(R)
+    si = np.zeros(len(roles), np.int32)
+    cfg = O.Cfg(d0=10.0, t0=3.0)  # time-headway spacing (task_2): t0 enters every position error
+    exp = solve_set([O.gear_pwa_system(800.0)], si, cfg, N, params, roles, quadratic=False)
+    save("l1_roles_n5_N5.npz", N, [800.0], cfg, params, roles, si, exp, quadratic=0)
+    g = O.gear_friction_mld_system(800.0)
+    params, roles, si, exp = decent_seeds(4, N, range(2), system=g, quadratic=False)
+    exp["gear"] = g["gear"][exp["region"]]
+    save("l1_gear_n4_N5.npz", N, [800.0], O.Cfg(), params, roles, si, exp, model=1, quadratic=0)
 
 
 def gear_model():
@@ -487,6 +520,9 @@ def main():
         return
     if len(sys.argv) > 1 and sys.argv[1] == "gear":
         gear_model()
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == "l1":
+        l1_fixtures()
         return
     N = 5
     params, roles, si, exp = hard_cases(N)

@@ -11,9 +11,15 @@ GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
 def fixture_names() -> list[str]:
-    """The decentralised local-MIQP fixtures (the ADMM and centralised ones have their own layouts)."""
+    """The decentralised local-MIQP fixtures (the ADMM and centralised ones have their own layouts,
+    the min_1_norm ones are listed by :func:`l1_fixture_names`)."""
     return sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLDEN, "*.npz"))
-                  if not os.path.basename(p).startswith(("admm_", "gadmm_", "cent_")))
+                  if not os.path.basename(p).startswith(("admm_", "gadmm_", "cent_", "l1_")))
+
+
+def l1_fixture_names() -> list[str]:
+    """The decentralised local-MILP fixtures of the min_1_norm cost (quadratic_cost=False)."""
+    return sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLDEN, "l1_*.npz")))
 
 
 def load(name: str) -> dict:
@@ -43,7 +49,8 @@ def product_problem(fx: dict):
     from hvp.models import PwaFrictionVehicle
 
     cp = CfgParams(fx["cfg"])
-    prob = tables.problem(int(fx["N"]), ConstantTimePolicy(cp.d0, cp.t0), accel_cnstr_tightening=cp.tight, params=cp)
+    prob = tables.problem(int(fx["N"]), ConstantTimePolicy(cp.d0, cp.t0), bool(int(fx.get("quadratic", 1))),
+                          accel_cnstr_tightening=cp.tight, params=cp)
     systems = []
     for m in fx["masses"]:
         if int(fx.get("model", 0)) == 1:  # LocalMpcGear on pwa_friction

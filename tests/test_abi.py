@@ -57,6 +57,14 @@ def test_invalid_arguments_fail_loudly_without_touching_the_gpu():
     assert "enumeration" in _abi.last_error()
     badm = tables.problem(5, method=7)
     assert lib.hvp_create(ctypes.byref(h), ctypes.byref(badm), sysv, 1, 0) == -1
-    l1 = tables.problem(5)
-    l1.quadratic_cost = 0
-    assert lib.hvp_create(ctypes.byref(h), ctypes.byref(l1), sysv, 1, 0) == -3
+    # min_1_norm runs for the decentralised formulation by enumeration (N <= HVP_MAX_N_ENUM) only
+    for l1 in (tables.problem(10, quadratic_cost=False), tables.problem(5, quadratic_cost=False, method=_abi.METHOD_BNB)):
+        assert lib.hvp_create(ctypes.byref(h), ctypes.byref(l1), sysv, 1, 0) == -3
+        assert "min_1_norm" in _abi.last_error()
+    from hvp.admm import admm_problem
+
+    l1a = admm_problem(5, 0.5, quadratic_cost=False)
+    assert lib.hvp_create(ctypes.byref(h), ctypes.byref(l1a), sysv, 1, 0) == -3
+    badq = tables.problem(5)
+    badq.quadratic_cost = 2
+    assert lib.hvp_create(ctypes.byref(h), ctypes.byref(badq), sysv, 1, 0) == -1

@@ -1,0 +1,129 @@
+"""GPU parity of the min_1_norm cost (quadratic_cost=False, fleet_decent_mld.py:73-76).
+
+The local MILP of LocalMpcMld / LocalMpcGear with the L1 norm: the device enumerates the
+velocity-feasible region sequences (k_enum), solves every fixed-sequence LP by the interior
+point of csrc/hvp_l1.h (k_qp_l1), prices it term by term (k_cost) and applies the same tie rule
+(k_select).  Checked against the oracle's MILP optima (the oracle's L1 path is pinned to HiGHS
+milp on the reference's big-M MLD, tests/test_oracle.py).  Bar: region sequences, gears and
+sequence counts exact; cost 1e-9 relative; u 1e-6; x 1e-4 (positions ~3e3).
+"""
+
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import oracle as O
+from golden_io import expected_gears, l1_fixture_names, load, product_problem
+from instances import decent_instances, leader_window, oracle_solve
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("name", l1_fixture_names())
+def test_l1_golden_fixture_on_gpu(gpu_available, name):
+    from hvp.solver import BatchSolver
+
+    fx = load(name)
+    prob, systems = product_problem(fx)
+    assert prob.quadratic_cost == 0
+    s = BatchSolver(prob, systems)
+    res = s.solve(fx["sys"], fx["roles"], fx["params"])
+    assert np.array_equal(res.status, fx["exp_status"])
+    assert np.array_equal(res.nodes, fx["exp_nodes"])
+    assert np.array_equal(res.region, fx["exp_region"])
+    assert np.array_equal(res.gear, expected_gears(fx))
+    ce = fx["exp_cost"]
+    assert np.all(np.abs(res.cost - ce) <= 1e-9 * np.maximum(1, np.abs(ce)))
+    assert np.abs(res.u - fx["exp_u"]).max() <= 1e-6
+    assert np.abs(res.x - fx["exp_x"]).max() <= 1e-4
+
+
+def _l1_cost(x, u, params, roles, N, cfg=O.Cfg()):
+    """min_1_norm objective of trajectories (numpy restatement of fleet_decent_mld.py:107-169)."""
+    K1 = N + 1
+    xf = params[:, 2:2 + 2 * K1].reshape(-1, 2, K1)
+    xb = params[:, 2 + 2 * K1:2 + 4 * K1].reshape(-1, 2, K1)
+    xl = params[:, 2 + 4 * K1:].reshape(-1, 2, K1)
+    p, v = x[:, 0, :], x[:, 1, :]
+    has = lambda bit: ((roles & bit) != 0)[:, None]  # noqa: E731
+    J = np.zeros(len(roles))
+    J += (has(O.ROLE_TRACK_FRONT) * (cfg.Qx[0] * np.abs(p + cfg.d0 - xf[:, 0]) + cfg.Qx[3] * np.abs(v - xf[:, 1]))).sum(1)
+    J += (has(O.ROLE_TRACK_BACK) * (cfg.Qx[0] * np.abs(xb[:, 0] + cfg.d0 - p) + cfg.Qx[3] * np.abs(xb[:, 1] - v))).sum(1)
+    J += (has(O.ROLE_TRACK_LEADER) * (cfg.Qx[0] * np.abs(p - xl[:, 0]) + cfg.Qx[3] * np.abs(v - xl[:, 1]))).sum(1)
+    J += (has(O.ROLE_SAFE_FRONT) * cfg.w * np.maximum(0, p - xf[:, 0] + cfg.d_safe)).sum(1)
+    J += (has(O.ROLE_SAFE_BACK) * cfg.w * np.maximum(0, xb[:, 0] + cfg.d_safe - p)).sum(1)
+    J += cfg.Qu * np.abs(u).sum(1)
+    return J
+
+
+def test_l1_platoon_batch(gpu_available):
+    """4096 local MILPs (n = 10, N = 5, 410 platoon seeds): every answer feasible, its reported
+    cost the min_1_norm objective of its own (x, u), deterministic, and a sample equal to the
+    oracle's MILP optimum (sequence, cost, u)."""
+    import torch
+
+    from hvp import tables
+    from hvp.models import PwaGearVehicle
+    from hvp.solver import BatchSolver
+
+    n, N = 10, 5
+    veh = PwaGearVehicle(800.0)
+    s = BatchSolver(tables.problem(N, quadratic_cost=False), [tables.system_from_dict(veh.get_discrete_system(1),
+                                                                                       tables.gears_of(veh))])
+    P, R = [], []
+    for seed in range(410):
+        p, r = decent_instances(O.env_initial_state(n, seed), N, leader_window(N))
+        P.append(p)
+        R.append(r)
+    params, roles = np.concatenate(P), np.concatenate(R)
+    dev = torch.device("cuda", 0)
+    tp, tr = torch.from_numpy(params).to(dev), torch.from_numpy(roles).to(dev)
+    ts = torch.zeros(len(roles), dtype=torch.int32, device=dev)
+    a = s.solve_device(ts, tr, tp)
+    b = s.solve_device(ts, tr, tp)
+    torch.cuda.synchronize()
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
+    st = a["status"].cpu().numpy()
+    assert (st == 0).all()
+    u, x, reg = a["u"].cpu().numpy(), a["x"].cpu().numpy(), a["region"].cpu().numpy()
+    cost = a["cost"].cpu().numpy()
+    assert np.abs(u).max() <= 1 + 1e-9
+    v = x[:, 1, :]
+    assert v[:, 1:].min() >= 3.94 - 1e-9 and v[:, 1:].max() <= 45.84 + 1e-9
+    dv = np.diff(v, axis=1)
+    assert dv.min() >= -2 - 1e-9 and dv.max() <= 2.5 + 1e-9
+    lim = np.array([-np.inf, 9.235, 12.855, 16.93, 22.92, 23.315, 32.47, np.inf])
+    assert np.all(v[:, :N] >= lim[reg] - 1e-7) and np.all(v[:, :N] <= lim[reg + 1] + 1e-7)
+    g = O.gear_pwa_system(800.0)
+    assert np.abs(g["A"][reg, 1, 1] * v[:, :N] + g["B"][reg, 1] * u + g["c"][reg, 1] - v[:, 1:]).max() <= 1e-9
+    assert np.all(np.abs(_l1_cost(x, u, params, roles, N) - cost) <= 1e-9 * np.maximum(1, np.abs(cost)))
+    rng = np.random.default_rng(1)
+    idx = rng.choice(len(roles), 40, replace=False)
+    ref = oracle_solve(g, O.Cfg(), N, params[idx], roles[idx], quadratic=False)
+    for j, r in zip(idx, ref):
+        assert list(reg[j]) == list(r.sigma), j
+        assert abs(cost[j] - r.cost) <= 1e-9 * max(1.0, abs(r.cost)), j
+        assert np.abs(u[j] - r.u).max() <= 1e-6, j
+
+
+def test_l1_local_mpc_api(gpu_available):
+    """The reference call surface: LocalMpcMld(quadratic_cost=False).solve_mpc after the setters."""
+    from hvp.models import PwaGearVehicle
+    from hvp.mpc import LocalMpcMld
+
+    N = 5
+    veh = PwaGearVehicle(800.0)
+    mpc = LocalMpcMld(N, veh.get_discrete_system(1), quadratic_cost=False)
+    x = O.env_initial_state(3, 7).reshape(-1)
+    xf = O.constant_velocity_prediction(x[0], x[1], N)
+    xb = O.constant_velocity_prediction(x[4], x[5], N)
+    mpc.set_x_front(xf)
+    mpc.set_x_back(xb)
+    u0, info = mpc.solve_mpc(x[2:4].reshape(2, 1))
+    r = O.solve_miqp(O.gear_pwa_system(800.0), O.Cfg(), N, O.role_bits(1, 3, 0, False), x[2:4], xf, xb,
+                     np.zeros((2, N + 1)), quadratic=False)
+    assert abs(info["cost"] - r.cost) <= 1e-9 * max(1.0, abs(r.cost))
+    assert np.abs(info["u"].ravel() - r.u).max() <= 1e-6
+    assert abs(float(u0[0, 0]) - r.u[0]) <= 1e-6
