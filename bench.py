@@ -112,7 +112,7 @@ def make_inputs(seeds, n: int, N: int):
     return params, roles
 
 
-def cpu_baseline(n: int, N: int, budget_s: float, threads: int):
+def cpu_baseline(n: int, N: int, budget_s: float, threads: int, quadratic: bool = True):
     """The CPU oracle (oracle/hvp_oracle.c, OpenMP over instances) on a bounded sample."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
@@ -126,14 +126,16 @@ def cpu_baseline(n: int, N: int, budget_s: float, threads: int):
     while time.perf_counter() - t0 < budget_s:
         params, roles = make_inputs(range(seed, seed + chunk), n, N)
         seed += chunk
-        O.solve_batch([sysd], O.Cfg(), N, np.zeros(len(roles), np.int32), roles, params, nthreads=threads)
+        O.solve_batch([sysd], O.Cfg(), N, np.zeros(len(roles), np.int32), roles, params, quadratic=quadratic,
+                      nthreads=threads)
         done += chunk
     dt = time.perf_counter() - t0
     return {"value": done / dt, "unit": "platoon-timesteps/s", "cores": threads, "kind": "port",
-            "sample": f"{done} platoons x {n} local MIQPs (N={N}) by oracle/hvp_oracle.c, {dt:.1f} s"}
+            "sample": f"{done} platoons x {n} local {'MIQPs' if quadratic else 'MILPs (min_1_norm)'} (N={N}) by "
+                      f"oracle/hvp_oracle.c, {dt:.1f} s"}
 
 
-def hostref_baseline(n: int, N: int, budget_s: float, threads: int, method: int = 0):
+def hostref_baseline(n: int, N: int, budget_s: float, threads: int, method: int = 0, quadratic: bool = True):
     """The product's lane algorithm compiled for the host cores (extra, fairer CPU number)."""
     import ctypes
 
@@ -145,7 +147,7 @@ def hostref_baseline(n: int, N: int, budget_s: float, threads: int, method: int 
     L = ctypes.CDLL(_abi.HOSTREF_PATH)
     veh = PwaGearVehicle(800)
     S = (_abi.HvpSystem * 1)(tables.system_from_dict(veh.get_discrete_system(1), tables.gears_of(veh)))
-    prob = tables.problem(N, method=method)
+    prob = tables.problem(N, quadratic_cost=quadratic, method=method)
     done, seed = 0, 20_000_000
     chunk = max(threads, 1) * 16
     t0 = time.perf_counter()
@@ -782,6 +784,8 @@ def main() -> None:
     ap.add_argument("--no-warm-incumbent", action="store_true",
                     help="admm: do not try the previous iteration's sequences as incumbents (A/B)")
     ap.add_argument("--gadmm-layout", choices=["replicas", "vehicles"], default="replicas")
+    ap.add_argument("--cost", choices=["quadratic", "l1"], default="quadratic",
+                    help="decent: min_2_norm (default) or min_1_norm (the MILP variant, enumeration, N <= 8)")
     args = ap.parse_args()
 
     import torch
@@ -814,6 +818,9 @@ def main() -> None:
     veh = PwaGearVehicle(800)
     system = tables.system_from_dict(veh.get_discrete_system(1), tables.gears_of(veh))
     method = {"auto": 0, "enum": 1, "bnb": 2}[args.method]
+    quadratic = args.cost == "quadratic"
+    if not quadratic:
+        method = 1  # the min_1_norm LPs run under exhaustive enumeration (hvp_l1.h)
     # each rank owns a disjoint seed range: platoons are independent (weak scaling)
     params, roles = make_inputs(range(rank * S, (rank + 1) * S), n, N)
     B = len(roles)
@@ -827,7 +834,7 @@ def main() -> None:
     chunks = []
     for j in range(K):
         a, b = cuts[j], cuts[j + 1]
-        sv = BatchSolver(tables.problem(N, method=method), [system], device=local)
+        sv = BatchSolver(tables.problem(N, quadratic_cost=quadratic, method=method), [system], device=local)
         sv.reserve(b - a)
         chunks.append((sv, torch.zeros(b - a, dtype=torch.int32, device=dev), t_roles_all[a:b].contiguous(),
                        t_params_all[a:b].contiguous(), sv.alloc_outputs(b - a, dev),
@@ -891,17 +898,17 @@ def main() -> None:
         qk = [("k_bnb_root_coop", 1), ("k_bnb_bound_coop", N)] if N > 8 else [("k_bnb_root", 1),
                                                                               ("k_bnb_bound_refill", N)]
     else:
-        qk = [("k_qp_gi", 1)]
+        qk = [("k_qp_gi", 1)] if quadratic else [("k_qp_l1", 1)]
     # the PMC figures are per launch over the WHOLE batch (profiles are taken with --streams 1);
     # with K streams the K chunks' QP launches overlap, so the time is the step's wall time
     roofline = qp_roofline(qp_step_ms if K == 1 else dt / args.steps * 1e3, qk, notional,
-                           f"decent_n{n}_N{N}" + ("" if bnb else "_enum"))
+                           f"decent_n{n}_N{N}" + ("" if bnb else "_enum") + ("" if quadratic else "_l1"))
     if K > 1:
         roofline["time_basis"] = (f"wall time of the step: the QP launches of the {K} streams overlap "
                                   f"(their sequential event time is {qp_step_ms:.3f} ms)")
 
     result = {
-        "metric": f"MPC timesteps/sec (whole platoon) at n={n} N={N} decent_mld",
+        "metric": f"MPC timesteps/sec (whole platoon) at n={n} N={N} decent_mld" + ("" if quadratic else " min_1_norm"),
         "value": value,
         "unit": "platoon-timesteps/s",
         "n_gpus": world,
@@ -917,6 +924,7 @@ def main() -> None:
         "config": {"workload": (f"fleet_decent_mld n={n} N={N} pwa_gear"
                                 + (" (configs[1])" if (n, N) == (10, 5) else " (configs[4] sweep point)")),
                    "n_vehicles": n, "horizon": N, "search": "branch-and-bound" if bnb else "enumeration",
+                   "cost": "min_2_norm (MIQP)" if quadratic else "min_1_norm (MILP)",
                    "platoons_per_gpu": S, "local_miqps_per_step": B * world, "streams_per_gpu": K,
                    "parallelism": f"seeds-sharded x{world}"},
         "roofline": roofline,
@@ -929,12 +937,13 @@ def main() -> None:
         # every core this job may use: the pool gives each GPU a 16-core share (OMP_NUM_THREADS=16
         # on the box; nproc shows the whole machine), plus a 1-core run
         threads = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16")), 16)
-        result["cpu_baseline"] = cpu_baseline(n, N, args.cpu_budget, threads)
-        result["cpu_baseline_1core"] = cpu_baseline(n, N, args.cpu_budget * 0.5, 1)
-        hr = hostref_baseline(n, N, min(args.cpu_budget, 10.0), threads, method)
+        result["cpu_baseline"] = cpu_baseline(n, N, args.cpu_budget, threads, quadratic)
+        result["cpu_baseline_1core"] = cpu_baseline(n, N, args.cpu_budget * 0.5, 1, quadratic)
+        hr = hostref_baseline(n, N, min(args.cpu_budget, 10.0), threads, method, quadratic)
         if hr:
             result["cpu_same_algorithm"] = hr
-            result["cpu_same_algorithm_1core"] = hostref_baseline(n, N, min(args.cpu_budget, 10.0) * 0.5, 1, method)
+            result["cpu_same_algorithm_1core"] = hostref_baseline(n, N, min(args.cpu_budget, 10.0) * 0.5, 1, method,
+                                                                  quadratic)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist:

@@ -292,9 +292,10 @@ HVP_HD inline int l1_solve(L1Lp<N>& L, double v0, int max_iter, int& iters) {
         wmax = fmax(wmax, L.wp[j]);
         hscale = fmax(hscale, fabs(L.e0[j]));
     }
+    // the corrector overwrites the predictor's directions in place (row i reads its own
+    // predictor ds_i dl_i before writing them), which keeps the lane's private segment small
     double dy[N], dt[L1Lp<N>::MP];
-    double dsh[L1Lp<N>::MH], dlh[L1Lp<N>::MH], ds1[L1Lp<N>::MP], dl1[L1Lp<N>::MP], ds2[L1Lp<N>::MP],
-        dl2[L1Lp<N>::MP];
+    double *dsh = L.dsh, *dlh = L.dlh, *ds1 = L.ds1, *dl1 = L.dl1, *ds2 = L.ds2, *dl2 = L.dl2;
     for (iters = 0; iters < max_iter; ++iters) {
         // residuals and the duality measure
         double gap = 0.0, obj = 0.0, rpmax = 0.0, rdmax = 0.0;

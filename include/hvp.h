@@ -67,7 +67,10 @@ typedef struct hvp_system {
  * (misc/common_controller_params.py:14-23, fleet_decent_mld.py:61-208). */
 typedef struct hvp_problem {
     int32_t N;              /* prediction horizon (2..HVP_MAX_N)                      */
-    int32_t quadratic_cost; /* 1 = min_2_norm (only form supported on the GPU)         */
+    int32_t quadratic_cost; /* 1 = min_2_norm (MIQP); 0 = min_1_norm (MILP,
+                               fleet_decent_mld.py:73-76): HVP_FORM_DECENT with N <=
+                               HVP_MAX_N_ENUM by enumeration (method AUTO / ENUMERATE;
+                               fixed-sequence LPs of csrc/hvp_l1.h), else HVP_E_UNSUPPORTED */
     double Qx[4];           /* 2x2 row-major state-tracking weight                     */
     double Qu;              /* control weight                                          */
     double Qdu;             /* control-variation weight                                */
