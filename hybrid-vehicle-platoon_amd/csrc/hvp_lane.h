@@ -1480,8 +1480,8 @@ int launch_all(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
     HIP_TRY(hipEventRecord(h->evq0, st));
     const size_t lds = sizeof(double) * hvp::F_COUNT * N * kBlock;
     if (h->C.l1) {
-        // min_1_norm: the fixed-sequence LPs (4 waves per CU: bounded private-segment footprint)
-        hipLaunchKernelGGL(k_qp_l1<N>, dim3(std::max(1, h->n_cu) * 4), dim3(kL1Block), 0, st, h->d_sys, sys, role,
+        // min_1_norm: the fixed-sequence LPs (16 one-wave blocks per CU, 8 resident: the private segment and VGPRs bound the occupancy to 2 waves per SIMD; grid-stride over the candidates)
+        hipLaunchKernelGGL(k_qp_l1<N>, dim3(std::max(1, h->n_cu) * 16), dim3(kL1Block), 0, st, h->d_sys, sys, role,
                            params, h->C, ws);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(h->evq1, st));
