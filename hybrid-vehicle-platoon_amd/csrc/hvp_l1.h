@@ -61,32 +61,33 @@ HVP_HD inline double l1_dot(const double* g, const double* y) {
 }
 
 // Rows of the fixed-sequence LP of instance params prm (x0, x_front, x_back, leader_x) and
-// region code.  Returns false when the constant row p_1 in [pmin, pmax] is violated.
-template <int N>
-HVP_HD inline bool l1_setup(L1Lp<N>& L, const hvp_system& S, const Consts& C, int role, const double* prm,
-                            uint64_t code) {
+// region code, in a fixed order: hard(idx, g, sgn, h) for the row sgn*g.y <= h and
+// pair(idx, g, e0, w, alpha) for every term with a variable part (zero-weight and constant terms
+// are skipped, so the indices are dense).  Both callbacks see every row in the same order on
+// every lane: the per-lane host solver stores them all (l1_setup), the wave-cooperative kernel
+// (hvp_lane.h k_qp_l1) keeps the rows whose index maps to its lane.  Returns (mh, mp) through the
+// counters and false when the constant row p_1 in [pmin, pmax] is violated.
+template <int N, class FH, class FP>
+HVP_HD inline bool l1_rows(const hvp_system& S, const Consts& C, int role, const double* prm, uint64_t code,
+                           int& mh, int& mp, FH&& hard_cb, FP&& pair_cb) {
     const double p0 = prm[0], v0 = prm[1];
     const double* xf = prm + 2;
     const double* xb = prm + 2 + 2 * (N + 1);
     const double* xl = prm + 2 + 4 * (N + 1);
     const int K1 = N + 1;
     const double ts = S.ts, P1 = p0 + ts * v0;
-    L.mh = 0;
-    L.mp = 0;
+    mh = 0;
+    mp = 0;
     auto hard = [&](const double* g, double sgn, double hh) {
-        for (int i = 0; i < N; ++i) L.gh[L.mh][i] = sgn * g[i];
-        L.h[L.mh] = hh;
-        ++L.mh;
+        hard_cb(mh, g, sgn, hh);
+        ++mh;
     };
     auto pair = [&](const double* g, double e0, double w, double alpha) {
         bool any = false;
         for (int i = 0; i < N; ++i) any = any || g[i] != 0.0;
         if (!(w > 0.0) || !any) return;  // zero weight, or a constant term (in the direct cost)
-        for (int i = 0; i < N; ++i) L.gp[L.mp][i] = g[i];
-        L.e0[L.mp] = e0;
-        L.wp[L.mp] = w;
-        L.al[L.mp] = alpha;
-        ++L.mp;
+        pair_cb(mp, g, e0, w, alpha);
+        ++mp;
     };
     double a[N], b[N], c[N];
     for (int k = 0; k < N; ++k) {
@@ -182,6 +183,24 @@ HVP_HD inline bool l1_setup(L1Lp<N>& L, const hvp_system& S, const Consts& C, in
         uprev = ubar;
     }
     return P1 >= S.pmin - 1e-9 * (1.0 + fabs(S.pmin)) && P1 <= S.pmax + 1e-9 * (1.0 + fabs(S.pmax));
+}
+
+// All rows into the lane's arrays (host build and per-lane use).
+template <int N>
+HVP_HD inline bool l1_setup(L1Lp<N>& L, const hvp_system& S, const Consts& C, int role, const double* prm,
+                            uint64_t code) {
+    return l1_rows<N>(
+        S, C, role, prm, code, L.mh, L.mp,
+        [&](int i, const double* g, double sgn, double hh) {
+            for (int a = 0; a < N; ++a) L.gh[i][a] = sgn * g[a];
+            L.h[i] = hh;
+        },
+        [&](int j, const double* g, double e0, double w, double alpha) {
+            for (int a = 0; a < N; ++a) L.gp[j][a] = g[a];
+            L.e0[j] = e0;
+            L.wp[j] = w;
+            L.al[j] = alpha;
+        });
 }
 
 // Newton direction for the complementarity targets rc_i = s_i l_i (predictor) or

@@ -157,35 +157,294 @@ __global__ __launch_bounds__(kBlock) void k_qp_ipm(const hvp_system* __restrict_
 }
 
 // K_qp_l1: min_1_norm problems (hvp_l1.h), every candidate's fixed-sequence LP by the
-// interior-point method.  The rows live in the lane's private segment (dense, up to ~19 KB per
-// lane at N = 8), so the kernel runs small blocks over a grid-stride loop; this path is the
-// L1 / MILP variant of the reference, not the quadratic headline path.
-constexpr int kL1Block = 64;
+// interior-point method, ONE LP PER WAVEFRONT: lane l owns hard row l (8N - 2 <= 62 rows) and
+// pairs l, l + 64 (10N <= 80) in registers; the N x N Newton system is the wave sum of the
+// lanes' row contributions (butterfly all-reduce, bit-identical in every lane, so the control
+// flow stays wave-uniform), factorised redundantly per lane and reused by the corrector (only its
+// right-hand side is reduced again).  No private segment: the per-lane form of the same method
+// (hvp_l1.h l1_solve, the host build's) keeps ~10 KB per lane there and is bound by that traffic.
+__device__ inline double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+__device__ inline double wave_max(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
+    return v;
+}
+__device__ inline double wave_min(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fmin(v, __shfl_xor(v, off, 64));
+    return v;
+}
+
+template <int N>
+struct L1Wave {
+    static constexpr int NPS = (10 * N + 63) / 64;  // pair slots per lane
+    static constexpr int NT = N * (N + 1) / 2;
+    bool hon;
+    double hg[N], hh, hs, hl, hds, hdl;
+    bool pon[NPS];
+    double pg[NPS][N], pe0[NPS], pw[NPS], pal[NPS], pt[NPS], ps1[NPS], ps2[NPS], pl1[NPS], pl2[NPS];
+    double pds1[NPS], pdl1[NPS], pds2[NPS], pdl2[NPS], pdt[NPS];
+
+    // this lane's share of: residuals (gap, obj, rd_y, max |rp|, max |rd_t|) when res, and the
+    // Newton system (K when withK, rhs for targets rc = s l [+ ds dl - sigmu when corr])
+    __device__ void contrib(const double* y, bool corr, double sigmu, bool withK, double* K, double* rhs, double& gap,
+                            double& obj, double* rdy, double& rpm, double& rdm) const {
+        if (hon) {
+            const double gy = hvp::l1_dot<N>(hg, y);
+            const double rp = gy + hs - hh, D = hl / hs;
+            const double rc = hs * hl + (corr ? hds * hdl - sigmu : 0.0);
+            const double rho = (hl * rp - rc) / hs, coef = -(hl + rho);
+            gap += hs * hl;
+            rpm = fmax(rpm, fabs(rp));
+#pragma unroll
+            for (int a = 0; a < N; ++a) {
+                rdy[a] += hl * hg[a];
+                rhs[a] += coef * hg[a];
+                if (withK) {
+#pragma unroll
+                    for (int c = 0; c <= a; ++c) K[hvp::tri(a, c)] += D * hg[a] * hg[c];
+                }
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < NPS; ++q) {
+            if (!pon[q]) continue;
+            const double al = pal[q], gy = hvp::l1_dot<N>(pg[q], y);
+            const double rp1 = gy - pt[q] + ps1[q] + pe0[q];
+            const double rp2 = -al * gy - pt[q] + ps2[q] - al * pe0[q];
+            const double D1 = pl1[q] / ps1[q], D2 = pl2[q] / ps2[q];
+            const double rc1 = ps1[q] * pl1[q] + (corr ? pds1[q] * pdl1[q] - sigmu : 0.0);
+            const double rc2 = ps2[q] * pl2[q] + (corr ? pds2[q] * pdl2[q] - sigmu : 0.0);
+            const double rho1 = (pl1[q] * rp1 - rc1) / ps1[q], rho2 = (pl2[q] * rp2 - rc2) / ps2[q];
+            const double rdt = pw[q] - pl1[q] - pl2[q];
+            const double rhst = -rdt + rho1 + rho2;
+            const double mt = D1 + D2, m = al * D2 - D1;
+            const double ce = D1 * D2 * (1.0 + al) * (1.0 + al) / mt;
+            const double coef = -(pl1[q] - al * pl2[q]) - (rho1 - al * rho2) - m * rhst / mt;
+            gap += ps1[q] * pl1[q] + ps2[q] * pl2[q];
+            obj += pw[q] * pt[q];
+            rpm = fmax(rpm, fmax(fabs(rp1), fabs(rp2)));
+            rdm = fmax(rdm, fabs(rdt));
+#pragma unroll
+            for (int a = 0; a < N; ++a) {
+                rdy[a] += (pl1[q] - al * pl2[q]) * pg[q][a];
+                rhs[a] += coef * pg[q][a];
+                if (withK) {
+#pragma unroll
+                    for (int c = 0; c <= a; ++c) K[hvp::tri(a, c)] += ce * pg[q][a] * pg[q][c];
+                }
+            }
+        }
+    }
+
+    // directions of this lane's rows for dy (same targets as contrib), written over the stored
+    // ones (each row reads its predictor ds dl before writing); returns the local step limits
+    __device__ void directions(const double* y, const double* dy, bool corr, double sigmu, double& ap, double& ad) {
+        if (hon) {
+            const double gy = hvp::l1_dot<N>(hg, y), gd = hvp::l1_dot<N>(hg, dy);
+            const double rp = gy + hs - hh, D = hl / hs;
+            const double rc = hs * hl + (corr ? hds * hdl - sigmu : 0.0);
+            const double rho = (hl * rp - rc) / hs;
+            hds = -rp - gd;
+            hdl = D * gd + rho;
+            hvp::l1_ratio(ap, hs, hds);
+            hvp::l1_ratio(ad, hl, hdl);
+        }
+#pragma unroll
+        for (int q = 0; q < NPS; ++q) {
+            if (!pon[q]) continue;
+            const double al = pal[q], gy = hvp::l1_dot<N>(pg[q], y), gd = hvp::l1_dot<N>(pg[q], dy);
+            const double rp1 = gy - pt[q] + ps1[q] + pe0[q];
+            const double rp2 = -al * gy - pt[q] + ps2[q] - al * pe0[q];
+            const double D1 = pl1[q] / ps1[q], D2 = pl2[q] / ps2[q];
+            const double rc1 = ps1[q] * pl1[q] + (corr ? pds1[q] * pdl1[q] - sigmu : 0.0);
+            const double rc2 = ps2[q] * pl2[q] + (corr ? pds2[q] * pdl2[q] - sigmu : 0.0);
+            const double rho1 = (pl1[q] * rp1 - rc1) / ps1[q], rho2 = (pl2[q] * rp2 - rc2) / ps2[q];
+            const double rhst = -(pw[q] - pl1[q] - pl2[q]) + rho1 + rho2;
+            const double mt = D1 + D2, m = al * D2 - D1;
+            pdt[q] = (rhst - m * gd) / mt;
+            const double a1 = gd - pdt[q], a2 = -al * gd - pdt[q];
+            pds1[q] = -rp1 - a1;
+            pdl1[q] = D1 * a1 + rho1;
+            pds2[q] = -rp2 - a2;
+            pdl2[q] = D2 * a2 + rho2;
+            hvp::l1_ratio(ap, ps1[q], pds1[q]);
+            hvp::l1_ratio(ap, ps2[q], pds2[q]);
+            hvp::l1_ratio(ad, pl1[q], pdl1[q]);
+            hvp::l1_ratio(ad, pl2[q], pdl2[q]);
+        }
+    }
+};
+
+// Mehrotra predictor-corrector (the algorithm of hvp_l1.h l1_solve), wave-cooperative.
+// Returns 0 (converged) or 2; y (uniform) holds the iterate.
+template <int N>
+__device__ int l1_wave_solve(L1Wave<N>& W, double* y, double v0, int mh, int mp, int max_iter, int& iters) {
+    constexpr int NT = L1Wave<N>::NT, NPS = L1Wave<N>::NPS;
+    const int mtot = mh + 2 * mp;
+#pragma unroll
+    for (int i = 0; i < N; ++i) y[i] = v0;
+    double hsc = 1.0, wmx = 1.0;
+    if (W.hon) {
+        W.hs = fmax(W.hh - hvp::l1_dot<N>(W.hg, y), 1.0);
+        W.hl = 1.0;
+        hsc = fmax(hsc, fabs(W.hh));
+    }
+#pragma unroll
+    for (int q = 0; q < NPS; ++q) {
+        if (!W.pon[q]) continue;
+        const double e = hvp::l1_dot<N>(W.pg[q], y) + W.pe0[q];
+        W.pt[q] = (W.pal[q] > 0.0 ? fabs(e) : fmax(e, 0.0)) + 1.0;
+        W.ps1[q] = W.pt[q] - e;
+        W.ps2[q] = W.pt[q] + W.pal[q] * e;
+        W.pl1[q] = 0.5 * W.pw[q];
+        W.pl2[q] = 0.5 * W.pw[q];
+        wmx = fmax(wmx, W.pw[q]);
+        hsc = fmax(hsc, fabs(W.pe0[q]));
+    }
+    hsc = wave_max(hsc);
+    wmx = wave_max(wmx);
+    for (iters = 0; iters < max_iter; ++iters) {
+        double K[NT], rhs[N], rdy[N];
+#pragma unroll
+        for (int i = 0; i < NT; ++i) K[i] = 0.0;
+#pragma unroll
+        for (int i = 0; i < N; ++i) rhs[i] = rdy[i] = 0.0;
+        double gap = 0.0, obj = 0.0, rpm = 0.0, rdm = 0.0;
+        W.contrib(y, false, 0.0, true, K, rhs, gap, obj, rdy, rpm, rdm);
+        gap = wave_sum(gap);
+        obj = wave_sum(obj);
+        rpm = wave_max(rpm);
+        rdm = wave_max(rdm);
+#pragma unroll
+        for (int i = 0; i < N; ++i) rdm = fmax(rdm, fabs(wave_sum(rdy[i])));
+        if (rpm <= 1e-10 * hsc && rdm <= 1e-10 * wmx && gap <= 1e-12 * fmax(1.0, fabs(obj))) return 0;
+#pragma unroll
+        for (int i = 0; i < NT; ++i) K[i] = wave_sum(K[i]);
+#pragma unroll
+        for (int i = 0; i < N; ++i) rhs[i] = wave_sum(rhs[i]);
+        const double mu = gap / mtot;
+        if (!hvp::cholesky<N>(K)) return 2;
+        double dy[N];
+        hvp::chol_solve<N>(K, rhs, dy);
+        double ap = 1.0, ad = 1.0;
+        W.directions(y, dy, false, 0.0, ap, ad);
+        ap = wave_min(ap);
+        ad = wave_min(ad);
+        double gaff = 0.0;
+        if (W.hon) gaff += (W.hs + ap * W.hds) * (W.hl + ad * W.hdl);
+#pragma unroll
+        for (int q = 0; q < NPS; ++q)
+            if (W.pon[q])
+                gaff += (W.ps1[q] + ap * W.pds1[q]) * (W.pl1[q] + ad * W.pdl1[q]) +
+                        (W.ps2[q] + ap * W.pds2[q]) * (W.pl2[q] + ad * W.pdl2[q]);
+        gaff = wave_sum(gaff);
+        const double ratio = gaff / gap;
+        const double sigmu = ratio * ratio * ratio * mu;
+        // corrector: same K, new right-hand side
+        double rhs2[N], dum[N];
+#pragma unroll
+        for (int i = 0; i < N; ++i) rhs2[i] = dum[i] = 0.0;
+        double g2 = 0.0, o2 = 0.0, r2 = 0.0, d2 = 0.0;
+        W.contrib(y, true, sigmu, false, K, rhs2, g2, o2, dum, r2, d2);
+#pragma unroll
+        for (int i = 0; i < N; ++i) rhs2[i] = wave_sum(rhs2[i]);
+        hvp::chol_solve<N>(K, rhs2, dy);
+        ap = 1.0 / 0.995;
+        ad = 1.0 / 0.995;
+        W.directions(y, dy, true, sigmu, ap, ad);
+        ap = 0.995 * wave_min(ap);
+        ad = 0.995 * wave_min(ad);
+#pragma unroll
+        for (int a = 0; a < N; ++a) y[a] += ap * dy[a];
+        if (W.hon) {
+            W.hs += ap * W.hds;
+            W.hl += ad * W.hdl;
+        }
+#pragma unroll
+        for (int q = 0; q < NPS; ++q) {
+            if (!W.pon[q]) continue;
+            W.pt[q] += ap * W.pdt[q];
+            W.ps1[q] += ap * W.pds1[q];
+            W.ps2[q] += ap * W.pds2[q];
+            W.pl1[q] += ad * W.pdl1[q];
+            W.pl2[q] += ad * W.pdl2[q];
+        }
+    }
+    return 2;
+}
+
+constexpr int kL1Block = 256;
 template <int N>
 __global__ __launch_bounds__(kL1Block) void k_qp_l1(const hvp_system* __restrict__ systems,
                                                     const int32_t* __restrict__ sys, const int32_t* __restrict__ role,
                                                     const double* __restrict__ params, hvp::Consts C, Workspace ws) {
+    static_assert(8 * N - 2 <= 64, "one hard row per lane");
     const unsigned long long reserved = ws.counter[0];
     const long long total = (long long)(reserved < (unsigned long long)ws.cap ? reserved : ws.cap);
+    const int lane = threadIdx.x & 63;
+    const long long nwaves = ((long long)gridDim.x * blockDim.x) >> 6;
     unsigned long long iter_sum = 0;
-    for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
-         t += (long long)gridDim.x * blockDim.x) {
-        const int inst = ws.task_inst[t];
-        if (inst < 0) continue;  // dead slot of an overflowed instance
+    for (long long t = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6; t < total; t += nwaves) {
+        const int inst = ws.task_inst[t];  // wave-uniform
+        if (inst < 0) continue;             // dead slot of an overflowed instance
         const hvp_system& S = systems[sys[inst]];
         const double* prm = params + (size_t)inst * (2 + 6 * (N + 1));
-        hvp::L1Lp<N> L;
-        hvp::l1_setup<N>(L, S, C, role[inst], prm, ws.task_code[t]);
+        L1Wave<N> W;
+        W.hon = false;
+        W.hh = 0.0;
+        W.hs = 1.0;
+        W.hl = W.hds = W.hdl = 0.0;
+#pragma unroll
+        for (int a = 0; a < N; ++a) W.hg[a] = 0.0;
+#pragma unroll
+        for (int q = 0; q < L1Wave<N>::NPS; ++q) {
+            W.pon[q] = false;
+            W.pe0[q] = W.pw[q] = W.pal[q] = W.pt[q] = W.pl1[q] = W.pl2[q] = 0.0;
+            W.ps1[q] = W.ps2[q] = 1.0;
+            W.pds1[q] = W.pdl1[q] = W.pds2[q] = W.pdl2[q] = W.pdt[q] = 0.0;
+#pragma unroll
+            for (int a = 0; a < N; ++a) W.pg[q][a] = 0.0;
+        }
+        int mh = 0, mp = 0;
+        hvp::l1_rows<N>(
+            S, C, role[inst], prm, ws.task_code[t], mh, mp,
+            [&](int i, const double* g, double sgn, double hh) {
+                if (i == lane) {
+                    W.hon = true;
+#pragma unroll
+                    for (int a = 0; a < N; ++a) W.hg[a] = sgn * g[a];
+                    W.hh = hh;
+                }
+            },
+            [&](int j, const double* g, double e0, double w, double alpha) {
+#pragma unroll
+                for (int q = 0; q < L1Wave<N>::NPS; ++q) {
+                    if (j == lane + 64 * q) {
+                        W.pon[q] = true;
+#pragma unroll
+                        for (int a = 0; a < N; ++a) W.pg[q][a] = g[a];
+                        W.pe0[q] = e0;
+                        W.pw[q] = w;
+                        W.pal[q] = alpha;
+                    }
+                }
+            });
+        double y[N];
         int iters = 0;
-        const int status = hvp::l1_solve<N>(L, prm[1], hvp::kL1MaxIter, iters);
-        ws.task_stat[t] = status | (iters << 8);
+        const int status = l1_wave_solve<N>(W, y, prm[1], mh, mp, hvp::kL1MaxIter, iters);
+        if (lane == 0) {
+            ws.task_stat[t] = status | (iters << 8);
 #pragma unroll
-        for (int k = 0; k < N; ++k) ws.task_y[t * N + k] = L.y[k];
-        iter_sum += (unsigned long long)iters;
+            for (int k = 0; k < N; ++k) ws.task_y[t * N + k] = y[k];
+            iter_sum += (unsigned long long)iters;
+        }
     }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) iter_sum += __shfl_down(iter_sum, off, 64);
-    if ((threadIdx.x & 63) == 0 && iter_sum) atomicAdd(&ws.counter[1], iter_sum);
+    if (lane == 0 && iter_sum) atomicAdd(&ws.counter[1], iter_sum);
 }
 
 // ------------------------------------------------------------------ K_cost
@@ -1480,8 +1739,8 @@ int launch_all(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
     HIP_TRY(hipEventRecord(h->evq0, st));
     const size_t lds = sizeof(double) * hvp::F_COUNT * N * kBlock;
     if (h->C.l1) {
-        // min_1_norm: the fixed-sequence LPs (16 one-wave blocks per CU, 8 resident: the private segment and VGPRs bound the occupancy to 2 waves per SIMD; grid-stride over the candidates)
-        hipLaunchKernelGGL(k_qp_l1<N>, dim3(std::max(1, h->n_cu) * 16), dim3(kL1Block), 0, st, h->d_sys, sys, role,
+        // min_1_norm: the fixed-sequence LPs, one per wavefront (wave grid-stride over the candidates)
+        hipLaunchKernelGGL(k_qp_l1<N>, dim3(std::max(1, h->n_cu) * 8), dim3(kL1Block), 0, st, h->d_sys, sys, role,
                            params, h->C, ws);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(h->evq1, st));

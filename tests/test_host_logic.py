@@ -127,5 +127,6 @@ def test_local_mpc_parameter_plumbing():
     assert m.num_bin_vars == 7 * N
     with pytest.raises(ValueError):
         m.set_x_front(np.zeros((2, N)))
-    with pytest.raises(NotImplementedError):
-        LocalMpcMld(N, veh.get_discrete_system(1), quadratic_cost=False)
+    # min_1_norm: the same plumbing, the problem carries quadratic_cost = 0 (hvp_l1.h on the device)
+    l1 = LocalMpcMld(N, veh.get_discrete_system(1), quadratic_cost=False)
+    assert l1.problem.quadratic_cost == 0 and l1.role == O.role_bits(1, 3)
