@@ -159,7 +159,7 @@ __global__ __launch_bounds__(kBlock) void k_qp_ipm(const hvp_system* __restrict_
 // K_qp_l1: min_1_norm problems (hvp_l1.h), every candidate's fixed-sequence LP by the
 // interior-point method, ONE LP PER WAVEFRONT: lane l owns hard row l (8N - 2 <= 62 rows) and
 // pairs l, l + 64 (10N <= 80) in registers; the N x N Newton system is the wave sum of the
-// lanes' row contributions (butterfly all-reduce, bit-identical in every lane, so the control
+// lanes' row contributions (an LDS all-reduce per wave, bit-identical in every lane, so the control
 // flow stays wave-uniform), factorised redundantly per lane and reused by the corrector (only its
 // right-hand side is reduced again).  No private segment: the per-lane form of the same method
 // (hvp_l1.h l1_solve, the host build's) keeps ~10 KB per lane there and is bound by that traffic.
@@ -177,6 +177,33 @@ __device__ inline double wave_min(double v) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v = fmin(v, __shfl_xor(v, off, 64));
     return v;
+}
+
+// LDS all-reduce of M doubles per lane within one wavefront (no block barrier: the waves of a
+// block run different LPs).  red: this wave's buffer of M x 65 doubles (row j = value j of the
+// 64 lanes, padded to 65 so that lane j's reads of row j fall in distinct banks, slot 64 = the
+// sum).  Lane j < M sums row j in lane order; every lane reads the M sums back (broadcast reads),
+// so all lanes hold bit-identical results.
+__device__ inline void lds_wave_sync() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
+template <int M>
+__device__ inline void wave_sum_lds(double* v, double* red, int lane) {
+#pragma unroll
+    for (int j = 0; j < M; ++j) red[j * 65 + lane] = v[j];
+    lds_wave_sync();
+    if (lane < M) {
+        double acc = 0.0;
+        const double* row = red + lane * 65;
+#pragma unroll 16
+        for (int i = 0; i < 64; ++i) acc += row[i];
+        red[lane * 65 + 64] = acc;
+    }
+    lds_wave_sync();
+#pragma unroll
+    for (int j = 0; j < M; ++j) v[j] = red[j * 65 + 64];
+    lds_wave_sync();  // the buffer is reused by the next reduction
 }
 
 template <int N>
@@ -283,8 +310,12 @@ struct L1Wave {
 // Mehrotra predictor-corrector (the algorithm of hvp_l1.h l1_solve), wave-cooperative.
 // Returns 0 (converged) or 2; y (uniform) holds the iterate.
 template <int N>
-__device__ int l1_wave_solve(L1Wave<N>& W, double* y, double v0, int mh, int mp, int max_iter, int& iters) {
-    constexpr int NT = L1Wave<N>::NT, NPS = L1Wave<N>::NPS;
+constexpr int kL1Red = 2 + 2 * N + N * (N + 1) / 2;  // gap, obj, rd_y, rhs, K
+
+template <int N>
+__device__ int l1_wave_solve(L1Wave<N>& W, double* y, double v0, int mh, int mp, int max_iter, int& iters,
+                             double* red, int lane) {
+    constexpr int NPS = L1Wave<N>::NPS;
     const int mtot = mh + 2 * mp;
 #pragma unroll
     for (int i = 0; i < N; ++i) y[i] = v0;
@@ -309,24 +340,22 @@ __device__ int l1_wave_solve(L1Wave<N>& W, double* y, double v0, int mh, int mp,
     hsc = wave_max(hsc);
     wmx = wave_max(wmx);
     for (iters = 0; iters < max_iter; ++iters) {
-        double K[NT], rhs[N], rdy[N];
+        // acc = [gap, obj, rd_y (N), rhs (N), K (NT)]: one LDS all-reduce
+        double acc[kL1Red<N>];
 #pragma unroll
-        for (int i = 0; i < NT; ++i) K[i] = 0.0;
-#pragma unroll
-        for (int i = 0; i < N; ++i) rhs[i] = rdy[i] = 0.0;
-        double gap = 0.0, obj = 0.0, rpm = 0.0, rdm = 0.0;
-        W.contrib(y, false, 0.0, true, K, rhs, gap, obj, rdy, rpm, rdm);
-        gap = wave_sum(gap);
-        obj = wave_sum(obj);
+        for (int i = 0; i < kL1Red<N>; ++i) acc[i] = 0.0;
+        double* rdy = acc + 2;
+        double* rhs = acc + 2 + N;
+        double* K = acc + 2 + 2 * N;
+        double rpm = 0.0, rdm = 0.0;
+        W.contrib(y, false, 0.0, true, K, rhs, acc[0], acc[1], rdy, rpm, rdm);
+        wave_sum_lds<kL1Red<N>>(acc, red, lane);
+        const double gap = acc[0], obj = acc[1];
         rpm = wave_max(rpm);
         rdm = wave_max(rdm);
 #pragma unroll
-        for (int i = 0; i < N; ++i) rdm = fmax(rdm, fabs(wave_sum(rdy[i])));
+        for (int i = 0; i < N; ++i) rdm = fmax(rdm, fabs(rdy[i]));
         if (rpm <= 1e-10 * hsc && rdm <= 1e-10 * wmx && gap <= 1e-12 * fmax(1.0, fabs(obj))) return 0;
-#pragma unroll
-        for (int i = 0; i < NT; ++i) K[i] = wave_sum(K[i]);
-#pragma unroll
-        for (int i = 0; i < N; ++i) rhs[i] = wave_sum(rhs[i]);
         const double mu = gap / mtot;
         if (!hvp::cholesky<N>(K)) return 2;
         double dy[N];
@@ -351,8 +380,7 @@ __device__ int l1_wave_solve(L1Wave<N>& W, double* y, double v0, int mh, int mp,
         for (int i = 0; i < N; ++i) rhs2[i] = dum[i] = 0.0;
         double g2 = 0.0, o2 = 0.0, r2 = 0.0, d2 = 0.0;
         W.contrib(y, true, sigmu, false, K, rhs2, g2, o2, dum, r2, d2);
-#pragma unroll
-        for (int i = 0; i < N; ++i) rhs2[i] = wave_sum(rhs2[i]);
+        wave_sum_lds<N>(rhs2, red, lane);
         hvp::chol_solve<N>(K, rhs2, dy);
         ap = 1.0 / 0.995;
         ad = 1.0 / 0.995;
@@ -384,6 +412,7 @@ __global__ __launch_bounds__(kL1Block) void k_qp_l1(const hvp_system* __restrict
                                                     const int32_t* __restrict__ sys, const int32_t* __restrict__ role,
                                                     const double* __restrict__ params, hvp::Consts C, Workspace ws) {
     static_assert(8 * N - 2 <= 64, "one hard row per lane");
+    __shared__ double s_red[kL1Block / 64][kL1Red<N> * 65];
     const unsigned long long reserved = ws.counter[0];
     const long long total = (long long)(reserved < (unsigned long long)ws.cap ? reserved : ws.cap);
     const int lane = threadIdx.x & 63;
@@ -436,7 +465,7 @@ __global__ __launch_bounds__(kL1Block) void k_qp_l1(const hvp_system* __restrict
             });
         double y[N];
         int iters = 0;
-        const int status = l1_wave_solve<N>(W, y, prm[1], mh, mp, hvp::kL1MaxIter, iters);
+        const int status = l1_wave_solve<N>(W, y, prm[1], mh, mp, hvp::kL1MaxIter, iters, s_red[threadIdx.x >> 6], lane);
         if (lane == 0) {
             ws.task_stat[t] = status | (iters << 8);
 #pragma unroll
