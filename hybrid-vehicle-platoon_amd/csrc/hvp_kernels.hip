@@ -443,7 +443,6 @@ int hvp_evaluate_batch(hvp_handle* h, int B, const int32_t* sys, const int32_t* 
         return fail(HVP_E_ARG, "hvp_evaluate_batch: bad argument");
     if (h->prob.formulation != HVP_FORM_DECENT)
         return fail(HVP_E_UNSUPPORTED, "hvp_evaluate_batch: HVP_FORM_DECENT problems only");
-    if (h->C.l1) return fail(HVP_E_UNSUPPORTED, "hvp_evaluate_batch: min_2_norm problems only");
     if (B == 0) return 0;
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t st = (hipStream_t)stream;

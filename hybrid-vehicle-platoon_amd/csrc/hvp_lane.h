@@ -1445,7 +1445,7 @@ __global__ __launch_bounds__(kBlock) void k_evaluate(int B, const hvp_system* __
             x_out[(size_t)i * 2 * (N + 1) + N + 1 + k + 1] = v;
         }
     }
-    const double cost = hvp::direct_cost<N>(q, S, C, rl, prm, code);
+    const double cost = C.l1 ? hvp::l1_direct_cost<N>(q.y, S, C, rl, prm, code) : hvp::direct_cost<N>(q, S, C, rl, prm, code);
     cost_out[i] = ok ? cost : 1e300;
     status_out[i] = ok ? HVP_OPTIMAL : HVP_INFEASIBLE;
 }

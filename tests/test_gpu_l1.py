@@ -127,3 +127,27 @@ def test_l1_local_mpc_api(gpu_available):
     assert abs(info["cost"] - r.cost) <= 1e-9 * max(1.0, abs(r.cost))
     assert np.abs(info["u"].ravel() - r.u).max() <= 1e-6
     assert abs(float(u0[0, 0]) - r.u[0]) <= 1e-6
+
+
+def test_l1_local_mpc_gear_evaluate(gpu_available):
+    """LocalMpcGear (pwa_friction) with min_1_norm: solve_mpc against the oracle MILP, and
+    evaluate_cost (mpcs/mpc_gear.py:137-170) of its own optimum returns the same cost; an
+    infeasible (u, gear) returns 'inf'."""
+    from hvp.models import PwaFrictionVehicle
+    from hvp.mpc import LocalMpcGear
+
+    N = 5
+    veh = PwaFrictionVehicle(800.0)
+    m = LocalMpcGear(N, veh.get_discrete_system(1), quadratic_cost=False)
+    x = O.env_initial_state(3, 4).reshape(-1)
+    xf = O.constant_velocity_prediction(x[0], x[1], N)
+    xb = O.constant_velocity_prediction(x[4], x[5], N)
+    m.set_x_front(xf)
+    m.set_x_back(xb)
+    _, info = m.solve_mpc(x[2:4].reshape(2, 1))
+    r = O.solve_miqp(O.gear_friction_mld_system(800.0), O.Cfg(), N, O.role_bits(1, 3, 0, False), x[2:4], xf, xb,
+                     np.zeros((2, N + 1)), quadratic=False)
+    assert abs(info["cost"] - r.cost) <= 1e-9 * max(1.0, abs(r.cost))
+    c = m.evaluate_cost(x[2:4].reshape(2, 1), info["u"][[0]], info["u"][[1]])
+    assert abs(c - info["cost"]) <= 1e-9 * max(1.0, abs(info["cost"]))
+    assert m.evaluate_cost(x[2:4].reshape(2, 1), np.ones((1, N)), np.ones((1, N))) == "inf"
