@@ -182,8 +182,8 @@ __device__ inline double wave_min(double v) {
 // LDS all-reduce of M doubles per lane within one wavefront (no block barrier: the waves of a
 // block run different LPs).  red: this wave's buffer of M x 65 doubles (row j = value j of the
 // 64 lanes, padded to 65 so that lane j's reads of row j fall in distinct banks, slot 64 = the
-// sum).  Lane j < M sums row j in lane order; every lane reads the M sums back (broadcast reads),
-// so all lanes hold bit-identical results.
+// sum).  Lane j < M sums row j in lane order (M <= 32: lanes j and j + 32 a half each); every
+// lane reads the M sums back (broadcast reads), so all lanes hold bit-identical results.
 __device__ inline void lds_wave_sync() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
@@ -193,12 +193,26 @@ __device__ inline void wave_sum_lds(double* v, double* red, int lane) {
 #pragma unroll
     for (int j = 0; j < M; ++j) red[j * 65 + lane] = v[j];
     lds_wave_sync();
-    if (lane < M) {
+    if constexpr (M <= 32) {
+        // two lanes per value (j and j + 32, 32 entries each), halves combined across the wave
+        // halves (a + b == b + a: both lanes hold the same sum)
+        const int j = lane & 31;
         double acc = 0.0;
-        const double* row = red + lane * 65;
+        if (j < M) {
+            const double* row = red + j * 65 + (lane >> 5) * 32;
 #pragma unroll 16
-        for (int i = 0; i < 64; ++i) acc += row[i];
-        red[lane * 65 + 64] = acc;
+            for (int i = 0; i < 32; ++i) acc += row[i];
+        }
+        acc += __shfl_xor(acc, 32, 64);
+        if (lane < M) red[lane * 65 + 64] = acc;
+    } else {
+        if (lane < M) {
+            double acc = 0.0;
+            const double* row = red + lane * 65;
+#pragma unroll 16
+            for (int i = 0; i < 64; ++i) acc += row[i];
+            red[lane * 65 + 64] = acc;
+        }
     }
     lds_wave_sync();
 #pragma unroll
