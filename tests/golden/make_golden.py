@@ -146,6 +146,13 @@ def l1_fixtures():
     save("l1_gear_n4_N5.npz", N, [800.0], O.Cfg(), params, roles, si, exp, model=1, quadratic=0)
 
 
+def l1_rollout():
+    """min_1_norm along the platoon's own L1 trajectories: mid-episode states, where the LP optima
+    sit on region edges and ties between sequences are likeliest."""
+    params, roles, si, exp = rollout(4, 5, range(3), 8, quadratic=False)
+    save("l1_rollout_n4_N5.npz", 5, [800.0], O.Cfg(), params, roles, si, exp, quadratic=0)
+
+
 def gear_model():
     """LocalMpcGear on pwa_friction (mpcs/mpc_gear.py, fleet_decent_mld.py:226-253): model = 1.
     N = 5 by exhaustive enumeration (~1e3 mode sequences per vehicle), N = 8 by the oracle's
@@ -163,7 +170,7 @@ def gear_model():
         O.set_method(O.METHOD_ENUMERATE)
 
 
-def rollout(n, N, seeds, steps):
+def rollout(n, N, seeds, steps, quadratic=True):
     """States along the platoon's own predicted trajectories (x_1 of every local solution)."""
     cfg = O.Cfg()
     sysd = O.gear_pwa_system(800.0)
@@ -174,12 +181,12 @@ def rollout(n, N, seeds, steps):
             p, r = decent_instances(state, N, leader_window(N, t))
             P.append(p)
             R.append(r)
-            exp = solve_set([sysd], np.zeros(n, int), cfg, N, p, r)
+            exp = solve_set([sysd], np.zeros(n, int), cfg, N, p, r, quadratic)
             state = np.stack([exp["x"][i][:, 1] if exp["status"][i] == 0 else state[2 * i:2 * i + 2]
                               for i in range(n)]).reshape(-1)
     params, roles = np.concatenate(P), np.concatenate(R)
     sys_idx = np.zeros(len(roles), np.int32)
-    return params, roles, sys_idx, solve_set([sysd], sys_idx, cfg, N, params, roles)
+    return params, roles, sys_idx, solve_set([sysd], sys_idx, cfg, N, params, roles, quadratic)
 
 
 def task2(n, N, seeds, t_list):
@@ -523,6 +530,9 @@ def main():
         return
     if len(sys.argv) > 1 and sys.argv[1] == "l1":
         l1_fixtures()
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == "l1_rollout":
+        l1_rollout()
         return
     N = 5
     params, roles, si, exp = hard_cases(N)
