@@ -9,9 +9,12 @@ region (max over ranks).  Inputs are synthetic random-init platoon states (env.p
 distribution, seed s -> SeedSequence(s) derived env seed), constant-velocity neighbour
 predictions and the constant-velocity leader window, resident in HBM before timing starts.
 
-Multi-GPU: one process per GPU (torch.distributed.run); every rank owns a disjoint range of
-seeds (weak scaling, no collective in the data path -- the platoons are independent); the
-barrier / MAX-reduction only brackets the timing.
+Multi-GPU: one process per GPU; every rank owns a disjoint range of seeds (weak scaling, no
+collective in the data path -- the platoons are independent); the barrier / MAX-reduction only
+brackets the timing.  Either an external launcher starts the ranks (torch.distributed.run sets
+WORLD_SIZE / RANK / LOCAL_RANK), or ``--gpus N`` without WORLD_SIZE makes this process a launcher:
+it starts N rank processes itself (never touching the GPU), prints rank 0's line and fails if any
+rank fails.
 """
 
 from __future__ import annotations
@@ -98,6 +101,85 @@ def qp_roofline(qp_step_ms: float, kernels: list, notional_bytes: float, tag: st
                         "frac": traffic / t / 1e9 / HBM_PEAK_GBS},
                 "profile": sorted(srcs), "profile_avg_ms": prof_ms})
     return out
+
+
+def seed_range(rank: int, S: int) -> range:
+    """The platoon seeds of one rank: a contiguous block of S, disjoint across ranks."""
+    return range(rank * S, (rank + 1) * S)
+
+
+def free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(argv: list, world: int) -> int:
+    """``--gpus N`` without an external launcher: start N rank processes of this script (RANK =
+    LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on 127.0.0.1), forward rank 0's output, and return
+    the first non-zero exit code.  This process never initialises the GPU (no exec either: the
+    ranks are children).  A rank that fails ends the others, which would otherwise wait in a
+    collective for it."""
+    import subprocess
+    import tempfile
+
+    port = free_port()
+    procs, outs = [], []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        out = tempfile.TemporaryFile(mode="w+") if r == 0 else None
+        outs.append(out)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env, stdout=out))
+    rc = 0
+    live = set(range(world))
+    while live:
+        for r in sorted(live):
+            c = procs[r].poll()
+            if c is None:
+                continue
+            live.discard(r)
+            if c != 0 and rc == 0:
+                rc = c
+                print(f"bench.py: rank {r} exited with {c}; stopping the other ranks", file=sys.stderr, flush=True)
+                for q in live:
+                    procs[q].terminate()
+        time.sleep(0.05)
+    outs[0].seek(0)
+    sys.stdout.write(outs[0].read())
+    sys.stdout.flush()
+    return rc
+
+
+def bench_dry_run(args, world: int, rank: int, dist) -> None:
+    """--dry-run: the multi-rank protocol without a GPU (gloo): seed shards, barrier + timed region
+    around an empty step, MAX over ranks, rank 0's line with every rank's seed range."""
+    import torch
+
+    S = args.platoons
+    seeds = seed_range(rank, S)
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pass
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    ranges = [[seeds.start, seeds.stop]]
+    if dist:
+        tt = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+        allr = [None] * world
+        dist.all_gather_object(allr, [seeds.start, seeds.stop])
+        ranges = allr
+    if rank == 0:
+        print(json.dumps({"metric": "dry run (no GPU work)", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "ms_per_step": dt / max(args.steps, 1) * 1e3,
+                          "seed_ranges": ranges, "backend": dist.get_backend() if dist else None}), flush=True)
 
 
 def make_inputs(seeds, n: int, N: int):
@@ -196,7 +278,7 @@ def bench_admm(args, world: int, rank: int, local: int, dist) -> None:
     n, N, S, iters = args.n, args.N, args.platoons, args.admm_iters
     veh = PwaGearVehicle(800)
     system = tables.system_from_dict(veh.get_discrete_system(1), tables.gears_of(veh))
-    seeds = range(rank * S, (rank + 1) * S)
+    seeds = seed_range(rank, S)
     states = np.stack([initial_platoon_state(n, derive_env_seed(int(s))).reshape(-1).astype(np.float64)
                        for s in seeds])
     T = args.warmup + args.steps + 1
@@ -524,7 +606,7 @@ def bench_closed_loop(args, world: int, rank: int, local: int, dist) -> None:
     solver = BatchSolver(tables.problem(N), [system], device=local)
     dev = torch.device("cuda", local)
     x0 = np.stack([initial_platoon_state(n, derive_env_seed(int(s))).reshape(-1).astype(np.float64)
-                   for s in range(rank * S, (rank + 1) * S)])
+                   for s in seed_range(rank, S)])
     T = args.warmup + args.steps + N + 2
     lx = np.stack([3000.0 + 20.0 * np.arange(T), np.full(T, 20.0)])
     wins = torch.from_numpy(np.ascontiguousarray(np.stack([np.broadcast_to(lx[:, t:t + N + 1], (S, 2, N + 1))
@@ -617,7 +699,7 @@ def bench_cent(args, world: int, rank: int, local: int, dist) -> None:
     veh = PwaGearVehicle(800)
     system = tables.system_from_dict(veh.get_discrete_system(1), tables.gears_of(veh))
     dev = torch.device("cuda", local)
-    seeds = range(rank * S, (rank + 1) * S)
+    seeds = seed_range(rank, S)
     x0 = np.stack([initial_platoon_state(n, derive_env_seed(int(s))).reshape(n, 2).astype(np.float64) for s in seeds])
     lead = np.stack([3000.0 + 20.0 * np.arange(N + 1), np.full(N + 1, 20.0)])
     # --streams K: the platoons over K handles, each solved by its own host thread on its own HIP
@@ -786,15 +868,34 @@ def main() -> None:
     ap.add_argument("--gadmm-layout", choices=["replicas", "vehicles"], default="replicas")
     ap.add_argument("--cost", choices=["quadratic", "l1"], default="quadratic",
                     help="decent: min_2_norm (default) or min_1_norm (the MILP variant, enumeration, N <= 8)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU work: start the ranks (gloo), shard the seeds, run the timing protocol around an "
+                         "empty step and print the line (tests the --gpus N launcher on a CPU)")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(sys.argv[1:], args.gpus))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus != world:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.platoons < 1 or args.steps < 1 or args.warmup < 0:
+        sys.exit("bench.py: --platoons and --steps must be >= 1, --warmup >= 0")
 
     import torch
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
     dist = None
+    if args.dry_run:
+        if world > 1:
+            import torch.distributed as dist
+
+            dist.init_process_group("gloo")
+        bench_dry_run(args, world, rank, dist)
+        if dist:
+            dist.destroy_process_group()
+        return
+    torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
 
@@ -822,7 +923,7 @@ def main() -> None:
     if not quadratic:
         method = 1  # the min_1_norm LPs run under exhaustive enumeration (hvp_l1.h)
     # each rank owns a disjoint seed range: platoons are independent (weak scaling)
-    params, roles = make_inputs(range(rank * S, (rank + 1) * S), n, N)
+    params, roles = make_inputs(seed_range(rank, S), n, N)
     B = len(roles)
     dev = torch.device("cuda", local)
     t_params_all = torch.from_numpy(params).to(dev)

@@ -64,3 +64,36 @@ def test_seed_shards_are_disjoint_and_time_is_max_over_ranks():
 
     full, _ = bench.make_inputs(range(world * S), n, N)
     assert np.array_equal(np.concatenate(gathered), full[:, 0])
+
+
+def _run_bench(args: list, env_extra: dict | None = None):
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(root, "bench.py")] + args, env=env, capture_output=True,
+                          text=True, timeout=240)
+
+
+def test_bench_gpus_n_launches_n_ranks():
+    """bench.py --gpus 2 without an external launcher starts two ranks itself (gloo in --dry-run),
+    prints rank 0's line once with n_gpus 2, and the ranks hold disjoint seed blocks."""
+    import json
+
+    r = _run_bench(["--gpus", "2", "--no-cpu", "--dry-run", "--platoons", "7", "--steps", "3"])
+    assert r.returncode == 0, r.stderr
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["backend"] == "gloo" and d["steps"] == 3
+    assert d["seed_ranges"] == [[0, 7], [7, 14]]
+
+
+def test_bench_launcher_fails_when_a_rank_fails():
+    """A rank that cannot run makes the launcher exit non-zero (no silent one-GPU line)."""
+    r = _run_bench(["--gpus", "2", "--no-cpu", "--dry-run", "--platoons", "-1"])
+    assert r.returncode != 0
+    r = _run_bench(["--gpus", "2", "--no-cpu", "--dry-run"], {"WORLD_SIZE": "3", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0 and "WORLD_SIZE=3" in r.stderr
