@@ -867,7 +867,8 @@ def main() -> None:
                     help="admm: do not try the previous iteration's sequences as incumbents (A/B)")
     ap.add_argument("--gadmm-layout", choices=["replicas", "vehicles"], default="replicas")
     ap.add_argument("--cost", choices=["quadratic", "l1"], default="quadratic",
-                    help="decent: min_2_norm (default) or min_1_norm (the MILP variant, enumeration, N <= 8)")
+                    help="decent: min_2_norm (default) or min_1_norm (the MILP variant: --method auto = enumeration "
+                         "up to N = 8, branch and bound beyond)")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU work: start the ranks (gloo), shard the seeds, run the timing protocol around an "
                          "empty step and print the line (tests the --gpus N launcher on a CPU)")
@@ -920,8 +921,8 @@ def main() -> None:
     system = tables.system_from_dict(veh.get_discrete_system(1), tables.gears_of(veh))
     method = {"auto": 0, "enum": 1, "bnb": 2}[args.method]
     quadratic = args.cost == "quadratic"
-    if not quadratic:
-        method = 1  # the min_1_norm LPs run under exhaustive enumeration (hvp_l1.h)
+    if not quadratic and method == 0:
+        method = 1 if N <= 8 else 2  # min_1_norm AUTO: enumeration up to N = 8 (hvp_lane.h kAutoEnumMaxNL1)
     # each rank owns a disjoint seed range: platoons are independent (weak scaling)
     params, roles = make_inputs(seed_range(rank, S), n, N)
     B = len(roles)
@@ -944,7 +945,7 @@ def main() -> None:
 
     # long horizons: a heavy-tailed search can outgrow an instance's workspace share; those
     # instances are re-solved inside the step (one synchronisation), so every step is complete
-    retry = N > 8
+    retry = N > 8 or not quadratic
 
     def step():
         for sv, ts, tr, tp, o, stm in chunks:
@@ -995,7 +996,9 @@ def main() -> None:
     qp_step_ms = float(np.mean(qp_ms))
     cand_per_step = cand / args.steps
     notional = cand_per_step * dense_qp_bytes(N) + B * instance_io_bytes(N)
-    if bnb:
+    if bnb and not quadratic:
+        qk = [("k_l1_root", 1), ("k_l1_bound", N)]
+    elif bnb:
         qk = [("k_bnb_root_coop", 1), ("k_bnb_bound_coop", N)] if N > 8 else [("k_bnb_root", 1),
                                                                               ("k_bnb_bound_refill", N)]
     else:

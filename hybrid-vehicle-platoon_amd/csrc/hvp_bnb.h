@@ -34,7 +34,9 @@ namespace hvp {
 // window and far above the bound's rounding (costs are evaluated term by term, ~1e-15 relative).
 constexpr double kPruneRel = 1e-7;
 
-HVP_HD inline bool bnb_pruned(double lb, double inc) { return lb > inc + kPruneRel * (1.0 + fabs(inc)); }
+// A bound of 1e300 or more marks a node proven to hold no feasible completion (min_1_norm's
+// certified infeasible relaxations): pruned whatever the incumbent, even before there is one.
+HVP_HD inline bool bnb_pruned(double lb, double inc) { return lb >= 1e300 || lb > inc + kPruneRel * (1.0 + fabs(inc)); }
 
 // Lexicographic key of a full sequence (step 0 most significant): numeric order of the key is
 // the enumeration order of enumerate_sequences.

@@ -16,7 +16,8 @@
 
 namespace {
 
-constexpr int kAutoEnumMaxN = 0;  // same crossover as hvp_kernels.hip (HVP_METHOD_AUTO)
+constexpr int kAutoEnumMaxN = 0;    // same crossovers as hvp_lane.h (HVP_METHOD_AUTO)
+constexpr int kAutoEnumMaxNL1 = 8;
 
 // 0: interior point only; 1: Goldfarb-Idnani active set, interior point on failure
 int g_solver = 1;
@@ -39,7 +40,7 @@ hvp::Consts make_consts(const hvp_problem& p) {
         C.acc[k] = p.a_acc * p.ts_acc - k * p.accel_tightening;
     }
     C.tol = p.tol > 0 ? p.tol : 1e-12;
-    C.max_iter = p.max_iter > 0 ? p.max_iter : 60;
+    C.max_iter = p.max_iter > 0 ? p.max_iter : (p.quadratic_cost ? 60 : hvp::kL1MaxIter);
     C.N = p.N;
     C.form = p.formulation;
     C.stride = p.formulation == HVP_FORM_ADMM    ? hvp_params_stride_admm(p.N)
@@ -72,7 +73,11 @@ void solve_one(const hvp_system& S, const hvp::Consts& C, int role, const double
                 hvp::l1_setup<N>(lp, S, C, role, prm, code);
                 Cand c;
                 c.code = code;
-                c.status = hvp::l1_solve<N>(lp, prm[1], hvp::kL1MaxIter, c.iters);
+                c.iters = 0;
+                for (int i = 0; i < N; ++i) lp.y[i] = prm[1];
+                c.status = hvp::l1_infeasible<N>(S, C, prm, code, N, 0.0, -1.0)
+                               ? hvp::L1_INFEASIBLE
+                               : hvp::l1_solve<N>(lp, prm[1], C.max_iter, c.iters, S.vmin, S.vmax);
                 c.cost = c.status == 0 ? hvp::l1_direct_cost<N>(lp.y, S, C, role, prm, code) : 1e300;
                 for (int i = 0; i < N; ++i) c.y[i] = lp.y[i];
                 cands.push_back(c);
@@ -120,12 +125,14 @@ void solve_one(const hvp_system& S, const hvp::Consts& C, int role, const double
     }
     double best = 1e300;
     int tot = 0;
+    bool unresolved = false;  // min_1_norm: an LP neither solved nor proven infeasible (k_select)
     for (const Cand& c : cands) {
         tot += c.iters;
         if (c.status == 0 && c.cost < best) best = c.cost;
+        unresolved = unresolved || (C.l1 && c.status == hvp::L1_FAIL);
     }
     int win = -1;
-    if (best < 1e300) {
+    if (best < 1e300 && !unresolved) {
         const double tol = 1e-9 * fmax(1.0, fabs(best));
         for (size_t i = 0; i < cands.size(); ++i)
             if (cands[i].status == 0 && cands[i].cost <= best + tol) { win = (int)i; break; }
@@ -137,7 +144,8 @@ void solve_one(const hvp_system& S, const hvp::Consts& C, int role, const double
     *nodes = n;
     *iters = tot;
     if (win < 0) {
-        *status = (!ok || n == 0) ? HVP_INFEASIBLE : HVP_MAXITER;
+        // min_1_norm: every LP proven infeasible -> infeasible; an unresolved one -> MAXITER
+        *status = (!ok || n == 0 || (C.l1 && !unresolved)) ? HVP_INFEASIBLE : HVP_MAXITER;
         *cost = 1e300;
         return;
     }
@@ -174,9 +182,24 @@ void solve_one_bnb(const hvp_system& S, const hvp::Consts& C, int role, const do
         double y[N];
     };
     int nq = 0, nit = 0;
+    int l1_st = 0;  // status of the last min_1_norm LP (hvp_l1.h L1_*)
     auto qp = [&](uint64_t code, int K, double lo, double hi, double& c, double* y) {
         hvp::LaneQp<N> q;
         int it = 0;
+        if (C.l1) {  // min_1_norm: the node LP (relaxed after K steps), as k_l1_root / k_l1_bound
+            hvp::L1Lp<N> lp;
+            hvp::l1_setup<N>(lp, S, C, role, prm, code, K, lo, hi);
+            l1_st = hvp::l1_infeasible<N>(S, C, prm, code, K, lo, hi)
+                        ? hvp::L1_INFEASIBLE
+                        : hvp::l1_solve<N>(lp, prm[1], C.max_iter, it, S.vmin, S.vmax);
+            ++nq;
+            nit += it;
+            if (l1_st != hvp::L1_OK) return false;
+            c = hvp::l1_direct_cost<N>(lp.y, S, C, role, prm, code, K, lo, hi);
+            if (y)
+                for (int i = 0; i < N; ++i) y[i] = lp.y[i];
+            return true;
+        }
         if (C.form == HVP_FORM_ADMM) {
             const int r = hvp::solve_admm_lane<N>(q, S, C, role, prm, code, K, 8 * hvp::GiConstraintSet<N>::NC, it);
             ++nq;
@@ -220,6 +243,8 @@ void solve_one_bnb(const hvp_system& S, const hvp::Consts& C, int role, const do
             uint64_t code;
             double c1;
             if (hvp::bnb_dive<N>(S, C, v0, root.y, &code) && qp(code, N, 0.0, -1.0, c1, nullptr)) inc = c1;
+        } else if (C.l1 && l1_st == hvp::L1_INFEASIBLE) {
+            root.lb = 1e300;  // the root relaxation is infeasible: so is every sequence
         }
         lvl.push_back(root);
     }
@@ -231,15 +256,22 @@ void solve_one_bnb(const hvp_system& S, const hvp::Consts& C, int role, const do
                 Node c;
                 if (!hvp::bnb_child(S, C, k - 1, p.lo, p.hi, r, &c.lo, &c.hi)) continue;
                 c.code = hvp::code_with(p.code, k - 1, r);
+                c.lb = p.lb;
                 nxt.push_back(c);
             }
         }
         if (k == N) nleaves += (int)nxt.size();
         for (Node& c : nxt) {
             double lb;
+            const double plb = c.lb;  // the parent's bound (min_1_norm: kept by an unresolved leaf)
             const bool good = qp(c.code, k, c.lo, c.hi, lb, c.y);
             c.stat = good ? 0 : HVP_MAXITER;
             c.lb = good ? lb : (k < N ? -1e300 : 1e300);
+            if (!good && C.l1) {
+                const bool infeasible = l1_st == hvp::L1_INFEASIBLE;
+                c.stat = infeasible ? HVP_INFEASIBLE : HVP_MAXITER;
+                c.lb = k < N ? (infeasible ? 1e300 : -1e300) : (infeasible ? 1e300 : plb);
+            }
             if (k == N && good) inc = fmin(inc, lb);
         }
         lvl.swap(nxt);
@@ -248,7 +280,11 @@ void solve_one_bnb(const hvp_system& S, const hvp::Consts& C, int role, const do
     *iters = nit;
     int win = -1;
     uint64_t wkey = ~0ull;
-    if (ok && inc < HUGE_VAL) {
+    bool contention = false;  // min_1_norm: an unresolved leaf that may hold the optimum (k_bnb_key)
+    if (C.l1)
+        for (const Node& c : lvl)
+            contention = contention || (c.stat == HVP_MAXITER && !hvp::bnb_pruned(c.lb, inc));
+    if (ok && inc < HUGE_VAL && !contention) {
         for (int i = 0; i < (int)lvl.size(); ++i) {
             const Node& c = lvl[i];
             if (c.stat != 0 || c.lb > inc + 1e-9 * fmax(1.0, fabs(inc))) continue;
@@ -257,7 +293,10 @@ void solve_one_bnb(const hvp_system& S, const hvp::Consts& C, int role, const do
         }
     }
     if (win < 0) {
-        *status = (ok && !lvl.empty() && lvl.size() > 0 && nleaves > 0) ? HVP_MAXITER : HVP_INFEASIBLE;
+        bool unresolved = false;  // min_1_norm: only an unresolved leaf makes it MAXITER (k_bnb_finish)
+        for (const Node& c : lvl) unresolved = unresolved || c.stat == HVP_MAXITER;
+        *status = C.l1 ? (unresolved ? HVP_MAXITER : HVP_INFEASIBLE)
+                       : ((ok && !lvl.empty() && lvl.size() > 0 && nleaves > 0) ? HVP_MAXITER : HVP_INFEASIBLE);
         *cost = 1e300;
         if (xf) memset(xf, 0, sizeof(double) * 2 * (N + 1));
         if (xb) memset(xb, 0, sizeof(double) * 2 * (N + 1));
@@ -306,7 +345,8 @@ void solve_range(const hvp_problem& P, const hvp_system* systems, int B, const i
     const int stride = C.stride;
 #pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1)
     for (int i = 0; i < B; ++i) {
-        const bool bnb = !C.l1 && (P.method == HVP_METHOD_BNB || (P.method == HVP_METHOD_AUTO && N > kAutoEnumMaxN));
+        const bool bnb = P.method == HVP_METHOD_BNB ||
+                         (P.method == HVP_METHOD_AUTO && N > (C.l1 ? kAutoEnumMaxNL1 : kAutoEnumMaxN));
         if (bnb || N > HVP_MAX_N_ENUM || C.form == HVP_FORM_ADMM) {
             solve_one_bnb<N>(systems[sys[i]], C, role[i], params + (size_t)i * stride, u + (size_t)i * N,
                              x + (size_t)i * 2 * (N + 1), region + (size_t)i * N, cost + i, status + i, nodes + i,

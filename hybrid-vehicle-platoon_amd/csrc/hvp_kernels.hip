@@ -50,7 +50,9 @@ hvp::Consts make_consts(const hvp_problem& p) {
         C.acc[k] = p.a_acc * p.ts_acc - k * p.accel_tightening;
     }
     C.tol = p.tol > 0 ? p.tol : 1e-12;
-    C.max_iter = p.max_iter > 0 ? p.max_iter : 60;
+    // max_iter: the quadratic path's fallback IPM cap (default 60); min_1_norm: the LP interior
+    // point's cap (default hvp::kL1MaxIter)
+    C.max_iter = p.max_iter > 0 ? p.max_iter : (p.quadratic_cost ? 60 : hvp::kL1MaxIter);
     C.N = p.N;
     C.form = p.formulation;
     C.stride = p.formulation == HVP_FORM_ADMM    ? hvp_params_stride_admm(p.N)
@@ -288,10 +290,8 @@ int hvp_create(hvp_handle** out, const hvp_problem* problem, const hvp_system* s
         return fail(HVP_E_ARG, "hvp_create: the ADMM formulation needs rho > 0");
     if (problem->quadratic_cost != 1 && problem->quadratic_cost != 0)
         return fail(HVP_E_ARG, "hvp_create: quadratic_cost must be 1 (min_2_norm) or 0 (min_1_norm)");
-    if (problem->quadratic_cost == 0 &&
-        (problem->formulation != HVP_FORM_DECENT || problem->N > HVP_MAX_N_ENUM || problem->method == HVP_METHOD_BNB))
-        return fail(HVP_E_UNSUPPORTED, "hvp_create: the min_1_norm cost runs for HVP_FORM_DECENT problems with N <= " +
-                                           std::to_string(HVP_MAX_N_ENUM) + " by enumeration");
+    if (problem->quadratic_cost == 0 && problem->formulation != HVP_FORM_DECENT)
+        return fail(HVP_E_UNSUPPORTED, "hvp_create: the min_1_norm cost runs for HVP_FORM_DECENT problems");
     for (int i = 0; i < n_systems; ++i) {
         std::string why;
         if (!valid_system(systems[i], &why)) return fail(HVP_E_ARG, "hvp_create: system " + std::to_string(i) + ": " + why);
@@ -301,8 +301,8 @@ int hvp_create(hvp_handle** out, const hvp_problem* problem, const hvp_system* s
     h->device = device;
     h->prob = *problem;
     h->C = make_consts(*problem);
-    h->bnb = problem->quadratic_cost == 1 && (problem->method == HVP_METHOD_BNB ||
-                                             (problem->method == HVP_METHOD_AUTO && problem->N > kAutoEnumMaxN));
+    h->bnb = problem->method == HVP_METHOD_BNB ||
+             (problem->method == HVP_METHOD_AUTO && problem->N > (problem->quadratic_cost ? kAutoEnumMaxN : kAutoEnumMaxNL1));
     h->n_systems = n_systems;
     for (int i = 0; i < n_systems; ++i) h->nreg_max = std::max(h->nreg_max, (int)systems[i].n_regions);
     (void)hipDeviceGetAttribute(&h->n_cu, hipDeviceAttributeMultiprocessorCount, device);

@@ -34,7 +34,35 @@
 
 namespace hvp {
 
-constexpr int kL1MaxIter = 120;
+constexpr int kL1MaxIter = 120;  // interior-point iteration cap (hvp_problem.max_iter > 0 overrides it)
+#ifndef HVP_L1_SHORT
+#define HVP_L1_SHORT 0.1
+#endif
+#ifndef HVP_L1_CENTRE
+#define HVP_L1_CENTRE 0.5
+#endif
+constexpr double kL1Short = HVP_L1_SHORT;    // corrector steps shorter than this fall back to centring
+constexpr double kL1Centre = HVP_L1_CENTRE;  // sigma of that centring step
+
+// LP status: converged / proven infeasible (a Farkas certificate of the hard rows, l1_farkas) /
+// unresolved (iteration cap or a numerical failure without a certificate: the search reports
+// HVP_MAXITER for an instance where such an LP may hold the optimum, never a worse sequence).
+enum { L1_OK = 0, L1_INFEASIBLE = 1, L1_FAIL = 2 };
+
+// Infeasibility certificate of the hard rows G y <= h from nonnegative multipliers lam: every
+// feasible y lies in the velocity box [ylo, yhi]^N (the V rows), so lam'G y >= sum_a min(r_a ylo,
+// r_a yhi) with r = G' lam; if that exceeds lam'h (with a relative margin), no y satisfies the
+// rows.  On a primal-infeasible LP the interior point's hard-row multipliers grow along such a
+// ray.  r (N) and hl = lam'h are the sums over the rows; scale = sum |lam_i h_i|.
+template <int N>
+HVP_HD inline bool l1_farkas(const double* r, double hl, double scale, double ylo, double yhi) {
+    double lower = 0.0, mag = scale;
+    for (int a = 0; a < N; ++a) {
+        lower += fmin(r[a] * ylo, r[a] * yhi);
+        mag += fabs(r[a]) * fmax(fabs(ylo), fabs(yhi));
+    }
+    return mag > 0.0 && mag < 1e250 && lower > hl + 1e-9 * mag;
+}
 
 template <int N>
 struct L1Lp {
@@ -52,6 +80,32 @@ struct L1Lp {
     double dsh[MH], dlh[MH], ds1[MP], dl1[MP], ds2[MP], dl2[MP];
 };
 
+// Cholesky factorisation of the LP's Newton matrix (inverse diagonal stored, as hvp_ipm.h cholesky)
+// with the "Cholesky infinity" rule of LP interior points: near a degenerate vertex the matrix
+// sum_r D_r g_r g_r' spans scalings 1e-12 .. 1e12 and a pivot can lose all its digits; such a pivot
+// (<= 1e-13 of its diagonal before elimination) is taken as infinite, i.e. the direction leaves
+// that component where it is.  The iteration continues instead of stopping at a converged-but-
+// degenerate point (the oracle solves those LPs; without the rule they ended unresolved).
+template <int N>
+HVP_HD inline void cholesky_l1(double* K) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        const double d = K[tri(j, j)];
+        double s = d;
+#pragma unroll
+        for (int k = 0; k < j; ++k) s -= K[tri(j, k)] * K[tri(j, k)];
+        const double il = s > 1e-13 * d ? frcp(sqrt(s)) : 0.0;
+        K[tri(j, j)] = il;
+#pragma unroll
+        for (int i = j + 1; i < N; ++i) {
+            double v = K[tri(i, j)];
+#pragma unroll
+            for (int k = 0; k < j; ++k) v -= K[tri(i, k)] * K[tri(j, k)];
+            K[tri(i, j)] = v * il;
+        }
+    }
+}
+
 template <int N>
 HVP_HD inline double l1_dot(const double* g, const double* y) {
     double s = 0.0;
@@ -60,16 +114,61 @@ HVP_HD inline double l1_dot(const double* g, const double* y) {
     return s;
 }
 
+// Per-step data of a (node) LP: the dynamics (a, b, c) of every step, which steps carry their
+// input rows and |u| cost (bit k of `on`), and the bounds of v_{k+1}.  Steps k < K take the
+// regions of `code`; steps k >= K are RELAXED exactly as the quadratic bound (hvp_ipm.h
+// setup_input / relax_step): from the exact interval [rlo, rhi] of v_K each undecided v_{k+1} keeps
+// its reachable interval and, where the regions step k may take share (a, c), the step takes the
+// virtual region (a, b_max, c) with its input rows and cost (Q_u |s| <= Q_u |u| for s = u b_r / b_max);
+// otherwise the step's input rows and cost are dropped.  rlo > rhi (the default) = no relaxation
+// information (K = N leaves, enumeration candidates).
+template <int N>
+HVP_HD inline void l1_steps(const hvp_system& S, const Consts& C, uint64_t code, int K, double rlo, double rhi,
+                            double* a, double* b, double* c, unsigned& on, double* vlo, double* vhi) {
+    bool relax = rlo <= rhi;
+    on = 0;
+    for (int k = 0; k < N; ++k) {
+        const bool fixed = k < K;
+        int vr = -1;
+        double bm = 1.0, nlo = S.vmin, nhi = S.vmax;
+        if (!fixed && relax) {
+            bool dead;
+            vr = relax_step(S, C, k, rlo, rhi, nlo, nhi, bm, dead);
+            relax = !dead;
+            rlo = nlo;
+            rhi = nhi;
+        }
+        const bool st_on = fixed || vr >= 0;
+        const int r = fixed ? code_region(code, k) : (vr >= 0 ? vr : 0);
+        a[k] = st_on ? S.a[r] : 1.0;
+        b[k] = fixed ? S.b[r] : (vr >= 0 ? bm : 1.0);
+        c[k] = st_on ? S.c[r] : 0.0;
+        on |= st_on ? 1u << k : 0u;
+        if (k + 1 < K) {  // v_{k+1} in region sigma_{k+1} and the state box
+            const int r1 = code_region(code, k + 1);
+            vlo[k] = fmax(S.vmin, S.vlo[r1]);
+            vhi[k] = fmin(S.vmax, S.vhi[r1]);
+        } else if (!fixed && relax) {  // a relaxed v_{k+1}: its reachable interval
+            vlo[k] = fmax(S.vmin, nlo);
+            vhi[k] = fmin(S.vmax, nhi);
+        } else {
+            vlo[k] = S.vmin;
+            vhi[k] = S.vmax;
+        }
+    }
+}
+
 // Rows of the fixed-sequence LP of instance params prm (x0, x_front, x_back, leader_x) and
-// region code, in a fixed order: hard(idx, g, sgn, h) for the row sgn*g.y <= h and
+// region code -- or, with K < N, of the branch-and-bound relaxation of the prefix code[0..K-1]
+// (l1_steps) -- in a fixed order: hard(idx, g, sgn, h) for the row sgn*g.y <= h and
 // pair(idx, g, e0, w, alpha) for every term with a variable part (zero-weight and constant terms
 // are skipped, so the indices are dense).  Both callbacks see every row in the same order on
-// every lane: the per-lane host solver stores them all (l1_setup), the wave-cooperative kernel
-// (hvp_lane.h k_qp_l1) keeps the rows whose index maps to its lane.  Returns (mh, mp) through the
+// every lane: the per-lane host solver stores them all (l1_setup), the wave-cooperative kernels
+// (hvp_lane.h) keep the rows whose index maps to their lane.  Returns (mh, mp) through the
 // counters and false when the constant row p_1 in [pmin, pmax] is violated.
 template <int N, class FH, class FP>
-HVP_HD inline bool l1_rows(const hvp_system& S, const Consts& C, int role, const double* prm, uint64_t code,
-                           int& mh, int& mp, FH&& hard_cb, FP&& pair_cb) {
+HVP_HD inline bool l1_rows(const hvp_system& S, const Consts& C, int role, const double* prm, uint64_t code, int K,
+                           double rlo, double rhi, int& mh, int& mp, FH&& hard_cb, FP&& pair_cb) {
     const double p0 = prm[0], v0 = prm[1];
     const double* xf = prm + 2;
     const double* xb = prm + 2 + 2 * (N + 1);
@@ -89,37 +188,30 @@ HVP_HD inline bool l1_rows(const hvp_system& S, const Consts& C, int role, const
         pair_cb(mp, g, e0, w, alpha);
         ++mp;
     };
-    double a[N], b[N], c[N];
-    for (int k = 0; k < N; ++k) {
-        const int r = code_region(code, k);
-        a[k] = S.a[r];
-        b[k] = S.b[r];
-        c[k] = S.c[r];
-    }
+    double a[N], b[N], c[N], vlo[N], vhi[N];
+    unsigned on;
+    l1_steps<N>(S, C, code, K, rlo, rhi, a, b, c, on, vlo, vhi);
     double g[N];
     auto zero = [&]() {
         for (int i = 0; i < N; ++i) g[i] = 0.0;
     };
     // ---- hard rows
     for (int j = 0; j < N; ++j) {
-        // V: v_{j+1} in region sigma_{j+1} (k < N) and the state box
-        double vlo = S.vmin, vhi = S.vmax;
-        if (j + 1 < N) {
-            const int r1 = code_region(code, j + 1);
-            vlo = fmax(vlo, S.vlo[r1]);
-            vhi = fmin(vhi, S.vhi[r1]);
+        // V: v_{j+1} in region sigma_{j+1} (k < N) and the state box (relaxed: reachable interval)
+        zero();
+        g[j] = 1.0;
+        hard(g, 1.0, vhi[j]);
+        hard(g, -1.0, -vlo[j]);
+        // U: c + b umin <= v_{j+1} - a v_j <= c + b umax   (F u <= G); dropped on a relaxed step
+        // without a virtual region
+        if ((on >> j) & 1u) {
+            const double cu = j == 0 ? a[0] * v0 : 0.0;
+            zero();
+            g[j] = 1.0;
+            if (j) g[j - 1] = -a[j];
+            hard(g, 1.0, c[j] + b[j] * S.umax + cu);
+            hard(g, -1.0, -(c[j] + b[j] * S.umin + cu));
         }
-        zero();
-        g[j] = 1.0;
-        hard(g, 1.0, vhi);
-        hard(g, -1.0, -vlo);
-        // U: c + b umin <= v_{j+1} - a v_j <= c + b umax   (F u <= G)
-        const double cu = j == 0 ? a[0] * v0 : 0.0;
-        zero();
-        g[j] = 1.0;
-        if (j) g[j - 1] = -a[j];
-        hard(g, 1.0, c[j] + b[j] * S.umax + cu);
-        hard(g, -1.0, -(c[j] + b[j] * S.umin + cu));
         // A: dec_j <= v_{j+1} - v_j <= acc_j   (fleet_decent_mld.py:172-188)
         const double ca = j == 0 ? v0 : 0.0;
         zero();
@@ -166,15 +258,16 @@ HVP_HD inline bool l1_rows(const hvp_system& S, const Consts& C, int role, const
             pair(tmp, xb[k] + C.d_safe - P1, C.w, 0.0);
         }
     }
-    // inputs u_k = ubar_k + gu_k.y ; Q_u |u_k| and Q_du |u_{k+1} - u_k|
+    // inputs u_k = ubar_k + gu_k.y ; Q_u |u_k| (steps carrying their input) and Q_du |u_{k+1} - u_k|
+    // (both steps decided)
     double gprev[N], uprev = 0.0;
     for (int k = 0; k < N; ++k) {
         double gu[N];
         const double ib = 1.0 / b[k];
         for (int i = 0; i < N; ++i) gu[i] = i == k ? ib : (i + 1 == k ? -a[k] * ib : 0.0);
         const double ubar = k == 0 ? -(a[0] * v0 + c[0]) * ib : -c[k] * ib;
-        pair(gu, ubar, C.Qu, 1.0);
-        if (k >= 1) {
+        if ((on >> k) & 1u) pair(gu, ubar, C.Qu, 1.0);
+        if (k >= 1 && k < K) {
             double gd[N];
             for (int i = 0; i < N; ++i) gd[i] = gu[i] - gprev[i];
             pair(gd, ubar - uprev, C.Qdu, 1.0);
@@ -185,12 +278,92 @@ HVP_HD inline bool l1_rows(const hvp_system& S, const Consts& C, int role, const
     return P1 >= S.pmin - 1e-9 * (1.0 + fabs(S.pmin)) && P1 <= S.pmax + 1e-9 * (1.0 + fabs(S.pmax));
 }
 
+// Exact infeasibility test of the hard rows (V, U, A, P of l1_rows with the same relaxation),
+// run before the interior point: with v_{k+1} in [L_k(v_k), U_k(v_k)] and L_k, U_k nondecreasing
+// (a > 0), the velocity-feasible trajectories form a lattice, so the interval of each v_k over all
+// of them is the forward-reachable interval intersected with the backward-feasible one, and the
+// componentwise lowest / highest trajectories are feasible.  They give every prefix sum its exact
+// minimum / maximum, so
+//   * an empty interval, or
+//   * a position row p_m <= pmax violated by the lowest trajectory (or p_m >= pmin by the highest)
+// proves the LP infeasible (margin 1e-9 relative).  The one case it cannot decide -- rows on both
+// sides of the position box binding within one horizon -- is reported feasible: the interior point
+// then runs and, if it does not converge, the LP stays unresolved (L1_FAIL), never "infeasible".
+template <int N>
+HVP_HD inline bool l1_infeasible(const hvp_system& S, const Consts& C, const double* prm, uint64_t code, int K,
+                                 double rlo, double rhi) {
+    double a[N], b[N], c[N], vlo[N], vhi[N];
+    unsigned on;
+    l1_steps<N>(S, C, code, K, rlo, rhi, a, b, c, on, vlo, vhi);
+    const double v0 = prm[1], P1 = prm[0] + S.ts * v0;
+    auto tol = [](double x) { return 1e-9 * (1.0 + fabs(x)); };
+    // the v_j for which step j admits some v_{j+1}: L_j(v) <= U_j(v)
+    auto step_ok = [&](int j, double& lo, double& hi) {
+        if ((on >> j) & 1u) {
+            if (!(a[j] > 0.0)) return false;
+            const double cl = c[j] + b[j] * S.umin, cu = c[j] + b[j] * S.umax, oma = 1.0 - a[j];
+            if (cu < cl - tol(cl)) return false;
+            if (oma > 0.0) {
+                lo = fmax(lo, -(C.acc[j] - cl) / oma);
+                hi = fmin(hi, (cu - C.dec[j]) / oma);
+            } else if (oma < 0.0) {
+                hi = fmin(hi, (C.acc[j] - cl) / (-oma));
+                lo = fmax(lo, (cu - C.dec[j]) / oma);
+            } else if (C.acc[j] - cl < -tol(cl) || cu - C.dec[j] < -tol(cu)) {
+                return false;
+            }
+        }
+        return C.acc[j] >= C.dec[j] - tol(C.dec[j]);
+    };
+    auto Lmap = [&](int j, double v) {
+        return ((on >> j) & 1u) ? fmax(a[j] * v + c[j] + b[j] * S.umin, v + C.dec[j]) : v + C.dec[j];
+    };
+    auto Umap = [&](int j, double v) {
+        return ((on >> j) & 1u) ? fmin(a[j] * v + c[j] + b[j] * S.umax, v + C.acc[j]) : v + C.acc[j];
+    };
+    double flo[N + 1], fhi[N + 1];
+    flo[0] = fhi[0] = v0;
+    for (int j = 0; j < N; ++j) {  // forward: v_{j+1} reachable
+        double lo = flo[j], hi = fhi[j];
+        if (!step_ok(j, lo, hi) || lo > hi + tol(hi)) return true;
+        if (lo > hi) lo = hi = 0.5 * (lo + hi);
+        flo[j + 1] = fmax(vlo[j], Lmap(j, lo));
+        fhi[j + 1] = fmin(vhi[j], Umap(j, hi));
+        if (flo[j + 1] > fhi[j + 1] + tol(fhi[j + 1])) return true;
+        if (flo[j + 1] > fhi[j + 1]) flo[j + 1] = fhi[j + 1] = 0.5 * (flo[j + 1] + fhi[j + 1]);
+    }
+    for (int j = N - 1; j >= 1; --j) {  // backward: v_j with a continuation (flo/fhi = projection)
+        double lo = flo[j], hi = fhi[j];
+        if (!step_ok(j, lo, hi)) return true;
+        const double B = fhi[j + 1], A = flo[j + 1];
+        hi = fmin(hi, B - C.dec[j]);  // L_j(v) <= B
+        lo = fmax(lo, A - C.acc[j]);  // U_j(v) >= A
+        if ((on >> j) & 1u) {
+            hi = fmin(hi, (B - c[j] - b[j] * S.umin) / a[j]);
+            lo = fmax(lo, (A - c[j] - b[j] * S.umax) / a[j]);
+        }
+        if (lo > hi + tol(hi)) return true;
+        if (lo > hi) lo = hi = 0.5 * (lo + hi);
+        flo[j] = lo;
+        fhi[j] = hi;
+    }
+    // position rows p_{m+2} = P1 + ts (v_1 + .. + v_{m+1}) on the lowest / highest trajectories
+    double smin = 0.0, smax = 0.0;
+    for (int m = 0; m + 2 <= N; ++m) {
+        smin += flo[m + 1];
+        smax += fhi[m + 1];
+        const double pl = P1 + S.ts * smin, ph = P1 + S.ts * smax;
+        if (pl > S.pmax + tol(S.pmax) || ph < S.pmin - tol(S.pmin)) return true;
+    }
+    return false;
+}
+
 // All rows into the lane's arrays (host build and per-lane use).
 template <int N>
 HVP_HD inline bool l1_setup(L1Lp<N>& L, const hvp_system& S, const Consts& C, int role, const double* prm,
-                            uint64_t code) {
+                            uint64_t code, int K = N, double rlo = 0.0, double rhi = -1.0) {
     return l1_rows<N>(
-        S, C, role, prm, code, L.mh, L.mp,
+        S, C, role, prm, code, K, rlo, rhi, L.mh, L.mp,
         [&](int i, const double* g, double sgn, double hh) {
             for (int a = 0; a < N; ++a) L.gh[i][a] = sgn * g[a];
             L.h[i] = hh;
@@ -203,8 +376,9 @@ HVP_HD inline bool l1_setup(L1Lp<N>& L, const hvp_system& S, const Consts& C, in
         });
 }
 
-// Newton direction for the complementarity targets rc_i = s_i l_i (predictor) or
-// s_i l_i + ds_i dl_i - sigma mu (corrector, with the predictor's directions held in L); the
+// Newton direction for the complementarity targets rc_i = s_i l_i - sigmu (predictor: sigmu = 0;
+// centring: sigmu > 0) or s_i l_i + ds_i dl_i - sigmu (corr: the corrector, with the predictor's
+// directions held in L); the
 // residuals of the current iterate are recomputed here.  Returns false if the N x N Schur
 // complement is not positive definite.
 template <int N>
@@ -220,7 +394,7 @@ HVP_HD inline bool l1_direction(L1Lp<N>& L, double sigmu, bool corr, double* dy,
         const double gy = l1_dot<N>(g, L.y);
         const double rp = gy + L.sh[i] - L.h[i];
         const double D = L.lh[i] / L.sh[i];
-        const double rc = L.sh[i] * L.lh[i] + (corr ? L.dsh[i] * L.dlh[i] - sigmu : 0.0);
+        const double rc = L.sh[i] * L.lh[i] + (corr ? L.dsh[i] * L.dlh[i] : 0.0) - sigmu;
         const double rho = (L.lh[i] * rp - rc) / L.sh[i];
         const double coef = -(L.lh[i] + rho);
         for (int a = 0; a < N; ++a) {
@@ -235,8 +409,8 @@ HVP_HD inline bool l1_direction(L1Lp<N>& L, double sigmu, bool corr, double* dy,
         const double rp1 = gy - L.t[j] + L.s1[j] + L.e0[j];
         const double rp2 = -al * gy - L.t[j] + L.s2[j] - al * L.e0[j];
         const double D1 = L.l1[j] / L.s1[j], D2 = L.l2[j] / L.s2[j];
-        const double rc1 = L.s1[j] * L.l1[j] + (corr ? L.ds1[j] * L.dl1[j] - sigmu : 0.0);
-        const double rc2 = L.s2[j] * L.l2[j] + (corr ? L.ds2[j] * L.dl2[j] - sigmu : 0.0);
+        const double rc1 = L.s1[j] * L.l1[j] + (corr ? L.ds1[j] * L.dl1[j] : 0.0) - sigmu;
+        const double rc2 = L.s2[j] * L.l2[j] + (corr ? L.ds2[j] * L.dl2[j] : 0.0) - sigmu;
         const double rho1 = (L.l1[j] * rp1 - rc1) / L.s1[j], rho2 = (L.l2[j] * rp2 - rc2) / L.s2[j];
         const double rdt = L.wp[j] - L.l1[j] - L.l2[j];
         const double rhst = -rdt + rho1 + rho2;
@@ -249,14 +423,14 @@ HVP_HD inline bool l1_direction(L1Lp<N>& L, double sigmu, bool corr, double* dy,
             for (int b = 0; b <= a; ++b) K[tri(a, b)] += ce * g[a] * g[b];
         }
     }
-    if (!cholesky<N>(K)) return false;
+    cholesky_l1<N>(K);
     chol_solve<N>(K, rhs, dy);
     for (int i = 0; i < mh; ++i) {
         const double* g = L.gh[i];
         const double gy = l1_dot<N>(g, L.y), gd = l1_dot<N>(g, dy);
         const double rp = gy + L.sh[i] - L.h[i];
         const double D = L.lh[i] / L.sh[i];
-        const double rc = L.sh[i] * L.lh[i] + (corr ? L.dsh[i] * L.dlh[i] - sigmu : 0.0);
+        const double rc = L.sh[i] * L.lh[i] + (corr ? L.dsh[i] * L.dlh[i] : 0.0) - sigmu;
         const double rho = (L.lh[i] * rp - rc) / L.sh[i];
         dsh[i] = -rp - gd;
         dlh[i] = D * gd + rho;
@@ -268,8 +442,8 @@ HVP_HD inline bool l1_direction(L1Lp<N>& L, double sigmu, bool corr, double* dy,
         const double rp1 = gy - L.t[j] + L.s1[j] + L.e0[j];
         const double rp2 = -al * gy - L.t[j] + L.s2[j] - al * L.e0[j];
         const double D1 = L.l1[j] / L.s1[j], D2 = L.l2[j] / L.s2[j];
-        const double rc1 = L.s1[j] * L.l1[j] + (corr ? L.ds1[j] * L.dl1[j] - sigmu : 0.0);
-        const double rc2 = L.s2[j] * L.l2[j] + (corr ? L.ds2[j] * L.dl2[j] - sigmu : 0.0);
+        const double rc1 = L.s1[j] * L.l1[j] + (corr ? L.ds1[j] * L.dl1[j] : 0.0) - sigmu;
+        const double rc2 = L.s2[j] * L.l2[j] + (corr ? L.ds2[j] * L.dl2[j] : 0.0) - sigmu;
         const double rho1 = (L.l1[j] * rp1 - rc1) / L.s1[j], rho2 = (L.l2[j] * rp2 - rc2) / L.s2[j];
         const double rdt = L.wp[j] - L.l1[j] - L.l2[j];
         const double rhst = -rdt + rho1 + rho2;
@@ -277,9 +451,17 @@ HVP_HD inline bool l1_direction(L1Lp<N>& L, double sigmu, bool corr, double* dy,
         dt[j] = (rhst - m * gd) / mt;
         const double a1 = gd - dt[j], a2 = -al * gd - dt[j];
         ds1[j] = -rp1 - a1;
-        dl1[j] = D1 * a1 + rho1;
         ds2[j] = -rp2 - a2;
-        dl2[j] = D2 * a2 + rho2;
+        // the multiplier of the side with the smaller scaling from its complementarity row, the
+        // other from the t row dl1 + dl2 = w - l1 - l2 exactly: D a of the side with D ~ 1e10
+        // carries the cancellation of a = gd - dt (the t row's residual grew iterate by iterate)
+        if (D1 >= D2) {
+            dl2[j] = D2 * a2 + rho2;
+            dl1[j] = rdt - dl2[j];
+        } else {
+            dl1[j] = D1 * a1 + rho1;
+            dl2[j] = rdt - dl1[j];
+        }
     }
     return true;
 }
@@ -288,10 +470,22 @@ HVP_HD inline void l1_ratio(double& a, double v, double dv) {
     if (dv < 0.0) a = fmin(a, -v / dv);
 }
 
-// Interior point on the rows of l1_setup.  Returns 0 (converged) or 2 (not converged /
-// numerical failure); the iterate is left in L.y.
+// Interior point on the rows of l1_setup.  Returns L1_OK, L1_INFEASIBLE (certificate, l1_farkas,
+// velocity box [ylo, yhi]) or L1_FAIL; the iterate is left in L.y.
 template <int N>
-HVP_HD inline int l1_solve(L1Lp<N>& L, double v0, int max_iter, int& iters) {
+HVP_HD inline int l1_cert(const L1Lp<N>& L, double ylo, double yhi) {
+    double r[N], hl = 0.0, sc = 0.0;
+    for (int a = 0; a < N; ++a) r[a] = 0.0;
+    for (int i = 0; i < L.mh; ++i) {
+        for (int a = 0; a < N; ++a) r[a] += L.lh[i] * L.gh[i][a];
+        hl += L.lh[i] * L.h[i];
+        sc += fabs(L.lh[i] * L.h[i]);
+    }
+    return l1_farkas<N>(r, hl, sc, ylo, yhi) ? L1_INFEASIBLE : L1_FAIL;
+}
+
+template <int N>
+HVP_HD inline int l1_solve(L1Lp<N>& L, double v0, int max_iter, int& iters, double ylo = -1e300, double yhi = 1e300) {
     const int mh = L.mh, mp = L.mp;
     const int mtot = mh + 2 * mp;
     double hscale = 1.0, wmax = 1.0;
@@ -335,10 +529,10 @@ HVP_HD inline int l1_solve(L1Lp<N>& L, double v0, int max_iter, int& iters) {
             for (int a = 0; a < N; ++a) rdy[a] += (L.l1[j] - al * L.l2[j]) * L.gp[j][a];
         }
         for (int a = 0; a < N; ++a) rdmax = fmax(rdmax, fabs(rdy[a]));
-        if (rpmax <= 1e-10 * hscale && rdmax <= 1e-10 * wmax && gap <= 1e-12 * fmax(1.0, fabs(obj))) return 0;
+        if (rpmax <= 1e-10 * hscale && rdmax <= 1e-10 * wmax && gap <= 1e-12 * fmax(1.0, fabs(obj))) return L1_OK;
         const double mu = gap / mtot;
         // predictor
-        if (!l1_direction<N>(L, 0.0, false, dy, dt, L.dsh, L.dlh, L.ds1, L.dl1, L.ds2, L.dl2)) return 2;
+        if (!l1_direction<N>(L, 0.0, false, dy, dt, L.dsh, L.dlh, L.ds1, L.dl1, L.ds2, L.dl2)) return l1_cert<N>(L, ylo, yhi);
         double ap = 1.0, ad = 1.0;
         for (int i = 0; i < mh; ++i) {
             l1_ratio(ap, L.sh[i], L.dsh[i]);
@@ -357,19 +551,26 @@ HVP_HD inline int l1_solve(L1Lp<N>& L, double v0, int max_iter, int& iters) {
                     (L.s2[j] + ap * L.ds2[j]) * (L.l2[j] + ad * L.dl2[j]);
         const double ratio = gaff / gap;
         const double sigma = ratio * ratio * ratio;
-        // corrector (centring + second-order term)
-        if (!l1_direction<N>(L, sigma * mu, true, dy, dt, dsh, dlh, ds1, dl1, ds2, dl2)) return 2;
-        ap = 1.0 / 0.995;
-        ad = 1.0 / 0.995;
-        for (int i = 0; i < mh; ++i) {
-            l1_ratio(ap, L.sh[i], dsh[i]);
-            l1_ratio(ad, L.lh[i], dlh[i]);
-        }
-        for (int j = 0; j < mp; ++j) {
-            l1_ratio(ap, L.s1[j], ds1[j]);
-            l1_ratio(ap, L.s2[j], ds2[j]);
-            l1_ratio(ad, L.l1[j], dl1[j]);
-            l1_ratio(ad, L.l2[j], dl2[j]);
+        // corrector (centring + second-order term); a corrector step shorter than kL1Short is
+        // replaced by a pure centring step (the second-order term can lock the iterate into a cycle
+        // of short steps near a degenerate optimum)
+        for (int pass = 0; pass < 2; ++pass) {
+            if (!l1_direction<N>(L, pass ? kL1Centre * mu : sigma * mu, pass == 0, dy, dt, dsh, dlh, ds1, dl1, ds2,
+                                 dl2))
+                return l1_cert<N>(L, ylo, yhi);
+            ap = 1.0 / 0.995;
+            ad = 1.0 / 0.995;
+            for (int i = 0; i < mh; ++i) {
+                l1_ratio(ap, L.sh[i], dsh[i]);
+                l1_ratio(ad, L.lh[i], dlh[i]);
+            }
+            for (int j = 0; j < mp; ++j) {
+                l1_ratio(ap, L.s1[j], ds1[j]);
+                l1_ratio(ap, L.s2[j], ds2[j]);
+                l1_ratio(ad, L.l1[j], dl1[j]);
+                l1_ratio(ad, L.l2[j], dl2[j]);
+            }
+            if (fmin(ap, ad) >= kL1Short) break;
         }
         ap *= 0.995;
         ad *= 0.995;
@@ -386,15 +587,17 @@ HVP_HD inline int l1_solve(L1Lp<N>& L, double v0, int max_iter, int& iters) {
             L.l2[j] += ad * dl2[j];
         }
     }
-    return 2;
+    return l1_cert<N>(L, ylo, yhi);
 }
 
 // Objective of a trajectory (y = v_1 .. v_N under region code), term by term as the reference
 // writes it with min_1_norm (fleet_decent_mld.py:107-169): Q_ii |e_i| of the tracking errors,
-// Q_u |u|, Q_du |du| and w * max(0, .) slacks, constants included.
+// Q_u |u|, Q_du |du| and w * max(0, .) slacks, constants included.  K < N: the objective of the
+// relaxation of the prefix (l1_steps: virtual-region inputs priced, dropped ones not, Q_du only
+// between decided steps) -- the branch-and-bound bound.
 template <int N>
 HVP_HD inline double l1_direct_cost(const double* y, const hvp_system& S, const Consts& C, int role, const double* prm,
-                                    uint64_t code) {
+                                    uint64_t code, int K = N, double rlo = 0.0, double rhi = -1.0) {
     const double* xf = prm + 2;
     const double* xb = prm + 2 + 2 * (N + 1);
     const double* xl = prm + 2 + 4 * (N + 1);
@@ -402,6 +605,9 @@ HVP_HD inline double l1_direct_cost(const double* y, const hvp_system& S, const 
     const bool tf = (role & HVP_ROLE_TRACK_FRONT) != 0, tb = (role & HVP_ROLE_TRACK_BACK) != 0;
     const bool tl = (role & HVP_ROLE_TRACK_LEADER) != 0, lsp = (role & HVP_ROLE_LEADER_SPACING) != 0;
     const bool sf = (role & HVP_ROLE_SAFE_FRONT) != 0, sb = (role & HVP_ROLE_SAFE_BACK) != 0;
+    double a[N], b[N], c[N], vlo[N], vhi[N];
+    unsigned on;
+    l1_steps<N>(S, C, code, K, rlo, rhi, a, b, c, on, vlo, vhi);
     double J = 0.0, p = prm[0], v = prm[1], uprev = 0.0;
     for (int k = 0; k <= N; ++k) {
         auto nrm = [&](double ep, double ev) { return C.Qpp * fabs(ep) + C.Qvv * fabs(ev); };
@@ -411,10 +617,9 @@ HVP_HD inline double l1_direct_cost(const double* y, const hvp_system& S, const 
         if (sf) J += C.w * fmax(0.0, p - xf[k] + C.d_safe);
         if (sb) J += C.w * fmax(0.0, xb[k] + C.d_safe - p);
         if (k < N) {
-            const int r = code_region(code, k);
-            const double u = (y[k] - S.a[r] * v - S.c[r]) / S.b[r];
-            J += C.Qu * fabs(u);
-            if (k >= 1) J += C.Qdu * fabs(u - uprev);
+            const double u = (y[k] - a[k] * v - c[k]) / b[k];
+            if ((on >> k) & 1u) J += C.Qu * fabs(u);
+            if (k >= 1 && k < K) J += C.Qdu * fabs(u - uprev);
             uprev = u;
             p = p + S.ts * v;
             v = y[k];

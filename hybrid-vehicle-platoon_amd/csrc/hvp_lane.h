@@ -31,6 +31,7 @@ using hvp_detail::Workspace;
 constexpr int kBlock = 256;
 // HVP_METHOD_AUTO: exhaustive enumeration up to this horizon, branch and bound beyond
 constexpr int kAutoEnumMaxN = 0;  // measured: B&B beats enumeration already at N = 5 (profiles/)
+constexpr int kAutoEnumMaxNL1 = 8;  // min_1_norm: enumeration up to N = 8, branch and bound beyond
 // active-set iteration cap (then the interior-point fallback takes the candidate)
 template <int N>
 constexpr int kGiMaxIter = 8 * hvp::GiConstraintSet<N>::NC;
@@ -180,74 +181,158 @@ __device__ inline double wave_min(double v) {
 }
 
 // LDS all-reduce of M doubles per lane within one wavefront (no block barrier: the waves of a
-// block run different LPs).  red: this wave's buffer of M x 65 doubles (row j = value j of the
-// 64 lanes, padded to 65 so that lane j's reads of row j fall in distinct banks, slot 64 = the
-// sum).  Lane j < M sums row j in lane order (M <= 32: lanes j and j + 32 a half each); every
-// lane reads the M sums back (broadcast reads), so all lanes hold bit-identical results.
+// block run different LPs).  red: this wave's buffer of kRedRows<M> x 65 doubles (row j = value j
+// of the 64 lanes, padded to 65 so that lane j's reads of row j fall in distinct banks, slot 64 =
+// the sum).  Lane j < M sums row j in lane order (M <= 32: lanes j and j + 32 a half each); every
+// lane reads the M sums back (broadcast reads), so all lanes hold bit-identical results.  M > 64
+// (the Newton systems of N >= 9) goes through the buffer in chunks of 32 values.
 __device__ inline void lds_wave_sync() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
 }
 template <int M>
-__device__ inline void wave_sum_lds(double* v, double* red, int lane) {
-#pragma unroll
-    for (int j = 0; j < M; ++j) red[j * 65 + lane] = v[j];
-    lds_wave_sync();
-    if constexpr (M <= 32) {
-        // two lanes per value (j and j + 32, 32 entries each), halves combined across the wave
-        // halves (a + b == b + a: both lanes hold the same sum)
-        const int j = lane & 31;
-        double acc = 0.0;
-        if (j < M) {
-            const double* row = red + j * 65 + (lane >> 5) * 32;
+constexpr int kRedRows = M <= 64 ? M : 32;
+
+// rows [0, m) of the buffer: two lanes per value (j and j + 32, 32 entries each), halves combined
+// across the wave halves (a + b == b + a: both lanes hold the same sum)
+__device__ inline void lds_rows_sum32(double* red, int lane, int m) {
+    const int j = lane & 31;
+    double acc = 0.0;
+    if (j < m) {
+        const double* row = red + j * 65 + (lane >> 5) * 32;
 #pragma unroll 16
-            for (int i = 0; i < 32; ++i) acc += row[i];
-        }
-        acc += __shfl_xor(acc, 32, 64);
-        if (lane < M) red[lane * 65 + 64] = acc;
-    } else {
-        if (lane < M) {
-            double acc = 0.0;
-            const double* row = red + lane * 65;
-#pragma unroll 16
-            for (int i = 0; i < 64; ++i) acc += row[i];
-            red[lane * 65 + 64] = acc;
-        }
+        for (int i = 0; i < 32; ++i) acc += row[i];
     }
-    lds_wave_sync();
-#pragma unroll
-    for (int j = 0; j < M; ++j) v[j] = red[j * 65 + 64];
-    lds_wave_sync();  // the buffer is reused by the next reduction
+    acc += __shfl_xor(acc, 32, 64);
+    if (lane < m) red[lane * 65 + 64] = acc;
 }
 
+template <int M>
+__device__ inline void wave_sum_lds(double* v, double* red, int lane) {
+    if constexpr (M <= 64) {
+#pragma unroll
+        for (int j = 0; j < M; ++j) red[j * 65 + lane] = v[j];
+        lds_wave_sync();
+        if constexpr (M <= 32) {
+            lds_rows_sum32(red, lane, M);
+        } else {
+            if (lane < M) {
+                double acc = 0.0;
+                const double* row = red + lane * 65;
+#pragma unroll 16
+                for (int i = 0; i < 64; ++i) acc += row[i];
+                red[lane * 65 + 64] = acc;
+            }
+        }
+        lds_wave_sync();
+#pragma unroll
+        for (int j = 0; j < M; ++j) v[j] = red[j * 65 + 64];
+        lds_wave_sync();  // the buffer is reused by the next reduction
+    } else {
+#pragma unroll
+        for (int c0 = 0; c0 < M; c0 += 32) {
+            constexpr int CH = 32;
+#pragma unroll
+            for (int j = 0; j < CH; ++j)
+                if (c0 + j < M) red[j * 65 + lane] = v[c0 + j];
+            lds_wave_sync();
+            lds_rows_sum32(red, lane, M - c0 < CH ? M - c0 : CH);
+            lds_wave_sync();
+#pragma unroll
+            for (int j = 0; j < CH; ++j)
+                if (c0 + j < M) v[c0 + j] = red[j * 65 + 64];
+            lds_wave_sync();
+        }
+    }
+}
+
+// One LP per wavefront: lane l owns hard rows l, l + 64 (8N - 2 <= 126) and pairs l, l + 64,
+// l + 128 (10N <= 160) in registers.
 template <int N>
 struct L1Wave {
-    static constexpr int NPS = (10 * N + 63) / 64;  // pair slots per lane
+    static constexpr int NHS = (8 * N - 2 + 63) / 64;  // hard-row slots per lane
+    static constexpr int NPS = (10 * N + 63) / 64;     // pair slots per lane
     static constexpr int NT = N * (N + 1) / 2;
-    bool hon;
-    double hg[N], hh, hs, hl, hds, hdl;
+    bool hon[NHS];
+    double hg[NHS][N], hh[NHS], hs[NHS], hl[NHS], hds[NHS], hdl[NHS];
     bool pon[NPS];
     double pg[NPS][N], pe0[NPS], pw[NPS], pal[NPS], pt[NPS], ps1[NPS], ps2[NPS], pl1[NPS], pl2[NPS];
     double pds1[NPS], pdl1[NPS], pds2[NPS], pdl2[NPS], pdt[NPS];
+
+    __device__ void clear() {
+#pragma unroll
+        for (int q = 0; q < NHS; ++q) {
+            hon[q] = false;
+            hh[q] = 0.0;
+            hs[q] = 1.0;
+            hl[q] = hds[q] = hdl[q] = 0.0;
+#pragma unroll
+            for (int a = 0; a < N; ++a) hg[q][a] = 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < NPS; ++q) {
+            pon[q] = false;
+            pe0[q] = pw[q] = pal[q] = pt[q] = pl1[q] = pl2[q] = 0.0;
+            ps1[q] = ps2[q] = 1.0;
+            pds1[q] = pdl1[q] = pds2[q] = pdl2[q] = pdt[q] = 0.0;
+#pragma unroll
+            for (int a = 0; a < N; ++a) pg[q][a] = 0.0;
+        }
+    }
+
+    // the rows of the LP of (prm, code) relaxed after K steps (hvp_l1.h l1_rows) that map to this
+    // lane; false when the constant p_1 row is violated
+    __device__ bool load(const hvp_system& S, const hvp::Consts& C, int rl, const double* prm, uint64_t code, int K,
+                         double rlo, double rhi, int lane, int& mh, int& mp) {
+        clear();
+        return hvp::l1_rows<N>(
+            S, C, rl, prm, code, K, rlo, rhi, mh, mp,
+            [&](int i, const double* g, double sgn, double h) {
+#pragma unroll
+                for (int q = 0; q < NHS; ++q) {
+                    if (i == lane + 64 * q) {
+                        hon[q] = true;
+#pragma unroll
+                        for (int a = 0; a < N; ++a) hg[q][a] = sgn * g[a];
+                        hh[q] = h;
+                    }
+                }
+            },
+            [&](int j, const double* g, double e0, double w, double alpha) {
+#pragma unroll
+                for (int q = 0; q < NPS; ++q) {
+                    if (j == lane + 64 * q) {
+                        pon[q] = true;
+#pragma unroll
+                        for (int a = 0; a < N; ++a) pg[q][a] = g[a];
+                        pe0[q] = e0;
+                        pw[q] = w;
+                        pal[q] = alpha;
+                    }
+                }
+            });
+    }
 
     // this lane's share of: residuals (gap, obj, rd_y, max |rp|, max |rd_t|) when res, and the
     // Newton system (K when withK, rhs for targets rc = s l [+ ds dl - sigmu when corr])
     __device__ void contrib(const double* y, bool corr, double sigmu, bool withK, double* K, double* rhs, double& gap,
                             double& obj, double* rdy, double& rpm, double& rdm) const {
-        if (hon) {
-            const double gy = hvp::l1_dot<N>(hg, y);
-            const double rp = gy + hs - hh, D = hl / hs;
-            const double rc = hs * hl + (corr ? hds * hdl - sigmu : 0.0);
-            const double rho = (hl * rp - rc) / hs, coef = -(hl + rho);
-            gap += hs * hl;
+#pragma unroll
+        for (int q = 0; q < NHS; ++q) {
+            if (!hon[q]) continue;
+            const double gy = hvp::l1_dot<N>(hg[q], y);
+            const double rp = gy + hs[q] - hh[q], D = hl[q] / hs[q];
+            const double rc = hs[q] * hl[q] + (corr ? hds[q] * hdl[q] : 0.0) - sigmu;
+            const double rho = (hl[q] * rp - rc) / hs[q], coef = -(hl[q] + rho);
+            gap += hs[q] * hl[q];
             rpm = fmax(rpm, fabs(rp));
 #pragma unroll
             for (int a = 0; a < N; ++a) {
-                rdy[a] += hl * hg[a];
-                rhs[a] += coef * hg[a];
+                rdy[a] += hl[q] * hg[q][a];
+                rhs[a] += coef * hg[q][a];
                 if (withK) {
 #pragma unroll
-                    for (int c = 0; c <= a; ++c) K[hvp::tri(a, c)] += D * hg[a] * hg[c];
+                    for (int c = 0; c <= a; ++c) K[hvp::tri(a, c)] += D * hg[q][a] * hg[q][c];
                 }
             }
         }
@@ -258,8 +343,8 @@ struct L1Wave {
             const double rp1 = gy - pt[q] + ps1[q] + pe0[q];
             const double rp2 = -al * gy - pt[q] + ps2[q] - al * pe0[q];
             const double D1 = pl1[q] / ps1[q], D2 = pl2[q] / ps2[q];
-            const double rc1 = ps1[q] * pl1[q] + (corr ? pds1[q] * pdl1[q] - sigmu : 0.0);
-            const double rc2 = ps2[q] * pl2[q] + (corr ? pds2[q] * pdl2[q] - sigmu : 0.0);
+            const double rc1 = ps1[q] * pl1[q] + (corr ? pds1[q] * pdl1[q] : 0.0) - sigmu;
+            const double rc2 = ps2[q] * pl2[q] + (corr ? pds2[q] * pdl2[q] : 0.0) - sigmu;
             const double rho1 = (pl1[q] * rp1 - rc1) / ps1[q], rho2 = (pl2[q] * rp2 - rc2) / ps2[q];
             const double rdt = pw[q] - pl1[q] - pl2[q];
             const double rhst = -rdt + rho1 + rho2;
@@ -285,15 +370,17 @@ struct L1Wave {
     // directions of this lane's rows for dy (same targets as contrib), written over the stored
     // ones (each row reads its predictor ds dl before writing); returns the local step limits
     __device__ void directions(const double* y, const double* dy, bool corr, double sigmu, double& ap, double& ad) {
-        if (hon) {
-            const double gy = hvp::l1_dot<N>(hg, y), gd = hvp::l1_dot<N>(hg, dy);
-            const double rp = gy + hs - hh, D = hl / hs;
-            const double rc = hs * hl + (corr ? hds * hdl - sigmu : 0.0);
-            const double rho = (hl * rp - rc) / hs;
-            hds = -rp - gd;
-            hdl = D * gd + rho;
-            hvp::l1_ratio(ap, hs, hds);
-            hvp::l1_ratio(ad, hl, hdl);
+#pragma unroll
+        for (int q = 0; q < NHS; ++q) {
+            if (!hon[q]) continue;
+            const double gy = hvp::l1_dot<N>(hg[q], y), gd = hvp::l1_dot<N>(hg[q], dy);
+            const double rp = gy + hs[q] - hh[q], D = hl[q] / hs[q];
+            const double rc = hs[q] * hl[q] + (corr ? hds[q] * hdl[q] : 0.0) - sigmu;
+            const double rho = (hl[q] * rp - rc) / hs[q];
+            hds[q] = -rp - gd;
+            hdl[q] = D * gd + rho;
+            hvp::l1_ratio(ap, hs[q], hds[q]);
+            hvp::l1_ratio(ad, hl[q], hdl[q]);
         }
 #pragma unroll
         for (int q = 0; q < NPS; ++q) {
@@ -302,17 +389,21 @@ struct L1Wave {
             const double rp1 = gy - pt[q] + ps1[q] + pe0[q];
             const double rp2 = -al * gy - pt[q] + ps2[q] - al * pe0[q];
             const double D1 = pl1[q] / ps1[q], D2 = pl2[q] / ps2[q];
-            const double rc1 = ps1[q] * pl1[q] + (corr ? pds1[q] * pdl1[q] - sigmu : 0.0);
-            const double rc2 = ps2[q] * pl2[q] + (corr ? pds2[q] * pdl2[q] - sigmu : 0.0);
+            const double rc1 = ps1[q] * pl1[q] + (corr ? pds1[q] * pdl1[q] : 0.0) - sigmu;
+            const double rc2 = ps2[q] * pl2[q] + (corr ? pds2[q] * pdl2[q] : 0.0) - sigmu;
             const double rho1 = (pl1[q] * rp1 - rc1) / ps1[q], rho2 = (pl2[q] * rp2 - rc2) / ps2[q];
-            const double rhst = -(pw[q] - pl1[q] - pl2[q]) + rho1 + rho2;
+            const double rdt = pw[q] - pl1[q] - pl2[q];
+            const double rhst = -rdt + rho1 + rho2;
             const double mt = D1 + D2, m = al * D2 - D1;
             pdt[q] = (rhst - m * gd) / mt;
             const double a1 = gd - pdt[q], a2 = -al * gd - pdt[q];
             pds1[q] = -rp1 - a1;
-            pdl1[q] = D1 * a1 + rho1;
             pds2[q] = -rp2 - a2;
-            pdl2[q] = D2 * a2 + rho2;
+            // as hvp_l1.h l1_direction: the larger-scaled side's multiplier from the t row
+            const bool big1 = D1 >= D2;
+            const double dls = big1 ? D2 * a2 + rho2 : D1 * a1 + rho1;
+            pdl1[q] = big1 ? rdt - dls : dls;
+            pdl2[q] = big1 ? dls : rdt - dls;
             hvp::l1_ratio(ap, ps1[q], pds1[q]);
             hvp::l1_ratio(ap, ps2[q], pds2[q]);
             hvp::l1_ratio(ad, pl1[q], pdl1[q]);
@@ -322,22 +413,42 @@ struct L1Wave {
 };
 
 // Mehrotra predictor-corrector (the algorithm of hvp_l1.h l1_solve), wave-cooperative.
-// Returns 0 (converged) or 2; y (uniform) holds the iterate.
+// Returns L1_OK, L1_INFEASIBLE (Farkas certificate of the hard rows over the velocity box
+// [ylo, yhi], hvp_l1.h l1_farkas) or L1_FAIL; y (uniform) holds the iterate.
 template <int N>
 constexpr int kL1Red = 2 + 2 * N + N * (N + 1) / 2;  // gap, obj, rd_y, rhs, K
 
 template <int N>
+__device__ int l1_wave_cert(const L1Wave<N>& W, double* red, int lane, double ylo, double yhi) {
+    double v[N + 2];
+#pragma unroll
+    for (int a = 0; a < N + 2; ++a) v[a] = 0.0;
+#pragma unroll
+    for (int q = 0; q < L1Wave<N>::NHS; ++q) {
+        if (!W.hon[q]) continue;
+#pragma unroll
+        for (int a = 0; a < N; ++a) v[a] += W.hl[q] * W.hg[q][a];
+        v[N] += W.hl[q] * W.hh[q];
+        v[N + 1] += fabs(W.hl[q] * W.hh[q]);
+    }
+    wave_sum_lds<N + 2>(v, red, lane);
+    return hvp::l1_farkas<N>(v, v[N], v[N + 1], ylo, yhi) ? hvp::L1_INFEASIBLE : hvp::L1_FAIL;
+}
+
+template <int N>
 __device__ int l1_wave_solve(L1Wave<N>& W, double* y, double v0, int mh, int mp, int max_iter, int& iters,
-                             double* red, int lane) {
-    constexpr int NPS = L1Wave<N>::NPS;
+                             double* red, int lane, double ylo, double yhi) {
+    constexpr int NPS = L1Wave<N>::NPS, NHS = L1Wave<N>::NHS;
     const int mtot = mh + 2 * mp;
 #pragma unroll
     for (int i = 0; i < N; ++i) y[i] = v0;
     double hsc = 1.0, wmx = 1.0;
-    if (W.hon) {
-        W.hs = fmax(W.hh - hvp::l1_dot<N>(W.hg, y), 1.0);
-        W.hl = 1.0;
-        hsc = fmax(hsc, fabs(W.hh));
+#pragma unroll
+    for (int q = 0; q < NHS; ++q) {
+        if (!W.hon[q]) continue;
+        W.hs[q] = fmax(W.hh[q] - hvp::l1_dot<N>(W.hg[q], y), 1.0);
+        W.hl[q] = 1.0;
+        hsc = fmax(hsc, fabs(W.hh[q]));
     }
 #pragma unroll
     for (int q = 0; q < NPS; ++q) {
@@ -369,9 +480,9 @@ __device__ int l1_wave_solve(L1Wave<N>& W, double* y, double v0, int mh, int mp,
         rdm = wave_max(rdm);
 #pragma unroll
         for (int i = 0; i < N; ++i) rdm = fmax(rdm, fabs(rdy[i]));
-        if (rpm <= 1e-10 * hsc && rdm <= 1e-10 * wmx && gap <= 1e-12 * fmax(1.0, fabs(obj))) return 0;
+        if (rpm <= 1e-10 * hsc && rdm <= 1e-10 * wmx && gap <= 1e-12 * fmax(1.0, fabs(obj))) return hvp::L1_OK;
         const double mu = gap / mtot;
-        if (!hvp::cholesky<N>(K)) return 2;
+        hvp::cholesky_l1<N>(K);
         double dy[N];
         hvp::chol_solve<N>(K, rhs, dy);
         double ap = 1.0, ad = 1.0;
@@ -379,7 +490,9 @@ __device__ int l1_wave_solve(L1Wave<N>& W, double* y, double v0, int mh, int mp,
         ap = wave_min(ap);
         ad = wave_min(ad);
         double gaff = 0.0;
-        if (W.hon) gaff += (W.hs + ap * W.hds) * (W.hl + ad * W.hdl);
+#pragma unroll
+        for (int q = 0; q < NHS; ++q)
+            if (W.hon[q]) gaff += (W.hs[q] + ap * W.hds[q]) * (W.hl[q] + ad * W.hdl[q]);
 #pragma unroll
         for (int q = 0; q < NPS; ++q)
             if (W.pon[q])
@@ -388,24 +501,34 @@ __device__ int l1_wave_solve(L1Wave<N>& W, double* y, double v0, int mh, int mp,
         gaff = wave_sum(gaff);
         const double ratio = gaff / gap;
         const double sigmu = ratio * ratio * ratio * mu;
-        // corrector: same K, new right-hand side
-        double rhs2[N], dum[N];
+        // corrector: same K, new right-hand side; a step shorter than kL1Short is replaced by a pure
+        // centring step (hvp_l1.h l1_solve)
+        for (int pass = 0; pass < 2; ++pass) {
+            const bool corr = pass == 0;
+            const double sm = corr ? sigmu : hvp::kL1Centre * mu;
+            double rhs2[N], dum[N];
 #pragma unroll
-        for (int i = 0; i < N; ++i) rhs2[i] = dum[i] = 0.0;
-        double g2 = 0.0, o2 = 0.0, r2 = 0.0, d2 = 0.0;
-        W.contrib(y, true, sigmu, false, K, rhs2, g2, o2, dum, r2, d2);
-        wave_sum_lds<N>(rhs2, red, lane);
-        hvp::chol_solve<N>(K, rhs2, dy);
-        ap = 1.0 / 0.995;
-        ad = 1.0 / 0.995;
-        W.directions(y, dy, true, sigmu, ap, ad);
-        ap = 0.995 * wave_min(ap);
-        ad = 0.995 * wave_min(ad);
+            for (int i = 0; i < N; ++i) rhs2[i] = dum[i] = 0.0;
+            double g2 = 0.0, o2 = 0.0, r2 = 0.0, d2 = 0.0;
+            W.contrib(y, corr, sm, false, K, rhs2, g2, o2, dum, r2, d2);
+            wave_sum_lds<N>(rhs2, red, lane);
+            hvp::chol_solve<N>(K, rhs2, dy);
+            ap = 1.0 / 0.995;
+            ad = 1.0 / 0.995;
+            W.directions(y, dy, corr, sm, ap, ad);
+            ap = wave_min(ap);
+            ad = wave_min(ad);
+            if (fmin(ap, ad) >= hvp::kL1Short) break;
+        }
+        ap *= 0.995;
+        ad *= 0.995;
 #pragma unroll
         for (int a = 0; a < N; ++a) y[a] += ap * dy[a];
-        if (W.hon) {
-            W.hs += ap * W.hds;
-            W.hl += ad * W.hdl;
+#pragma unroll
+        for (int q = 0; q < NHS; ++q) {
+            if (!W.hon[q]) continue;
+            W.hs[q] += ap * W.hds[q];
+            W.hl[q] += ad * W.hdl[q];
         }
 #pragma unroll
         for (int q = 0; q < NPS; ++q) {
@@ -417,16 +540,40 @@ __device__ int l1_wave_solve(L1Wave<N>& W, double* y, double v0, int mh, int mp,
             W.pl2[q] += ad * W.pdl2[q];
         }
     }
-    return 2;
+    return l1_wave_cert<N>(W, red, lane, ylo, yhi);
+}
+
+// one (node) LP of instance (S, rl, prm): the rows relaxed after K steps from v_K in [rlo, rhi]
+// (K = N: the fixed-sequence LP of code); y (uniform) receives the iterate, cost (on L1_OK) the
+// objective term by term (l1_direct_cost of the same relaxation).  Every lane of the wave calls it.
+template <int N>
+__device__ int l1_node_lp(const hvp_system& S, const hvp::Consts& C, int rl, const double* prm, uint64_t code, int K,
+                          double rlo, double rhi, double* y, double& cost, int& iters, double* red, int lane) {
+    if (hvp::l1_infeasible<N>(S, C, prm, code, K, rlo, rhi)) {  // exact test of the hard rows
+        iters = 0;
+        cost = 0.0;
+#pragma unroll
+        for (int i = 0; i < N; ++i) y[i] = prm[1];
+        return hvp::L1_INFEASIBLE;
+    }
+    L1Wave<N> W;
+    int mh = 0, mp = 0;
+    W.load(S, C, rl, prm, code, K, rlo, rhi, lane, mh, mp);
+    const int st = l1_wave_solve<N>(W, y, prm[1], mh, mp, C.max_iter, iters, red, lane, S.vmin, S.vmax);
+    cost = st == hvp::L1_OK ? hvp::l1_direct_cost<N>(y, S, C, rl, prm, code, K, rlo, rhi) : 0.0;
+    return st;
 }
 
 constexpr int kL1Block = 256;
 template <int N>
+constexpr int kL1BlockOf = N <= HVP_MAX_N_ENUM ? kL1Block : 128;  // LDS: kRedRows x 65 doubles per wave
+
+template <int N>
 __global__ __launch_bounds__(kL1Block) void k_qp_l1(const hvp_system* __restrict__ systems,
                                                     const int32_t* __restrict__ sys, const int32_t* __restrict__ role,
                                                     const double* __restrict__ params, hvp::Consts C, Workspace ws) {
-    static_assert(8 * N - 2 <= 64, "one hard row per lane");
-    __shared__ double s_red[kL1Block / 64][kL1Red<N> * 65];
+    static_assert(8 * N - 2 <= 64, "enumeration: one hard row per lane");
+    __shared__ double s_red[kL1Block / 64][kRedRows<kL1Red<N>> * 65];
     const unsigned long long reserved = ws.counter[0];
     const long long total = (long long)(reserved < (unsigned long long)ws.cap ? reserved : ws.cap);
     const int lane = threadIdx.x & 63;
@@ -437,49 +584,10 @@ __global__ __launch_bounds__(kL1Block) void k_qp_l1(const hvp_system* __restrict
         if (inst < 0) continue;             // dead slot of an overflowed instance
         const hvp_system& S = systems[sys[inst]];
         const double* prm = params + (size_t)inst * (2 + 6 * (N + 1));
-        L1Wave<N> W;
-        W.hon = false;
-        W.hh = 0.0;
-        W.hs = 1.0;
-        W.hl = W.hds = W.hdl = 0.0;
-#pragma unroll
-        for (int a = 0; a < N; ++a) W.hg[a] = 0.0;
-#pragma unroll
-        for (int q = 0; q < L1Wave<N>::NPS; ++q) {
-            W.pon[q] = false;
-            W.pe0[q] = W.pw[q] = W.pal[q] = W.pt[q] = W.pl1[q] = W.pl2[q] = 0.0;
-            W.ps1[q] = W.ps2[q] = 1.0;
-            W.pds1[q] = W.pdl1[q] = W.pds2[q] = W.pdl2[q] = W.pdt[q] = 0.0;
-#pragma unroll
-            for (int a = 0; a < N; ++a) W.pg[q][a] = 0.0;
-        }
-        int mh = 0, mp = 0;
-        hvp::l1_rows<N>(
-            S, C, role[inst], prm, ws.task_code[t], mh, mp,
-            [&](int i, const double* g, double sgn, double hh) {
-                if (i == lane) {
-                    W.hon = true;
-#pragma unroll
-                    for (int a = 0; a < N; ++a) W.hg[a] = sgn * g[a];
-                    W.hh = hh;
-                }
-            },
-            [&](int j, const double* g, double e0, double w, double alpha) {
-#pragma unroll
-                for (int q = 0; q < L1Wave<N>::NPS; ++q) {
-                    if (j == lane + 64 * q) {
-                        W.pon[q] = true;
-#pragma unroll
-                        for (int a = 0; a < N; ++a) W.pg[q][a] = g[a];
-                        W.pe0[q] = e0;
-                        W.pw[q] = w;
-                        W.pal[q] = alpha;
-                    }
-                }
-            });
-        double y[N];
+        double y[N], cost;
         int iters = 0;
-        const int status = l1_wave_solve<N>(W, y, prm[1], mh, mp, hvp::kL1MaxIter, iters, s_red[threadIdx.x >> 6], lane);
+        const int status = l1_node_lp<N>(S, C, role[inst], prm, ws.task_code[t], N, 0.0, -1.0, y, cost, iters,
+                                         s_red[threadIdx.x >> 6], lane);
         if (lane == 0) {
             ws.task_stat[t] = status | (iters << 8);
 #pragma unroll
@@ -526,7 +634,8 @@ __global__ __launch_bounds__(kBlock) void k_select(int B, const hvp_system* __re
                                                    Workspace ws, double* __restrict__ u_out, double* __restrict__ x_out,
                                                    int8_t* __restrict__ region_out, int8_t* __restrict__ gear_out,
                                                    double* __restrict__ cost_out, int32_t* __restrict__ status_out,
-                                                   int32_t* __restrict__ nodes_out, int32_t* __restrict__ iters_out) {
+                                                   int32_t* __restrict__ nodes_out, int32_t* __restrict__ iters_out,
+                                                   int l1) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= B) return;
     const int cnt = ws.inst_cnt[i], off = ws.inst_off[i];
@@ -541,10 +650,12 @@ __global__ __launch_bounds__(kBlock) void k_select(int B, const hvp_system* __re
         status = HVP_OVERFLOW;
     } else {
         double best = 1e300;
+        bool unresolved = false;  // min_1_norm: an LP neither solved nor proven infeasible
         for (int j = 0; j < cnt; ++j) {
             const int st = ws.task_stat[off + j];
             iters += st >> 8;
             if ((st & 0xff) == 0) best = fmin(best, ws.task_cost[off + j]);
+            unresolved = unresolved || (l1 && (st & 0xff) == hvp::L1_FAIL);
         }
         if (best < 1e300) {
             const double tol = 1e-9 * fmax(1.0, fabs(best));
@@ -554,7 +665,12 @@ __global__ __launch_bounds__(kBlock) void k_select(int B, const hvp_system* __re
                     break;
                 }
         }
-        status = win >= 0 ? HVP_OPTIMAL : HVP_MAXITER;
+        // an unresolved LP may hold the optimum (its cost is unknown): never report a possibly
+        // worse sequence as optimal.  (The quadratic path's fallback IPM leaves only infeasible
+        // candidates unsolved: excluded, as the oracle excludes them.)
+        status = win >= 0 && !unresolved ? HVP_OPTIMAL : HVP_MAXITER;
+        if (l1 && best >= 1e300 && !unresolved) status = HVP_INFEASIBLE;  // every LP proven infeasible
+        if (status != HVP_OPTIMAL) win = -1;
     }
     if (status_out) status_out[i] = status;
     if (nodes_out) nodes_out[i] = cnt;
@@ -1021,6 +1137,133 @@ __global__ __launch_bounds__(kBnbBlock<N>) HVP_LANE_OCC void k_bnb_bound(int k, 
     (void)fails;
 }
 
+// ---- min_1_norm (the MILP, hvp_l1.h): the same level-synchronous search with the node LPs solved
+// one per WAVEFRONT (l1_node_lp).  Root: the fully relaxed LP (K = 0) gives the root bound and the
+// greedy dive's target velocities; the dive's leaf LP (and the hinted sequence's, if any) the
+// initial incumbent.  Node statuses: an LP proven infeasible prunes its subtree (bound +inf) or
+// drops its leaf; an unresolved LP prunes nothing (bound -inf) and, at a leaf still in contention,
+// makes the instance HVP_MAXITER (k_bnb_key).  Children: k_bnb_expand per level.
+template <int N>
+__global__ __launch_bounds__(kL1BlockOf<N>) void k_l1_root(int B, const hvp_system* __restrict__ systems,
+                                                           const int32_t* __restrict__ sys,
+                                                           const int32_t* __restrict__ role,
+                                                           const double* __restrict__ params, hvp::Consts C,
+                                                           Workspace ws) {
+    __shared__ double s_red[kL1BlockOf<N> / 64][kRedRows<kL1Red<N>> * 65];
+    double* red = s_red[threadIdx.x >> 6];
+    const int lane = threadIdx.x & 63;
+    const long long nwaves = ((long long)gridDim.x * blockDim.x) >> 6;
+    if (blockIdx.x == 0 && threadIdx.x == 0) ws.lvl[0] = (unsigned long long)B;
+    for (long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6; i < B; i += nwaves) {
+        const hvp_system& S = systems[sys[i]];
+        const int rl = role[i];
+        const double* prm = params + (size_t)i * C.stride;
+        const double v0 = prm[1], P1 = prm[0] + S.ts * v0;
+        const bool ok = P1 >= S.pmin - 1e-9 * (1.0 + fabs(S.pmin)) && P1 <= S.pmax + 1e-9 * (1.0 + fabs(S.pmax));
+        double inc = __longlong_as_double(0x7ff0000000000000ll);  // +inf: no incumbent
+        double lb = -1e300;
+        int nodes = 0, iters = 0;
+        // up to three LPs with ONE call site (the LP body is inlined once): 0 the root relaxation,
+        // 1 the greedy dive's leaf, 2 the hinted sequence's leaf
+        uint64_t code = 0, dive_code = 0;
+        int job = ok ? 0 : 3, K = 0;
+        double rlo = v0, rhi = v0;
+        bool dived = false;
+        while (job < 3) {
+            double y[N], c = 0.0;
+            int it = 0;
+            const int st = l1_node_lp<N>(S, C, rl, prm, code, K, rlo, rhi, y, c, it, red, lane);
+            ++nodes;
+            iters += it;
+            int next = 3;
+            if (job == 0) {
+                if (st == hvp::L1_INFEASIBLE) lb = 1e300;  // no completion is feasible
+                if (st == hvp::L1_OK) {
+                    lb = c;
+                    dived = hvp::bnb_dive<N>(S, C, v0, y, &dive_code);
+                    next = dived ? 1 : 2;
+                }
+            } else {
+                if (st == hvp::L1_OK && !(c >= inc)) inc = c;
+                next = job + 1;
+            }
+            if (next == 1) code = dive_code;
+            if (next == 2) {
+                uint64_t hc = 0;
+                if (ws.hint && hint_code<N>(ws, (int)i, S, C, v0, &hc) && !(dived && hc == dive_code)) code = hc;
+                else next = 3;
+            }
+            job = next;
+            K = N;
+            rlo = 0.0;
+            rhi = -1.0;
+        }
+        if (lane == 0) {
+            ws.key[i] = ~0ull;
+            ws.inst_flag[i] = ok ? 0 : 1;
+            ws.nd_inst[0][i] = ok ? (int)i : -1;
+            ws.nd_code[0][i] = 0;
+            ws.nd_lo[0][i] = v0;
+            ws.nd_hi[0][i] = v0;
+            ws.nd_lb[0][i] = lb;
+            ws.inc[i] = cost_key(inc);
+            ws.nodes[i] = nodes;
+            ws.iters[i] = iters;
+            atomicAdd(&ws.counter[3], (unsigned long long)nodes);
+            atomicAdd(&ws.counter[1], (unsigned long long)iters);
+        }
+    }
+}
+
+template <int N>
+__global__ __launch_bounds__(kL1BlockOf<N>) void k_l1_bound(int k, const hvp_system* __restrict__ systems,
+                                                            const int32_t* __restrict__ sys,
+                                                            const int32_t* __restrict__ role,
+                                                            const double* __restrict__ params, hvp::Consts C,
+                                                            Workspace ws) {
+    __shared__ double s_red[kL1BlockOf<N> / 64][kRedRows<kL1Red<N>> * 65];
+    double* red = s_red[threadIdx.x >> 6];
+    const int lane = threadIdx.x & 63;
+    const int dst = k & 1;
+    const unsigned long long nn = ws.lvl[k];
+    const long long total = (long long)(nn < (unsigned long long)ws.cap ? nn : ws.cap);
+    const long long nwaves = ((long long)gridDim.x * blockDim.x) >> 6;
+    unsigned long long iter_sum = 0;
+    for (long long t = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6; t < total; t += nwaves) {
+        const int inst = ws.nd_inst[dst][t];  // wave-uniform
+        if (inst < 0) {                        // dead slot of an overflowed reservation
+            if (lane == 0) {
+                if (k == N) ws.leaf_stat[t] = HVP_OVERFLOW;
+                else ws.nd_lb[dst][t] = 1e300;
+            }
+            continue;
+        }
+        const hvp_system& S = systems[sys[inst]];
+        const double* prm = params + (size_t)inst * C.stride;
+        double y[N], c = 0.0;
+        int it = 0;
+        const int st = l1_node_lp<N>(S, C, role[inst], prm, ws.nd_code[dst][t], k, ws.nd_lo[dst][t],
+                                     ws.nd_hi[dst][t], y, c, it, red, lane);
+        iter_sum += (unsigned long long)it;
+        if (lane != 0) continue;
+        atomicAdd(&ws.nodes[inst], 1);
+        atomicAdd(&ws.iters[inst], it);
+        if (k < N) {
+            // proven infeasible: the subtree holds no feasible completion; unresolved: prunes nothing
+            ws.nd_lb[dst][t] = st == hvp::L1_OK ? c : (st == hvp::L1_INFEASIBLE ? 1e300 : -1e300);
+            if (st == hvp::L1_FAIL) atomicAdd(&ws.counter[4], 1ull);
+        } else {
+            if (st == hvp::L1_OK) ws.nd_lb[dst][t] = c;  // an unresolved leaf keeps its parent's bound
+            ws.leaf_stat[t] = st == hvp::L1_OK ? 0 : (st == hvp::L1_INFEASIBLE ? HVP_INFEASIBLE : HVP_MAXITER);
+#pragma unroll
+            for (int j = 0; j < N; ++j) ws.task_y[t * N + j] = y[j];
+            if (st == hvp::L1_OK) atomicMin(&ws.inc[inst], cost_key(c));
+            if (st == hvp::L1_FAIL) atomicOr(&ws.inst_flag[inst], 8);  // a sequence exists, unresolved
+        }
+    }
+    if (lane == 0 && iter_sum) atomicAdd(&ws.counter[1], iter_sum);
+}
+
 // ---- the same bound / leaf QPs, persistent waves (decentralised form, N <= 8)
 // Every wave loops over { one active-set trip per busy lane (scan if due, one step) } and, when
 // at least kRefillMin lanes are free, an EVENT: the lanes whose QP finished write their results
@@ -1266,7 +1509,7 @@ __global__ __launch_bounds__(kBnbBlock<N>) void k_bnb_ipm(const hvp_system* __re
 
 // tie rule: the lexicographically first leaf within 1e-9 relative of the minimum
 template <int N>
-__global__ __launch_bounds__(kBlock) void k_bnb_key(Workspace ws, int form) {
+__global__ __launch_bounds__(kBlock) void k_bnb_key(Workspace ws, int form, int l1) {
     const int src = N & 1;
     const unsigned long long nn = ws.lvl[N];
     const long long total = (long long)(nn < (unsigned long long)ws.cap ? nn : ws.cap);
@@ -1279,8 +1522,10 @@ __global__ __launch_bounds__(kBlock) void k_bnb_key(Workspace ws, int form) {
             // Up to HVP_MAX_N_ENUM a leaf that fails the active-set method AND the interior-point
             // fallback is an infeasible QP (position box), excluded exactly as the enumeration
             // path and the oracle exclude it.  Beyond, there is no fallback: a failed leaf still
-            // in contention makes the instance MAXITER rather than a possibly wrong answer.
-            if ((N > HVP_MAX_N_ENUM || form != HVP_FORM_DECENT) && !hvp::bnb_pruned(ws.nd_lb[src][t], best))
+            // in contention makes the instance MAXITER rather than a possibly wrong answer.  The
+            // min_1_norm leaves are HVP_INFEASIBLE (certified, excluded) or HVP_MAXITER (unresolved).
+            const bool strict = N > HVP_MAX_N_ENUM || form != HVP_FORM_DECENT || l1;
+            if (ws.leaf_stat[t] == HVP_MAXITER && strict && !hvp::bnb_pruned(ws.nd_lb[src][t], best))
                 atomicOr(&ws.inst_flag[inst], 4);
             continue;
         }
@@ -1693,7 +1938,11 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
     HIP_TRY(hipEventRecord(h->evq0, st));
     const size_t lds = sizeof(double) * hvp::F_COUNT * N * BS;
     HIP_TRY(hipEventRecord(h->evb[0], st));
-    if constexpr (kCoop<N>) {
+    const int g_l1 = std::max(1, h->n_cu) * (N <= HVP_MAX_N_ENUM ? 8 : 16);  // waves grid-stride over nodes
+    if (h->C.l1) {
+        hipLaunchKernelGGL(k_l1_root<N>, dim3(g_l1), dim3(kL1BlockOf<N>), 0, st, B, h->d_sys, sys, role, params, h->C,
+                           ws);
+    } else if constexpr (kCoop<N>) {
         hipLaunchKernelGGL(k_bnb_root_coop<N>, dim3((B + kCoopGroups - 1) / kCoopGroups), dim3(kCoopBlock), 0, st, B,
                            h->d_sys, sys, role, params, h->C, ws);
     } else {
@@ -1718,13 +1967,16 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
     const int g_qp = (int)std::min<long long>((h->ws.cap + BS - 1) / BS, (long long)h->n_cu * 8 * (kBlock / BS));
     // the decentralised lane path generates every level's nodes inside k_bnb_root / the bound
     // kernel of the level above (fused expand); the other paths run k_bnb_expand per level
-    const bool fused = !kCoop<N> && h->C.form == HVP_FORM_DECENT;
+    const bool fused = !kCoop<N> && h->C.form == HVP_FORM_DECENT && !h->C.l1;
     for (int k = 1; k <= N; ++k) {
         if (!fused)
             hipLaunchKernelGGL(k_bnb_expand<N>, dim3(g_small), dim3(kBlock), 0, st, k, h->d_sys, sys, h->C, ws);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(h->evb[2 * k], st));
-        if constexpr (kCoop<N>) {
+        if (h->C.l1) {
+            hipLaunchKernelGGL(k_l1_bound<N>, dim3(g_l1), dim3(kL1BlockOf<N>), 0, st, k, h->d_sys, sys, role, params,
+                               h->C, ws);
+        } else if constexpr (kCoop<N>) {
             const int g_coop = (int)std::min<long long>((h->ws.cap + kCoopGroups - 1) / kCoopGroups,
                                                         (long long)h->n_cu * 32);
             hipLaunchKernelGGL(k_bnb_bound_coop<N>, dim3(g_coop), dim3(kCoopBlock), 0, st, k, h->d_sys, sys, role,
@@ -1746,12 +1998,12 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
     }
     HIP_TRY(hipEventRecord(h->evq1, st));
     if constexpr (N <= HVP_MAX_N_ENUM) {
-        if (h->C.form == HVP_FORM_DECENT)
+        if (h->C.form == HVP_FORM_DECENT && !h->C.l1)
         hipLaunchKernelGGL(k_bnb_ipm<N>, dim3(std::max(1, h->n_cu)), dim3(BS), lds, st, h->d_sys, sys, role, params,
                            h->C, ws);
         HIP_TRY(hipGetLastError());
     }
-    hipLaunchKernelGGL(k_bnb_key<N>, dim3(g_small), dim3(kBlock), 0, st, ws, h->C.form);
+    hipLaunchKernelGGL(k_bnb_key<N>, dim3(g_small), dim3(kBlock), 0, st, ws, h->C.form, h->C.l1);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_bnb_write<N>, dim3(g_small), dim3(kBlock), 0, st, h->d_sys, sys, role, params, h->C, ws,
                        u_out, x_out, region_out, gear_out, cost_out, xf_out, xb_out);
@@ -1799,7 +2051,7 @@ int launch_all(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
     hipLaunchKernelGGL(k_cost<N>, dim3((int)want), dim3(kBlock), 0, st, h->d_sys, sys, role, params, h->C, ws);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_select<N>, dim3(grid_for(B)), dim3(kBlock), 0, st, B, h->d_sys, sys, params, ws, u_out,
-                       x_out, region_out, gear_out, cost_out, status_out, nodes_out, iters_out);
+                       x_out, region_out, gear_out, cost_out, status_out, nodes_out, iters_out, h->C.l1);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(h->ev1, st));
     h->last_stream = st;

@@ -152,9 +152,9 @@ class LocalMpcMld(MpcMld):
     def setup_cost_and_constraints(self, u, spacing_policy=ConstantSpacingPolicy(50), quadratic_cost: bool = True,
                                    is_front: bool = False, is_leader=False, is_trailer=False,
                                    accel_cnstr_tightening: float = 0.0, real_vehicle_as_reference: bool = False):
-        # quadratic_cost=False (min_1_norm, fleet_decent_mld.py:73-76): the fixed-sequence LPs of
-        # csrc/hvp_l1.h under exhaustive enumeration (N <= HVP_MAX_N_ENUM; hvp_create refuses longer
-        # horizons with HVP_E_UNSUPPORTED)
+        # quadratic_cost=False (min_1_norm, fleet_decent_mld.py:73-76): the local MILP by the
+        # fixed-sequence LPs of csrc/hvp_l1.h, exhaustive enumeration up to N = 8 and branch and
+        # bound over node LPs beyond (any horizon up to HVP_MAX_N)
         self.quadratic_cost = quadratic_cost
         self.is_front, self.is_leader, self.is_trailer = is_front, is_leader, is_trailer
         self.spacing_policy = spacing_policy

@@ -42,7 +42,10 @@ Files (numpy .npz, no pickles):
                       n = 3 at N = 10, n = 10 at N = 3, variants (real_vehicle_as_reference, leader
                       index, task_2 masses / ConstantTime / stop-and-go, Q_du), mid-rollout states,
                       the gear model (MpcGearCent, model = 1)
-Run:  python tests/golden/make_golden.py [sweep | gear | admm | admm_gear | gadmm | cent [n10] | configs admm|gadmm]
+  l1_long_*_N{9,10}.npz  min_1_norm at the MILP-vs-MIQP study's longer horizons (oracle branch
+                      and bound, "method" = 1, "quadratic" = 0): t = 0 states, Q_du, a rollout
+Run:  python tests/golden/make_golden.py [sweep | gear | admm | admm_gear | gadmm | cent [n10] | configs admm|gadmm
+                                          | l1 | l1_rollout | l1_long]
 """
 
 from __future__ import annotations
@@ -151,6 +154,26 @@ def l1_rollout():
     sit on region edges and ties between sequences are likeliest."""
     params, roles, si, exp = rollout(4, 5, range(3), 8, quadratic=False)
     save("l1_rollout_n4_N5.npz", 5, [800.0], O.Cfg(), params, roles, si, exp, quadratic=0)
+
+
+def l1_long():
+    """min_1_norm at the longer horizons of the reference's MILP-vs-MIQP study (N = 5..10,
+    results_analysis/analyse_results_MILP_MIQP.py:9-12): the oracle's branch and bound (its L1 path
+    at N = 9 agrees with its exhaustive enumeration on the seed-0 platoon: same sequences and costs,
+    2437 / 7104 / 1399 / 1416 sequences against 29 / 31 / 86 / 46 node LPs)."""
+    O.set_method(O.METHOD_BNB)
+    try:
+        params, roles, si, exp = decent_seeds(4, 9, range(3), quadratic=False)
+        save("l1_long_n4_N9.npz", 9, [800.0], O.Cfg(), params, roles, si, exp, method=1, quadratic=0)
+        params, roles, si, exp = decent_seeds(5, 10, range(3), quadratic=False)
+        save("l1_long_n5_N10.npz", 10, [800.0], O.Cfg(), params, roles, si, exp, method=1, quadratic=0)
+        cfg = O.Cfg(Qdu=0.5)
+        params, roles, si, exp = decent_seeds(4, 10, range(2), cfg=cfg, quadratic=False)
+        save("l1_long_qdu_n4_N10.npz", 10, [800.0], cfg, params, roles, si, exp, method=1, quadratic=0)
+        params, roles, si, exp = rollout(4, 10, range(2), 4, quadratic=False)
+        save("l1_long_rollout_n4_N10.npz", 10, [800.0], O.Cfg(), params, roles, si, exp, method=1, quadratic=0)
+    finally:
+        O.set_method(O.METHOD_ENUMERATE)
 
 
 def gear_model():
@@ -530,6 +553,9 @@ def main():
         return
     if len(sys.argv) > 1 and sys.argv[1] == "l1":
         l1_fixtures()
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == "l1_long":
+        l1_long()
         return
     if len(sys.argv) > 1 and sys.argv[1] == "l1_rollout":
         l1_rollout()

@@ -126,6 +126,8 @@ def test_l1_lane_matches_golden(hostref, name):
     L1 path is pinned to HiGHS milp on the reference's big-M MLD, tests/test_oracle.py).
     Bar: sequences and sequence counts exact, cost 1e-9 relative, u 1e-6."""
     fx = load(name)
+    if int(fx["N"]) > 8:
+        pytest.skip("beyond exhaustive enumeration (HVP_MAX_N_ENUM): branch and bound only")
     prob, systems = product_problem(fx)
     assert prob.quadratic_cost == 0
     prob.method = 1
@@ -139,3 +141,22 @@ def test_l1_lane_matches_golden(hostref, name):
     assert np.all(np.abs(c - ce) <= 1e-9 * np.maximum(1, np.abs(ce)))
     assert np.abs(out["u"] - fx["exp_u"]).max() <= 1e-6
     assert np.abs(out["x"] - fx["exp_x"]).max() <= 1e-4
+
+
+@pytest.mark.parametrize("name", l1_fixture_names())
+def test_l1_branch_and_bound_matches_golden(hostref, name):
+    """min_1_norm by branch and bound (hvp_l1.h node LPs relaxed after K steps, the product's
+    k_l1_root / k_l1_bound search): the same sequences, costs and trajectories as the oracle's
+    MILP optima, with fewer LPs than the sequences enumerated."""
+    fx = load(name)
+    prob, systems = product_problem(fx)
+    prob.method = 2  # HVP_METHOD_BNB
+    out = run(hostref, prob, systems, fx)
+    assert np.array_equal(out["status"], fx["exp_status"])
+    assert np.array_equal(out["region"], fx["exp_region"])
+    c, ce = out["cost"], fx["exp_cost"]
+    assert np.all(np.abs(c - ce) <= 1e-9 * np.maximum(1, np.abs(ce)))
+    assert np.abs(out["u"] - fx["exp_u"]).max() <= 1e-6
+    assert np.abs(out["x"] - fx["exp_x"]).max() <= 1e-4
+    if int(fx["N"]) >= 5 and int(fx.get("method", 0)) == 0:  # exp_nodes = sequences enumerated
+        assert out["nodes"].mean() < fx["exp_nodes"].mean()
