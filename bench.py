@@ -867,8 +867,8 @@ def main() -> None:
                     help="admm: do not try the previous iteration's sequences as incumbents (A/B)")
     ap.add_argument("--gadmm-layout", choices=["replicas", "vehicles"], default="replicas")
     ap.add_argument("--cost", choices=["quadratic", "l1"], default="quadratic",
-                    help="decent: min_2_norm (default) or min_1_norm (the MILP variant: --method auto = enumeration "
-                         "up to N = 8, branch and bound beyond)")
+                    help="decent: min_2_norm (default) or min_1_norm (the MILP variant; --method auto = branch and "
+                         "bound, enum = exhaustive enumeration up to N = 8)")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU work: start the ranks (gloo), shard the seeds, run the timing protocol around an "
                          "empty step and print the line (tests the --gpus N launcher on a CPU)")
@@ -922,7 +922,7 @@ def main() -> None:
     method = {"auto": 0, "enum": 1, "bnb": 2}[args.method]
     quadratic = args.cost == "quadratic"
     if not quadratic and method == 0:
-        method = 1 if N <= 8 else 2  # min_1_norm AUTO: enumeration up to N = 8 (hvp_lane.h kAutoEnumMaxNL1)
+        method = 2  # min_1_norm AUTO: branch and bound at every horizon (hvp_lane.h kAutoEnumMaxNL1)
     # each rank owns a disjoint seed range: platoons are independent (weak scaling)
     params, roles = make_inputs(seed_range(rank, S), n, N)
     B = len(roles)

@@ -17,7 +17,7 @@
 namespace {
 
 constexpr int kAutoEnumMaxN = 0;    // same crossovers as hvp_lane.h (HVP_METHOD_AUTO)
-constexpr int kAutoEnumMaxNL1 = 8;
+constexpr int kAutoEnumMaxNL1 = 0;
 
 // 0: interior point only; 1: Goldfarb-Idnani active set, interior point on failure
 int g_solver = 1;

@@ -21,10 +21,12 @@
 // Solver: Mehrotra predictor-corrector primal-dual interior point in (y, t), every epigraph
 // variable eliminated analytically from its two rows (Schur complement per pair:
 // D1 D2 (1 + alpha)^2 / (D1 + D2) g g'), so the Newton system is N x N whatever the number of
-// terms.  Rows are stored densely per lane (N <= HVP_MAX_N_ENUM = 8: at most 62 hard rows and
-// 80 pairs); this path runs with exhaustive enumeration only.  The interior point converges to
-// a point of the optimal face; the objective -- what the sequence search compares -- is
-// evaluated term by term on it (l1_direct_cost).
+// terms.  The interior point converges to a point of the optimal face; the objective -- what
+// the sequence search compares -- is evaluated term by term on it (l1_direct_cost).  Before it
+// runs, l1_infeasible decides the hard rows exactly (velocity lattice + position extremes); an LP
+// it cannot solve is L1_FAIL (unresolved), never silently dropped.  Search: enumeration (N <= 8)
+// or branch and bound with the node LPs relaxed after K steps (l1_steps, the quadratic path's
+// tail relaxation).
 //
 // No HIP dependency: hvp_lane.h compiles it for gfx950, the test-only host build
 // (hvp_hostref.cpp) with g++.

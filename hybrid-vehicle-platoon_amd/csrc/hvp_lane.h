@@ -31,7 +31,9 @@ using hvp_detail::Workspace;
 constexpr int kBlock = 256;
 // HVP_METHOD_AUTO: exhaustive enumeration up to this horizon, branch and bound beyond
 constexpr int kAutoEnumMaxN = 0;  // measured: B&B beats enumeration already at N = 5 (profiles/)
-constexpr int kAutoEnumMaxNL1 = 8;  // min_1_norm: enumeration up to N = 8, branch and bound beyond
+// min_1_norm: branch and bound at every horizon too -- C2 (16,384 platoons): 78.0k platoon-steps/s
+// against 56.6k by enumeration (2.71M vs 5.0M LPs per step, profiles/r03e_*)
+constexpr int kAutoEnumMaxNL1 = 0;
 // active-set iteration cap (then the interior-point fallback takes the candidate)
 template <int N>
 constexpr int kGiMaxIter = 8 * hvp::GiConstraintSet<N>::NC;
@@ -546,7 +548,7 @@ __device__ int l1_wave_solve(L1Wave<N>& W, double* y, double v0, int mh, int mp,
 // one (node) LP of instance (S, rl, prm): the rows relaxed after K steps from v_K in [rlo, rhi]
 // (K = N: the fixed-sequence LP of code); y (uniform) receives the iterate, cost (on L1_OK) the
 // objective term by term (l1_direct_cost of the same relaxation).  Every lane of the wave calls it.
-template <int N>
+template <int N, bool COST = true>
 __device__ int l1_node_lp(const hvp_system& S, const hvp::Consts& C, int rl, const double* prm, uint64_t code, int K,
                           double rlo, double rhi, double* y, double& cost, int& iters, double* red, int lane) {
     if (hvp::l1_infeasible<N>(S, C, prm, code, K, rlo, rhi)) {  // exact test of the hard rows
@@ -560,7 +562,7 @@ __device__ int l1_node_lp(const hvp_system& S, const hvp::Consts& C, int rl, con
     int mh = 0, mp = 0;
     W.load(S, C, rl, prm, code, K, rlo, rhi, lane, mh, mp);
     const int st = l1_wave_solve<N>(W, y, prm[1], mh, mp, C.max_iter, iters, red, lane, S.vmin, S.vmax);
-    cost = st == hvp::L1_OK ? hvp::l1_direct_cost<N>(y, S, C, rl, prm, code, K, rlo, rhi) : 0.0;
+    cost = COST && st == hvp::L1_OK ? hvp::l1_direct_cost<N>(y, S, C, rl, prm, code, K, rlo, rhi) : 0.0;
     return st;
 }
 
@@ -586,8 +588,8 @@ __global__ __launch_bounds__(kL1Block) void k_qp_l1(const hvp_system* __restrict
         const double* prm = params + (size_t)inst * (2 + 6 * (N + 1));
         double y[N], cost;
         int iters = 0;
-        const int status = l1_node_lp<N>(S, C, role[inst], prm, ws.task_code[t], N, 0.0, -1.0, y, cost, iters,
-                                         s_red[threadIdx.x >> 6], lane);
+        const int status = l1_node_lp<N, false>(S, C, role[inst], prm, ws.task_code[t], N, 0.0, -1.0, y, cost,
+                                                iters, s_red[threadIdx.x >> 6], lane);  // k_cost prices it
         if (lane == 0) {
             ws.task_stat[t] = status | (iters << 8);
 #pragma unroll
@@ -1143,8 +1145,12 @@ __global__ __launch_bounds__(kBnbBlock<N>) HVP_LANE_OCC void k_bnb_bound(int k, 
 // initial incumbent.  Node statuses: an LP proven infeasible prunes its subtree (bound +inf) or
 // drops its leaf; an unresolved LP prunes nothing (bound -inf) and, at a leaf still in contention,
 // makes the instance HVP_MAXITER (k_bnb_key).  Children: k_bnb_expand per level.
+// 2 waves per SIMD up to N = 8 (the wave solver fits 256 registers; at 1 wave the LP rate halves)
 template <int N>
-__global__ __launch_bounds__(kL1BlockOf<N>) void k_l1_root(int B, const hvp_system* __restrict__ systems,
+constexpr int kL1Waves = N <= HVP_MAX_N_ENUM ? 2 : 1;
+
+template <int N>
+__global__ __launch_bounds__(kL1BlockOf<N>) __attribute__((amdgpu_waves_per_eu(kL1Waves<N>))) void k_l1_root(int B, const hvp_system* __restrict__ systems,
                                                            const int32_t* __restrict__ sys,
                                                            const int32_t* __restrict__ role,
                                                            const double* __restrict__ params, hvp::Consts C,
@@ -1216,7 +1222,7 @@ __global__ __launch_bounds__(kL1BlockOf<N>) void k_l1_root(int B, const hvp_syst
 }
 
 template <int N>
-__global__ __launch_bounds__(kL1BlockOf<N>) void k_l1_bound(int k, const hvp_system* __restrict__ systems,
+__global__ __launch_bounds__(kL1BlockOf<N>) __attribute__((amdgpu_waves_per_eu(kL1Waves<N>))) void k_l1_bound(int k, const hvp_system* __restrict__ systems,
                                                             const int32_t* __restrict__ sys,
                                                             const int32_t* __restrict__ role,
                                                             const double* __restrict__ params, hvp::Consts C,

@@ -68,9 +68,11 @@ typedef struct hvp_system {
 typedef struct hvp_problem {
     int32_t N;              /* prediction horizon (2..HVP_MAX_N)                      */
     int32_t quadratic_cost; /* 1 = min_2_norm (MIQP); 0 = min_1_norm (MILP,
-                               fleet_decent_mld.py:73-76): HVP_FORM_DECENT with N <=
-                               HVP_MAX_N_ENUM by enumeration (method AUTO / ENUMERATE;
-                               fixed-sequence LPs of csrc/hvp_l1.h), else HVP_E_UNSUPPORTED */
+                               fleet_decent_mld.py:73-76): HVP_FORM_DECENT, any N, by branch
+                               and bound over node LPs (AUTO / BNB) or enumeration (ENUMERATE,
+                               N <= HVP_MAX_N_ENUM); LPs of csrc/hvp_l1.h; an LP neither solved
+                               nor proven infeasible makes its instance HVP_MAXITER.  Other
+                               formulations: HVP_E_UNSUPPORTED */
     double Qx[4];           /* 2x2 row-major state-tracking weight                     */
     double Qu;              /* control weight                                          */
     double Qdu;             /* control-variation weight                                */
@@ -81,7 +83,8 @@ typedef struct hvp_problem {
     double accel_tightening;
     double spacing_d0;      /* spacing(x) = [-d0 - t0 * v, 0]                          */
     double spacing_t0;
-    int32_t max_iter;       /* fallback IPM iteration cap per candidate (<=0: 60)      */
+    int32_t max_iter;       /* fallback IPM iteration cap per candidate (<=0: 60);
+                               min_1_norm: the LP interior point's cap (<=0: 120)       */
     int32_t method;         /* HVP_METHOD_*: how the region sequences are searched     */
     double tol;             /* fallback IPM relative tolerance (<=0: 1e-12)            */
     int32_t formulation;    /* HVP_FORM_*: which local MPC (parameter layout, cost)    */

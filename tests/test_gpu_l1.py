@@ -25,16 +25,21 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("name", l1_fixture_names())
-def test_l1_golden_fixture_on_gpu(gpu_available, name):
+def test_l1_enumeration_fixture_on_gpu(gpu_available, name):
     from hvp.solver import BatchSolver
 
+    from hvp import _abi
+
     fx = load(name)
+    if int(fx["N"]) > 8:
+        pytest.skip("beyond exhaustive enumeration (HVP_MAX_N_ENUM): branch and bound only")
     prob, systems = product_problem(fx)
     assert prob.quadratic_cost == 0
+    prob.method = _abi.METHOD_ENUMERATE
     s = BatchSolver(prob, systems)
     res = s.solve(fx["sys"], fx["roles"], fx["params"])
     assert np.array_equal(res.status, fx["exp_status"])
-    if int(fx["N"]) <= 8 and int(fx.get("method", 0)) == 0:  # enumeration on both sides: same counts
+    if int(fx.get("method", 0)) == 0:  # enumeration on both sides: same sequence counts
         assert np.array_equal(res.nodes, fx["exp_nodes"])
     assert np.array_equal(res.region, fx["exp_region"])
     assert np.array_equal(res.gear, expected_gears(fx))
