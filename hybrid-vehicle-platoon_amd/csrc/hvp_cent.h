@@ -37,20 +37,23 @@ constexpr int kMaxVeh = 16;
 constexpr int ROWS = 9;       // rows per lane
 constexpr int REV = 1 << 10;  // reversed copy of a saturated soft row
 
-// LDS carve of one wave: J, R (V x (V+1), row stride V + 1) and a 64-entry vector
+// LDS carve of one wave: J, R (V x (V+1), row stride V + 1), a 64-entry vector and the
+// min_1_norm LP's row-descriptor buffer (64 rows x 10 doubles, hvp_cent_l1.h)
 struct Lds {
     double* J;
     double* R;
     double* v;
+    double* desc;
     int LD;
 };
-HVP_HD inline size_t lds_doubles(int V) { return (size_t)2 * V * (V + 1) + W; }
+HVP_HD inline size_t lds_doubles(int V, bool l1 = false) { return (size_t)2 * V * (V + 1) + W + (l1 ? W * 10 : 0); }
 __device__ inline Lds lds_carve(double* base, int V) {
     Lds s;
     s.LD = V + 1;
     s.J = base;
     s.R = base + (size_t)V * (V + 1);
     s.v = s.R + (size_t)V * (V + 1);
+    s.desc = s.v + W;
     return s;
 }
 

@@ -111,6 +111,7 @@ __global__ __launch_bounds__(64) void k_cent_init(int P, hvp::cent::PlatoonRec* 
     rec[p].flags = 0;
 }
 
+template <bool L1>
 __global__ __launch_bounds__(64) void k_cent_bnb(int P, int n, int N, int leader, int lsp,
                                                  const hvp_system* __restrict__ systems,
                                                  const int32_t* __restrict__ sys, const double* __restrict__ x0,
@@ -143,14 +144,15 @@ __global__ __launch_bounds__(64) void k_cent_bnb(int P, int n, int N, int leader
         sa.out_count = ws.out_count;
         sa.out_cap = ws.out_cap;
     }
-    bnb_platoon(L, S, C, I, st, frames + (size_t)p * V * nreg_max, nreg_max, ties + (size_t)p * kTie * n, max_nodes,
-                exhaustive != 0, max_iter, res, split ? &sa : nullptr);
+    bnb_platoon<L1>(L, S, C, I, st, frames + (size_t)p * V * nreg_max, nreg_max, ties + (size_t)p * kTie * n,
+                    max_nodes, exhaustive != 0, max_iter, res, split ? &sa : nullptr);
     if (res.status == kSplit) return;  // k_cent_final writes it
     cent_write(p, L, C, I, st, res, E);
 }
 
 // One round of subtree tasks: persistent waves claim tasks of any split platoon.  Each wave has
 // its own DFS frames and tie slice (frames_w, ties_w at its wave index).
+template <bool L1>
 __global__ __launch_bounds__(64) void k_cent_tasks(int n, int N, int leader, int lsp,
                                                    const hvp_system* __restrict__ systems,
                                                    const int32_t* __restrict__ sys, const double* __restrict__ x0,
@@ -201,7 +203,7 @@ __global__ __launch_bounds__(64) void k_cent_tasks(int n, int N, int leader, int
         Search st;
         Result res;
         const long long c0 = debug ? (long long)wall_clock64() : 0;
-        bnb_platoon(L, S, C, I, st, frames, nreg_max, ties, max_nodes - (int)done_nodes, false, max_iter, res, &sa);
+        bnb_platoon<L1>(L, S, C, I, st, frames, nreg_max, ties, max_nodes - (int)done_nodes, false, max_iter, res, &sa);
         const long long dt = debug ? (long long)wall_clock64() - c0 : 0;
         if (t == 0 && (debug >= 4 || (debug && (dt > 50000000ll || res.iters > 200 * (res.nodes + 1)))))
             printf("[cent-task] p %d d0 %d lb %.6g inc %.6g nodes %d iters %d ticks %lld\n", p, tk->d0, tk->lb, incg,
@@ -219,6 +221,7 @@ __global__ __launch_bounds__(64) void k_cent_abandon(const hvp::cent::Task* task
 
 // Winner of every split platoon: the lexicographically first (time-major) merged leaf within
 // 1e-9 relative of the shared incumbent, re-solved for its trajectory (the oracle's rule).
+template <bool L1>
 __global__ __launch_bounds__(64) void k_cent_final(int P, int n, int N, int leader, int lsp,
                                                    const hvp_system* __restrict__ systems,
                                                    const int32_t* __restrict__ sys, const double* __restrict__ x0,
@@ -266,7 +269,7 @@ __global__ __launch_bounds__(64) void k_cent_final(int P, int n, int N, int lead
         double c = 0.0;
         int it = 0;
         Prof pf;
-        const int q = win < 0 ? QP_FAILED : platoon_qp(L, S, C, I, st.vcode, 0.0, 0.0, V, max_iter, c, it, pf);
+        const int q = win < 0 ? QP_FAILED : platoon_qp<L1>(L, S, C, I, st.vcode, 0.0, 0.0, V, max_iter, c, it, pf);
         // a failed leaf whose bound is not above the incumbent could hide the optimum
         res.status = (fail_lb < __builtin_inf() && !hvp::bnb_pruned(fail_lb, inc)) ? HVP_MAXITER : HVP_OPTIMAL;
         if (q != QP_OK) res.status = HVP_MAXITER;
@@ -325,10 +328,15 @@ int hvp_cent_solve_batch(hvp_handle* h, int P, int n, int leader_index, int real
             return fail(HVP_E_NOMEM, "hvp_cent_solve_batch: device allocation failed");
         HIP_TRY(hipMemcpy(h->d_consts, &h->C, sizeof(hvp::Consts), hipMemcpyHostToDevice));
     }
-    const size_t lds = hvp::cent::lds_doubles(V) * sizeof(double);
-    HIP_TRY(hipFuncSetAttribute((const void*)k_cent_bnb, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    HIP_TRY(hipFuncSetAttribute((const void*)k_cent_tasks, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    HIP_TRY(hipFuncSetAttribute((const void*)k_cent_final, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    // the min_1_norm cost (the MILP, hvp_cent_l1.h) runs its own instantiation of the search kernels
+    const bool l1 = h->C.l1 != 0;
+    const void* kb = l1 ? (const void*)k_cent_bnb<true> : (const void*)k_cent_bnb<false>;
+    const void* kt = l1 ? (const void*)k_cent_tasks<true> : (const void*)k_cent_tasks<false>;
+    const void* kf = l1 ? (const void*)k_cent_final<true> : (const void*)k_cent_final<false>;
+    const size_t lds = hvp::cent::lds_doubles(V, l1) * sizeof(double);
+    HIP_TRY(hipFuncSetAttribute(kb, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    HIP_TRY(hipFuncSetAttribute(kt, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    HIP_TRY(hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     HIP_TRY(hipMemsetAsync(h->g_counter, 0, 8 * sizeof(unsigned long long), st));
     const int exhaustive = h->prob.method == HVP_METHOD_ENUMERATE ? 1 : 0;
     const char* dbg = std::getenv("HVP_CENT_DEBUG");  // diagnostics: printf of failing QPs
@@ -377,9 +385,14 @@ int hvp_cent_solve_batch(hvp_handle* h, int P, int n, int leader_index, int real
     HIP_TRY(hipEventRecord(h->evq0, st));
     ws.out = lists[0];
     ws.out_count = cnt + 0;
-    hipLaunchKernelGGL(k_cent_bnb, dim3(P), dim3(64), lds, st, P, n, N, leader_index, real_vehicle_as_reference ? 1 : 0,
-                       h->d_sys, sys, x0, leader_x, h->d_consts, h->nreg_max, cap, exhaustive, max_iter, debug, h->cent_frames,
-                       h->cent_ties, ws, E);
+    if (l1)
+        hipLaunchKernelGGL(k_cent_bnb<true>, dim3(P), dim3(64), lds, st, P, n, N, leader_index,
+                           real_vehicle_as_reference ? 1 : 0, h->d_sys, sys, x0, leader_x, h->d_consts, h->nreg_max, cap,
+                           exhaustive, max_iter, debug, h->cent_frames, h->cent_ties, ws, E);
+    else
+        hipLaunchKernelGGL(k_cent_bnb<false>, dim3(P), dim3(64), lds, st, P, n, N, leader_index,
+                           real_vehicle_as_reference ? 1 : 0, h->d_sys, sys, x0, leader_x, h->d_consts, h->nreg_max, cap,
+                           exhaustive, max_iter, debug, h->cent_frames, h->cent_ties, ws, E);
     HIP_TRY(hipGetLastError());
     if (ws.budget > 0) {
         // rounds of subtree tasks until none is left (one host read of the task count per round)
@@ -404,9 +417,14 @@ int hvp_cent_solve_batch(hvp_handle* h, int P, int n, int leader_index, int real
             ws.out_count = cnt + (cur ^ 1);
             HIP_TRY(hipMemsetAsync(cnt + 2, 0, sizeof(unsigned long long), st));
             HIP_TRY(hipMemsetAsync(cnt + (cur ^ 1), 0, sizeof(unsigned long long), st));
-            hipLaunchKernelGGL(k_cent_tasks, dim3(waves), dim3(64), lds, st, n, N, leader_index,
-                               real_vehicle_as_reference ? 1 : 0, h->d_sys, sys, x0, leader_x, h->d_consts, h->nreg_max,
-                               cap, max_iter, debug, frames_w, ties_w, ws);
+            if (l1)
+                hipLaunchKernelGGL(k_cent_tasks<true>, dim3(waves), dim3(64), lds, st, n, N, leader_index,
+                                   real_vehicle_as_reference ? 1 : 0, h->d_sys, sys, x0, leader_x, h->d_consts,
+                                   h->nreg_max, cap, max_iter, debug, frames_w, ties_w, ws);
+            else
+                hipLaunchKernelGGL(k_cent_tasks<false>, dim3(waves), dim3(64), lds, st, n, N, leader_index,
+                                   real_vehicle_as_reference ? 1 : 0, h->d_sys, sys, x0, leader_x, h->d_consts,
+                                   h->nreg_max, cap, max_iter, debug, frames_w, ties_w, ws);
             HIP_TRY(hipGetLastError());
             cur ^= 1;
             left = 0;
@@ -420,9 +438,14 @@ int hvp_cent_solve_batch(hvp_handle* h, int P, int n, int leader_index, int real
             hipLaunchKernelGGL(k_cent_abandon, dim3((unsigned)((c + 63) / 64)), dim3(64), 0, st, lists[cur], c, ws.rec);
             HIP_TRY(hipGetLastError());
         }
-        hipLaunchKernelGGL(k_cent_final, dim3(P), dim3(64), lds, st, P, n, N, leader_index,
-                           real_vehicle_as_reference ? 1 : 0, h->d_sys, sys, x0, leader_x, h->d_consts, max_iter, debug,
-                           ws, E);
+        if (l1)
+            hipLaunchKernelGGL(k_cent_final<true>, dim3(P), dim3(64), lds, st, P, n, N, leader_index,
+                               real_vehicle_as_reference ? 1 : 0, h->d_sys, sys, x0, leader_x, h->d_consts, max_iter,
+                               debug, ws, E);
+        else
+            hipLaunchKernelGGL(k_cent_final<false>, dim3(P), dim3(64), lds, st, P, n, N, leader_index,
+                               real_vehicle_as_reference ? 1 : 0, h->d_sys, sys, x0, leader_x, h->d_consts, max_iter,
+                               debug, ws, E);
         HIP_TRY(hipGetLastError());
     }
 #ifdef HVP_CENT_PROF

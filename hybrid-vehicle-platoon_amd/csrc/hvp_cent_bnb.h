@@ -24,11 +24,12 @@
 
 #include "hvp_bnb.h"
 #include "hvp_cent.h"
+#include "hvp_cent_l1.h"
 
 namespace hvp {
 namespace cent {
 
-constexpr int kTie = 16;  // near-optimal leaves kept for the tie rule (per search / task)
+constexpr int kTie = 64;  // near-optimal leaves kept for the tie rule (per search / task; <= W: lane j holds cost j)
 constexpr int kTieG = 64; // near-optimal leaves kept per platoon across the tasks of a split search
 
 // ---- split searches (heavy platoons): a search that exceeds its QP budget exports the
@@ -123,6 +124,10 @@ __device__ inline int fixed_steps(int d, int n, int i) { return d / n + (i < d %
 
 // Platoon QP with the first `d` decisions fixed; lane j < n holds vehicle j's code and the exact
 // interval [vlo, vhi] of its first undecided velocity.  QP_OK with the cost and the lanes' y.
+// L1: the min_1_norm LP of the same rows (hvp_cent_l1.h): QP_INFEASIBLE when a vehicle's hard rows
+// are proven infeasible (hvp_l1.h l1_infeasible, per vehicle: the hard rows do not couple
+// vehicles), QP_FAILED when the interior point leaves it unresolved.
+template <bool L1>
 __device__ inline int platoon_qp(Lane& L, const Lds& S, const Consts& C, const Inst& I, uint64_t vcode, double vlo,
                                  double vhi, int d, int max_iter, double& cost, int& iters, Prof& pf) {
     const int t = lane();
@@ -136,6 +141,27 @@ __device__ inline int platoon_qp(Lane& L, const Lds& S, const Consts& C, const I
     pf.mark(10);
     pf.count(10);
     if (!setup(L, S, C, I, ci, Ki, lo, hi)) return QP_INFEASIBLE;
+    if constexpr (L1) {
+        const int N = I.N;
+        int bad = 0;
+        if (t < I.V && t % N == 0)
+            bad = l1_infeasible_rt(I.systems[I.vsys[i]], C, I.x0[2 * i], I.x0[2 * i + 1], ci, Ki,
+                                   Ki < N ? lo : 0.0, Ki < N ? hi : -1.0, N)
+                      ? 1
+                      : 0;
+        if (wor(bad)) return QP_INFEASIBLE;
+        LpCtx X;
+        X.P1m = __shfl(L.P1, t >= N ? t - N : t, W);
+        X.amm = shift_up1(L.am);
+        X.ubm = shift_up1(L.ub);
+        X.ucm = shift_up1(L.uc);
+        X.Ki = Ki;
+        const int r = lp_solve(L, S, C, I, X, C.max_iter, it);
+        iters = it;
+        if (r != L1_OK) return QP_FAILED;
+        cost = lp_direct_cost(L, C, I, Ki);
+        return QP_OK;
+    }
     pf.mark(0);
     const int r = solve(L, S, C, I, max_iter, it, pf);
     iters = it;
@@ -185,6 +211,7 @@ __device__ inline Child load_child(const Child* c) {
 // past its budget).  Both prune against the platoon's shared incumbent.  Without sp the search
 // runs to the end (the exhaustive mode and the searches that fit their budget behave alike:
 // a platoon alone on its record sees only its own incumbent, so its QP count is the oracle's).
+template <bool L1>
 __device__ inline void bnb_platoon(Lane& L, const Lds& S, const Consts& C, const Inst& I, Search& st, Child* frames,
                                    int nreg_max, uint64_t* tie_codes, int max_nodes, bool exhaustive, int max_iter,
                                    Result& res, const SplitArgs* sp = nullptr) {
@@ -293,8 +320,13 @@ __device__ inline void bnb_platoon(Lane& L, const Lds& S, const Consts& C, const
     };
     // split searches: this search's leaves, counters and flags into the platoon's record
     auto merge = [&]() {
+        // leaves outside the tie window of the platoon's incumbent (this task's local window
+        // opened at +inf, and later improvements leave stale entries) take no slot
+        const double incs = shared_inc();
+        const double win = incs + 1e-9 * fmax(1.0, fabs(incs));
         for (int j = 0; j < ntie; ++j) {
             const double cj = bcu(st.tie_c, j);
+            if (incs < INF && cj > win) continue;
             int slot = 0;
             if (t == 0) slot = atomicAdd(&sp->rec->tie_count, 1);
             slot = bcu(slot, 0);
@@ -461,7 +493,7 @@ __device__ inline void bnb_platoon(Lane& L, const Lds& S, const Consts& C, const
                 qhi = chi;
             }
         }
-        const int q = platoon_qp(L, S, C, I, st.vcode, qlo, qhi, dfix, max_iter, c, it, pf);
+        const int q = platoon_qp<L1>(L, S, C, I, st.vcode, qlo, qhi, dfix, max_iter, c, it, pf);
         iters += it;
         if (I.debug && I.debug < 3 && q != QP_OK) {
             const uint64_t c0 = bc(st.vcode, 0), c1 = bc(st.vcode, 1 < n ? 1 : 0), c2 = bc(st.vcode, 2 < n ? 2 : 0);

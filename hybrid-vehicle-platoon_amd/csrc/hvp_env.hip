@@ -6,7 +6,8 @@
 //             the PWA-gear model for the current velocity (env.py:198-204 ->
 //             models.py:494-515: half-open bands between v_gear_lim = band midpoints of gears
 //             2..6; below the first -> 1, from the last on -> 6), held over the sample;
-//   stage     cost of (x, u) before the step (env.py:126-180, quadratic cost): leader tracking
+//   stage     cost of (x, u) before the step (env.py:126-180; quad_cost, or lin_cost = ||Q e||_1
+//             when the handle's problem has quadratic_cost = 0, env.py:118-124): leader tracking
 //             (or real vehicle as reference with its spacing), the chain spacing terms,
 //             Q_u u^2, Q_du (u - u_prev)^2, and the violation flag (100 when any gap
 //             p_i - p_{i+1} < d_safe, or the leader gap with real_vehicle_as_reference);
@@ -80,14 +81,17 @@ __global__ __launch_bounds__(64) void k_env_step(int P, int n, const double* __r
     // PlatoonEnv's own weights (env.py:16-18: Q_x = diag(1, 0.1), Q_u = 1, Q_du = 0), not the
     // controller's: the env prices every controller's actions alike
     constexpr double kQpp = 1.0, kQvv = 0.1, kQu = 1.0;
-    auto quad = [&](double ep, double ev) { return kQpp * ep * ep + kQvv * ev * ev; };
+    const bool lin = C.l1 != 0;  // lin_cost (env.py:122-124): |Q_pp e_p| + |Q_vv e_v|, |Q_u u|
+    auto quad = [&](double ep, double ev) {
+        return lin ? fabs(kQpp * ep) + fabs(kQvv * ev) : kQpp * ep * ep + kQvv * ev * ev;
+    };
     double c = 0.0;
     int close = 0;
     if (on) {
         const double rp = leader_x[(size_t)p * 2], rv = leader_x[(size_t)p * 2 + 1];
         if (rvar ? i == 0 : i == leader) c += quad(pos - rp + (rvar ? C.d0 + C.t0 * vel : 0.0), vel - rv);
         if (i >= 1) c += quad(pos - pm + C.d0 + C.t0 * vel, vel - vm);
-        c += kQu * ui * ui;  // + Q_du (u - u_prev)^2 with Q_du = 0
+        c += lin ? fabs(kQu * ui) : kQu * ui * ui;  // + the Q_du term, zero with Q_du = 0
         (void)upi;
         if (i + 1 < n && pos - pn < C.d_safe) close = 1;
         if (rvar && i == 0 && rp - pos < C.d_safe) close = 1;

@@ -53,6 +53,8 @@ struct Consts {
     int stride;    // parameter block stride (doubles)
     double rho;    // ADMM penalty
     int l1;        // 1: min_1_norm cost (hvp_l1.h), 0: min_2_norm
+    int leaf_cap;  // > 0: active-set cap of the long-horizon leaf QPs (HVP_LEAF_GI_CAP, tests of
+                   // the interior-point leaf fallback); 0: the solver's own cap
 };
 
 struct QpOut {

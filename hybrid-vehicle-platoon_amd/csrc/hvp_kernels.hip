@@ -19,6 +19,9 @@
 //
 // Memory: everything lives in caller-owned device buffers plus a handle-owned workspace sized
 // once by hvp_reserve (no allocation inside hvp_solve_batch, so a call can be graph-captured).
+#include <algorithm>
+#include <cstdlib>
+
 #include "hvp_lane.h"
 
 namespace hvp_detail {
@@ -60,6 +63,8 @@ hvp::Consts make_consts(const hvp_problem& p) {
                                                  : hvp_params_stride(p.N);
     C.rho = p.rho;
     C.l1 = p.quadratic_cost ? 0 : 1;
+    const char* lc = std::getenv("HVP_LEAF_GI_CAP");
+    C.leaf_cap = lc && lc[0] ? std::max(0, std::atoi(lc)) : 0;
     return C;
 }
 
@@ -290,8 +295,9 @@ int hvp_create(hvp_handle** out, const hvp_problem* problem, const hvp_system* s
         return fail(HVP_E_ARG, "hvp_create: the ADMM formulation needs rho > 0");
     if (problem->quadratic_cost != 1 && problem->quadratic_cost != 0)
         return fail(HVP_E_ARG, "hvp_create: quadratic_cost must be 1 (min_2_norm) or 0 (min_1_norm)");
-    if (problem->quadratic_cost == 0 && problem->formulation != HVP_FORM_DECENT)
-        return fail(HVP_E_UNSUPPORTED, "hvp_create: the min_1_norm cost runs for HVP_FORM_DECENT problems");
+    if (problem->quadratic_cost == 0 && problem->formulation != HVP_FORM_DECENT && problem->formulation != HVP_FORM_CENT)
+        return fail(HVP_E_UNSUPPORTED, "hvp_create: the min_1_norm cost runs for the HVP_FORM_DECENT and HVP_FORM_CENT "
+                                       "problems");
     for (int i = 0; i < n_systems; ++i) {
         std::string why;
         if (!valid_system(systems[i], &why)) return fail(HVP_E_ARG, "hvp_create: system " + std::to_string(i) + ": " + why);

@@ -124,9 +124,8 @@ HVP_HD inline double l1_dot(const double* g, const double* y) {
 // virtual region (a, b_max, c) with its input rows and cost (Q_u |s| <= Q_u |u| for s = u b_r / b_max);
 // otherwise the step's input rows and cost are dropped.  rlo > rhi (the default) = no relaxation
 // information (K = N leaves, enumeration candidates).
-template <int N>
-HVP_HD inline void l1_steps(const hvp_system& S, const Consts& C, uint64_t code, int K, double rlo, double rhi,
-                            double* a, double* b, double* c, unsigned& on, double* vlo, double* vhi) {
+HVP_HD inline void l1_steps_rt(const hvp_system& S, const Consts& C, uint64_t code, int K, double rlo, double rhi, int N,
+                               double* a, double* b, double* c, unsigned& on, double* vlo, double* vhi) {
     bool relax = rlo <= rhi;
     on = 0;
     for (int k = 0; k < N; ++k) {
@@ -158,6 +157,12 @@ HVP_HD inline void l1_steps(const hvp_system& S, const Consts& C, uint64_t code,
             vhi[k] = S.vmax;
         }
     }
+}
+
+template <int N>
+HVP_HD inline void l1_steps(const hvp_system& S, const Consts& C, uint64_t code, int K, double rlo, double rhi,
+                            double* a, double* b, double* c, unsigned& on, double* vlo, double* vhi) {
+    l1_steps_rt(S, C, code, K, rlo, rhi, N, a, b, c, on, vlo, vhi);
 }
 
 // Rows of the fixed-sequence LP of instance params prm (x0, x_front, x_back, leader_x) and
@@ -291,13 +296,12 @@ HVP_HD inline bool l1_rows(const hvp_system& S, const Consts& C, int role, const
 // proves the LP infeasible (margin 1e-9 relative).  The one case it cannot decide -- rows on both
 // sides of the position box binding within one horizon -- is reported feasible: the interior point
 // then runs and, if it does not converge, the LP stays unresolved (L1_FAIL), never "infeasible".
-template <int N>
-HVP_HD inline bool l1_infeasible(const hvp_system& S, const Consts& C, const double* prm, uint64_t code, int K,
-                                 double rlo, double rhi) {
-    double a[N], b[N], c[N], vlo[N], vhi[N];
+HVP_HD inline bool l1_infeasible_rt(const hvp_system& S, const Consts& C, double p0, double v0, uint64_t code, int K,
+                                    double rlo, double rhi, int N) {
+    double a[HVP_MAX_N], b[HVP_MAX_N], c[HVP_MAX_N], vlo[HVP_MAX_N], vhi[HVP_MAX_N];
     unsigned on;
-    l1_steps<N>(S, C, code, K, rlo, rhi, a, b, c, on, vlo, vhi);
-    const double v0 = prm[1], P1 = prm[0] + S.ts * v0;
+    l1_steps_rt(S, C, code, K, rlo, rhi, N, a, b, c, on, vlo, vhi);
+    const double P1 = p0 + S.ts * v0;
     auto tol = [](double x) { return 1e-9 * (1.0 + fabs(x)); };
     // the v_j for which step j admits some v_{j+1}: L_j(v) <= U_j(v)
     auto step_ok = [&](int j, double& lo, double& hi) {
@@ -323,7 +327,7 @@ HVP_HD inline bool l1_infeasible(const hvp_system& S, const Consts& C, const dou
     auto Umap = [&](int j, double v) {
         return ((on >> j) & 1u) ? fmin(a[j] * v + c[j] + b[j] * S.umax, v + C.acc[j]) : v + C.acc[j];
     };
-    double flo[N + 1], fhi[N + 1];
+    double flo[HVP_MAX_N + 1], fhi[HVP_MAX_N + 1];
     flo[0] = fhi[0] = v0;
     for (int j = 0; j < N; ++j) {  // forward: v_{j+1} reachable
         double lo = flo[j], hi = fhi[j];
@@ -358,6 +362,12 @@ HVP_HD inline bool l1_infeasible(const hvp_system& S, const Consts& C, const dou
         if (pl > S.pmax + tol(S.pmax) || ph < S.pmin - tol(S.pmin)) return true;
     }
     return false;
+}
+
+template <int N>
+HVP_HD inline bool l1_infeasible(const hvp_system& S, const Consts& C, const double* prm, uint64_t code, int K,
+                                 double rlo, double rhi) {
+    return l1_infeasible_rt(S, C, prm[0], prm[1], code, K, rlo, rhi, N);
 }
 
 // All rows into the lane's arrays (host build and per-lane use).

@@ -1015,7 +1015,8 @@ __global__ __launch_bounds__(kCoopBlock) void k_bnb_bound_coop(int k, const hvp_
         hvp::coop::Lane<N> L;
         double c = 0.0;
         int it = 0;
-        const int st = hvp::coop::solve_qp<N>(L, lds[g], S, C, rl, prm, code, k, kGiMaxIter<N>, it, &c, nullptr,
+        const int cap = k == N && C.leaf_cap > 0 ? C.leaf_cap : kGiMaxIter<N>;
+        const int st = hvp::coop::solve_qp<N>(L, lds[g], S, C, rl, prm, code, k, cap, it, &c, nullptr,
                                               ws.nd_lo[dst][q], ws.nd_hi[dst][q]);
         const bool ok = st == hvp::GI_OK;
         if (k == N && t < N) ws.task_y[q * N + t] = L.y;
@@ -1029,8 +1030,15 @@ __global__ __launch_bounds__(kCoopBlock) void k_bnb_bound_coop(int k, const hvp_
             } else {
                 if (ok) ws.nd_lb[dst][q] = c;
                 ws.leaf_stat[q] = ok ? 0 : HVP_MAXITER;
-                if (ok) atomicMin(&ws.inc[inst], cost_key(c));
-                else atomicOr(&ws.inst_flag[inst], 8);
+                if (ok) {
+                    atomicMin(&ws.inc[inst], cost_key(c));
+                } else {
+                    atomicOr(&ws.inst_flag[inst], 8);
+                    if (C.form == HVP_FORM_DECENT) {  // K_bnb_ipm re-solves it
+                        const unsigned long long r = atomicAdd(&ws.counter[2], 1ull);
+                        if (r < (unsigned long long)ws.cap) ws.redo[r] = (int32_t)q;
+                    }
+                }
             }
         }
     }
@@ -1126,7 +1134,7 @@ __global__ __launch_bounds__(kBnbBlock<N>) HVP_LANE_OCC void k_bnb_bound(int k, 
             } else {
                 ++fails;
                 atomicOr(&ws.inst_flag[inst], 8);  // a velocity-feasible sequence exists
-                if (N <= HVP_MAX_N_ENUM && C.form == HVP_FORM_DECENT) {  // K_bnb_ipm re-solves it
+                if (C.form == HVP_FORM_DECENT) {  // K_bnb_ipm re-solves it
                     const unsigned long long r = atomicAdd(&ws.counter[2], 1ull);
                     if (r < (unsigned long long)ws.cap) ws.redo[r] = (int32_t)t;
                 }
@@ -1362,7 +1370,7 @@ __device__ inline void bnb_node_done(int k, long long t, int inst, bool ok, int 
             atomicMin(&ws.inc[inst], cost_key(c));
         } else {
             atomicOr(&ws.inst_flag[inst], 8);  // a velocity-feasible sequence exists
-            if (C.form == HVP_FORM_DECENT) {   // K_bnb_ipm re-solves it
+            if (C.form == HVP_FORM_DECENT) {  // K_bnb_ipm re-solves it
                 const unsigned long long r = atomicAdd(&ws.counter[2], 1ull);
                 if (r < (unsigned long long)ws.cap) ws.redo[r] = (int32_t)t;
             }
@@ -1525,12 +1533,13 @@ __global__ __launch_bounds__(kBlock) void k_bnb_key(Workspace ws, int form, int 
         if (inst < 0) continue;
         const double best = inc_of(ws, inst);
         if (ws.leaf_stat[t] != 0) {
-            // Up to HVP_MAX_N_ENUM a leaf that fails the active-set method AND the interior-point
-            // fallback is an infeasible QP (position box), excluded exactly as the enumeration
-            // path and the oracle exclude it.  Beyond, there is no fallback: a failed leaf still
-            // in contention makes the instance MAXITER rather than a possibly wrong answer.  The
-            // min_1_norm leaves are HVP_INFEASIBLE (certified, excluded) or HVP_MAXITER (unresolved).
-            const bool strict = N > HVP_MAX_N_ENUM || form != HVP_FORM_DECENT || l1;
+            // A decentralised leaf that fails the active-set method AND the interior-point
+            // fallback (K_bnb_ipm, every N) is an infeasible QP (position box), excluded exactly as
+            // the enumeration path and the oracle exclude it.  The other forms have no fallback: a
+            // failed leaf still in contention makes the instance MAXITER rather than a possibly
+            // wrong answer.  The min_1_norm leaves are HVP_INFEASIBLE (certified, excluded) or
+            // HVP_MAXITER (unresolved).
+            const bool strict = form != HVP_FORM_DECENT || l1;
             if (ws.leaf_stat[t] == HVP_MAXITER && strict && !hvp::bnb_pruned(ws.nd_lb[src][t], best))
                 atomicOr(&ws.inst_flag[inst], 4);
             continue;
@@ -2003,8 +2012,7 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
         HIP_TRY(hipEventRecord(h->evb[2 * k + 1], st));
     }
     HIP_TRY(hipEventRecord(h->evq1, st));
-    if constexpr (N <= HVP_MAX_N_ENUM) {
-        if (h->C.form == HVP_FORM_DECENT && !h->C.l1)
+    if (h->C.form == HVP_FORM_DECENT && !h->C.l1) {  // failed leaves (normally none: reads a zero count)
         hipLaunchKernelGGL(k_bnb_ipm<N>, dim3(std::max(1, h->n_cu)), dim3(BS), lds, st, h->d_sys, sys, role, params,
                            h->C, ws);
         HIP_TRY(hipGetLastError());

@@ -185,9 +185,9 @@ class MpcMldCent:
     def setup_cost_and_constraints(self, u, spacing_policy=ConstantSpacingPolicy(50), leader_index: int = 0,
                                    quadratic_cost: bool = True, accel_cnstr_tightening: float = 0.0,
                                    real_vehicle_as_reference: bool = False) -> None:
-        """mpcs/cent_mld.py:48-177: the cost / constraint constants become the handle's problem."""
-        if not quadratic_cost:
-            raise NotImplementedError("the GPU path implements the quadratic cost (min_2_norm) only")
+        """mpcs/cent_mld.py:48-177: the cost / constraint constants become the handle's problem
+        (quadratic_cost=False: the min_1_norm objective, epigraph variables per vehicle and step,
+        solved as LPs by csrc/hvp_cent_l1.h)."""
         if leader_index != 0 and real_vehicle_as_reference:
             raise NotImplementedError("Not implemented for real vehicle with leader not 0.")
         self.leader_index = int(leader_index)

@@ -13,6 +13,7 @@ There is no CPU fallback: constructing a solver without the HIP library raises.
 
 from __future__ import annotations
 
+import contextlib
 import ctypes
 from dataclasses import dataclass
 
@@ -148,13 +149,9 @@ class BatchSolver:
                 break
             if attempt:
                 self.reserve(int(roles.shape[0]), 4 * self.stats().capacity)
-            hint = getattr(self, "_hint", None)
-            if hint is not None:  # the hint rows are indexed by the full batch: not for the subset
-                self.set_region_hint(None)
-            sub = self._launch(sys_idx[over].contiguous(), roles[over].contiguous(), params[over].contiguous(),
-                               None, stream)
-            if hint is not None:
-                self.set_region_hint(hint)
+            with self._hint_cleared():  # the hint rows are indexed by the full batch: not for the subset
+                sub = self._launch(sys_idx[over].contiguous(), roles[over].contiguous(), params[over].contiguous(),
+                                   None, stream)
             for k, v in sub.items():
                 out[k][over] = v
         return out
@@ -169,6 +166,7 @@ class BatchSolver:
                 raise ValueError(f"{name} must be a contiguous CUDA tensor of dtype {dt}")
         if params.numel() != B * self.params_stride or sys_idx.numel() != B:
             raise ValueError("params must be (B, params_stride), sys_idx (B,)")
+        self._check_hint(B)
         out = out or self.alloc_outputs(B, params.device)
         if stream is None:
             stream = torch.cuda.current_stream(params.device)
@@ -251,9 +249,32 @@ class BatchSolver:
         of the previous ADMM iteration, or the previous time step's sequences shifted by one step)
         that later solves try as a second initial incumbent -- naive-ADMM solves and decentralised
         solves with N > 8; None clears it.  Only pruning changes, never the answer."""
-        self._hint = region
+        import torch
+
+        if region is not None and (not region.is_cuda or region.dtype != torch.int8 or not region.is_contiguous()
+                                   or region.dim() != 2 or int(region.shape[1]) != self.N):
+            raise ValueError(f"the region hint must be a contiguous CUDA (B, {self.N}) int8 tensor")
         rc = self._lib.hvp_set_region_hint(self._h, ctypes.c_void_p(region.data_ptr() if region is not None else 0))
         _abi.check(rc, "hvp_set_region_hint")
+        self._hint = region
+
+    def _check_hint(self, B: int) -> None:
+        """The kernels read hint[i * N + k] for every instance i < B."""
+        hint = getattr(self, "_hint", None)
+        if hint is not None and int(hint.shape[0]) < B:
+            raise ValueError(f"the region hint holds {int(hint.shape[0])} rows for a batch of {B}: "
+                             "set a matching hint or clear it (set_region_hint(None))")
+
+    @contextlib.contextmanager
+    def _hint_cleared(self):
+        hint = getattr(self, "_hint", None)
+        if hint is not None:
+            self.set_region_hint(None)
+        try:
+            yield
+        finally:
+            if hint is not None:
+                self.set_region_hint(hint)
 
     def solve_admm_device(self, sys_idx, roles, params, out: dict, stream=None, retry_overflow: bool = False) -> dict:
         """hvp_solve_admm_batch on device tensors; ``out`` also needs "x_front", "x_back".
@@ -268,13 +289,9 @@ class BatchSolver:
             if attempt:
                 self.reserve(int(roles.shape[0]), 4 * self.stats().capacity)
             sub = {k: torch.empty_like(v[over]) for k, v in out.items()}
-            hint = getattr(self, "_hint", None)
-            if hint is not None:  # the hint rows are indexed by the full batch: not for the subset
-                self.set_region_hint(None)
-            self._launch_admm(sys_idx[over].contiguous(), roles[over].contiguous(), params[over].contiguous(), sub,
-                              stream)
-            if hint is not None:
-                self.set_region_hint(hint)
+            with self._hint_cleared():  # the hint rows are indexed by the full batch: not for the subset
+                self._launch_admm(sys_idx[over].contiguous(), roles[over].contiguous(), params[over].contiguous(),
+                                  sub, stream)
             for k, v in sub.items():
                 out[k][over] = v
         return out
@@ -285,6 +302,7 @@ class BatchSolver:
         B = int(roles.shape[0])
         if params.numel() != B * self.params_stride:
             raise ValueError("params must be (B, hvp_params_stride_admm)")
+        self._check_hint(B)
         if stream is None:
             stream = torch.cuda.current_stream(params.device)
         ptr = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731

@@ -67,6 +67,10 @@ def run_point(n: int, N: int, seeds, ep_len: int = 150, device: int = 0, out_dir
         sims = [Sim_n_task_2(n, seed=int(s), N=N) for s in seeds]
         x_init = np.stack([initial_platoon_state(n, derive_env_seed(int(s))).reshape(-1).astype(np.float64)
                            for s in seeds])
+    leader_x = sims[0].leader_trajectory.get_leader_trajectory()  # (2, ep_len + 50), seed-independent
+    if T + N + 1 > leader_x.shape[1]:  # Sim_n_task_2 builds the trajectory for its own ep_len (150)
+        raise ValueError(f"ep_len {T} with N = {N} needs {T + N + 1} leader samples; the Sim_n_task_2 "
+                         f"trajectory holds {leader_x.shape[1]} (ep_len <= {leader_x.shape[1] - N - 1})")
     systems, masses = [], []
     for sim in sims:
         pl = Platoon(n, vehicle_type="pwa_gear", masses=sim.masses)
@@ -77,7 +81,6 @@ def run_point(n: int, N: int, seeds, ep_len: int = 150, device: int = 0, out_dir
     solver = BatchSolver(tables.problem(N, sims[0].spacing_policy), systems, device=device)
     B = S * n
     solver.reserve(B)
-    leader_x = sims[0].leader_trajectory.get_leader_trajectory()  # (2, ep_len + 50), seed-independent
     lx = torch.from_numpy(np.ascontiguousarray(leader_x)).to(dev)
     x = torch.from_numpy(x_init).to(dev)
     env = DeviceEnv(solver, torch.tensor(masses, dtype=torch.float64, device=dev))

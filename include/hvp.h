@@ -294,8 +294,9 @@ int hvp_cent_solve_batch(hvp_handle* h, int P, int n, int leader_index, int real
  *   gear [P][n] int8 from the action, or NULL / entries <= 0: the PWA-gear model's gear of the
  *   current velocity (env.py:198-204, models.py:494-515); u_prev [P][n] the previous action
  *   (= u on the first step, env.py:127-128); leader_x [P][2] the leader state of this step.
- * Outputs: cost [P] the stage cost of (x, u) before the step (env.py:126-180, quadratic, with the
- * handle's weights / spacing / d_safe), viol [P] 100 when a gap is below d_safe (else 0),
+ * Outputs: cost [P] the stage cost of (x, u) before the step (env.py:126-180: quad_cost, or
+ * lin_cost = ||Q e||_1 when the handle's problem has quadratic_cost = 0, env.py:118-124; the
+ * env's own weights, the handle's spacing / d_safe), viol [P] 100 when a gap is below d_safe (else 0),
  * status [P] 0 ok, 1 a velocity left the traction curve (the reference raises RuntimeError). */
 int hvp_env_step_batch(hvp_handle* h, int P, int n, const double* masses, double* x, const double* u,
                        const int8_t* gear, const double* u_prev, const double* leader_x, int leader_index,

@@ -1616,7 +1616,12 @@ static int build_cent_qp(or_qp* qp, const or_model* md, const or_cfg* cf, or_cen
                 qp_add_lin(qp, &ws);
             }
     }
-    /* tracking: leader and chain terms, k = 0..N */
+    /* tracking: leader and chain terms, k = 0..N.  min_1_norm: every |Q_ii e_i| term gets its
+     * epigraph variable appended after the platoon's variables (add_norm through AL) */
+    or_layout AL;
+    memset(&AL, 0, sizeof(AL));
+    AL.nsb_idx = nz;
+    if (!cf->quadratic && nz + 2 * (N + 1) * n + 2 * n * N > OR_MAX_NZ) return 0;
     for (int k = 0; k <= N; ++k) {
         for (int i = 0; i < n; ++i) {
             lin p = CX(CL, x0, N, i, k, 0), v = CX(CL, x0, N, i, k, 1);
@@ -1626,7 +1631,7 @@ static int build_cent_qp(or_qp* qp, const or_model* md, const or_cfg* cf, or_cen
                 else e[0] = p;
                 e[0].cst -= par(xl, N, 0, k);
                 e[1] = v; e[1].cst -= par(xl, N, 1, k);
-                add_norm(qp, NULL, cf, e, cf->Qx, 2);
+                add_norm(qp, &AL, cf, e, cf->Qx, 2);
             }
             if (i >= 1) {
                 lin pm = CX(CL, x0, N, i - 1, k, 0), vm = CX(CL, x0, N, i - 1, k, 1);
@@ -1634,7 +1639,7 @@ static int build_cent_qp(or_qp* qp, const or_model* md, const or_cfg* cf, or_cen
                 e[0].cst += cf->d0;
                 e[0] = lin_axpy(-1.0, &pm, &e[0]);
                 e[1] = lin_axpy(-1.0, &vm, &v);
-                add_norm(qp, NULL, cf, e, cf->Qx, 2);
+                add_norm(qp, &AL, cf, e, cf->Qx, 2);
             }
         }
     }
@@ -1643,7 +1648,7 @@ static int build_cent_qp(or_qp* qp, const or_model* md, const or_cfg* cf, or_cen
         for (int k = 0; k < N; ++k) {
             if (k >= K[i] && RX[i].virt[k] < 0) continue;
             lin e[2]; e[0] = lin_const(0.0); lin_add(&e[0], CL->uo[i] + k, 1.0); e[1] = lin_const(0.0);
-            add_norm(qp, NULL, cf, e, Qu, 1);
+            add_norm(qp, &AL, cf, e, Qu, 1);
         }
         for (int k = 0; k + 1 < K[i]; ++k) {
             if (cf->Qdu == 0.0) continue;
@@ -1651,11 +1656,11 @@ static int build_cent_qp(or_qp* qp, const or_model* md, const or_cfg* cf, or_cen
             lin_add(&e[0], CL->uo[i] + k + 1, 1.0);
             lin_add(&e[0], CL->uo[i] + k, -1.0);
             e[1] = lin_const(0.0);
-            add_norm(qp, NULL, cf, e, Qdu, 1);
+            add_norm(qp, &AL, cf, e, Qdu, 1);
         }
     }
-    qp->nz = nz;
-    return nz;
+    qp->nz = nz + AL.naux;
+    return qp->nz;
 }
 
 /* direct objective of a centralised solution z (relaxed steps without input cost) */
@@ -1667,17 +1672,22 @@ static double cent_objective(const or_cfg* cf, const or_cent_layout* CL, const i
         for (int i = 0; i < n; ++i) {
             double p = k ? z[CL->xo[i] + 2 * (k - 1)] : x0[2 * i], v = k ? z[CL->xo[i] + 2 * (k - 1) + 1] : x0[2 * i + 1];
             double e0, e1;
+            /* min_2_norm e'Qe, min_1_norm sum_i |Q_ii e_i| (cent_mld.py:58-61) */
+#define CENT_NORM(e0, e1) (cf->quadratic ? cf->Qx[0][0] * (e0) * (e0) + (cf->Qx[0][1] + cf->Qx[1][0]) * (e0) * (e1) + \
+                                               cf->Qx[1][1] * (e1) * (e1)                                          \
+                                         : fabs(cf->Qx[0][0] * (e0)) + fabs(cf->Qx[1][1] * (e1)))
             if (i == CL->L) {
                 e0 = p - par(xl, N, 0, k) + (CL->lsp ? cf->t0 * v + cf->d0 : 0.0);
                 e1 = v - par(xl, N, 1, k);
-                J += cf->Qx[0][0] * e0 * e0 + (cf->Qx[0][1] + cf->Qx[1][0]) * e0 * e1 + cf->Qx[1][1] * e1 * e1;
+                J += CENT_NORM(e0, e1);
             }
             if (i >= 1) {
                 double pm = k ? z[CL->xo[i - 1] + 2 * (k - 1)] : x0[2 * (i - 1)];
                 double vm = k ? z[CL->xo[i - 1] + 2 * (k - 1) + 1] : x0[2 * (i - 1) + 1];
                 e0 = p + cf->t0 * v + cf->d0 - pm;
                 e1 = v - vm;
-                J += cf->Qx[0][0] * e0 * e0 + (cf->Qx[0][1] + cf->Qx[1][0]) * e0 * e1 + cf->Qx[1][1] * e1 * e1;
+                J += CENT_NORM(e0, e1);
+#undef CENT_NORM
                 J += cf->w * fmax(0.0, p - pm + cf->d_safe);
             } else if (CL->lsp && CL->L == 0) {
                 J += cf->w * fmax(0.0, p - par(xl, N, 0, k) + cf->d_safe);
@@ -1687,8 +1697,11 @@ static double cent_objective(const or_cfg* cf, const or_cent_layout* CL, const i
         for (int k = 0; k < N; ++k) {
             if (k >= K[i] && RX[i].virt[k] < 0) continue;
             double u = z[CL->uo[i] + k];
-            J += cf->Qu * u * u;
-            if (k + 1 < K[i]) { double du = z[CL->uo[i] + k + 1] - u; J += cf->Qdu * du * du; }
+            J += cf->quadratic ? cf->Qu * u * u : fabs(cf->Qu * u);
+            if (k + 1 < K[i]) {
+                double du = z[CL->uo[i] + k + 1] - u;
+                J += cf->quadratic ? cf->Qdu * du * du : fabs(cf->Qdu * du);
+            }
         }
     return J;
 }
@@ -1816,7 +1829,8 @@ static void cent_dfs(or_cent* C, int d, int* sigma, int* K, double* lo, double* 
 /* Centralised MIQP of one platoon: sys models stacked per vehicle (as oracle_solve_batch), x0
  * (2n), xl (2, N+1), role = leader index | real_vehicle_as_reference << 8.  Outputs x (n, 2, N+1),
  * u (n, N), sigma (n, N), info = [objective, status (0 optimal, 1 infeasible), QPs solved].
- * role bit 16: exhaustive enumeration of the joint sequences instead of branch and bound. */
+ * role bit 16: exhaustive enumeration of the joint sequences instead of branch and bound; bit 17: the
+ * min_1_norm cost (quadratic_cost=False, cent_mld.py:58-61). */
 int oracle_solve_cent(int n, int N, int nreg, int nsr, const double* S, const double* R, const double* T,
                       const double* A, const double* B, const double* c, int nd, const double* D, const double* E, int nf,
                       const double* F, const double* G, const double* cfgp, int role, const double* x0,
@@ -1832,7 +1846,7 @@ int oracle_solve_cent(int n, int N, int nreg, int nsr, const double* S, const do
         if (make_vmodel(&md[i], &vm[i]) || !oracle_bnb_ok(&md[i])) return -2;
     }
     or_cfg cf;
-    unpack_cfg(&cf, N, 1, 0, cfgp);
+    unpack_cfg(&cf, N, (role >> 17) & 1 ? 0 : 1, 0, cfgp); /* role bit 17: min_1_norm (the MILP) */
     or_cent* C = (or_cent*)calloc(1, sizeof(or_cent));
     or_qp* qp = (or_qp*)malloc(sizeof(or_qp));
     or_work* w = (or_work*)malloc(sizeof(or_work));

@@ -843,10 +843,12 @@ def set_cent_relax(on: bool) -> None:
 
 
 def solve_cent(systems: list[dict], cfg: Cfg, N: int, x0, leader_x, leader_index: int = 0,
-               real_vehicle_as_reference: bool = False, exhaustive: bool = False) -> CentResult:
+               real_vehicle_as_reference: bool = False, exhaustive: bool = False,
+               quadratic: bool = True) -> CentResult:
     """MpcMldCent's MIQP (mpcs/cent_mld.py:48-182) for one platoon: full (x, u, s) space, branch
     and bound over the joint region sequences in time-major order (or exhaustive enumeration);
-    ties to the lexicographically first joint sequence in that order (hvp_oracle.c oracle_solve_cent)."""
+    ties to the lexicographically first joint sequence in that order (hvp_oracle.c oracle_solve_cent).
+    quadratic=False: the min_1_norm cost (cent_mld.py:58-61), a MILP."""
     L = lib()
     n = len(systems)
     arrs = [_model_arrays(s)[2] for s in systems]
@@ -857,7 +859,8 @@ def solve_cent(systems: list[dict], cfg: Cfg, N: int, x0, leader_x, leader_index
     xl = np.ascontiguousarray(np.asarray(leader_x, dtype=np.float64).reshape(2, N + 1))
     x_out, u_out = np.zeros((n, 2, N + 1)), np.zeros((n, N))
     sig, info = np.zeros((n, N), dtype=np.int32), np.zeros(3)
-    role = int(leader_index) | (256 if real_vehicle_as_reference else 0) | (65536 if exhaustive else 0)
+    role = (int(leader_index) | (256 if real_vehicle_as_reference else 0) | (65536 if exhaustive else 0)
+            | (0 if quadratic else 131072))
     rc = L.oracle_solve_cent(n, N, nreg, nsr, _d(st["S"]), _d(st["R"]), _d(st["T"]), _d(st["A"]), _d(st["B"]),
                              _d(st["c"]), st["D"].shape[1], _d(st["D"]), _d(st["E"]), st["F"].shape[1], _d(st["F"]),
                              _d(st["G"]), _d(cv), role, _d(x0), _d(xl), _d(x_out), _d(u_out), _i(sig), _d(info))
@@ -898,10 +901,11 @@ def _gear_pwa(v: float) -> int:
 
 
 def env_step(x, u, masses, leader_state, u_prev=None, gears=None, leader_index: int = 0,
-             real_vehicle_as_reference: bool = False, cfg: Cfg | None = None, ts: float = 1.0):
-    """PlatoonEnv.step for one platoon (env.py:126-212 with the quadratic cost; models.py:99-125,
-    236-257): returns (x_next (2n,), stage cost, violation 0/100, ok).  gears None: the PWA-gear
-    model's gear of each velocity (env.py:198-204)."""
+             real_vehicle_as_reference: bool = False, cfg: Cfg | None = None, ts: float = 1.0,
+             quadratic: bool = True):
+    """PlatoonEnv.step for one platoon (env.py:126-212; models.py:99-125, 236-257): returns
+    (x_next (2n,), stage cost, violation 0/100, ok).  gears None: the PWA-gear model's gear of
+    each velocity (env.py:198-204).  quadratic=False: lin_cost = ||Q e||_1 (env.py:122-124)."""
     cfg = cfg or Cfg()
     x = np.asarray(x, dtype=float).reshape(-1).copy()
     u = np.asarray(u, dtype=float).reshape(-1)
@@ -911,12 +915,16 @@ def env_step(x, u, masses, leader_state, u_prev=None, gears=None, leader_index: 
     sp = lambda xi: np.array([-cfg.d0 - cfg.t0 * xi[1], 0.0])  # noqa: E731  spacing_policy.spacing
     xs = [x[2 * i:2 * i + 2] for i in range(n)]
     ref = np.asarray(leader_state, dtype=float).reshape(2)
+    stage = (lambda e: float(e @ Q @ e)) if quadratic else (lambda e: float(np.abs(Q @ e).sum()))
     e = xs[0] - ref - sp(xs[0]) if real_vehicle_as_reference else xs[leader_index] - ref
-    cost = float(e @ Q @ e)
+    cost = stage(e)
     for i in range(1, n):
         e = xs[i] - xs[i - 1] - sp(xs[i])
-        cost += float(e @ Q @ e)
-    cost += sum(1.0 * u[i] ** 2 for i in range(n)) + sum(0.0 * (u[i] - up[i]) ** 2 for i in range(n))
+        cost += stage(e)
+    if quadratic:
+        cost += sum(1.0 * u[i] ** 2 for i in range(n)) + sum(0.0 * (u[i] - up[i]) ** 2 for i in range(n))
+    else:
+        cost += sum(abs(1.0 * u[i]) for i in range(n)) + sum(abs(0.0 * (u[i] - up[i])) for i in range(n))
     close = any(xs[i][0] - xs[i + 1][0] < cfg.d_safe for i in range(n - 1))
     if real_vehicle_as_reference and ref[0] - xs[0][0] < cfg.d_safe:
         close = True

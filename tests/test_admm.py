@@ -317,3 +317,33 @@ def test_warm_incumbent_does_not_change_answers(gpu_available, N, P):
             assert np.array_equal(a[k], b[k]), k
     if N > 8:  # the deep trees, where AdmmEngine uses it by default
         assert sum(o["nodes"].sum() for o in res[0]) < sum(o["nodes"].sum() for o in res[1])
+
+
+@pytest.mark.gpu
+def test_region_hint_is_checked(gpu_available):
+    """set_region_hint takes a contiguous CUDA (B, N) int8 tensor; a solve over more instances
+    than the hint holds rows is refused before any launch (the kernels read hint[i * N + k])."""
+    import torch
+
+    from hvp import tables
+    from hvp.solver import BatchSolver
+
+    N, B = 5, 32
+    s = BatchSolver(tables.problem(N), [_system()])
+    dev = torch.device("cuda", 0)
+    with pytest.raises(ValueError):
+        s.set_region_hint(torch.full((B, N + 1), -1, dtype=torch.int8, device=dev))
+    with pytest.raises(ValueError):
+        s.set_region_hint(torch.full((B, N), -1, dtype=torch.int32, device=dev))
+    s.set_region_hint(torch.full((B // 2, N), -1, dtype=torch.int8, device=dev))
+    x = np.stack([O.env_initial_state(2, k).astype(float) for k in range(B // 2)]).reshape(B, 2)
+    params = np.zeros((B, s.params_stride))
+    params[:, :2] = x
+    roles = np.full(B, O.role_bits(0, 1), np.int32)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    with pytest.raises(ValueError, match="region hint"):
+        s.solve_device(t(np.zeros(B, np.int32)), t(roles), t(params))
+    s.set_region_hint(None)
+    out = s.solve_device(t(np.zeros(B, np.int32)), t(roles), t(params))
+    torch.cuda.synchronize()
+    assert out["status"].shape == (B,)

@@ -4,9 +4,10 @@ CPU: the oracle's joint branch and bound equals its exhaustive joint enumeration
 reproduces the committed fixtures; the host-side API raises like the reference.
 GPU (through hvp_cent_solve_batch): the committed fixtures -- region sequences and gears
 bit-exact, cost within 1e-9 relative, u within 1e-6, x within 1e-4 (positions ~3e3), QP counts
-equal to the oracle's (same exploration order); exhaustive mode = branch and bound; at the
-configs[1] size (n = 10, N = 5) determinism, the PWA dynamics of the chosen regions, and the
-drop-in MpcMldCent / simulate surface.
+equal to the oracle's (same exploration order; min_1_norm: not compared, exact LP bound ties make
+the order noise-driven); exhaustive mode = branch and bound; at the configs[1] size (n = 10,
+N = 5) determinism, the PWA dynamics of the chosen regions, and the drop-in MpcMldCent /
+simulate surface, for both costs (cent_l1_*.npz: the min_1_norm MILP, cent_mld.py:58-61).
 """
 
 from __future__ import annotations
@@ -22,7 +23,13 @@ from golden_io import GOLDEN, CfgParams, load
 from instances import leader_window
 
 CENT = sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLDEN, "cent_*.npz")))
-FAST = [c for c in CENT if c.startswith(("cent_n2_", "cent_n4_", "cent_lsp", "cent_lead2", "cent_qdu", "cent_n10_N3"))]
+FAST = [c for c in CENT if c.startswith(("cent_n2_", "cent_n4_", "cent_lsp", "cent_lead2", "cent_qdu", "cent_n10_N3",
+                                         "cent_l1_n3_N5", "cent_l1_lead1", "cent_l1_gear", "cent_l1_qdu"))]
+
+
+def _quadratic(fx) -> bool:
+    """Fixtures of the min_1_norm controller carry quadratic = 0 (older files: the MIQP)."""
+    return bool(int(fx["quadratic"])) if "quadratic" in fx else True
 
 
 def _cfg(v) -> O.Cfg:
@@ -47,6 +54,23 @@ def test_oracle_bnb_equals_exhaustive(n, N, seed):
     assert np.array_equal(a.sigma, b.sigma)
     assert abs(a.cost - b.cost) <= 1e-9 * abs(b.cost)
     assert a.n_qps <= b.n_qps
+
+
+@pytest.mark.parametrize("n,N,seed,model", [(2, 3, 0, 0), (2, 4, 1, 0), (3, 3, 2, 0), (2, 3, 3, 1)])
+def test_oracle_l1_bnb_equals_exhaustive(n, N, seed, model):
+    """min_1_norm (cent_mld.py:58-61, a MILP): the joint branch and bound over LP relaxations
+    equals the exhaustive joint enumeration of fixed-sequence LPs."""
+    mk = O.gear_friction_mld_system if model else O.gear_pwa_system
+    systems = [mk(800.0)] * n
+    x0 = O.env_initial_state(n, seed).astype(float)
+    a = O.solve_cent(systems, O.Cfg(), N, x0, leader_window(N), quadratic=False)
+    b = O.solve_cent(systems, O.Cfg(), N, x0, leader_window(N), exhaustive=True, quadratic=False)
+    assert a.status == b.status == 0
+    assert np.array_equal(a.sigma, b.sigma)
+    assert abs(a.cost - b.cost) <= 1e-9 * abs(b.cost)
+    assert a.n_qps <= b.n_qps
+    q = O.solve_cent(systems, O.Cfg(), N, x0, leader_window(N))
+    assert q.status == 0 and abs(q.cost - a.cost) > 1e-6 * abs(a.cost)  # a different objective
 
 
 @pytest.mark.parametrize("n,N,seed", [(2, 3, 0), (2, 4, 1), (3, 3, 2)])
@@ -94,7 +118,7 @@ def test_oracle_reproduces_cent_golden(name):
     cfg = _cfg(fx["cfg"])
     for p in range(len(fx["x0"])):
         r = O.solve_cent(_oracle_systems(fx, p), cfg, N, fx["x0"][p].reshape(-1), fx["leader_x"][p],
-                         int(fx["leader_index"][p]), bool(fx["lsp"][p]))
+                         int(fx["leader_index"][p]), bool(fx["lsp"][p]), quadratic=_quadratic(fx))
         assert r.status == fx["exp_status"][p]
         assert np.array_equal(r.sigma, fx["exp_region"][p])
         assert abs(r.cost - fx["exp_cost"][p]) <= 1e-10 * abs(fx["exp_cost"][p])
@@ -121,13 +145,12 @@ def test_api_raises_like_the_reference():
     systems = Platoon(3, vehicle_type="pwa_gear").get_vehicle_system_dicts(1)
     with pytest.raises(NotImplementedError):
         MpcMldCent(3, 5, systems, leader_index=1, real_vehicle_as_reference=True)
-    with pytest.raises(NotImplementedError):
-        MpcMldCent(3, 5, systems, quadratic_cost=False)
     with pytest.raises(ValueError):
         MpcMldCent(4, 5, systems)
     p = cent_problem(5)
     assert int(p.formulation) == 3 and int(p.method) == 2
     assert int(cent_problem(5, exhaustive=True).method) == 1
+    assert int(cent_problem(5, quadratic_cost=False).quadratic_cost) == 0
 
 
 # ------------------------------------------------------------------ GPU
@@ -138,7 +161,8 @@ def _product(fx):
     from hvp.params import ConstantTimePolicy
 
     cp = CfgParams(fx["cfg"])
-    prob = cent_problem(int(fx["N"]), ConstantTimePolicy(cp.d0, cp.t0), accel_cnstr_tightening=cp.tight, params=cp)
+    prob = cent_problem(int(fx["N"]), ConstantTimePolicy(cp.d0, cp.t0), quadratic_cost=_quadratic(fx),
+                        accel_cnstr_tightening=cp.tight, params=cp)
     masses = np.unique(fx["masses"].reshape(-1))
     systems = []
     for m in masses:
@@ -148,7 +172,50 @@ def _product(fx):
             veh = PwaGearVehicle(float(m))
             systems.append(tables.system_from_dict(veh.get_discrete_system(float(cp.ts)), tables.gears_of(veh)))
     sys_idx = np.searchsorted(masses, fx["masses"]).astype(np.int32)
-    return CentSolver(prob, systems), sys_idx
+    s = CentSolver(prob, systems)
+    s.tables = systems
+    return s, sys_idx
+
+
+def _l1_objective(fx, p, x, u) -> float:
+    """min_1_norm objective of a platoon trajectory (numpy restatement of cent_mld.py:83-140 with
+    the L1 norms, as hvp_oracle.c cent_objective prices a leaf): x (n, 2, N+1), u (n, N)."""
+    c = _cfg(fx["cfg"])
+    N = int(fx["N"])
+    L, lsp, xl = int(fx["leader_index"][p]), bool(fx["lsp"][p]), fx["leader_x"][p]
+    n = x.shape[0]
+    J = 0.0
+    for k in range(N + 1):
+        for i in range(n):
+            pp, v = x[i, 0, k], x[i, 1, k]
+            if i == L:
+                J += abs(c.Qx[0] * (pp - xl[0, k] + (c.t0 * v + c.d0 if lsp else 0.0))) + abs(c.Qx[3] * (v - xl[1, k]))
+            if i >= 1:
+                pm, vm = x[i - 1, 0, k], x[i - 1, 1, k]
+                J += abs(c.Qx[0] * (pp + c.t0 * v + c.d0 - pm)) + abs(c.Qx[3] * (v - vm))
+                J += c.w * max(0.0, pp - pm + c.d_safe)
+            elif lsp and L == 0:
+                J += c.w * max(0.0, pp - xl[0, k] + c.d_safe)
+    J += np.abs(c.Qu * u).sum() + np.abs(c.Qdu * np.diff(u, axis=1)).sum()
+    return J
+
+
+def _check_alternative_optimum(fx, p, s, sys_idx, res, j, name):
+    """A min_1_norm LP may have a face of optima (the oracle's interior point and the device's stop
+    at different points of it): the device's (x, u) must then follow the PWA dynamics of the
+    returned regions inside the boxes and price at the oracle's optimal cost."""
+    N = int(fx["N"])
+    for i in range(res.u.shape[1]):
+        st = s.tables[int(sys_idx[p, i])]
+        for k in range(N):
+            r = int(res.region[j, i, k])
+            v, vn = res.x[j, i, 1, k], res.x[j, i, 1, k + 1]
+            assert st.vlo[r] - 1e-6 <= v <= st.vhi[r] + 1e-6, (name, p, i, k)
+            assert abs(vn - (st.a[r] * v + st.b[r] * res.u[j, i, k] + st.c[r])) <= 1e-8, (name, p, i, k)
+            assert abs(res.x[j, i, 0, k + 1] - (res.x[j, i, 0, k] + st.ts * v)) <= 1e-8, (name, p, i, k)
+            assert st.umin - 1e-7 <= res.u[j, i, k] <= st.umax + 1e-7, (name, p, i, k)
+    J = _l1_objective(fx, p, res.x[j], res.u[j])
+    assert abs(J - fx["exp_cost"][p]) <= 1e-9 * abs(fx["exp_cost"][p]), (name, p, J, fx["exp_cost"][p])
 
 
 @pytest.mark.gpu
@@ -168,15 +235,21 @@ def test_gpu_matches_cent_golden(gpu_available, name):
                                                                         res.cost[j], fx["exp_cost"][p])
             assert np.array_equal(res.gear[j], fx["exp_gear"][p]), (name, p)
             assert abs(res.cost[j] - fx["exp_cost"][p]) <= 1e-9 * abs(fx["exp_cost"][p]), (name, p)
-            assert np.abs(res.u[j] - fx["exp_u"][p]).max() <= 1e-6, (name, p)
-            assert np.abs(res.x[j] - fx["exp_x"][p]).max() <= 1e-4, (name, p)
-            assert res.nodes[j] == fx["exp_nodes"][p], (name, p, res.nodes[j], fx["exp_nodes"][p])
+            if _quadratic(fx) or np.abs(res.u[j] - fx["exp_u"][p]).max() <= 1e-6:
+                assert np.abs(res.u[j] - fx["exp_u"][p]).max() <= 1e-6, (name, p)
+                assert np.abs(res.x[j] - fx["exp_x"][p]).max() <= 1e-4, (name, p)
+            else:
+                _check_alternative_optimum(fx, p, s, sys_idx, res, j, name)
+            if _quadratic(fx):  # LP bounds tie exactly between sibling regions: the visiting order
+                # (and so the LP count) of the min_1_norm search follows 1e-12 noise on both sides
+                assert res.nodes[j] == fx["exp_nodes"][p], (name, p, res.nodes[j], fx["exp_nodes"][p])
     assert P == len(fx["exp_status"])
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,split", [("cent_n6_N5.npz", 40), ("cent_n8_N5.npz", 25), ("cent_n3_N10.npz", 30),
-                                        ("cent_gear_n3_N4.npz", 10), ("cent_task2_n5_N5.npz", 20)])
+                                        ("cent_gear_n3_N4.npz", 10), ("cent_task2_n5_N5.npz", 20),
+                                        ("cent_l1_n3_N8.npz", 20), ("cent_l1_n4_N5.npz", 15)])
 def test_gpu_split_search_matches_cent_golden(gpu_available, monkeypatch, name, split):
     """The split search (heavy platoons: open DFS frames exported as subtree tasks run by every
     wave, shared incumbent, tie rule over the merged leaves) forced on the fixtures by a tiny
@@ -196,8 +269,34 @@ def test_gpu_split_search_matches_cent_golden(gpu_available, monkeypatch, name, 
             assert np.array_equal(res.region[j], fx["exp_region"][p]), (name, p, res.region[j], fx["exp_region"][p])
             assert np.array_equal(res.gear[j], fx["exp_gear"][p]), (name, p)
             assert abs(res.cost[j] - fx["exp_cost"][p]) <= 1e-9 * abs(fx["exp_cost"][p]), (name, p)
-            assert np.abs(res.u[j] - fx["exp_u"][p]).max() <= 1e-6, (name, p)
-            assert np.abs(res.x[j] - fx["exp_x"][p]).max() <= 1e-4, (name, p)
+            if _quadratic(fx) or np.abs(res.u[j] - fx["exp_u"][p]).max() <= 1e-6:
+                assert np.abs(res.u[j] - fx["exp_u"][p]).max() <= 1e-6, (name, p)
+                assert np.abs(res.x[j] - fx["exp_x"][p]).max() <= 1e-4, (name, p)
+            else:
+                _check_alternative_optimum(fx, p, s, sys_idx, res, j, name)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["cent_n6_N5.npz", "cent_n4_N5.npz"])
+def test_gpu_small_task_budget_no_overflow(gpu_available, monkeypatch, name):
+    """A tiny task budget (HVP_CENT_TASK_BUDGET=16, split past 10 QPs) makes many short tasks;
+    merge() keeps only leaves inside the shared incumbent's tie window, so the platoon's tie list
+    does not fill up (no HVP_OVERFLOW) and the answer is the oracle's."""
+    from hvp import _abi
+
+    monkeypatch.setenv("HVP_CENT_SPLIT", "10")
+    monkeypatch.setenv("HVP_CENT_TASK_BUDGET", "16")
+    fx = load(name)
+    s, sys_idx = _product(fx)
+    for lead_idx, lsp in sorted({(int(a), int(b)) for a, b in zip(fx["leader_index"], fx["lsp"])}):
+        sel = np.flatnonzero((fx["leader_index"] == lead_idx) & (fx["lsp"] == lsp))
+        res = s.solve(sys_idx[sel], fx["x0"][sel], fx["leader_x"][sel], lead_idx, bool(lsp))
+        assert not (res.status == _abi.OVERFLOW).any(), res.status
+        for j, p in enumerate(sel):
+            assert res.status[j] == fx["exp_status"][p], (name, p, res.status[j])
+            if fx["exp_status"][p] == 0:
+                assert np.array_equal(res.region[j], fx["exp_region"][p]), (name, p)
+                assert abs(res.cost[j] - fx["exp_cost"][p]) <= 1e-9 * abs(fx["exp_cost"][p]), (name, p)
 
 
 @pytest.mark.gpu
@@ -277,3 +376,37 @@ def test_gpu_mpc_cent_drop_in_and_simulate(gpu_available):
     assert isinstance(agent, TrackingCentralizedAgent)
     assert X.shape[0] == sim.ep_len + 1 and U.shape[0] == sim.ep_len
     assert np.all(agent.node_counts > 0)
+
+
+@pytest.mark.gpu
+def test_gpu_mpc_cent_l1_drop_in_and_simulate(gpu_available):
+    """MpcMldCent(quadratic_cost=False) (cent_mld.py:58-61): the min_1_norm MILP of one platoon
+    equals the oracle's, and the fleet_cent_mld.py loop runs on it."""
+    from hvp.cent import MpcMldCent, simulate
+    from hvp.models import Platoon
+    from hvp.params import Sim
+
+    n, N = 3, 5
+    platoon = Platoon(n, vehicle_type="pwa_gear")
+    mpc = MpcMldCent(n, N, platoon.get_vehicle_system_dicts(1), quadratic_cost=False)
+    mpc.set_leader_traj(leader_window(N))
+    for seed in range(3):
+        state = O.env_initial_state(n, seed).astype(float).reshape(2 * n, 1)
+        u, info = mpc.solve_mpc(state)
+        r = O.solve_cent([O.gear_pwa_system(800.0)] * n, O.Cfg(), N, state.reshape(-1), leader_window(N),
+                         quadratic=False)
+        assert r.status == 0 and info["status"] == 0
+        assert np.array_equal(mpc.regions_pred, r.sigma), seed
+        assert abs(info["cost"] - r.cost) <= 1e-9 * abs(r.cost)
+        assert np.abs(info["u"] - r.u).max() <= 1e-6
+        assert np.abs(info["x"] - r.x.reshape(2 * n, N + 1)).max() <= 1e-4
+
+    class Short(Sim):
+        n, N, ep_len = 3, 4, 6
+        quadratic_cost = False
+        id = "test_cent_l1"
+
+    sim = Short()
+    X, U, R, agent, env = simulate(sim, seed=2)
+    assert X.shape[0] == sim.ep_len + 1 and U.shape[0] == sim.ep_len
+    assert np.all(agent.node_counts > 0) and np.all(np.isfinite(R))

@@ -21,20 +21,23 @@ def _platoons(P, n, seed=0):
     return X, U, Up, M, L
 
 
-def test_oracle_step_matches_host_env():
+@pytest.mark.parametrize("quadratic", [True, False])
+def test_oracle_step_matches_host_env(quadratic):
     from hvp.env import PlatoonEnv
     from hvp.models import Platoon
     from hvp.params import ConstantVelocityLeaderTrajectory
 
     n = 6
     pl = Platoon(n, vehicle_type="pwa_gear")
-    env = PlatoonEnv(n=n, platoon=pl, ep_len=20, leader_trajectory=ConstantVelocityLeaderTrajectory(3000, 20, 70, 1))
+    env = PlatoonEnv(n=n, platoon=pl, ep_len=20, leader_trajectory=ConstantVelocityLeaderTrajectory(3000, 20, 70, 1),
+                     quadratic_cost=quadratic)
     x, _ = env.reset(seed=5)
     rng = np.random.default_rng(1)
     prev = None
     for t in range(5):
         u = rng.uniform(-1, 1, (n, 1))
-        xo, c, viol, ok = O.env_step(x, u, [800.0] * n, env.leader_x[:, t], u_prev=prev if prev is not None else u)
+        xo, c, viol, ok = O.env_step(x, u, [800.0] * n, env.leader_x[:, t], u_prev=prev if prev is not None else u,
+                                     quadratic=quadratic)
         x, r, *_ = env.step(u)
         assert ok and np.array_equal(xo, np.asarray(x, float).reshape(-1))
         assert abs(c - r) <= 1e-12 * abs(r) and viol == env.viol_counter[-1][t]
@@ -53,8 +56,9 @@ class _OtherWeights:
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("rvar,weights", [(False, False), (True, False), (False, True)])
-def test_device_step_matches_oracle(gpu_available, rvar, weights):
+@pytest.mark.parametrize("rvar,weights,quadratic", [(False, False, True), (True, False, True), (False, True, True),
+                                                    (False, False, False), (True, True, False)])
+def test_device_step_matches_oracle(gpu_available, rvar, weights, quadratic):
     import torch
 
     from hvp import tables
@@ -65,7 +69,7 @@ def test_device_step_matches_oracle(gpu_available, rvar, weights):
     P, n = 64, 10
     X, U, Up, M, L = _platoons(P, n)
     veh = PwaGearVehicle(800)
-    prob = tables.problem(5, params=_OtherWeights) if weights else tables.problem(5)
+    prob = tables.problem(5, quadratic_cost=quadratic, params=_OtherWeights if weights else tables.Params)
     s = BatchSolver(prob, [tables.system_from_dict(veh.get_discrete_system(1), tables.gears_of(veh))])
     dev = torch.device("cuda", 0)
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
@@ -77,7 +81,7 @@ def test_device_step_matches_oracle(gpu_available, rvar, weights):
     xd = tx.cpu().numpy()
     for p in range(P):
         xo, c, viol, ok = O.env_step(X[p], U[p], M[p], L[p], u_prev=Up[p], gears=None if gears is None else gears[p],
-                                     real_vehicle_as_reference=rvar)
+                                     real_vehicle_as_reference=rvar, quadratic=quadratic)
         assert int(out["status"][p]) == (0 if ok else 1), p
         assert int(out["viol"][p]) == viol, p
         assert abs(float(out["cost"][p]) - c) <= 1e-12 * max(1.0, abs(c)), p

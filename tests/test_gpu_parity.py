@@ -268,3 +268,54 @@ def test_sweep_horizons_full_batch(gpu_available, n, NN):
         assert list(reg[j]) == list(r.sigma)
         assert abs(float(a["cost"][j]) - r.cost) <= 1e-9 * max(1.0, abs(r.cost))
         assert np.abs(u[j] - r.u).max() <= 1e-6
+
+
+@pytest.mark.parametrize("name", ["sweep_n5_N10.npz", "sweep_n10_N15.npz", "sweep_rollout_n5_N10.npz"])
+def test_long_horizon_leaf_fallback(gpu_available, monkeypatch, name):
+    """N > 8 (the 16-lane group path): leaf QPs whose active-set solve fails are re-solved by the
+    interior-point fallback (K_bnb_ipm) instead of turning the instance into HVP_MAXITER.  Forced
+    here by capping the leaves' active-set iterations (HVP_LEAF_GI_CAP=2, read at hvp_create):
+    most leaves take the fallback, and the answers stay the oracle's."""
+    from hvp.solver import BatchSolver
+
+    monkeypatch.setenv("HVP_LEAF_GI_CAP", "2")
+    fx = load(name)
+    prob, systems = product_problem(fx)
+    s = BatchSolver(prob, systems)
+    res = s.solve(fx["sys"], fx["roles"], fx["params"])
+    assert s.stats().n_fallback > 0
+    ok = fx["exp_status"] == 0
+    assert np.array_equal(res.status, fx["exp_status"])
+    assert np.array_equal(res.region[ok], fx["exp_region"][ok])
+    ce = fx["exp_cost"][ok]
+    assert np.all(np.abs(res.cost[ok] - ce) <= 1e-9 * np.maximum(1, np.abs(ce)))
+    assert np.abs(res.u[ok] - fx["exp_u"][ok]).max() <= 1e-6
+    assert np.abs(res.x[ok] - fx["exp_x"][ok]).max() <= 1e-4
+
+
+def test_position_box_long_horizon(gpu_available):
+    """Vehicles near p_max at N = 10 (the oracle's own search does not finish these deep,
+    infeasibility-riddled trees in minutes, so this test checks the answers, not the optimality):
+    leaves infeasible in the position box fail both solvers and are excluded; an instance whose
+    sequences all fail is HVP_MAXITER (the oracle's convention: candidates exist, none converged,
+    as test_position_box_fallback shows at N = 5); every returned sequence's fixed-sequence QP,
+    priced by the oracle, has the returned cost and respects p <= p_max."""
+    NL = 10
+    s = _solver([_gear_system()], N=NL)
+    sysd = O.gear_pwa_system(800.0)
+    P, R = [], []
+    for p0, v0, vl in [(9870, 30, 40), (9800, 25, 45), (9900, 20, 30), (9700, 35, 45), (9890, 22, 32)]:
+        lead = np.stack([p0 + 60 + vl * np.arange(NL + 1), np.full(NL + 1, float(vl))])
+        xb = O.constant_velocity_prediction(p0 - 80, v0, NL)
+        P.append(np.concatenate([[p0, v0], np.zeros(2 * (NL + 1)), xb.ravel(), lead.ravel()]))
+        R.append(O.role_bits(0, 2))
+    params, roles = np.array(P), np.array(R, np.int32)
+    res = s.solve(np.zeros(len(R), np.int32), roles, params)
+    assert set(res.status.tolist()) <= {0, 2} and (res.status == 0).any(), res.status
+    from instances import split_params
+
+    for i in np.flatnonzero(res.status == 0):
+        x0, xf, xb, xl = split_params(params[i], NL)
+        obj, conv, _, _, _ = O.solve_qp(sysd, O.Cfg(), NL, int(roles[i]), res.region[i], x0, xf, xb, xl)
+        assert conv and abs(res.cost[i] - obj) <= 1e-9 * max(1.0, abs(obj)), (i, res.cost[i], obj)
+        assert res.x[i, 0].max() <= 10000 + 1e-6

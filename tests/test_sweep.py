@@ -118,3 +118,12 @@ def test_run_points_blocks_equal_one_batch(gpu_available):
     R = np.concatenate([b["R"] for b in blocks], axis=1)
     np.testing.assert_array_equal(X, one["X"])
     np.testing.assert_array_equal(R, one["R"])
+
+
+def test_ep_len_beyond_the_leader_trajectory_raises():
+    """Sim_n_task_2's leader trajectory holds ep_len (150) + 50 samples: a longer episode is
+    refused up front with a clear error (before any device work)."""
+    from hvp.sweep import run_point
+
+    with pytest.raises(ValueError, match="leader samples"):
+        run_point(5, 10, [0], ep_len=190)
