@@ -20,6 +20,7 @@
 // Memory: everything lives in caller-owned device buffers plus a handle-owned workspace sized
 // once by hvp_reserve (no allocation inside hvp_solve_batch, so a call can be graph-captured).
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 
 #include "hvp_lane.h"
@@ -601,6 +602,18 @@ int hvp_get_stats(hvp_handle* h, hvp_stats* out) {
     }
     out->qp_iterations = (int64_t)c[1];
     out->n_fallback = (int64_t)c[2];
+#ifdef HVP_REFILL_PROF
+    {
+        unsigned long long lv2[2 * (HVP_MAX_N + 1)];
+        HIP_TRY(hipMemcpy(lv2, h->ws.lvl, sizeof(lv2), hipMemcpyDeviceToHost));
+        const unsigned long long* pf = lv2 + 2 * (HVP_MAX_N + 1) - 8;
+        std::fprintf(stderr,
+                     "[refill-prof] event cycles %llu of %llu (%.3f), wave trips %llu, busy lane-trips %llu (%.3f); "
+                     "write-back %llu (until cost %llu, until children %llu), claim %llu\n",
+                     pf[0], pf[1], pf[1] ? (double)pf[0] / (double)pf[1] : 0.0, pf[3], pf[2],
+                     pf[3] ? (double)pf[2] / (64.0 * (double)pf[3]) : 0.0, pf[4], pf[6], pf[7], pf[5]);
+    }
+#endif
     out->capacity = h->ws.cap;
     out->last_ms = ms;
     return 0;

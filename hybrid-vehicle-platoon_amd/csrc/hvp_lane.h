@@ -1408,6 +1408,11 @@ __device__ inline void gi_trip(Q& q, hvp::GiLane<N>& g, const hvp::Consts& C, in
     }
 }
 
+#ifdef HVP_REFILL_PROF
+// [0, 64): busy trips per node; [64, 128): trips per generation (event to event)
+__device__ unsigned long long g_pf_hist[128];
+#endif
+
 template <int N>
 __global__ __launch_bounds__(kBnbBlock<N>) __attribute__((amdgpu_waves_per_eu(HVP_REFILL_WAVES)))
 void k_bnb_bound_refill(int k, const hvp_system* __restrict__ systems, const int32_t* __restrict__ sys,
@@ -1428,10 +1433,29 @@ void k_bnb_bound_refill(int k, const hvp_system* __restrict__ systems, const int
     uint64_t code = 0;
     bool exhausted = false;
     unsigned long long iter_sum = 0;
+#ifdef HVP_REFILL_PROF  // diagnostics build: event / trip cycles and busy lane-trips per wave
+    unsigned long long pf_ev = 0, pf_all = 0, pf_busy = 0, pf_trips = 0, pf_wb = 0, pf_cl = 0, pf_dc = 0, pf_rs = 0;
+    const unsigned long long pf_t0 = __builtin_amdgcn_s_memtime();
+    int pf_mine = 0, pf_gen = 0;
+#endif
     for (;;) {
         const bool done = stage >= RS_FAIL;
         const unsigned long long free = __ballot(stage == RS_IDLE || done);
         const int nfree = __popcll(free);
+#ifdef HVP_REFILL_PROF
+        const unsigned long long pf_e0 = __builtin_amdgcn_s_memtime();
+        const bool pf_event = nfree >= kRefillMin || nfree == 64;
+        pf_busy += (unsigned long long)(64 - nfree);
+        pf_trips += 1;
+        if (pf_event) {
+            if (done) atomicAdd(&g_pf_hist[pf_mine < 63 ? pf_mine : 63], 1ull);
+            if (lane == 0) atomicAdd(&g_pf_hist[64 + (pf_gen < 63 ? pf_gen : 63)], 1ull);
+            pf_gen = 0;
+            pf_mine = 0;
+        }
+        ++pf_gen;
+        if (stage == RS_SCAN || stage == RS_STEP) ++pf_mine;
+#endif
         if (nfree >= kRefillMin || nfree == 64) {
             // ---- event: write the finished lanes' results, then refill every free lane
             unsigned cmask = 0;  // children of a finished bound node (k_bnb_expand's work, fused)
@@ -1443,6 +1467,13 @@ void k_bnb_bound_refill(int k, const hvp_system* __restrict__ systems, const int
                                                           params + (size_t)inst * C.stride, code, k)
                                     : 0.0;
                 iter_sum += (unsigned long long)g.iter;
+#ifdef HVP_REFILL_PROF
+                {
+                    const double cc = __builtin_amdgcn_readfirstlane(__double_as_longlong(c) & 0xffffffff);
+                    (void)cc;
+                    pf_dc += __builtin_amdgcn_s_memtime() - pf_e0;
+                }
+#endif
                 bnb_node_done<N>(k, t, inst, ok, g.iter, c, q.y, C, ws);
                 stage = RS_IDLE;
                 // the incumbent only changes at the leaves (level N): below N this pruning test
@@ -1457,10 +1488,24 @@ void k_bnb_bound_refill(int k, const hvp_system* __restrict__ systems, const int
                 if (cmask)
                     bnb_put_children(ws, k + 1, off, cmask, inst, systems[sys[inst]], C, code, ws.nd_lo[dst][t],
                                      ws.nd_hi[dst][t], clb);
+#ifdef HVP_REFILL_PROF
+                pf_rs += __builtin_amdgcn_s_memtime() - pf_e0;
+#endif
             }
             if (exhausted && nfree == 64) break;
+#ifdef HVP_REFILL_PROF
+            const unsigned long long pf_w1 = __builtin_amdgcn_s_memtime();
+            pf_wb += pf_w1 - pf_e0;
+#endif
             if (!exhausted) {
                 const unsigned long long base = wave_claim(claim, free, nfree, lane);
+#ifdef HVP_REFILL_PROF
+                {
+                    const unsigned long long bb = __builtin_amdgcn_readfirstlane((unsigned)base);
+                    (void)bb;
+                    pf_cl += __builtin_amdgcn_s_memtime() - pf_w1;
+                }
+#endif
                 if (base + nfree >= (unsigned long long)total) exhausted = true;
                 const long long mine = (long long)base + wave_rank(free);
                 if (stage == RS_IDLE && mine < total) {
@@ -1479,11 +1524,28 @@ void k_bnb_bound_refill(int k, const hvp_system* __restrict__ systems, const int
                 }
             }
         }
+#ifdef HVP_REFILL_PROF
+        if (pf_event) pf_ev += __builtin_amdgcn_s_memtime() - pf_e0;
+#endif
         if (stage == RS_SCAN || stage == RS_STEP) gi_trip<N>(q, g, C, stage, fail);
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) iter_sum += __shfl_down(iter_sum, off, 64);
     if (lane == 0 && iter_sum) atomicAdd(&ws.counter[1], iter_sum);
+#ifdef HVP_REFILL_PROF
+    pf_all = __builtin_amdgcn_s_memtime() - pf_t0;
+    if (lane == 0) {  // the claim slots of levels > N are free (prof builds need N <= 8)
+        unsigned long long* pf = ws.lvl + 2 * (HVP_MAX_N + 1) - 8;
+        atomicAdd(&pf[0], pf_ev);
+        atomicAdd(&pf[1], pf_all);
+        atomicAdd(&pf[2], pf_busy);
+        atomicAdd(&pf[3], pf_trips);
+        atomicAdd(&pf[4], pf_wb);
+        atomicAdd(&pf[5], pf_cl);
+        atomicAdd(&pf[6], pf_dc);
+        atomicAdd(&pf[7], pf_rs);
+    }
+#endif
 }
 
 // Leaves whose active-set solve failed its verification (degenerate vertices, e.g. the
@@ -2030,6 +2092,20 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
     h->last_stream = st;
     h->last_B = B;
     h->last_bnb = true;
+#ifdef HVP_REFILL_PROF
+    if constexpr (N <= HVP_MAX_N_ENUM) {
+        unsigned long long hist[128];
+        HIP_TRY(hipStreamSynchronize(st));
+        HIP_TRY(hipMemcpyFromSymbol(hist, HIP_SYMBOL(g_pf_hist), sizeof(hist)));
+        std::fprintf(stderr, "[refill-hist] node trips:");
+        for (int i = 0; i < 64; ++i) std::fprintf(stderr, " %llu", hist[i]);
+        std::fprintf(stderr, "\n[refill-hist] generation trips:");
+        for (int i = 64; i < 128; ++i) std::fprintf(stderr, " %llu", hist[i]);
+        std::fprintf(stderr, "\n");
+        std::memset(hist, 0, sizeof(hist));
+        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_pf_hist), hist, sizeof(hist)));
+    }
+#endif
     return 0;
 }
 
