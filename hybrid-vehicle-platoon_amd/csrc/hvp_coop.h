@@ -400,15 +400,166 @@ __device__ inline void row_owner(int id_in, int& lane, int& bit) {
     }
 }
 
+// Final state of one QP's active-set solve, kept in HBM between the ADMM iterations of the
+// switching ADMM (one record per local QP): the region code and hinge states it was solved for,
+// the active rows in position order and the factors J (= L^-T Q, rows) and R (upper, rows) of
+// that active set.  Next iteration the QP differs only in its linear term and row bounds (the
+// ADMM y, z terms), so with the same code and hinge states the Hessian -- and J, R -- are the
+// same, and the equality-constrained optimum on the old active set is two triangular solves and
+// two N x N products away (warm_start below).
+struct WarmQp {
+    uint64_t code, hs;
+    int32_t nact, valid;
+    int32_t ids[G];
+    double J[G * G];
+    double R[G * G];
+};
+
+// right-hand side dd of row p in the group's >= form (n = -c, slack dd + n.y): every lane
+// calls it with the same p; the owner lane computes the bound, the group receives it
+template <int N>
+__device__ inline double row_dd(const Lane<N>& L, int p) {
+    const int t = lane16();
+    const int base = p & (GI_REV - 1);
+    const bool rev = (p & GI_REV) != 0;
+    double dloc = 0.0;
+    int ol, ob;
+    row_owner<N>(p, ol, ob);
+    if (base < 6 * N) {
+        const int rj = base / 6, r = base % 6, pair = r / 2;
+        if (t == rj) {
+            const double a = pair == 1 ? L.am : (pair == 2 ? 1.0 : 0.0);
+            double lo, hi;
+            if (pair == 0) { lo = L.vlo; hi = L.vhi; }
+            else if (pair == 1) { lo = L.ulo; hi = L.uhi; }
+            else { lo = L.dec; hi = L.acc; }
+            const double cst = rj == 0 ? -a * L.v0 : 0.0;
+            dloc = (r & 1) ? hi - cst : -(lo - cst);
+        }
+    } else {
+        const int rm = (base - 6 * N) / 4, r = (base - 6 * N) % 4;
+        if (t == rm + 1) {
+            if (r == 0) dloc = L.P1 - L.pmin;
+            else if (r == 1) dloc = L.pmax - L.P1;
+            else if (r == 2) dloc = L.hf - L.P1;
+            else dloc = L.P1 - L.hb;
+        }
+    }
+    return (rev ? -1.0 : 1.0) * bcast(dloc, ol);
+}
+
+// The equality-constrained optimum on the active set of the last solve (WarmQp), if it is dual
+// feasible: y = J1 R^-T b - J2 J2' f, u = R^-1 (R^-T b + J1' f) with b_j = -dd of active row j
+// (n_j.y = b_j).  On success J, R are in LDS, L.y, u, id, act, nact set, and the Goldfarb-Idnani
+// loop continues from there (it adds any row the new bounds violate); false leaves the LDS (H)
+// untouched for the cold start.  Multipliers down to -1e-9 w count as zero (clamped).
+template <int N>
+__device__ inline bool warm_start(Lane<N>& L, GroupLds& Sg, const Consts& C, const WarmQp* wq, double& u, int& id,
+                                  unsigned& act, int& nact) {
+    const int t = lane16();
+    const int na = wq->nact;
+    if (na < 0 || na > N) return false;
+    const double* Jg = wq->J;
+    const double* Rg = wq->R;
+    const int myid = t < na ? wq->ids[t] : -1;
+    // b_j = -dd of active row j, lane j
+    double b = 0.0;
+    for (int j = 0; j < na; ++j) {
+        const double dd = row_dd<N>(L, bcast(myid, j));
+        if (t == j) b = -dd;
+    }
+    // s_c = (J' f)_c
+    double* v = Sg.v;
+    gsync();
+    v[t] = t < N ? L.f : 0.0;
+    gsync();
+    double s = 0.0;
+    if (t < N) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) s += Jg[i * G + t] * v[i];
+    }
+    // w1 = R^-T b (forward substitution over the active positions), w2 = -s
+    double w = t < N && t >= na ? -s : 0.0;
+    {
+        double acc = t < na ? b : 0.0;
+        for (int j = 0; j < na; ++j) {
+            double wj = 0.0;
+            if (t == j) wj = acc / Rg[j * G + j];
+            wj = bcast(wj, j);
+            if (t == j) w = wj;
+            if (t > j && t < na) acc -= Rg[j * G + t] * wj;
+        }
+    }
+    // u = R^-1 (w1 + s1) (back substitution)
+    double uu = 0.0;
+    {
+        double acc = t < na ? w + s : 0.0;
+        for (int j = na - 1; j >= 0; --j) {
+            double uj = 0.0;
+            if (t == j) uj = acc / Rg[j * G + j];
+            uj = bcast(uj, j);
+            if (t == j) uu = uj;
+            if (t < j) acc -= Rg[t * G + j] * uj;
+        }
+    }
+    const double wgt = C.w;
+    int bad = 0;
+    if (t < na) {
+        if (!(uu >= -1e-9 * wgt)) bad = 1;  // NaN-safe
+        if (gi_soft<N>(myid) && uu > wgt) bad = 1;
+    }
+    if (gor(bad)) return false;
+    // y_t = sum_c J[t][c] w_c
+    gsync();
+    v[t] = w;
+    gsync();
+    double y = 0.0;
+    if (t < N) {
+#pragma unroll
+        for (int c = 0; c < N; ++c) y += Jg[t * G + c] * v[c];
+    }
+    // commit: factors into LDS, the GI state into the lanes
+    if (t < N) {
+#pragma unroll
+        for (int c = 0; c < N; ++c) {
+            Sg.J[t * LD + c] = Jg[t * G + c];
+            Sg.R[t * LD + c] = Rg[t * G + c];
+        }
+        L.y = y;
+    }
+    u = t < na ? fmax(uu, 0.0) : 0.0;
+    id = myid;
+    act = 0;
+    for (int j = 0; j < na; ++j) {
+        int ol, ob;
+        row_owner<N>(bcast(myid, j), ol, ob);
+        if (t == ol) act |= 1u << ob;
+    }
+    nact = na;
+    gsync();
+    return true;
+}
+
 // Cooperative Goldfarb-Idnani.  On GI_OK lane t < N holds y_t in L.y.
+// wq (optional): the QP's WarmQp record -- tried as the starting active set when it was written
+// for the same code and hinge states (wcode, whs) and wtry is set; rewritten on success.
 template <int N>
 __device__ inline int solve(Lane<N>& L, GroupLds& Sg, const Consts& C, int max_iter, int& iters,
-                            unsigned* edge = nullptr) {
+                            unsigned* edge = nullptr, WarmQp* wq = nullptr, uint64_t wcode = 0, uint64_t whs = 0,
+                            bool wtry = false) {
     const int t = lane16();
     iters = 0;
     double* J = Sg.J;  // holds H on entry (row t written by lane t)
     double* R = Sg.R;
+    double u = 0.0;  // multiplier of active position t
+    int id = -1;     // row id of active position t
+    int nact = 0;
+    unsigned act = 0;  // active bits of the rows lane t owns
     gsync();
+    bool warmed = false;
+    if (wq && wtry && wq->valid && wq->code == wcode && wq->hs == whs)  // group-uniform
+        warmed = warm_start<N>(L, Sg, C, wq, u, id, act, nact);
+    if (!warmed) {
     // ---- Cholesky H = L L' into R area (lower, row-major), column by column
 #pragma unroll
     for (int j = 0; j < N; ++j) {
@@ -470,10 +621,7 @@ __device__ inline int solve(Lane<N>& L, GroupLds& Sg, const Consts& C, int max_i
             for (int c = 0; c < N; ++c) R[t * LD + c] = 0.0;
         gsync();
     }
-    double u = 0.0;  // multiplier of active position t
-    int id = -1;     // row id of active position t
-    int nact = 0;
-    unsigned act = 0;  // active bits of the rows lane t owns
+    }  // cold start
     unsigned sat = 0;  // saturation bits (SF = 1, SB = 2) of lane t's prefix rows
     const double wgt = C.w;
     const double tol = 1e-11;
@@ -707,7 +855,24 @@ __device__ inline int solve(Lane<N>& L, GroupLds& Sg, const Consts& C, int max_i
         if (t < nact && id >= 0 && id < 6 * N && id % 6 < 2 && u > kEdgeMultTol) bit = 1 << (2 * (id / 6) + id % 6);
         *edge = (unsigned)gor(bit);
     }
-    return gor(bad) ? GI_FAIL_VERIFY : GI_OK;
+    const bool ok = gor(bad) == 0;
+    if (wq) {  // the final active set and factors for the next ADMM iteration
+        const bool keep = ok && gor((int)sat) == 0;  // saturated soft rows: not warm-startable
+        if (t < N) {
+            for (int c = 0; c < N; ++c) {
+                wq->J[t * G + c] = J[t * LD + c];
+                wq->R[t * G + c] = R[t * LD + c];
+            }
+            wq->ids[t] = t < nact ? id : -1;
+        }
+        if (t == 0) {
+            wq->code = wcode;
+            wq->hs = whs;
+            wq->nact = nact;
+            wq->valid = keep ? 1 : 0;
+        }
+    }
+    return ok ? GI_OK : GI_FAIL_VERIFY;
 }
 
 // ------------------------------------------------------------------ trajectory helpers
@@ -850,14 +1015,24 @@ __device__ inline uint64_t admm_initial_states(Lane<N>& L, const Consts& C, int 
 
 // One fixed-sequence (relaxed beyond K) QP of either formulation, solved by the group.
 // Returns GI_OK with y in L.y (lane t < N) and the direct objective in *cost.
+//
+// wq (ADMM forms, optional): this QP's WarmQp record.  With warm set its hinge states replace
+// the constant-velocity guess as the starting states (the iterates change little from one ADMM
+// iteration to the next, so the first solve is usually consistent) and its active set / factors
+// start the active-set method (solve); every solve writes the record back.  The fixed point
+// reached is the QP's optimum either way (the Huber pieces are convex and C1, so the states only
+// decide which solve certifies it).
 template <int N>
 __device__ inline int solve_qp(Lane<N>& L, GroupLds& Sg, const hvp_system& S, const Consts& C, int role,
                                const double* prm, uint64_t code, int K, int max_iter, int& iters, double* cost,
-                               unsigned* edge = nullptr, double lo = 0.0, double hi = -1.0) {
+                               unsigned* edge = nullptr, double lo = 0.0, double hi = -1.0,
+                               WarmQp* wq = nullptr, bool warm = false) {
     iters = 0;
     if (C.form == HVP_FORM_ADMM || C.form == HVP_FORM_GADMM) {
         uint64_t hs;
-        {
+        if (wq && warm && wq->valid) {
+            hs = wq->hs;  // one address for the whole group
+        } else {
             // lane data for the classification helpers
             Lane<N> L0;
             setup<N>(L0, Sg, S, C, role, prm, code, K, 0);
@@ -867,7 +1042,7 @@ __device__ inline int solve_qp(Lane<N>& L, GroupLds& Sg, const hvp_system& S, co
             gsync();
             setup<N>(L, Sg, S, C, role, prm, code, K, hs);
             int it = 0;
-            const int st = solve<N>(L, Sg, C, max_iter, it, edge);
+            const int st = solve<N>(L, Sg, C, max_iter, it, edge, wq, code, hs, warm);
             iters += it;
             if (st != GI_OK) return st;
             bool consistent;

@@ -89,6 +89,11 @@ struct hvp_handle {
     uint64_t* cent_ties = nullptr;
     hvp::Consts* d_consts = nullptr;  // device copy of C (the centralised kernel reads it by pointer)
     size_t cent_split_bytes = 0;      // split-search workspace of the centralised path (hvp_cent.hip)
+    // switching ADMM: every local QP's final hinge states, active set and factors (hvp_coop.h
+    // WarmQp), the next ADMM iteration's start; not used after hvp_gadmm_rollout (a new warm start)
+    void* gadmm_hs = nullptr;
+    long long gadmm_hs_cap = 0;
+    int gadmm_hs_valid = 0;
     char* cent_split = nullptr;
     const int8_t* region_hint = nullptr;  // hvp_set_region_hint (copied into ws.hint per solve)
 };

@@ -497,6 +497,7 @@ int hvp_gadmm_rollout(hvp_handle* h, int P, int n, int lo, int m, const int32_t*
         return fail(HVP_E_ARG, "hvp_gadmm_rollout: bad argument");
     HIP_TRY(hipSetDevice(h->device));
     HIP_TRY(hipMemsetAsync(h->g_counter, 0, 8 * sizeof(unsigned long long), (hipStream_t)stream));
+    h->gadmm_hs_valid = 0;  // a new warm start: the local QPs start from their own hinge guess
     switch (h->prob.N) {
 #define HVP_CASE(nn) \
     case nn: return launch_gadmm_rollout<nn>(h, P, n, lo, m, sys, params, mode, u_prev, x, seq, u_ws, state, (hipStream_t)stream);
@@ -683,6 +684,7 @@ void hvp_destroy(hvp_handle* h) {
     if (h->cent_frames) (void)hipFree(h->cent_frames);
     if (h->cent_ties) (void)hipFree(h->cent_ties);
     if (h->cent_split) (void)hipFree(h->cent_split);
+    if (h->gadmm_hs) (void)hipFree(h->gadmm_hs);
     if (h->d_consts) (void)hipFree(h->d_consts);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);

@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -1961,7 +1962,8 @@ __global__ __launch_bounds__(kCoopBlock) void k_gadmm_qp_coop(int P, int n, int 
                                                               int32_t* __restrict__ status_out,
                                                               uint32_t* __restrict__ edge_out,
                                                               int32_t* __restrict__ iters_out,
-                                                              unsigned long long* __restrict__ counter) {
+                                                              unsigned long long* __restrict__ counter,
+                                                              hvp::coop::WarmQp* __restrict__ warm_ws, int warm) {
     __shared__ hvp::coop::GroupLds lds[kCoopGroups];
     const int g = threadIdx.x / hvp::coop::G, t = threadIdx.x % hvp::coop::G;
     const int b = blockIdx.x * kCoopGroups + g;
@@ -1976,7 +1978,8 @@ __global__ __launch_bounds__(kCoopBlock) void k_gadmm_qp_coop(int P, int n, int 
     double cost = 0.0;
     int it = 0;
     unsigned raw = 0;
-    const int st = hvp::coop::solve_qp<N>(L, lds[g], S, C, rl, prm, code, N, kGiMaxIter<N>, it, &cost, &raw);
+    const int st = hvp::coop::solve_qp<N>(L, lds[g], S, C, rl, prm, code, N, kGiMaxIter<N>, it, &cost, &raw, 0.0,
+                                          -1.0, warm_ws ? warm_ws + b : nullptr, warm != 0);
     if (st == hvp::GI_OK) {
         lds[g].v[t] = t < N ? L.y : 0.0;
         hvp::coop::gsync();
@@ -2158,9 +2161,25 @@ int launch_gadmm_qp(hvp_handle* h, int P, int n, int lo, int m, const int32_t* s
     const int B = P * m;
     HIP_TRY(hipEventRecord(h->evq0, st));
     if constexpr (kCoop<N>) {
+        // each local QP's final hinge states, active set and factors, carried from one ADMM
+        // iteration to the next (hvp_coop.h WarmQp)
+        if (B > h->gadmm_hs_cap) {
+            HIP_TRY(hipDeviceSynchronize());
+            (void)hipFree(h->gadmm_hs);
+            h->gadmm_hs = nullptr;
+            h->gadmm_hs_cap = 0;
+            if (hipMalloc(&h->gadmm_hs, sizeof(hvp::coop::WarmQp) * (size_t)B) != hipSuccess)
+                return fail(HVP_E_NOMEM, "hvp_gadmm_solve: device allocation failed");
+            h->gadmm_hs_cap = B;
+            h->gadmm_hs_valid = 0;
+        }
+        const char* wh = std::getenv("HVP_GADMM_WARM");  // "0": every QP from the cold start (A/B runs)
+        const int use = h->gadmm_hs_valid && !(wh && wh[0] == '0') ? 1 : 0;
         hipLaunchKernelGGL(k_gadmm_qp_coop<N>, dim3((B + kCoopGroups - 1) / kCoopGroups), dim3(kCoopBlock), 0, st, P, n,
                            lo, m, h->d_sys, sys, role, params, h->C, seq, state, u_out, x, xf, xb, cost_out,
-                           status_out, edge_out, iters_out, h->g_counter);
+                           status_out, edge_out, iters_out, h->g_counter,
+                           reinterpret_cast<hvp::coop::WarmQp*>(h->gadmm_hs), use);
+        h->gadmm_hs_valid = 1;
     } else {
         constexpr int BS = kBnbBlock<N>;
         const size_t lds = sizeof(double) * hvp::F_COUNT * N * BS;
