@@ -339,3 +339,23 @@ def test_gadmm_vehicle_sharded_engine_matches(gpu_available, name, world):
         for o in res:
             c = o[0]["cost"].cpu().numpy()
             assert np.all(np.abs(c - fx["exp_cost"][rows]) <= 1e-8 * np.abs(fx["exp_cost"][rows]))
+
+
+@pytest.mark.gpu
+def test_gadmm_warm_start_keeps_the_answers(gpu_available, monkeypatch):
+    """Every local QP starts from the previous ADMM iteration's hinge states, active set and
+    factors (hvp_coop.h warm_start); the cold start (HVP_GADMM_WARM=0) reaches the same optima:
+    sequences, rounds and warm-start choices identical, controls to 1e-9, costs to 1e-10."""
+    fx = load("gadmm_steps_n20_N10.npz")
+    P = len(fx["states"]) // int(fx["steps"])
+    warm = _run_steps(fx, [_engine(fx, P)])
+    monkeypatch.setenv("HVP_GADMM_WARM", "0")
+    cold = _run_steps(fx, [_engine(fx, P)])
+    for ((wo, wr),), ((co, cr),) in zip(warm, cold):
+        assert np.abs(wo["u"].cpu().numpy() - co["u"].cpu().numpy()).max() <= 1e-9
+        wc, cc = wo["cost"].cpu().numpy(), co["cost"].cpu().numpy()
+        assert np.all(np.abs(wc - cc) <= 1e-10 * np.abs(cc))
+        assert np.array_equal(wo["warm_start"].cpu().numpy(), co["warm_start"].cpu().numpy())
+        for a, b in zip(wr, cr):
+            assert np.array_equal(a["seq"].cpu().numpy(), b["seq"].cpu().numpy())
+            assert np.array_equal(a["platoon_rounds"].cpu().numpy(), b["platoon_rounds"].cpu().numpy())
