@@ -787,6 +787,8 @@ def bench_cent(args, world: int, rank: int, local: int, dist) -> None:
         "roofline": qp_roofline(kernel_ms, cent_kernels(f"cent_n{n}_N{N}"), notional, f"cent_n{n}_N{N}"),
         "qps_per_step": qps, "qp_iters_per_qp": float(iters.sum()) / max(qps, 1),
         "nodes_per_platoon": {"p50": float(q[0]), "p90": float(q[1]), "p99": float(q[2]), "max": float(q[3])},
+        # the heaviest searches of the rank (seed, QPs, status): where the step's time goes
+        "heaviest": [[int(seeds[j]), int(nodes[j]), int(status[j])] for j in np.argsort(-nodes, kind="stable")[:8]],
         "status_counts": {"optimal": int((status == 0).sum()), "infeasible": int((status == 1).sum()),
                           "node_limit": int((status == 2).sum()), "overflow": int((status == 3).sum())},
     }
