@@ -510,8 +510,18 @@ __device__ inline void most_violated(const Lane& L, const Consts& C, double y, d
 }
 
 // Cooperative Goldfarb-Idnani over the wave (the algorithm of hvp_coop.h::solve).
+//
+// Early stop (cut < inf): every iterate of the dual method is the optimum of a relaxation of the
+// QP (the active rows as inequalities, the saturated soft rows' penalties linear, every other
+// soft row's penalty dropped; multipliers feasible), so its objective (direct_cost in dual mode)
+// is a lower bound of the QP's optimum.  Every fourth scan the objective is evaluated; once it
+// exceeds `cut` the solve returns GI_CUT with that bound in `bound` -- the branch and bound prunes
+// such a QP anyway, so the search tree is unchanged.
+constexpr int GI_CUT = 9;
+__device__ inline double direct_cost(const Lane& L, const Consts& C, const Inst& I, uint64_t ci, int Ki,
+                                     double* u_lane, int dual_sat);
 __device__ inline int solve(Lane& L, const Lds& Sg, const Consts& C, const Inst& I, int max_iter, int& iters,
-                            Prof& pf) {
+                            Prof& pf, int Ki = 0, double cut = __builtin_inf(), double* bound = nullptr) {
     const int t = lane();
     const int N = I.N, V = I.V, LD = Sg.LD;
     iters = 0;
@@ -575,8 +585,16 @@ __device__ inline int solve(Lane& L, const Lds& Sg, const Consts& C, const Inst&
     unsigned act = 0, sat = 0;
     const double wgt = C.w;
     const double tol = 1e-11;
-    int iter = 0;
+    int iter = 0, scans = 0;
     for (;;) {
+        if (cut < 1e300 && (++scans & 3) == 0) {
+            const double lb = direct_cost(L, C, I, 0, Ki, nullptr, (int)(sat & 1u));
+            if (lb > cut) {
+                iters = iter;
+                *bound = lb;
+                return GI_CUT;
+            }
+        }
         pf.mark(2);
         // ---------------- most violated row
         const double yv = t < V ? L.y : 0.0;
@@ -813,8 +831,12 @@ __device__ inline int solve(Lane& L, const Lds& Sg, const Consts& C, const Inst&
 // Objective of the platoon trajectory, term by term (cent_mld.py:83-140; relaxed steps a >= K_i
 // carry no input cost).  Lane t adds the terms of state a + 1 of vehicle i and of input a; lane
 // a = 0 also those of state 0.  u_lane (optional) receives the lane's input u_{i,a}.
+//
+// dual_sat >= 0: the objective of a Goldfarb-Idnani iterate instead (solve's early stop): the soft
+// safe-distance rows of states >= 2 contribute w (c.y - d) when saturated (bit 0 of dual_sat, the
+// lane's own row) and nothing otherwise; the constant rows of states 0 and 1 keep their penalty.
 __device__ inline double direct_cost(const Lane& L, const Consts& C, const Inst& I, uint64_t ci, int Ki,
-                                     double* u_lane = nullptr) {
+                                     double* u_lane = nullptr, int dual_sat = -1) {
     const int t = lane();
     const int N = I.N;
     const double yv = L.on ? L.y : 0.0;
@@ -828,15 +850,20 @@ __device__ inline double direct_cost(const Lane& L, const Consts& C, const Inst&
     const double p0m = L.on && L.i >= 1 ? I.x0[2 * (L.i - 1)] : 0.0, v0m = L.on && L.i >= 1 ? I.x0[2 * L.i - 1] : 0.0;
     const double Qpv2 = 2.0 * C.Qpv;
     auto quad = [&](double ep, double ev) { return C.Qpp * ep * ep + Qpv2 * ep * ev + C.Qvv * ev * ev; };
+    // penalty w max(0, g) of a safe row; in dual mode the row of a state >= 2 is the QP's soft row
+    auto pen = [&](int k, double g) {
+        if (dual_sat < 0 || k < 2) return C.w * fmax(0.0, g);
+        return (dual_sat & 1) ? C.w * g : 0.0;
+    };
     auto state_terms = [&](int k, double p, double v, double pm, double vm) {
         double Jt = 0.0;
         if (L.i == I.L)
             Jt += quad(p - I.xl[k] + (I.lsp ? C.t0 * v + C.d0 : 0.0), v - I.xl[N + 1 + k]);
         if (L.i >= 1) {
             Jt += quad(p + C.t0 * v + C.d0 - pm, v - vm);
-            Jt += C.w * fmax(0.0, p - pm + C.d_safe);
+            Jt += pen(k, p - pm + C.d_safe);
         } else if (I.lsp && I.L == 0) {
-            Jt += C.w * fmax(0.0, p - I.xl[k] + C.d_safe);
+            Jt += pen(k, p - I.xl[k] + C.d_safe);
         }
         return Jt;
     };

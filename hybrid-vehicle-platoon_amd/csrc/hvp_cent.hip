@@ -205,7 +205,7 @@ __global__ __launch_bounds__(64) void k_cent_tasks(int n, int N, int leader, int
         const long long c0 = debug ? (long long)wall_clock64() : 0;
         bnb_platoon<L1>(L, S, C, I, st, frames, nreg_max, ties, max_nodes - (int)done_nodes, false, max_iter, res, &sa);
         const long long dt = debug ? (long long)wall_clock64() - c0 : 0;
-        if (t == 0 && (debug >= 4 || (debug && (dt > 50000000ll || res.iters > 200 * (res.nodes + 1)))))
+        if (t == 0 && debug != 6 && (debug >= 4 || (debug && (dt > 50000000ll || res.iters > 200 * (res.nodes + 1)))))
             printf("[cent-task] p %d d0 %d lb %.6g inc %.6g nodes %d iters %d ticks %lld\n", p, tk->d0, tk->lb, incg,
                    res.nodes, res.iters, dt);
     }
@@ -340,7 +340,7 @@ int hvp_cent_solve_batch(hvp_handle* h, int P, int n, int leader_index, int real
     HIP_TRY(hipMemsetAsync(h->g_counter, 0, 8 * sizeof(unsigned long long), st));
     const int exhaustive = h->prob.method == HVP_METHOD_ENUMERATE ? 1 : 0;
     const char* dbg = std::getenv("HVP_CENT_DEBUG");  // diagnostics: printf of failing QPs
-    const int debug = dbg && dbg[0] ? std::atoi(dbg) : 0;  // 1: failures, 2: + every GI step
+    const int debug = dbg && dbg[0] ? std::atoi(dbg) : 0;  // 1: failures, 2: + every GI step, 6: QPs per depth
     const int cap = max_nodes > 0 ? max_nodes : 2000000;
     const int max_iter = 8 * hvp::cent::ROWS * V;  // active-set iterations per QP
     // split-search workspace: platoon records, merged tie lists, two task lists (ping-pong),
@@ -447,6 +447,17 @@ int hvp_cent_solve_batch(hvp_handle* h, int P, int n, int leader_index, int real
                                real_vehicle_as_reference ? 1 : 0, h->d_sys, sys, x0, leader_x, h->d_consts, max_iter,
                                debug, ws, E);
         HIP_TRY(hipGetLastError());
+    }
+    if (debug == 6) {  // QPs per depth of the search (hvp_cent_bnb.h g_cent_depth), summed over all platoons
+        unsigned long long hist[3][64];
+        HIP_TRY(hipStreamSynchronize(st));
+        HIP_TRY(hipMemcpyFromSymbol(hist, HIP_SYMBOL(hvp::cent::g_cent_depth), sizeof(hist)));
+        for (int d = 0; d < 64; ++d)
+            if (hist[0][d] || hist[1][d])
+                std::fprintf(stderr, "[cent-depth] fixed %2d (vehicle %d step %d): bound QPs %llu (above incumbent %llu), visits %llu\n",
+                             d, d > 0 ? (d - 1) % n : -1, d > 0 ? (d - 1) / n : -1, hist[0][d], hist[2][d], hist[1][d]);
+        const unsigned long long zero[3][64] = {};
+        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(hvp::cent::g_cent_depth), zero, sizeof(zero)));
     }
 #ifdef HVP_CENT_PROF
     if (debug >= 3) {  // phase profile of the wave QP (hvp_cent.h Prof), summed over all platoons

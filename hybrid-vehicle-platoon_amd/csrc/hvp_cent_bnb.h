@@ -92,7 +92,11 @@ struct SplitArgs {
     long long out_cap;
 };
 
-enum { QP_OK = 0, QP_INFEASIBLE = 1, QP_FAILED = 2 };
+enum { QP_OK = 0, QP_INFEASIBLE = 1, QP_FAILED = 2, QP_CUT = 3 };  // QP_CUT: bound above the cut (solve's early stop)
+
+// HVP_CENT_DEBUG=6 diagnostics: QPs per number of fixed decisions, [0] bound QPs of expansions,
+// [1] visits (leaves / final), [2] bound QPs whose bound ended above the incumbent
+__device__ unsigned long long g_cent_depth[3][64];
 
 struct Child {
     double lb, lo, hi;
@@ -127,9 +131,13 @@ __device__ inline int fixed_steps(int d, int n, int i) { return d / n + (i < d %
 // L1: the min_1_norm LP of the same rows (hvp_cent_l1.h): QP_INFEASIBLE when a vehicle's hard rows
 // are proven infeasible (hvp_l1.h l1_infeasible, per vehicle: the hard rows do not couple
 // vehicles), QP_FAILED when the interior point leaves it unresolved.
+//
+// cut < inf (quadratic cost): the QP may stop as soon as its dual bound exceeds cut (QP_CUT, cost =
+// that bound): the caller passes a value above which the QP is pruned whatever its optimum.
 template <bool L1>
 __device__ inline int platoon_qp(Lane& L, const Lds& S, const Consts& C, const Inst& I, uint64_t vcode, double vlo,
-                                 double vhi, int d, int max_iter, double& cost, int& iters, Prof& pf) {
+                                 double vhi, int d, int max_iter, double& cost, int& iters, Prof& pf,
+                                 double cut = __builtin_inf()) {
     const int t = lane();
     const int i = t < I.V ? t / I.N : 0;
     const uint64_t ci = bc(vcode, i);
@@ -163,8 +171,9 @@ __device__ inline int platoon_qp(Lane& L, const Lds& S, const Consts& C, const I
         return QP_OK;
     }
     pf.mark(0);
-    const int r = solve(L, S, C, I, max_iter, it, pf);
+    const int r = solve(L, S, C, I, max_iter, it, pf, Ki, cut, &cost);
     iters = it;
+    if (r == GI_CUT) return QP_CUT;
     if (r == GI_FAIL_DUAL) return QP_INFEASIBLE;
     if (r != GI_OK) return QP_FAILED;
     cost = direct_cost(L, C, I, ci, Ki);
@@ -493,8 +502,23 @@ __device__ inline void bnb_platoon(Lane& L, const Lds& S, const Consts& C, const
                 qhi = chi;
             }
         }
-        const int q = platoon_qp<L1>(L, S, C, I, st.vcode, qlo, qhi, dfix, max_iter, c, it, pf);
+        // early stop of QPs that end pruned: 10x the prune margin above the incumbent (the dual
+        // bound's rounding is ~1e-9 relative); not for the final re-solve
+        double cut = INF;
+        if (phase != FINAL && C.cent_cut && !L1) {
+            const double incc = shared_inc();
+            if (incc < INF) cut = incc + 10.0 * kPruneRel * (1.0 + fabs(incc));
+        }
+        const int q = platoon_qp<L1>(L, S, C, I, st.vcode, qlo, qhi, dfix, max_iter, c, it, pf, cut);
         iters += it;
+        if (I.debug == 6) {
+            const double incd = shared_inc();
+            const int dd = dfix < 63 ? dfix : 63;
+            if (t == 0) {
+                atomicAdd(&g_cent_depth[phase == EXPAND ? 0 : 1][dd], 1ull);
+                if (phase == EXPAND && q == QP_OK && bnb_pruned(c, incd)) atomicAdd(&g_cent_depth[2][dd], 1ull);
+            }
+        }
         if (I.debug && I.debug < 3 && q != QP_OK) {
             const uint64_t c0 = bc(st.vcode, 0), c1 = bc(st.vcode, 1 < n ? 1 : 0), c2 = bc(st.vcode, 2 < n ? 2 : 0);
             if (t == 0)
@@ -504,7 +528,7 @@ __device__ inline void bnb_platoon(Lane& L, const Lds& S, const Consts& C, const
         }
         // ---- use its result
         if (phase == EXPAND) {
-            const double lb = q == QP_OK ? c : (q == QP_INFEASIBLE ? INF : -INF);
+            const double lb = (q == QP_OK || q == QP_CUT) ? c : (q == QP_INFEASIBLE ? INF : -INF);
             if (t == ex_r) ex_lb = lb;
             ex_todo &= ex_todo - 1;
         } else if (phase == VISIT) {

@@ -449,7 +449,7 @@ __device__ inline int lp_solve(Lane& L, const Lds& S, const Consts& C, const Ins
     wmx = wmax(wmx);
     const double mtot = fmax(wsum(cnt), 1.0);
     double ybest = L.y, best = __builtin_inf();  // best iterate (relative gap) for the rescue
-    if (I.debug >= 5) {  // diagnostics: every lane's rows (g, h / e0, w, al) at the start
+    if (I.debug == 5) {  // diagnostics: every lane's rows (g, h / e0, w, al) at the start
 #pragma unroll
         for (int r = 0; r < kLpHard; ++r) {
             LpG g;
@@ -475,7 +475,7 @@ __device__ inline int lp_solve(Lane& L, const Lds& S, const Consts& C, const Ins
         obj = wsum(obj);
         rpm = wmax(rpm);
         rdm = fmax(wmax(rdm), wmax(L.on ? fabs(rdy) : 0.0));
-        if (I.debug >= 4 && lane() == 0)
+        if ((I.debug == 4 || I.debug == 5) && lane() == 0)
             printf("[lp] it %d rpm %.3e/%.3e rdm %.3e/%.3e gap %.3e obj %.9e\n", iters, rpm, 1e-10 * hsc, rdm,
                    1e-10 * wmx, gap, obj);
         const double rgap = gap / fmax(1.0, fabs(obj));
@@ -527,7 +527,7 @@ __device__ inline int lp_solve(Lane& L, const Lds& S, const Consts& C, const Ins
         }
         ap *= 0.995;
         ad *= 0.995;
-        if (I.debug >= 4) {
+        if (I.debug == 4 || I.debug == 5) {
             const double rdiag = lane() < V ? S.R[lane() * S.LD + lane()] : 1.0;
             const double rmin = wmin(lane() < V ? rdiag : 1e300), rmax = wmax(lane() < V ? rdiag : 0.0);
             const double dyn = wmax(L.on ? fabs(dy) : 0.0);

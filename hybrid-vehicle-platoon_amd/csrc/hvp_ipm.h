@@ -55,6 +55,8 @@ struct Consts {
     int l1;        // 1: min_1_norm cost (hvp_l1.h), 0: min_2_norm
     int leaf_cap;  // > 0: active-set cap of the long-horizon leaf QPs (HVP_LEAF_GI_CAP, tests of
                    // the interior-point leaf fallback); 0: the solver's own cap
+    int cent_cut;  // 1: the centralised search stops a QP once its dual bound passes the incumbent
+                   // (hvp_cent.h solve; HVP_CENT_CUT=0 turns it off)
 };
 
 struct QpOut {

@@ -757,15 +757,16 @@ __device__ inline unsigned bnb_children(const hvp_system& S, const hvp::Consts& 
 }
 
 // writes the children (regions in mask) of a level-(lv-1) node into level lv's list at slots
-// off.. (reserved by the caller); past the capacity the instance is flagged HVP_OVERFLOW
-__device__ inline void bnb_put_children(Workspace& ws, int lv, unsigned long long off, unsigned mask, int inst,
-                                        const hvp_system& S, const hvp::Consts& C, uint64_t code, double lo,
-                                        double hi, double plb) {
+// off.. (reserved by the caller) below `limit` (the end of the list's half, LevelList); past it
+// the instance is flagged HVP_OVERFLOW
+__device__ inline void bnb_put_children(Workspace& ws, int lv, unsigned long long off, unsigned long long limit,
+                                        unsigned mask, int inst, const hvp_system& S, const hvp::Consts& C,
+                                        uint64_t code, double lo, double hi, double plb) {
     const int nc = __popc(mask), d = lv & 1;
-    if (off + nc > (unsigned long long)ws.cap) {
+    if (off + nc > limit) {
         atomicOr(&ws.inst_flag[inst], 2);  // overflow: reported, never truncated silently
-        // the slots of this reservation below the capacity are swept by the next kernels
-        for (unsigned long long t = off; t < (unsigned long long)ws.cap && t < off + nc; ++t) ws.nd_inst[d][t] = -1;
+        // the slots of this reservation below the limit are swept by the next kernels
+        for (unsigned long long t = off; t < limit && t < off + nc; ++t) ws.nd_inst[d][t] = -1;
         return;
     }
     int j = 0;
@@ -784,7 +785,7 @@ __device__ inline void bnb_put_children(Workspace& ws, int lv, unsigned long lon
 
 // wave-level reservation of nc slots per lane in level lv's list (an inclusive scan, one atomic
 // by the last lane); every lane of the wave must call it.  Returns the lane's first slot.
-__device__ inline unsigned long long wave_reserve(Workspace& ws, int lv, int nc, int lane, bool& any) {
+__device__ inline unsigned long long wave_reserve(unsigned long long* counter, int nc, int lane, bool& any) {
     int incl = nc;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
@@ -794,10 +795,58 @@ __device__ inline unsigned long long wave_reserve(Workspace& ws, int lv, int nc,
     const int wave_total = __shfl(incl, 63, 64);
     any = wave_total != 0;
     unsigned long long base = 0;
-    if (lane == 63 && wave_total) base = atomicAdd(&ws.lvl[lv], (unsigned long long)wave_total);
+    if (lane == 63 && wave_total) base = atomicAdd(counter, (unsigned long long)wave_total);
     base = ((unsigned long long)(unsigned)__shfl((int)(base >> 32), 63, 64) << 32) |
            (unsigned)__shfl((int)(base & 0xffffffffu), 63, 64);
     return base + (unsigned long long)(incl - nc);
+}
+
+// Level lists of the decentralised lane path (k_bnb_root, k_bnb_bound_refill; Workspace::split)
+// are kept in two halves of the capacity: the children of a parent whose QP took fewer than
+// kSlowSteps active-set steps fill [0, cap/2), the others [cap/2, cap).  A child's step count
+// follows its parent's (correlation 0.84 at C2, profiles/diag_dualstop.cpp), and the refill
+// kernel claims the first half before the second, so its 64-node generations -- as long as their
+// slowest lane -- hold QPs of similar length.  The order of a level's nodes changes nothing else:
+// the incumbent only moves at the leaves, where the tie rule is order-free.  Every other path
+// keeps one list over the whole capacity (split = 0: nb = 0, slot(c) = c).
+#ifndef HVP_SLOW_STEPS
+#define HVP_SLOW_STEPS 6
+#endif
+constexpr int kSlowSteps = HVP_SLOW_STEPS;
+constexpr int kLvlBack = 2 * (HVP_MAX_N + 1);  // ws.lvl[kLvlBack + k]: nodes of level k's second half
+
+struct LevelList {
+    unsigned long long nf, nb, half;
+    __device__ long long count() const { return (long long)(nf + nb); }
+    __device__ long long slot(long long c) const {
+        return c < (long long)nf ? c : (long long)half + (c - (long long)nf);
+    }
+};
+__device__ inline LevelList level_list(const Workspace& ws, int k) {
+    const unsigned long long cap = (unsigned long long)ws.cap;
+    LevelList L;
+    L.half = ws.split ? cap / 2 : cap;
+    const unsigned long long a = ws.lvl[k], b = ws.split ? ws.lvl[kLvlBack + k] : 0ull;
+    L.nf = a < L.half ? a : L.half;
+    L.nb = b < cap - L.half ? b : cap - L.half;
+    return L;
+}
+
+// reserves nc slots per lane of level lv in the half the lane's parent belongs to (slow: its QP
+// took >= kSlowSteps steps); returns the lane's first slot and the end of its half
+__device__ inline unsigned long long split_reserve(Workspace& ws, int lv, int nc, bool slow, int lane,
+                                                   unsigned long long& limit) {
+    const unsigned long long cap = (unsigned long long)ws.cap;
+    if (!ws.split) {
+        bool any;
+        limit = cap;
+        return wave_reserve(&ws.lvl[lv], nc, lane, any);
+    }
+    bool any0, any1;
+    const unsigned long long o0 = wave_reserve(&ws.lvl[lv], slow ? 0 : nc, lane, any0);
+    const unsigned long long o1 = wave_reserve(&ws.lvl[kLvlBack + lv], slow ? nc : 0, lane, any1);
+    limit = slow ? cap : cap / 2;
+    return slow ? cap / 2 + o1 : o0;
 }
 
 // The region sequence of hvp_set_region_hint for instance i as a leaf code, if every step is a
@@ -845,7 +894,7 @@ __global__ __launch_bounds__(kBnbBlock<N>) HVP_LANE_OCC void k_bnb_root(int B, c
     ws.nd_hi[0][i] = v0;
     double inc = __longlong_as_double(0x7ff0000000000000ll);  // +inf: no incumbent
     double lb = -1e300;
-    int nodes = 0, iters = 0;
+    int nodes = 0, iters = 0, iters_root = 0;
     if (ok) {
         hvp::LaneQp<N, LdsMem<N, BS>> q;
         q.mem.lane = threadIdx.x;
@@ -853,6 +902,7 @@ __global__ __launch_bounds__(kBnbBlock<N>) HVP_LANE_OCC void k_bnb_root(int B, c
         int it = bnb_qp<N, BS, ADMM>(q, S, C, rl, prm, 0, 0, v0, v0, c0);
         ++nodes;
         iters += it >= 0 ? it : -1 - it;
+        iters_root = it >= 0 ? it : -1 - it;
         if (it >= 0) {
             lb = c0;
             double ystar[N];
@@ -891,8 +941,13 @@ __global__ __launch_bounds__(kBnbBlock<N>) HVP_LANE_OCC void k_bnb_root(int B, c
         if (ok && !hvp::bnb_pruned(lb, inc)) {
             const unsigned mask = bnb_children(S, C, 0, v0, v0);
             if (mask) {
-                const unsigned long long off = atomicAdd(&ws.lvl[1], (unsigned long long)__popc(mask));
-                bnb_put_children(ws, 1, off, mask, i, S, C, 0, v0, v0, lb);
+                const int root_steps = iters_root;
+                const bool slow = ws.split && root_steps >= kSlowSteps;
+                const unsigned long long cap = (unsigned long long)ws.cap;
+                const unsigned long long off =
+                    slow ? cap / 2 + atomicAdd(&ws.lvl[kLvlBack + 1], (unsigned long long)__popc(mask))
+                         : atomicAdd(&ws.lvl[1], (unsigned long long)__popc(mask));
+                bnb_put_children(ws, 1, off, slow || !ws.split ? cap : cap / 2, mask, i, S, C, 0, v0, v0, lb);
             }
         }
     }
@@ -1081,9 +1136,9 @@ __global__ __launch_bounds__(kBlock) void k_bnb_expand(int k, const hvp_system* 
             }
         }
         bool any;
-        const unsigned long long off = wave_reserve(ws, k, __popc(mask), lane, any);
+        const unsigned long long off = wave_reserve(&ws.lvl[k], __popc(mask), lane, any);
         if (!any || !mask) continue;
-        bnb_put_children(ws, k, off, mask, inst, systems[sys[inst]], C, code, lo, hi, plb);
+        bnb_put_children(ws, k, off, (unsigned long long)ws.cap, mask, inst, systems[sys[inst]], C, code, lo, hi, plb);
     }
 }
 
@@ -1422,8 +1477,8 @@ void k_bnb_bound_refill(int k, const hvp_system* __restrict__ systems, const int
     constexpr int BS = kBnbBlock<N>;
     static_assert(N <= HVP_MAX_N_ENUM, "lane refill is the N <= 8 path");
     const int dst = k & 1;
-    const unsigned long long nn = ws.lvl[k];
-    const long long total = (long long)(nn < (unsigned long long)ws.cap ? nn : ws.cap);
+    const LevelList lvl = level_list(ws, k);
+    const long long total = lvl.count();
     unsigned long long* claim = ws.lvl + (HVP_MAX_N + 1) + k;
     const int lane = threadIdx.x & 63;
     hvp::LaneQp<N, LdsMem<N, BS>> q;
@@ -1484,11 +1539,12 @@ void k_bnb_bound_refill(int k, const hvp_system* __restrict__ systems, const int
                     cmask = bnb_children(systems[sys[inst]], C, k, ws.nd_lo[dst][t], ws.nd_hi[dst][t]);
             }
             if (k < N) {
-                bool any;
-                const unsigned long long off = wave_reserve(ws, k + 1, __popc(cmask), lane, any);
+                unsigned long long limit;
+                const unsigned long long off =
+                    split_reserve(ws, k + 1, __popc(cmask), done && g.iter >= kSlowSteps, lane, limit);
                 if (cmask)
-                    bnb_put_children(ws, k + 1, off, cmask, inst, systems[sys[inst]], C, code, ws.nd_lo[dst][t],
-                                     ws.nd_hi[dst][t], clb);
+                    bnb_put_children(ws, k + 1, off, limit, cmask, inst, systems[sys[inst]], C, code,
+                                     ws.nd_lo[dst][t], ws.nd_hi[dst][t], clb);
 #ifdef HVP_REFILL_PROF
                 pf_rs += __builtin_amdgcn_s_memtime() - pf_e0;
 #endif
@@ -1508,8 +1564,9 @@ void k_bnb_bound_refill(int k, const hvp_system* __restrict__ systems, const int
                 }
 #endif
                 if (base + nfree >= (unsigned long long)total) exhausted = true;
-                const long long mine = (long long)base + wave_rank(free);
-                if (stage == RS_IDLE && mine < total) {
+                const long long mc = (long long)base + wave_rank(free);
+                const long long mine = lvl.slot(mc);
+                if (stage == RS_IDLE && mc < total) {
                     inst = ws.nd_inst[dst][mine];
                     if (inst < 0) {  // dead slot of an overflowed reservation
                         if (k == N) ws.leaf_stat[mine] = HVP_OVERFLOW;
@@ -1588,10 +1645,11 @@ __global__ __launch_bounds__(kBnbBlock<N>) void k_bnb_ipm(const hvp_system* __re
 template <int N>
 __global__ __launch_bounds__(kBlock) void k_bnb_key(Workspace ws, int form, int l1) {
     const int src = N & 1;
-    const unsigned long long nn = ws.lvl[N];
-    const long long total = (long long)(nn < (unsigned long long)ws.cap ? nn : ws.cap);
-    for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
-         t += (long long)gridDim.x * blockDim.x) {
+    const LevelList lvl = level_list(ws, N);
+    const long long total = lvl.count();
+    for (long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x; c < total;
+         c += (long long)gridDim.x * blockDim.x) {
+        const long long t = lvl.slot(c);
         const int inst = ws.nd_inst[src][t];
         if (inst < 0) continue;
         const double best = inc_of(ws, inst);
@@ -1677,10 +1735,11 @@ __global__ __launch_bounds__(kBlock) void k_bnb_write(const hvp_system* __restri
                                                       double* __restrict__ cost_out, double* __restrict__ xf_out,
                                                       double* __restrict__ xb_out) {
     const int src = N & 1;
-    const unsigned long long nn = ws.lvl[N];
-    const long long total = (long long)(nn < (unsigned long long)ws.cap ? nn : ws.cap);
-    for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
-         t += (long long)gridDim.x * blockDim.x) {
+    const LevelList lvl = level_list(ws, N);
+    const long long total = lvl.count();
+    for (long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x; c < total;
+         c += (long long)gridDim.x * blockDim.x) {
+        const long long t = lvl.slot(c);
         if (ws.leaf_stat[t] != 0) continue;
         const int inst = ws.nd_inst[src][t];
         if (inst < 0) continue;
@@ -2012,8 +2071,15 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
                double* xb_out = nullptr) {
     Workspace ws = h->ws;
     constexpr int BS = kBnbBlock<N>;
+    // the decentralised lane path generates every level's nodes inside k_bnb_root / the bound
+    // kernel of the level above (fused expand) and keeps each level in two halves (LevelList);
+    // the other paths run k_bnb_expand per level over one list
+    const bool fused = !kCoop<N> && h->C.form == HVP_FORM_DECENT && !h->C.l1;
+    const char* sp = std::getenv("HVP_SPLIT_LEVELS");  // "0": one list (A/B runs)
+    ws.split = fused && !(sp && sp[0] == '0') ? 1 : 0;
+    h->last_split = ws.split != 0;
     HIP_TRY(hipMemsetAsync(ws.counter, 0, 8 * sizeof(unsigned long long), st));
-    HIP_TRY(hipMemsetAsync(ws.lvl, 0, 2 * (HVP_MAX_N + 1) * sizeof(unsigned long long), st));  // + claims
+    HIP_TRY(hipMemsetAsync(ws.lvl, 0, 3 * (HVP_MAX_N + 1) * sizeof(unsigned long long), st));  // + claims, halves
     HIP_TRY(hipEventRecord(h->ev0, st));
     HIP_TRY(hipEventRecord(h->evq0, st));
     const size_t lds = sizeof(double) * hvp::F_COUNT * N * BS;
@@ -2045,9 +2111,6 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
     HIP_TRY(hipEventRecord(h->evb[1], st));
     const int g_small = (int)std::min<long long>(grid_for(h->ws.cap), (long long)h->n_cu * 8);
     const int g_qp = (int)std::min<long long>((h->ws.cap + BS - 1) / BS, (long long)h->n_cu * 8 * (kBlock / BS));
-    // the decentralised lane path generates every level's nodes inside k_bnb_root / the bound
-    // kernel of the level above (fused expand); the other paths run k_bnb_expand per level
-    const bool fused = !kCoop<N> && h->C.form == HVP_FORM_DECENT && !h->C.l1;
     for (int k = 1; k <= N; ++k) {
         if (!fused)
             hipLaunchKernelGGL(k_bnb_expand<N>, dim3(g_small), dim3(kBlock), 0, st, k, h->d_sys, sys, h->C, ws);

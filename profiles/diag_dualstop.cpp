@@ -211,15 +211,16 @@ extern "C" int diag_dualstop(const hvp_problem* P, const hvp_system* systems, in
         gf += mf;
         gs += ms;
     }
-    if (rec) {  // per QP: level, parent steps, parent nact, own steps, own nact
+    if (rec) {  // per QP: level, parent steps, parent nact, own steps, own nact, steps with the dual stop
         long long j = 0;
         for (auto& s : per)
             for (size_t a = 0; a < s.full.size(); ++a, ++j) {
-                rec[5 * j + 0] = s.lvl_of[a];
-                rec[5 * j + 1] = s.par_steps[a];
-                rec[5 * j + 2] = s.par_nact[a];
-                rec[5 * j + 3] = s.full[a];
-                rec[5 * j + 4] = s.nact[a];
+                rec[6 * j + 0] = s.lvl_of[a];
+                rec[6 * j + 5] = s.stop[a];
+                rec[6 * j + 1] = s.par_steps[a];
+                rec[6 * j + 2] = s.par_nact[a];
+                rec[6 * j + 3] = s.full[a];
+                rec[6 * j + 4] = s.nact[a];
             }
     }
     out[0] = tot.qps;

@@ -319,6 +319,33 @@ def test_gpu_exhaustive_equals_bnb(gpu_available):
 
 
 @pytest.mark.gpu
+def test_gpu_early_stop_keeps_the_search(gpu_available, monkeypatch):
+    """The dual-bound early stop (hvp_cent.h solve, GI_CUT) only ends QPs the search prunes anyway:
+    with and without it (HVP_CENT_CUT=0) the same regions, costs, trajectories and QP counts at
+    configs[1]'s platoon size (n = 10, N = 5), and fewer active-set iterations with it."""
+    from hvp import tables
+    from hvp.cent import CentSolver, cent_problem
+    from hvp.models import PwaGearVehicle
+
+    veh = PwaGearVehicle(800)
+    st = tables.system_from_dict(veh.get_discrete_system(1), tables.gears_of(veh))
+    n, N, P = 10, 5, 24
+    x0 = np.stack([O.env_initial_state(n, 300 + p).astype(float).reshape(n, 2) for p in range(P)])
+    a = CentSolver(cent_problem(N), [st]).solve(np.zeros((P, n), np.int32), x0, leader_window(N))
+    monkeypatch.setenv("HVP_CENT_CUT", "0")
+    b = CentSolver(cent_problem(N), [st]).solve(np.zeros((P, n), np.int32), x0, leader_window(N))
+    assert (a.status == 0).all() and (b.status == 0).all(), (a.status, b.status)
+    for k in ("region", "gear"):
+        assert np.array_equal(getattr(a, k), getattr(b, k)), k
+    # a search past 1000 QPs splits into tasks sharing one incumbent: its QP count follows their timing
+    seq = (a.nodes <= 1000) & (b.nodes <= 1000)
+    assert seq.sum() >= P // 2 and np.array_equal(a.nodes[seq], b.nodes[seq])
+    assert np.allclose(a.cost, b.cost, rtol=1e-12, atol=0)
+    assert np.abs(a.u - b.u).max() <= 1e-9 and np.abs(a.x - b.x).max() <= 1e-9
+    assert a.iters.sum() < b.iters.sum(), (a.iters.sum(), b.iters.sum())
+
+
+@pytest.mark.gpu
 def test_gpu_c2_size_properties(gpu_available):
     """configs[1] platoon size (n = 10, N = 5): every platoon optimal, deterministic, and the
     returned trajectory follows the PWA dynamics of the returned regions inside the boxes."""
