@@ -101,10 +101,10 @@ __device__ inline void cent_write(int p, hvp::cent::Lane& L, const hvp::Consts& 
     }
 }
 
-__global__ __launch_bounds__(64) void k_cent_init(int P, hvp::cent::PlatoonRec* rec) {
+__global__ __launch_bounds__(64) void k_cent_init(int P, hvp::cent::PlatoonRec* rec, double inc0) {
     const int p = blockIdx.x * 64 + threadIdx.x;
     if (p >= P) return;
-    rec[p].inc_key = ~0ull;
+    rec[p].inc_key = inc0 < 1e300 ? hvp::cent::ckey(inc0) : ~0ull;
     rec[p].fail_key = ~0ull;
     rec[p].nodes = rec[p].iters = 0;
     rec[p].tie_count = 0;
@@ -380,7 +380,10 @@ int hvp_cent_solve_batch(hvp_handle* h, int P, int n, int leader_index, int real
     if (const char* b = std::getenv("HVP_CENT_SPLIT")) ws.budget = std::atoi(b);  // 0: never split
     Epilogue E{u_out, x_out, region_out, gear_out, cost_out, status_out, nodes_out, iters_out, h->g_counter};
     HIP_TRY(hipMemsetAsync(cnt, 0, 8 * sizeof(unsigned long long), st));
-    hipLaunchKernelGGL(k_cent_init, dim3((P + 63) / 64), dim3(64), 0, st, P, ws.rec);
+    // diagnostics (HVP_CENT_INC, split searches only): every platoon starts from this incumbent
+    const char* ie = std::getenv("HVP_CENT_INC");
+    const double inc0 = ie && ie[0] && ws.budget > 0 ? std::atof(ie) : 1e300;
+    hipLaunchKernelGGL(k_cent_init, dim3((P + 63) / 64), dim3(64), 0, st, P, ws.rec, inc0);
     HIP_TRY(hipEventRecord(h->ev0, st));
     HIP_TRY(hipEventRecord(h->evq0, st));
     ws.out = lists[0];

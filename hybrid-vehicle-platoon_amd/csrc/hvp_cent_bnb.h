@@ -325,6 +325,10 @@ __device__ inline void bnb_platoon(Lane& L, const Lds& S, const Consts& C, const
             }
         }
         have_best = true;
+        if (I.debug == 6 && t == 0 && cost < inc + 1e-9 * fmax(1.0, fabs(inc)))
+            printf("[cent-inc] platoon %d task %d QPs %d (platoon: %llu in finished tasks) leaf cost %.9e\n",
+                   sp ? sp->p : (int)blockIdx.x, sp && sp->mode == 2 ? 1 : 0, nodes,
+                   sp ? __atomic_load_n(&sp->rec->nodes, __ATOMIC_RELAXED) : 0ull, cost);
         if (sp && t == 0) atomicMin(&sp->rec->inc_key, ckey(cost));
     };
     // split searches: this search's leaves, counters and flags into the platoon's record
