@@ -58,8 +58,9 @@ struct Workspace {
                                                  // instance (decentralised branch and bound, N <= 8)
     const int8_t* hint = nullptr;                // [B][N] regions of a previous solve of the same
                                                  // instances (hvp_set_region_hint; ADMM form only)
-    int split = 0;                               // 1: level lists in two halves (hvp_lane.h LevelList;
-                                                 // set per launch for the decentralised lane path)
+    int split = 1;                               // buckets per level list (hvp_lane.h LevelList; > 1
+                                                 // per launch for the decentralised lane path)
+    int split_shift = 0;                         // log2(split): a bucket's segment is cap >> split_shift
 };
 
 
@@ -79,7 +80,7 @@ struct hvp_handle {
     int last_B = 0;
     bool bnb = false;       // search method resolved at hvp_create (HVP_METHOD_*)
     bool last_bnb = false;
-    bool last_split = false;  // the last B&B solve kept its level lists in two halves (Workspace::split)
+    int last_split = 1;  // buckets of the last B&B solve's level lists (Workspace::split)
     int n_cu = 256;
     // host-pointer entry point staging (grown on demand)
     size_t stage_bytes = 0;

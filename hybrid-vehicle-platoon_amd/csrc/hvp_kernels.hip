@@ -362,7 +362,7 @@ int hvp_reserve(hvp_handle* h, int max_batch, int64_t cap) {
              hipMalloc(&w.key, sizeof(unsigned long long) * max_batch) == hipSuccess &&
              hipMalloc(&w.nodes, sizeof(int32_t) * max_batch) == hipSuccess &&
              hipMalloc(&w.iters, sizeof(int32_t) * max_batch) == hipSuccess &&
-             hipMalloc(&w.lvl, sizeof(unsigned long long) * 3 * (HVP_MAX_N + 1)) == hipSuccess;
+             hipMalloc(&w.lvl, sizeof(unsigned long long) * 6 * (HVP_MAX_N + 1)) == hipSuccess;  // hvp_lane.h LevelList
         // K_inst_prep's per-instance QP part: H (NT) + f (N) + hf, hb (N - 1 each)
         if (ok && N <= HVP_MAX_N_ENUM)
             ok = hipMalloc(&w.iq, sizeof(double) * (size_t)max_batch * (N * (N + 1) / 2 + 3 * N - 2)) == hipSuccess;
@@ -589,15 +589,18 @@ int hvp_get_stats(hvp_handle* h, hvp_stats* out) {
     out->n_failed_bounds = (int64_t)c[4];
     if (h->last_bnb) {
         // tree nodes solved: root + dive QPs (counter[3]) and every level's nodes
-        // (the decentralised lane path keeps each level in two halves of the capacity: the second
-        // half's counts follow the claim counters, hvp_lane.h LevelList)
-        unsigned long long lv[3 * (HVP_MAX_N + 1)];
+        // (the decentralised lane path keeps each level in `last_split` segments of the capacity;
+        // bucket b > 0 counts at (1 + b)(HVP_MAX_N + 1), hvp_lane.h LevelList)
+        constexpr int M = HVP_MAX_N + 1;
+        unsigned long long lv[6 * M];
         HIP_TRY(hipMemcpy(lv, h->ws.lvl, sizeof(lv), hipMemcpyDeviceToHost));
         int64_t n = (int64_t)c[3];
         const unsigned long long cap = (unsigned long long)h->ws.cap;
-        const unsigned long long half = h->last_split ? cap / 2 : cap;
+        const int nb = std::max(1, h->last_split);
+        const unsigned long long seg = cap >> (nb == 4 ? 2 : (nb == 2 ? 1 : 0));
         for (int k = 1; k <= h->prob.N; ++k)
-            n += (int64_t)(std::min(lv[k], half) + std::min(lv[2 * (HVP_MAX_N + 1) + k], cap - half));
+            for (int b = 0; b < nb; ++b)
+                n += (int64_t)std::min(b == 0 ? lv[k] : lv[(1 + b) * M + k], b + 1 < nb ? seg : cap - (nb - 1) * seg);
         out->n_candidates = n;
         // QP time = K_bnb_root + every K_bnb_bound launch (the expand / select kernels excluded)
         float sum = 0.f;

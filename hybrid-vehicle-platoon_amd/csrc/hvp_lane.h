@@ -802,51 +802,90 @@ __device__ inline unsigned long long wave_reserve(unsigned long long* counter, i
 }
 
 // Level lists of the decentralised lane path (k_bnb_root, k_bnb_bound_refill; Workspace::split)
-// are kept in two halves of the capacity: the children of a parent whose QP took fewer than
-// kSlowSteps active-set steps fill [0, cap/2), the others [cap/2, cap).  A child's step count
+// are kept in `split` equal segments of the capacity (buckets), by the active-set step count of
+// the parent's QP: 2 buckets split at 6 steps, 4 buckets at 4 / 6 / 8.  A child's step count
 // follows its parent's (correlation 0.84 at C2, profiles/diag_dualstop.cpp), and the refill
-// kernel claims the first half before the second, so its 64-node generations -- as long as their
-// slowest lane -- hold QPs of similar length.  The order of a level's nodes changes nothing else:
-// the incumbent only moves at the leaves, where the tie rule is order-free.  Every other path
-// keeps one list over the whole capacity (split = 0: nb = 0, slot(c) = c).
-#ifndef HVP_SLOW_STEPS
-#define HVP_SLOW_STEPS 6
+// kernel claims bucket 0 before bucket 1 and so on, so its 64-node generations -- as long as
+// their slowest lane -- hold QPs of similar length.  The order of a level's nodes changes nothing
+// else: the incumbent only moves at the leaves, where the tie rule is order-free.  Every other
+// path keeps one list over the whole capacity (split = 1: slot(c) = c).
+constexpr int kMaxBuckets = 4;
+#ifndef HVP_BUCKETS
+#define HVP_BUCKETS 2
 #endif
-constexpr int kSlowSteps = HVP_SLOW_STEPS;
-constexpr int kLvlBack = 2 * (HVP_MAX_N + 1);  // ws.lvl[kLvlBack + k]: nodes of level k's second half
+constexpr int kDefaultBuckets = HVP_BUCKETS;
+constexpr int kLvlM = HVP_MAX_N + 1;  // ws.lvl: [0, M) bucket-0 counts, [M, 2M) claims, [(1 + b) M, (2 + b) M) bucket b
+__device__ inline int bucket_of(int nb, int steps) {
+    return nb == 2 ? (steps >= 6 ? 1 : 0) : (nb == 4 ? (steps >= 4) + (steps >= 6) + (steps >= 8) : 0);
+}
+__device__ inline unsigned long long* bucket_count(const Workspace& ws, int b, int k) {
+    return b == 0 ? &ws.lvl[k] : &ws.lvl[(1 + b) * kLvlM + k];
+}
 
 struct LevelList {
-    unsigned long long nf, nb, half;
-    __device__ long long count() const { return (long long)(nf + nb); }
+    unsigned long long n[kMaxBuckets];  // nodes per bucket (clamped to the segment)
+    unsigned long long seg;             // segment size, cap / split
+    int nb;
+    __device__ long long count() const {
+        unsigned long long c = 0;
+        for (int b = 0; b < nb; ++b) c += n[b];
+        return (long long)c;
+    }
     __device__ long long slot(long long c) const {
-        return c < (long long)nf ? c : (long long)half + (c - (long long)nf);
+        for (int b = 0; b + 1 < nb; ++b) {
+            if (c < (long long)n[b]) return (long long)(b * seg) + c;
+            c -= (long long)n[b];
+        }
+        return (long long)((nb - 1) * seg) + c;
     }
 };
 __device__ inline LevelList level_list(const Workspace& ws, int k) {
-    const unsigned long long cap = (unsigned long long)ws.cap;
     LevelList L;
-    L.half = ws.split ? cap / 2 : cap;
-    const unsigned long long a = ws.lvl[k], b = ws.split ? ws.lvl[kLvlBack + k] : 0ull;
-    L.nf = a < L.half ? a : L.half;
-    L.nb = b < cap - L.half ? b : cap - L.half;
+    L.nb = ws.split > 1 ? ws.split : 1;
+    L.seg = (unsigned long long)ws.cap >> ws.split_shift;
+    for (int b = 0; b < kMaxBuckets; ++b) {
+        const unsigned long long v = b < L.nb ? *bucket_count(ws, b, k) : 0ull;
+        const unsigned long long lim = b + 1 < L.nb ? L.seg : (unsigned long long)ws.cap - (L.nb - 1) * L.seg;
+        L.n[b] = v < lim ? v : lim;
+    }
     return L;
 }
 
-// reserves nc slots per lane of level lv in the half the lane's parent belongs to (slow: its QP
-// took >= kSlowSteps steps); returns the lane's first slot and the end of its half
-__device__ inline unsigned long long split_reserve(Workspace& ws, int lv, int nc, bool slow, int lane,
+// wave-level reservation of nc slots per lane of level lv in the bucket of the lane's parent
+// (its QP took `steps` active-set steps): one packed scan of the per-bucket counts, one atomic per
+// non-empty bucket by the last lane.  Returns the lane's first slot and the end of its segment.
+__device__ inline unsigned long long split_reserve(Workspace& ws, int lv, int nc, int steps, int lane,
                                                    unsigned long long& limit) {
     const unsigned long long cap = (unsigned long long)ws.cap;
-    if (!ws.split) {
+    if (ws.split <= 1) {
         bool any;
         limit = cap;
         return wave_reserve(&ws.lvl[lv], nc, lane, any);
     }
-    bool any0, any1;
-    const unsigned long long o0 = wave_reserve(&ws.lvl[lv], slow ? 0 : nc, lane, any0);
-    const unsigned long long o1 = wave_reserve(&ws.lvl[kLvlBack + lv], slow ? nc : 0, lane, any1);
-    limit = slow ? cap : cap / 2;
-    return slow ? cap / 2 + o1 : o0;
+    const int nb = ws.split;
+    const unsigned long long seg = cap >> ws.split_shift;
+    const int b = bucket_of(nb, steps);
+    unsigned long long incl = (unsigned long long)nc << (16 * b);  // <= 64 lanes x 16 children per field
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const unsigned long long v = ((unsigned long long)(unsigned)__shfl_up((int)(incl >> 32), off, 64) << 32) |
+                                     (unsigned)__shfl_up((int)(incl & 0xffffffffu), off, 64);
+        if (lane >= off) incl += v;
+    }
+    unsigned long long base[kMaxBuckets] = {0ull, 0ull, 0ull, 0ull};
+    if (lane == 63)
+        for (int j = 0; j < nb; ++j) {
+            const unsigned long long tot = (incl >> (16 * j)) & 0xffffull;
+            if (tot) base[j] = atomicAdd(bucket_count(ws, j, lv), tot);
+        }
+    unsigned long long mine = 0;
+    for (int j = 0; j < nb; ++j) {
+        const unsigned long long bj = ((unsigned long long)(unsigned)__shfl((int)(base[j] >> 32), 63, 64) << 32) |
+                                      (unsigned)__shfl((int)(base[j] & 0xffffffffu), 63, 64);
+        mine = j == b ? bj : mine;
+    }
+    limit = b + 1 < nb ? (b + 1) * seg : cap;
+    return (unsigned long long)b * seg + mine + ((incl >> (16 * b)) & 0xffffull) - (unsigned long long)nc;
 }
 
 // The region sequence of hvp_set_region_hint for instance i as a leaf code, if every step is a
@@ -894,7 +933,7 @@ __global__ __launch_bounds__(kBnbBlock<N>) HVP_LANE_OCC void k_bnb_root(int B, c
     ws.nd_hi[0][i] = v0;
     double inc = __longlong_as_double(0x7ff0000000000000ll);  // +inf: no incumbent
     double lb = -1e300;
-    int nodes = 0, iters = 0, iters_root = 0;
+    int nodes = 0, iters = 0;
     if (ok) {
         hvp::LaneQp<N, LdsMem<N, BS>> q;
         q.mem.lane = threadIdx.x;
@@ -902,7 +941,6 @@ __global__ __launch_bounds__(kBnbBlock<N>) HVP_LANE_OCC void k_bnb_root(int B, c
         int it = bnb_qp<N, BS, ADMM>(q, S, C, rl, prm, 0, 0, v0, v0, c0);
         ++nodes;
         iters += it >= 0 ? it : -1 - it;
-        iters_root = it >= 0 ? it : -1 - it;
         if (it >= 0) {
             lb = c0;
             double ystar[N];
@@ -941,13 +979,11 @@ __global__ __launch_bounds__(kBnbBlock<N>) HVP_LANE_OCC void k_bnb_root(int B, c
         if (ok && !hvp::bnb_pruned(lb, inc)) {
             const unsigned mask = bnb_children(S, C, 0, v0, v0);
             if (mask) {
-                const int root_steps = iters_root;
-                const bool slow = ws.split && root_steps >= kSlowSteps;
-                const unsigned long long cap = (unsigned long long)ws.cap;
-                const unsigned long long off =
-                    slow ? cap / 2 + atomicAdd(&ws.lvl[kLvlBack + 1], (unsigned long long)__popc(mask))
-                         : atomicAdd(&ws.lvl[1], (unsigned long long)__popc(mask));
-                bnb_put_children(ws, 1, off, slow || !ws.split ? cap : cap / 2, mask, i, S, C, 0, v0, v0, lb);
+                // the root's children all go to bucket 0 (LevelList; level 1 is the smallest level,
+                // and a bucket choice here measured 3x slower in this kernel: r03v)
+                const unsigned long long off = atomicAdd(&ws.lvl[1], (unsigned long long)__popc(mask));
+                bnb_put_children(ws, 1, off, (unsigned long long)ws.cap >> ws.split_shift, mask, i, S, C, 0, v0,
+                                 v0, lb);
             }
         }
     }
@@ -1541,7 +1577,7 @@ void k_bnb_bound_refill(int k, const hvp_system* __restrict__ systems, const int
             if (k < N) {
                 unsigned long long limit;
                 const unsigned long long off =
-                    split_reserve(ws, k + 1, __popc(cmask), done && g.iter >= kSlowSteps, lane, limit);
+                    split_reserve(ws, k + 1, __popc(cmask), done ? g.iter : 0, lane, limit);
                 if (cmask)
                     bnb_put_children(ws, k + 1, off, limit, cmask, inst, systems[sys[inst]], C, code,
                                      ws.nd_lo[dst][t], ws.nd_hi[dst][t], clb);
@@ -1646,10 +1682,10 @@ template <int N>
 __global__ __launch_bounds__(kBlock) void k_bnb_key(Workspace ws, int form, int l1) {
     const int src = N & 1;
     const LevelList lvl = level_list(ws, N);
-    const long long total = lvl.count();
-    for (long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x; c < total;
+    for (int b = 0; b < lvl.nb; ++b)
+    for (long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x; c < (long long)lvl.n[b];
          c += (long long)gridDim.x * blockDim.x) {
-        const long long t = lvl.slot(c);
+        const long long t = (long long)(b * lvl.seg) + c;
         const int inst = ws.nd_inst[src][t];
         if (inst < 0) continue;
         const double best = inc_of(ws, inst);
@@ -1736,10 +1772,10 @@ __global__ __launch_bounds__(kBlock) void k_bnb_write(const hvp_system* __restri
                                                       double* __restrict__ xb_out) {
     const int src = N & 1;
     const LevelList lvl = level_list(ws, N);
-    const long long total = lvl.count();
-    for (long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x; c < total;
+    for (int b = 0; b < lvl.nb; ++b)
+    for (long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x; c < (long long)lvl.n[b];
          c += (long long)gridDim.x * blockDim.x) {
-        const long long t = lvl.slot(c);
+        const long long t = (long long)(b * lvl.seg) + c;
         if (ws.leaf_stat[t] != 0) continue;
         const int inst = ws.nd_inst[src][t];
         if (inst < 0) continue;
@@ -2075,11 +2111,13 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
     // kernel of the level above (fused expand) and keeps each level in two halves (LevelList);
     // the other paths run k_bnb_expand per level over one list
     const bool fused = !kCoop<N> && h->C.form == HVP_FORM_DECENT && !h->C.l1;
-    const char* sp = std::getenv("HVP_SPLIT_LEVELS");  // "0": one list (A/B runs)
-    ws.split = fused && !(sp && sp[0] == '0') ? 1 : 0;
-    h->last_split = ws.split != 0;
+    const char* sp = std::getenv("HVP_SPLIT_LEVELS");  // buckets per level list: 1 (one list), 2, 4 (A/B runs)
+    const int want = sp && sp[0] ? std::atoi(sp) : kDefaultBuckets;
+    ws.split = fused ? (want >= 4 ? 4 : (want >= 2 ? 2 : 1)) : 1;
+    ws.split_shift = ws.split == 4 ? 2 : (ws.split == 2 ? 1 : 0);
+    h->last_split = ws.split;
     HIP_TRY(hipMemsetAsync(ws.counter, 0, 8 * sizeof(unsigned long long), st));
-    HIP_TRY(hipMemsetAsync(ws.lvl, 0, 3 * (HVP_MAX_N + 1) * sizeof(unsigned long long), st));  // + claims, halves
+    HIP_TRY(hipMemsetAsync(ws.lvl, 0, (2 + kMaxBuckets) * (HVP_MAX_N + 1) * sizeof(unsigned long long), st));  // + claims, buckets
     HIP_TRY(hipEventRecord(h->ev0, st));
     HIP_TRY(hipEventRecord(h->evq0, st));
     const size_t lds = sizeof(double) * hvp::F_COUNT * N * BS;
