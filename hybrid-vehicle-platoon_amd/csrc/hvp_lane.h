@@ -826,23 +826,32 @@ struct LevelList {
     unsigned long long n[kMaxBuckets];  // nodes per bucket (clamped to the segment)
     unsigned long long seg;             // segment size, cap / split
     int nb;
+    // (loops over the static kMaxBuckets: a runtime-indexed n[] would live in scratch)
     __device__ long long count() const {
         unsigned long long c = 0;
-        for (int b = 0; b < nb; ++b) c += n[b];
+#pragma unroll
+        for (int b = 0; b < kMaxBuckets; ++b) c += n[b];  // n[b] = 0 for b >= nb
         return (long long)c;
     }
     __device__ long long slot(long long c) const {
-        for (int b = 0; b + 1 < nb; ++b) {
-            if (c < (long long)n[b]) return (long long)(b * seg) + c;
+        long long t = c, base = 0;
+        bool found = false;
+#pragma unroll
+        for (int b = 0; b < kMaxBuckets; ++b) {
+            const bool here = !found && (b + 1 >= nb || c < (long long)n[b]);
+            t = here ? base + c : t;
+            found = found || here;
             c -= (long long)n[b];
+            base += (long long)seg;
         }
-        return (long long)((nb - 1) * seg) + c;
+        return t;
     }
 };
 __device__ inline LevelList level_list(const Workspace& ws, int k) {
     LevelList L;
     L.nb = ws.split > 1 ? ws.split : 1;
     L.seg = (unsigned long long)ws.cap >> ws.split_shift;
+#pragma unroll
     for (int b = 0; b < kMaxBuckets; ++b) {
         const unsigned long long v = b < L.nb ? *bucket_count(ws, b, k) : 0ull;
         const unsigned long long lim = b + 1 < L.nb ? L.seg : (unsigned long long)ws.cap - (L.nb - 1) * L.seg;
@@ -873,13 +882,16 @@ __device__ inline unsigned long long split_reserve(Workspace& ws, int lv, int nc
         if (lane >= off) incl += v;
     }
     unsigned long long base[kMaxBuckets] = {0ull, 0ull, 0ull, 0ull};
-    if (lane == 63)
-        for (int j = 0; j < nb; ++j) {
+    if (lane == 63) {
+#pragma unroll
+        for (int j = 0; j < kMaxBuckets; ++j) {
             const unsigned long long tot = (incl >> (16 * j)) & 0xffffull;
-            if (tot) base[j] = atomicAdd(bucket_count(ws, j, lv), tot);
+            if (j < nb && tot) base[j] = atomicAdd(bucket_count(ws, j, lv), tot);
         }
+    }
     unsigned long long mine = 0;
-    for (int j = 0; j < nb; ++j) {
+#pragma unroll
+    for (int j = 0; j < kMaxBuckets; ++j) {
         const unsigned long long bj = ((unsigned long long)(unsigned)__shfl((int)(base[j] >> 32), 63, 64) << 32) |
                                       (unsigned)__shfl((int)(base[j] & 0xffffffffu), 63, 64);
         mine = j == b ? bj : mine;
@@ -1682,7 +1694,8 @@ template <int N>
 __global__ __launch_bounds__(kBlock) void k_bnb_key(Workspace ws, int form, int l1) {
     const int src = N & 1;
     const LevelList lvl = level_list(ws, N);
-    for (int b = 0; b < lvl.nb; ++b)
+#pragma unroll
+    for (int b = 0; b < kMaxBuckets; ++b)
     for (long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x; c < (long long)lvl.n[b];
          c += (long long)gridDim.x * blockDim.x) {
         const long long t = (long long)(b * lvl.seg) + c;
@@ -1772,7 +1785,8 @@ __global__ __launch_bounds__(kBlock) void k_bnb_write(const hvp_system* __restri
                                                       double* __restrict__ xb_out) {
     const int src = N & 1;
     const LevelList lvl = level_list(ws, N);
-    for (int b = 0; b < lvl.nb; ++b)
+#pragma unroll
+    for (int b = 0; b < kMaxBuckets; ++b)
     for (long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x; c < (long long)lvl.n[b];
          c += (long long)gridDim.x * blockDim.x) {
         const long long t = (long long)(b * lvl.seg) + c;
