@@ -45,17 +45,35 @@ def instance_io_bytes(N: int) -> int:
     return 8 * (2 + 6 * (N + 1) + N + 2 * (N + 1) + 1) + N
 
 
+def loaded_lib_sha() -> str:
+    """SHA-256 of the libhvpsolve.so this process loads (HVP_LIB or the in-tree build)."""
+    from hvp import _abi
+
+    return _abi.lib_sha256()
+
+
 def profiled(kernel: str, tag: str):
     """Per-launch PMC figures of `kernel` from the newest committed profiles/r*_<tag>_summary.json
-    (profiles/run_profiles.sh runs this bench's workload `tag` under rocprofv3)."""
+    whose ``lib_sha256`` stamp is the library this process loads (profiles/run_profiles.sh runs
+    this bench's workload `tag` under rocprofv3 and stamps the summary with the library's hash).
+    A summary of another build is never used: (None, reason) instead."""
     import glob
 
+    sha = loaded_lib_sha()
+    stale = None
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{tag}_summary.json")), reverse=True):
         with open(path) as f:
-            d = json.load(f)["kernels"].get(kernel)
-        if d:
-            return d, os.path.relpath(path, ROOT)
-    return None, None
+            meta = json.load(f)
+        d = meta["kernels"].get(kernel)
+        if not d:
+            continue
+        if meta.get("lib_sha256") != sha:
+            stale = stale or os.path.relpath(path, ROOT)
+            continue
+        return d, os.path.relpath(path, ROOT)
+    why = (f"newest profile of this workload ({stale}) is of another build of libhvpsolve.so" if stale
+           else f"no committed profile of workload {tag}")
+    return None, why
 
 
 def qp_roofline(qp_step_ms: float, kernels: list, notional_bytes: float, tag: str) -> dict:
@@ -72,10 +90,11 @@ def qp_roofline(qp_step_ms: float, kernels: list, notional_bytes: float, tag: st
                      labelled side figure only.
     kernels: [(name, launches per step)]; tag: the profiled workload (profiles/r*_<tag>_summary.json)."""
     flop = flop_all = traffic = 0.0
-    srcs, prof_ms = set(), {}
+    srcs, prof_ms, why = set(), {}, None
     for name, count in kernels:
         d, src = profiled(name, tag)
         if not d or "f64_flop_active" not in d or "hbm_bytes" not in d:
+            why = src if not d else f"{src} lacks the PMC passes of {name}"
             flop = None
             break
         flop += d["f64_flop_active"] * count
@@ -90,8 +109,8 @@ def qp_roofline(qp_step_ms: float, kernels: list, notional_bytes: float, tag: st
            "survey_8d": {"note": "notional dense-QP bytes of SURVEY 8(d), not moved by the kernels",
                          "bytes_per_step": notional_bytes, "GB_per_s": notional_bytes / t / 1e9}}
     if flop is None:
-        out.update({"achieved": None, "frac": None, "traffic": None,
-                    "note": "no committed PMC profile of this workload (profiles/run_profiles.sh)"})
+        out.update({"achieved": None, "frac": None, "traffic": None, "lib_sha256": loaded_lib_sha(),
+                    "note": f"{why}: roofline not reported (profiles/run_profiles.sh profiles this build)"})
         return out
     achieved = flop / t / 1e12
     out.update({"achieved": achieved, "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
@@ -99,7 +118,7 @@ def qp_roofline(qp_step_ms: float, kernels: list, notional_bytes: float, tag: st
                 "frac_all_lanes": flop_all / t / 1e12 / FP64_PEAK_TFLOPS,
                 "hbm": {"achieved": traffic / t / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": traffic / t / 1e9 / HBM_PEAK_GBS},
-                "profile": sorted(srcs), "profile_avg_ms": prof_ms})
+                "profile": sorted(srcs), "profile_avg_ms": prof_ms, "lib_sha256": loaded_lib_sha()})
     return out
 
 
@@ -371,8 +390,10 @@ def bench_admm(args, world: int, rank: int, local: int, dist) -> None:
     step(args.warmup + args.steps, on_solve=on_solve)
     value = S * world * args.steps / dt
     notional = acc["qps"] * dense_qp_bytes(N) + iters * n * S * instance_io_bytes(N)
-    qk = ([("k_bnb_root_coop", iters), ("k_bnb_bound_coop", iters * N)] if N > 8
-          else [("k_bnb_root", iters), ("k_bnb_bound", iters * N)])
+    # per-launch PMC figures of one engine's launches (profile: --streams 1 --platoons S/K); the
+    # event pass above ran the K engines one after the other, so acc["qp_ms"] is their summed time
+    qk = ([("k_bnb_root_coop", iters * K), ("k_bnb_bound_coop", iters * N * K)] if N > 8
+          else [("k_bnb_root", iters * K), ("k_bnb_bound", iters * N * K)])
     result = {
         "metric": f"MPC timesteps/sec (whole platoon) at n={n} N={N} naive_admm ({iters} ADMM iterations)",
         "value": value, "unit": "platoon-timesteps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -384,7 +405,7 @@ def bench_admm(args, world: int, rank: int, local: int, dist) -> None:
                    "horizon": N, "admm_iters": iters, "rho": 0.5, "platoons_per_gpu": S,
                    "local_miqps_per_step": iters * n * S * world, "warm_incumbent": N > 8 and not args.no_warm_incumbent,
                    "streams_per_gpu": K, "parallelism": f"seeds-sharded x{world}"},
-        "roofline": qp_roofline(acc["qp_ms"] if K == 1 else dt / args.steps * 1e3, qk, notional, f"admm_n{n}_N{N}"),
+        "roofline": qp_roofline(acc["qp_ms"], qk, notional, f"admm_n{n}_N{N}_P{S // K}"),
         "qps_per_step": acc["qps"], "qp_iters_per_qp": acc["it"] / max(acc["qps"], 1),
         "not_optimal_total": int(notopt.item()), "plant_failures_total": int(bad.item()),
     }
@@ -546,8 +567,10 @@ def bench_gadmm(args, world: int, rank: int, local: int, dist) -> None:
                    "streams_per_gpu": K,
                    "parallelism": (f"vehicles-sharded x{world} (RCCL halo send/recv per ADMM iteration)" if sharded
                                    else f"seeds-sharded x{world} (replicas, no collective)")},
-        "roofline": qp_roofline(qp_avg * n_qp_launch if K == 1 else dt / args.steps * 1e3, [("k_gadmm_qp_coop" if N > 8 else "k_gadmm_qp", n_qp_launch)],
-                                notional, f"gadmm_n{n}_N{N}"),
+        # the engines' QP launches timed one engine after the other (HIP events on the launch
+        # stream); per-launch PMC figures of one engine (profile: --streams 1 --platoons S/K)
+        "roofline": qp_roofline(qp_avg * n_qp_launch, [("k_gadmm_qp_coop" if N > 8 else "k_gadmm_qp", n_qp_launch)],
+                                notional, f"gadmm_n{n}_N{N}_P{S // K}"),
         "admm_rounds_per_step": rounds / args.steps, "qp_launches_per_step": launches / args.steps,
         "all_feasible": ok,
     }
@@ -764,11 +787,19 @@ def bench_cent(args, world: int, rank: int, local: int, dist) -> None:
         dt = float(tt.item())
     # kernel time: HIP events the library records around the search kernels on the solve stream
     # (K streams: their searches overlap, so the step's wall time)
+    # kernel time of the roofline: one more step as ONE handle over all S platoons (the launch size
+    # of the committed profile, run_profiles.sh ... --streams 1), HIP events around its kernels
     if K == 1:
         run()
         kernel_ms = solver.stats().last_ms
     else:
-        kernel_ms = dt / args.steps * 1e3
+        sv1 = CentSolver(cent_problem(N), [system], device=local)
+        sv1.solve_device(torch.zeros((S, n), dtype=torch.int32, device=dev), torch.from_numpy(x0).to(dev),
+                         torch.from_numpy(np.ascontiguousarray(np.broadcast_to(lead, (S, 2, N + 1)))).to(dev),
+                         max_nodes=args.max_nodes, out=sv1.alloc_outputs(S, n, dev))
+        torch.cuda.synchronize()
+        kernel_ms = sv1.stats().last_ms
+        del sv1
     qps = int(nodes.sum())
     notional = qps * cent_qp_bytes(n, N) + S * 8 * (2 * n + 2 * (N + 1) + n * (3 * N + 2) + 1)
     n_opt = int((status == 0).sum())
@@ -784,7 +815,7 @@ def bench_cent(args, world: int, rank: int, local: int, dist) -> None:
                    "platoons_per_gpu": S, "max_nodes": args.max_nodes, "streams_per_gpu": K,
                    "parallelism": f"seeds-sharded x{world}"},
         "value_optimal_only": n_opt * world * args.steps / dt,
-        "roofline": qp_roofline(kernel_ms, cent_kernels(f"cent_n{n}_N{N}"), notional, f"cent_n{n}_N{N}"),
+        "roofline": qp_roofline(kernel_ms, cent_kernels(f"cent_n{n}_N{N}_P{S}"), notional, f"cent_n{n}_N{N}_P{S}"),
         "qps_per_step": qps, "qp_iters_per_qp": float(iters.sum()) / max(qps, 1),
         "nodes_per_platoon": {"p50": float(q[0]), "p90": float(q[1]), "p99": float(q[2]), "max": float(q[3])},
         # the heaviest searches of the rank (seed, QPs, status): where the step's time goes
@@ -974,21 +1005,27 @@ def main() -> None:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
 
-    # per-launch kernel time (HIP events recorded by the library on the solve stream around
-    # K_qp_gi) and work counters: a second pass of the same steps, outside the timed region,
-    # since reading them synchronises the stream after every step
-    # (with K streams the chunks are timed one after the other here: qp_ms is their sum)
+    # per-launch kernel time (HIP events recorded by the library on the solve stream around the
+    # QP launches) and work counters: a second pass of the same steps, outside the timed region
+    # (reading them synchronises the stream after every step), as ONE handle over the whole batch
+    # -- the launch size of the committed profile (run_profiles.sh ... --streams 1)
+    if K == 1:
+        ev = chunks[0]
+    else:
+        sv1 = BatchSolver(tables.problem(N, quadratic_cost=quadratic, method=method), [system], device=local)
+        sv1.reserve(B)
+        ev = (sv1, torch.zeros(B, dtype=torch.int32, device=dev), t_roles_all, t_params_all,
+              sv1.alloc_outputs(B, dev), torch.cuda.current_stream(dev))
     qp_ms, cand, iters, fallback = [], 0, 0, 0
     for _ in range(args.steps):
-        t_qp = 0.0
-        for sv, ts, tr, tp, o, stm in chunks:
-            sv.solve_device(ts, tr, tp, o, stream=stm)
-            s = sv.stats()
-            t_qp += s.qp_ms
-            cand += s.n_candidates
-            iters += s.qp_iterations
-            fallback += s.n_fallback
-        qp_ms.append(t_qp)
+        sv, ts, tr, tp, o, stm = ev
+        sv.solve_device(ts, tr, tp, o, stream=stm)
+        s = sv.stats()
+        qp_ms.append(s.qp_ms)
+        cand += s.n_candidates
+        iters += s.qp_iterations
+        fallback += s.n_fallback
+    del ev
 
     steps_total = S * world * args.steps
     value = steps_total / dt
@@ -1005,13 +1042,12 @@ def main() -> None:
                                                                               ("k_bnb_bound_refill", N)]
     else:
         qk = [("k_qp_gi", 1)] if quadratic else [("k_qp_l1", 1)]
-    # the PMC figures are per launch over the WHOLE batch (profiles are taken with --streams 1);
-    # with K streams the K chunks' QP launches overlap, so the time is the step's wall time
-    roofline = qp_roofline(qp_step_ms if K == 1 else dt / args.steps * 1e3, qk, notional,
-                           f"decent_n{n}_N{N}" + ("" if bnb else "_enum") + ("" if quadratic else "_l1"))
-    if K > 1:
-        roofline["time_basis"] = (f"wall time of the step: the QP launches of the {K} streams overlap "
-                                  f"(their sequential event time is {qp_step_ms:.3f} ms)")
+    # the PMC figures are per launch over the WHOLE batch (the profile runs this workload with
+    # --streams 1); qp_step_ms is the HIP-event time of those launches in the one-handle pass
+    roofline = qp_roofline(qp_step_ms, qk, notional,
+                           f"decent_n{n}_N{N}" + ("" if bnb else "_enum") + ("" if quadratic else "_l1") + f"_P{S}")
+    roofline["time_basis"] = (f"HIP events around the QP launches of one handle over all {S} platoons (the timed "
+                              f"region splits them over {K} streams, whose launches overlap)")
 
     result = {
         "metric": f"MPC timesteps/sec (whole platoon) at n={n} N={N} decent_mld" + ("" if quadratic else " min_1_norm"),

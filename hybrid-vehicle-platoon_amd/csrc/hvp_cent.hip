@@ -383,6 +383,12 @@ int hvp_cent_solve_batch(hvp_handle* h, int P, int n, int leader_index, int real
     // diagnostics (HVP_CENT_INC, split searches only): every platoon starts from this incumbent
     const char* ie = std::getenv("HVP_CENT_INC");
     const double inc0 = ie && ie[0] && ws.budget > 0 ? std::atof(ie) : 1e300;
+    if (inc0 < 1e300) {  // a diagnostic that changes answers: never silent
+        static bool said = false;
+        if (!said) std::fprintf(stderr, "[hvp] HVP_CENT_INC=%g: every split search starts from this incumbent "
+                                        "(platoons whose optimum lies above it come back INFEASIBLE)\n", inc0);
+        said = true;
+    }
     hipLaunchKernelGGL(k_cent_init, dim3((P + 63) / 64), dim3(64), 0, st, P, ws.rec, inc0);
     HIP_TRY(hipEventRecord(h->ev0, st));
     HIP_TRY(hipEventRecord(h->evq0, st));

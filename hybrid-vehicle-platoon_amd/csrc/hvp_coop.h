@@ -406,9 +406,11 @@ __device__ inline void row_owner(int id_in, int& lane, int& bit) {
 // that active set.  Next iteration the QP differs only in its linear term and row bounds (the
 // ADMM y, z terms), so with the same code and hinge states the Hessian -- and J, R -- are the
 // same, and the equality-constrained optimum on the old active set is two triangular solves and
-// two N x N products away (warm_start below).
+// two N x N products away (warm_start below).  `key` names the rest of what the Hessian depends
+// on (system index, role bits): a record written for another QP -- a handle called again with a
+// different batch -- never starts this one.
 struct WarmQp {
-    uint64_t code, hs;
+    uint64_t code, hs, key;
     int32_t nact, valid;
     int32_t ids[G];
     double J[G * G];
@@ -546,7 +548,7 @@ __device__ inline bool warm_start(Lane<N>& L, GroupLds& Sg, const Consts& C, con
 template <int N>
 __device__ inline int solve(Lane<N>& L, GroupLds& Sg, const Consts& C, int max_iter, int& iters,
                             unsigned* edge = nullptr, WarmQp* wq = nullptr, uint64_t wcode = 0, uint64_t whs = 0,
-                            bool wtry = false) {
+                            bool wtry = false, uint64_t wkey = 0) {
     const int t = lane16();
     iters = 0;
     double* J = Sg.J;  // holds H on entry (row t written by lane t)
@@ -557,7 +559,7 @@ __device__ inline int solve(Lane<N>& L, GroupLds& Sg, const Consts& C, int max_i
     unsigned act = 0;  // active bits of the rows lane t owns
     gsync();
     bool warmed = false;
-    if (wq && wtry && wq->valid && wq->code == wcode && wq->hs == whs)  // group-uniform
+    if (wq && wtry && wq->valid && wq->code == wcode && wq->hs == whs && wq->key == wkey)  // group-uniform
         warmed = warm_start<N>(L, Sg, C, wq, u, id, act, nact);
     if (!warmed) {
     // ---- Cholesky H = L L' into R area (lower, row-major), column by column
@@ -868,6 +870,7 @@ __device__ inline int solve(Lane<N>& L, GroupLds& Sg, const Consts& C, int max_i
         if (t == 0) {
             wq->code = wcode;
             wq->hs = whs;
+            wq->key = wkey;
             wq->nact = nact;
             wq->valid = keep ? 1 : 0;
         }
@@ -1021,38 +1024,49 @@ __device__ inline uint64_t admm_initial_states(Lane<N>& L, const Consts& C, int 
 // iteration to the next, so the first solve is usually consistent) and its active set / factors
 // start the active-set method (solve); every solve writes the record back.  The fixed point
 // reached is the QP's optimum either way (the Huber pieces are convex and C1, so the states only
-// decide which solve certifies it).
+// decide which solve certifies it).  Should the warm-started run not settle (a solve fails, or the
+// hinge states still change after kHubRounds), the QP is solved once more from the cold start
+// (constant-velocity states, Cholesky of H), so a warm start never fails a QP the cold start solves.
+// wkey: the record's owner key (system index, role bits; WarmQp).
 template <int N>
 __device__ inline int solve_qp(Lane<N>& L, GroupLds& Sg, const hvp_system& S, const Consts& C, int role,
                                const double* prm, uint64_t code, int K, int max_iter, int& iters, double* cost,
                                unsigned* edge = nullptr, double lo = 0.0, double hi = -1.0,
-                               WarmQp* wq = nullptr, bool warm = false) {
+                               WarmQp* wq = nullptr, bool warm = false, uint64_t wkey = 0) {
     iters = 0;
     if (C.form == HVP_FORM_ADMM || C.form == HVP_FORM_GADMM) {
-        uint64_t hs;
-        if (wq && warm && wq->valid) {
-            hs = wq->hs;  // one address for the whole group
-        } else {
-            // lane data for the classification helpers
-            Lane<N> L0;
-            setup<N>(L0, Sg, S, C, role, prm, code, K, 0);
-            hs = admm_initial_states<N>(L0, C, role, prm);
-        }
-        for (int round = 0; round < kHubRounds; ++round) {
-            gsync();
-            setup<N>(L, Sg, S, C, role, prm, code, K, hs);
-            int it = 0;
-            const int st = solve<N>(L, Sg, C, max_iter, it, edge, wq, code, hs, warm);
-            iters += it;
-            if (st != GI_OK) return st;
-            bool consistent;
-            hs = admm_classify_group<N>(L, C, role, prm, hs, &consistent);
-            if (consistent) {
-                *cost = direct_cost_admm<N>(L, S, C, role, prm, code, K);
-                return GI_OK;
+        bool w = wq && warm && wq->valid && wq->key == wkey;  // group-uniform (one address per group)
+        int st = GI_FAIL_ITER;
+        for (int attempt = 0; attempt < 2; ++attempt) {
+            uint64_t hs;
+            if (w) {
+                hs = wq->hs;
+            } else {
+                // lane data for the classification helpers
+                Lane<N> L0;
+                setup<N>(L0, Sg, S, C, role, prm, code, K, 0);
+                hs = admm_initial_states<N>(L0, C, role, prm);
             }
+            st = GI_FAIL_ITER;
+            for (int round = 0; round < kHubRounds; ++round) {
+                gsync();
+                setup<N>(L, Sg, S, C, role, prm, code, K, hs);
+                int it = 0;
+                st = solve<N>(L, Sg, C, max_iter, it, edge, wq, code, hs, w, wkey);
+                iters += it;
+                if (st != GI_OK) break;
+                bool consistent;
+                hs = admm_classify_group<N>(L, C, role, prm, hs, &consistent);
+                if (consistent) {
+                    *cost = direct_cost_admm<N>(L, S, C, role, prm, code, K);
+                    return GI_OK;
+                }
+                st = GI_FAIL_ITER;
+            }
+            if (!w) break;  // the cold start was the last resort
+            w = false;
         }
-        return GI_FAIL_ITER;
+        return st;
     }
     gsync();
     setup<N>(L, Sg, S, C, role, prm, code, K, 0, lo, hi);

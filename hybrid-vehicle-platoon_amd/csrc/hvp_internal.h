@@ -58,6 +58,19 @@ struct Workspace {
                                                  // instance (decentralised branch and bound, N <= 8)
     const int8_t* hint = nullptr;                // [B][N] regions of a previous solve of the same
                                                  // instances (hvp_set_region_hint; ADMM form only)
+    // the greedy dive's leaf of every instance (decentralised lane path, N <= 8): a node list of
+    // its own, solved by the refill kernel after the root level (hvp_lane.h launch_bnb)
+    int32_t* dv_inst = nullptr;                  // [max_batch] instance (-1: no dive)
+    uint64_t* dv_code = nullptr;                 // [max_batch] the dive's sequence
+    double* dv_lo = nullptr;                     // [max_batch] (unused at K = N: 0)
+    double* dv_hi = nullptr;                     // [max_batch] (-1)
+    double* dv_lb = nullptr;                     // [max_batch] leaf cost
+    int32_t* dv_stat = nullptr;                  // [max_batch]
+    double* dv_y = nullptr;                      // [max_batch * N]
+    int32_t* dv_redo = nullptr;                  // [max_batch] (failed dives are not re-solved)
+    unsigned long long* dv_lvl = nullptr;        // [(2 + 4)(HVP_MAX_N + 1)] counts / claims of the dive list
+    unsigned long long* dv_counter = nullptr;    // [8]
+    char* dv_mem = nullptr;                      // the allocation the dv_* arrays live in
     int split = 1;                               // buckets per level list (hvp_lane.h LevelList; > 1
                                                  // per launch for the decentralised lane path)
     int split_shift = 0;                         // log2(split): a bucket's segment is cap >> split_shift
@@ -100,4 +113,10 @@ struct hvp_handle {
     int gadmm_hs_valid = 0;
     char* cent_split = nullptr;
     const int8_t* region_hint = nullptr;  // hvp_set_region_hint (copied into ws.hint per solve)
+    // device copies of the workspace descriptors the refill kernel reads in its event code
+    // (hvp_lane.h k_bnb_bound_refill): [0] the level lists, [1] the dive list; re-uploaded when
+    // they change (a reserve, another bucket split)
+    hvp_detail::Workspace* d_ws = nullptr;
+    hvp_detail::Workspace ws_up[2];
+    bool ws_up_valid = false;
 };

@@ -66,6 +66,12 @@ hvp::Consts make_consts(const hvp_problem& p) {
     C.l1 = p.quadratic_cost ? 0 : 1;
     const char* lc = std::getenv("HVP_LEAF_GI_CAP");
     C.leaf_cap = lc && lc[0] ? std::max(0, std::atoi(lc)) : 0;
+    if (C.leaf_cap > 0) {  // a test knob in the production library: never silent
+        static bool said = false;
+        if (!said) std::fprintf(stderr, "[hvp] HVP_LEAF_GI_CAP=%d: leaf QPs capped at %d active-set steps "
+                                        "(the rest go through the interior-point fallback)\n", C.leaf_cap, C.leaf_cap);
+        said = true;
+    }
     const char* cc = std::getenv("HVP_CENT_CUT");
     C.cent_cut = cc && cc[0] ? (std::atoi(cc) != 0 ? 1 : 0) : 1;
     return C;
@@ -220,6 +226,7 @@ void free_ws(Workspace& w) {
     (void)hipFree(w.iters);
     (void)hipFree(w.lvl);
     (void)hipFree(w.iq);
+    (void)hipFree(w.dv_mem);
     w = Workspace{};
 }
 
@@ -320,6 +327,9 @@ int hvp_create(hvp_handle** out, const hvp_problem* problem, const hvp_system* s
         hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess ||
         hipEventCreate(&h->evq0) != hipSuccess || hipEventCreate(&h->evq1) != hipSuccess ||
         hipMalloc(&h->g_counter, 8 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc(&h->d_consts, sizeof(hvp::Consts)) != hipSuccess ||
+        hipMemcpy(h->d_consts, &h->C, sizeof(hvp::Consts), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMalloc(&h->d_ws, 2 * sizeof(hvp_detail::Workspace)) != hipSuccess ||
         hipMemset(h->g_counter, 0, 8 * sizeof(unsigned long long)) != hipSuccess ||
         !create_events(h->evb, 2 * (HVP_MAX_N + 1))) {
         hvp_destroy(h);
@@ -366,6 +376,27 @@ int hvp_reserve(hvp_handle* h, int max_batch, int64_t cap) {
         // K_inst_prep's per-instance QP part: H (NT) + f (N) + hf, hb (N - 1 each)
         if (ok && N <= HVP_MAX_N_ENUM)
             ok = hipMalloc(&w.iq, sizeof(double) * (size_t)max_batch * (N * (N + 1) / 2 + 3 * N - 2)) == hipSuccess;
+        // the dive list of the lane path (hvp_lane.h launch_bnb): 8-byte fields first
+        if (ok && N <= HVP_MAX_N_ENUM) {
+            constexpr size_t M = HVP_MAX_N + 1;
+            const size_t mb = (size_t)max_batch;
+            const size_t bytes = 8 * (6 * M + 8) + mb * (8 * (4 + N) + 3 * 4);
+            ok = hipMalloc(&w.dv_mem, bytes) == hipSuccess;
+            if (ok) {
+                char* c = w.dv_mem;
+                auto take = [&c](size_t n) { char* r = c; c += n; return r; };
+                w.dv_lvl = (unsigned long long*)take(8 * 6 * M);
+                w.dv_counter = (unsigned long long*)take(8 * 8);
+                w.dv_code = (uint64_t*)take(8 * mb);
+                w.dv_lo = (double*)take(8 * mb);
+                w.dv_hi = (double*)take(8 * mb);
+                w.dv_lb = (double*)take(8 * mb);
+                w.dv_y = (double*)take(8 * mb * N);
+                w.dv_inst = (int32_t*)take(4 * mb);
+                w.dv_stat = (int32_t*)take(4 * mb);
+                w.dv_redo = (int32_t*)take(4 * mb);
+            }
+        }
     }
     if (!ok) {
         free_ws(w);
@@ -696,6 +727,7 @@ void hvp_destroy(hvp_handle* h) {
     if (h->cent_split) (void)hipFree(h->cent_split);
     if (h->gadmm_hs) (void)hipFree(h->gadmm_hs);
     if (h->d_consts) (void)hipFree(h->d_consts);
+    if (h->d_ws) (void)hipFree(h->d_ws);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
     if (h->evq0) (void)hipEventDestroy(h->evq0);

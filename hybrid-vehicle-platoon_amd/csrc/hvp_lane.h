@@ -759,7 +759,7 @@ __device__ inline unsigned bnb_children(const hvp_system& S, const hvp::Consts& 
 // writes the children (regions in mask) of a level-(lv-1) node into level lv's list at slots
 // off.. (reserved by the caller) below `limit` (the end of the list's half, LevelList); past it
 // the instance is flagged HVP_OVERFLOW
-__device__ inline void bnb_put_children(Workspace& ws, int lv, unsigned long long off, unsigned long long limit,
+__device__ inline void bnb_put_children(const Workspace& ws, int lv, unsigned long long off, unsigned long long limit,
                                         unsigned mask, int inst, const hvp_system& S, const hvp::Consts& C,
                                         uint64_t code, double lo, double hi, double plb) {
     const int nc = __popc(mask), d = lv & 1;
@@ -863,7 +863,7 @@ __device__ inline LevelList level_list(const Workspace& ws, int k) {
 // wave-level reservation of nc slots per lane of level lv in the bucket of the lane's parent
 // (its QP took `steps` active-set steps): one packed scan of the per-bucket counts, one atomic per
 // non-empty bucket by the last lane.  Returns the lane's first slot and the end of its segment.
-__device__ inline unsigned long long split_reserve(Workspace& ws, int lv, int nc, int steps, int lane,
+__device__ inline unsigned long long split_reserve(const Workspace& ws, int lv, int nc, int steps, int lane,
                                                    unsigned long long& limit) {
     const unsigned long long cap = (unsigned long long)ws.cap;
     if (ws.split <= 1) {
@@ -1417,10 +1417,27 @@ __global__ __launch_bounds__(kBlock) void k_inst_prep(int B, const hvp_system* _
                                                       const int32_t* __restrict__ role,
                                                       const double* __restrict__ params, hvp::Consts C, Workspace ws) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) ws.lvl[0] = (unsigned long long)B;
     if (i >= B) return;
     constexpr int NT = N * (N + 1) / 2;
     double H[NT], f[N], C0, hf[N - 1], hb[N - 1];
-    hvp::setup_track<N>(systems[sys[i]], C, role[i], params + (size_t)i * C.stride, H, f, C0, hf, hb);
+    const hvp_system& S = systems[sys[i]];
+    const double* prm = params + (size_t)i * C.stride;
+    hvp::setup_track<N>(S, C, role[i], prm, H, f, C0, hf, hb);
+    // the search's per-instance state and the root node (level 0, list 0), as k_bnb_root sets them:
+    // the refill kernel solves the root level like any other (launch_bnb)
+    const double v0 = prm[1], P1 = prm[0] + S.ts * v0;
+    const bool ok = P1 >= S.pmin - 1e-9 * (1.0 + fabs(S.pmin)) && P1 <= S.pmax + 1e-9 * (1.0 + fabs(S.pmax));
+    ws.key[i] = ~0ull;
+    ws.inst_flag[i] = ok ? 0 : 1;
+    ws.nd_inst[0][i] = ok ? i : -1;
+    ws.nd_code[0][i] = 0;
+    ws.nd_lo[0][i] = v0;
+    ws.nd_hi[0][i] = v0;
+    ws.nd_lb[0][i] = -1e300;
+    ws.inc[i] = cost_key(__longlong_as_double(0x7ff0000000000000ll));  // +inf: no incumbent
+    ws.nodes[i] = 0;
+    ws.iters[i] = 0;
     const size_t mb = (size_t)ws.max_batch;
     double* o = ws.iq + i;
 #pragma unroll
@@ -1432,6 +1449,38 @@ __global__ __launch_bounds__(kBlock) void k_inst_prep(int B, const hvp_system* _
         o[(NT + N + j) * mb] = hf[j];
         o[(NT + 2 * N - 1 + j) * mb] = hb[j];
     }
+}
+
+// The greedy dive of every instance whose root QP (level 0, solved by the refill kernel) succeeded:
+// its leaf goes to the dive list (ws.dv_*), which the refill kernel solves next as a level-N list
+// of its own (launch_bnb) -- its leaf costs set the incumbents before level 1, as in k_bnb_root.
+template <int N>
+__global__ __launch_bounds__(kBlock) void k_bnb_dive_prep(int B, const hvp_system* __restrict__ systems,
+                                                          const int32_t* __restrict__ sys,
+                                                          const double* __restrict__ params, hvp::Consts C,
+                                                          Workspace ws) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) {
+        ws.dv_lvl[N] = (unsigned long long)B;
+        ws.dv_lvl[(HVP_MAX_N + 1) + N] = 0ull;  // claims
+    }
+    if (i >= B) return;
+    const bool root_ok = ws.nd_inst[0][i] >= 0 && ws.nd_lb[0][i] > -1e300;
+    uint64_t code = 0;
+    bool dived = false;
+    if (root_ok) {
+        double ystar[N];
+#pragma unroll
+        for (int j = 0; j < N; ++j) ystar[j] = ws.task_y[(size_t)i * N + j];
+        dived = hvp::bnb_dive<N>(systems[sys[i]], C, params[(size_t)i * C.stride + 1], ystar, &code);
+    }
+    ws.dv_inst[i] = dived ? i : -1;
+    ws.dv_code[i] = code;
+    ws.dv_lo[i] = 0.0;
+    ws.dv_hi[i] = -1.0;
+    // root + dive QPs (hvp_get_stats counts the levels' nodes from their lists)
+    const unsigned qp = (ws.nd_inst[0][i] >= 0 ? 1u : 0u) + (dived ? 1u : 0u);
+    if (qp) atomicAdd(&ws.counter[3], (unsigned long long)qp);
 }
 
 // the node QP of instance inst from the per-instance part + the node's regions / relaxation
@@ -1458,13 +1507,17 @@ __device__ inline bool setup_node(Q& q, const hvp_system& S, const hvp::Consts& 
 
 template <int N>
 __device__ inline void bnb_node_done(int k, long long t, int inst, bool ok, int its, double c, const double* y,
-                                     const hvp::Consts& C, Workspace& ws) {
+                                     const hvp::Consts& C, const Workspace& ws) {
     const int dst = k & 1;
     atomicAdd(&ws.nodes[inst], 1);
     atomicAdd(&ws.iters[inst], its);
     if (k < N) {
         ws.nd_lb[dst][t] = ok ? c : -1e300;  // a failed bound QP prunes nothing
         if (!ok) atomicAdd(&ws.counter[4], 1ull);
+        if (k == 0 && ok) {  // the root's optimum: the greedy dive's target (k_bnb_dive_prep)
+#pragma unroll
+            for (int j = 0; j < N; ++j) ws.task_y[t * N + j] = y[j];
+        }
     } else {
         if (ok) ws.nd_lb[dst][t] = c;  // a failed leaf keeps its parent's bound
         ws.leaf_stat[t] = ok ? 0 : HVP_MAXITER;
@@ -1517,17 +1570,30 @@ __device__ inline void gi_trip(Q& q, hvp::GiLane<N>& g, const hvp::Consts& C, in
 __device__ unsigned long long g_pf_hist[128];
 #endif
 
+// A uniform pointer the compiler must treat as unknown at this point: loads through it cannot be
+// hoisted above it (k_bnb_bound_refill reads its event-only constants this way, so they occupy
+// scalar registers only inside the event instead of across the whole persistent loop).
+template <class T>
+__device__ inline const T* uniform_opaque(const T* p) {
+    asm volatile("" : "+s"(p));
+    return p;
+}
+
+// Persistent refill kernel.  Register discipline: the trip loop (gi_trip) keeps the lane QP and
+// the Goldfarb-Idnani state in VGPRs and only the trip constants (C.acc, C.dec, C.w of the kernel
+// argument) in SGPRs; everything the event needs -- the workspace descriptor (wsd), the rest of
+// the problem constants (cd: the handle's device copy of C), the level list's bucket counts -- is
+// loaded inside the event through uniform_opaque pointers.  (With both structures as kernel
+// arguments live across the loop, 128 SGPRs spilled into two VGPRs' lanes and 35 dwords of VGPRs
+// into scratch.)
 template <int N>
 __global__ __launch_bounds__(kBnbBlock<N>) __attribute__((amdgpu_waves_per_eu(HVP_REFILL_WAVES)))
 void k_bnb_bound_refill(int k, const hvp_system* __restrict__ systems, const int32_t* __restrict__ sys,
                         const int32_t* __restrict__ role, const double* __restrict__ params, hvp::Consts C,
-                        Workspace ws) {
+                        const Workspace* __restrict__ wsd, const hvp::Consts* __restrict__ cd) {
     constexpr int BS = kBnbBlock<N>;
     static_assert(N <= HVP_MAX_N_ENUM, "lane refill is the N <= 8 path");
     const int dst = k & 1;
-    const LevelList lvl = level_list(ws, k);
-    const long long total = lvl.count();
-    unsigned long long* claim = ws.lvl + (HVP_MAX_N + 1) + k;
     const int lane = threadIdx.x & 63;
     hvp::LaneQp<N, LdsMem<N, BS>> q;
     q.mem.lane = threadIdx.x;
@@ -1536,7 +1602,7 @@ void k_bnb_bound_refill(int k, const hvp_system* __restrict__ systems, const int
     int inst = 0, stage = RS_IDLE, fail = 0;
     uint64_t code = 0;
     bool exhausted = false;
-    unsigned long long iter_sum = 0;
+    unsigned iter_sum = 0;
 #ifdef HVP_REFILL_PROF  // diagnostics build: event / trip cycles and busy lane-trips per wave
     unsigned long long pf_ev = 0, pf_all = 0, pf_busy = 0, pf_trips = 0, pf_wb = 0, pf_cl = 0, pf_dc = 0, pf_rs = 0;
     const unsigned long long pf_t0 = __builtin_amdgcn_s_memtime();
@@ -1562,15 +1628,17 @@ void k_bnb_bound_refill(int k, const hvp_system* __restrict__ systems, const int
 #endif
         if (nfree >= kRefillMin || nfree == 64) {
             // ---- event: write the finished lanes' results, then refill every free lane
+            const Workspace& ws = *uniform_opaque(wsd);
+            const hvp::Consts& Ce = *uniform_opaque(cd);
             unsigned cmask = 0;  // children of a finished bound node (k_bnb_expand's work, fused)
             double clb = 0.0;
             if (done) {
-                const int st = stage == RS_OPT ? g.verify(C, nullptr) : fail;
+                const int st = stage == RS_OPT ? g.verify(Ce, nullptr) : fail;
                 const bool ok = st == hvp::GI_OK;
-                const double c = ok ? hvp::direct_cost<N>(q, systems[sys[inst]], C, role[inst],
-                                                          params + (size_t)inst * C.stride, code, k)
+                const double c = ok ? hvp::direct_cost<N>(q, systems[sys[inst]], Ce, role[inst],
+                                                          params + (size_t)inst * Ce.stride, code, k)
                                     : 0.0;
-                iter_sum += (unsigned long long)g.iter;
+                iter_sum += (unsigned)g.iter;
 #ifdef HVP_REFILL_PROF
                 {
                     const double cc = __builtin_amdgcn_readfirstlane(__double_as_longlong(c) & 0xffffffff);
@@ -1578,20 +1646,20 @@ void k_bnb_bound_refill(int k, const hvp_system* __restrict__ systems, const int
                     pf_dc += __builtin_amdgcn_s_memtime() - pf_e0;
                 }
 #endif
-                bnb_node_done<N>(k, t, inst, ok, g.iter, c, q.y, C, ws);
+                bnb_node_done<N>(k, t, inst, ok, g.iter, c, q.y, Ce, ws);
                 stage = RS_IDLE;
                 // the incumbent only changes at the leaves (level N): below N this pruning test
                 // sees the value a separate expand kernel would
                 clb = ok ? c : -1e300;
                 if (k < N && !(ws.inst_flag[inst] & 2) && !hvp::bnb_pruned(clb, inc_of(ws, inst)))
-                    cmask = bnb_children(systems[sys[inst]], C, k, ws.nd_lo[dst][t], ws.nd_hi[dst][t]);
+                    cmask = bnb_children(systems[sys[inst]], Ce, k, ws.nd_lo[dst][t], ws.nd_hi[dst][t]);
             }
             if (k < N) {
                 unsigned long long limit;
                 const unsigned long long off =
                     split_reserve(ws, k + 1, __popc(cmask), done ? g.iter : 0, lane, limit);
                 if (cmask)
-                    bnb_put_children(ws, k + 1, off, limit, cmask, inst, systems[sys[inst]], C, code,
+                    bnb_put_children(ws, k + 1, off, limit, cmask, inst, systems[sys[inst]], Ce, code,
                                      ws.nd_lo[dst][t], ws.nd_hi[dst][t], clb);
 #ifdef HVP_REFILL_PROF
                 pf_rs += __builtin_amdgcn_s_memtime() - pf_e0;
@@ -1603,7 +1671,10 @@ void k_bnb_bound_refill(int k, const hvp_system* __restrict__ systems, const int
             pf_wb += pf_w1 - pf_e0;
 #endif
             if (!exhausted) {
-                const unsigned long long base = wave_claim(claim, free, nfree, lane);
+                // this level's list (its bucket counts are final: this launch writes level k + 1)
+                const LevelList lvl = level_list(ws, k);
+                const long long total = lvl.count();
+                const unsigned long long base = wave_claim(ws.lvl + (HVP_MAX_N + 1) + k, free, nfree, lane);
 #ifdef HVP_REFILL_PROF
                 {
                     const unsigned long long bb = __builtin_amdgcn_readfirstlane((unsigned)base);
@@ -1622,7 +1693,7 @@ void k_bnb_bound_refill(int k, const hvp_system* __restrict__ systems, const int
                     } else {
                         t = mine;
                         code = ws.nd_code[dst][mine];
-                        setup_node<N>(q, systems[sys[inst]], C, ws, inst, role[inst], params + (size_t)inst * C.stride,
+                        setup_node<N>(q, systems[sys[inst]], Ce, ws, inst, role[inst], params + (size_t)inst * Ce.stride,
                                       code, k, ws.nd_lo[dst][mine], ws.nd_hi[dst][mine]);
                         stage = g.init(q) == hvp::GI_OK ? RS_SCAN : RS_FAIL;
                         fail = hvp::GI_FAIL_CHOL;
@@ -1637,7 +1708,8 @@ void k_bnb_bound_refill(int k, const hvp_system* __restrict__ systems, const int
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) iter_sum += __shfl_down(iter_sum, off, 64);
-    if (lane == 0 && iter_sum) atomicAdd(&ws.counter[1], iter_sum);
+    const Workspace& ws = *uniform_opaque(wsd);
+    if (lane == 0 && iter_sum) atomicAdd(&ws.counter[1], (unsigned long long)iter_sum);
 #ifdef HVP_REFILL_PROF
     pf_all = __builtin_amdgcn_s_memtime() - pf_t0;
     if (lane == 0) {  // the claim slots of levels > N are free (prof builds need N <= 8)
@@ -1818,6 +1890,7 @@ __global__ __launch_bounds__(kBlock) void k_bnb_finish(int B, const hvp_system* 
                                                        int32_t* __restrict__ iters_out,
                                                        double* __restrict__ xf_out, double* __restrict__ xb_out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0 && ws.dv_counter && ws.dv_counter[1]) atomicAdd(&ws.counter[1], ws.dv_counter[1]);  // the dives' steps
     if (i >= B) return;
     const int flag = ws.inst_flag[i];
     const bool win = ws.key[i] != ~0ull;
@@ -2088,7 +2161,8 @@ __global__ __launch_bounds__(kCoopBlock) void k_gadmm_qp_coop(int P, int n, int 
     int it = 0;
     unsigned raw = 0;
     const int st = hvp::coop::solve_qp<N>(L, lds[g], S, C, rl, prm, code, N, kGiMaxIter<N>, it, &cost, &raw, 0.0,
-                                          -1.0, warm_ws ? warm_ws + b : nullptr, warm != 0);
+                                          -1.0, warm_ws ? warm_ws + b : nullptr, warm != 0,
+                                          ((uint64_t)(uint32_t)sys[b] << 32) | (uint32_t)rl);
     if (st == hvp::GI_OK) {
         lds[g].v[t] = t < N ? L.y : 0.0;
         hvp::coop::gsync();
@@ -2130,8 +2204,34 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
     ws.split = fused ? (want >= 4 ? 4 : (want >= 2 ? 2 : 1)) : 1;
     ws.split_shift = ws.split == 4 ? 2 : (ws.split == 2 ? 1 : 0);
     h->last_split = ws.split;
+    if (fused) {
+        // the refill kernel's workspace descriptors ([0] the level lists, [1] the dive list in
+        // place of level N's), uploaded when they change
+        Workspace up[2] = {ws, ws};
+        Workspace& wd = up[1];
+        wd.nd_inst[N & 1] = ws.dv_inst;
+        wd.nd_code[N & 1] = ws.dv_code;
+        wd.nd_lo[N & 1] = ws.dv_lo;
+        wd.nd_hi[N & 1] = ws.dv_hi;
+        wd.nd_lb[N & 1] = ws.dv_lb;
+        wd.leaf_stat = ws.dv_stat;
+        wd.task_y = ws.dv_y;
+        wd.redo = ws.dv_redo;
+        wd.lvl = ws.dv_lvl;
+        wd.counter = ws.dv_counter;
+        wd.cap = ws.max_batch;
+        wd.split = 1;
+        wd.split_shift = 0;
+        if (!h->ws_up_valid || std::memcmp(up, h->ws_up, sizeof(up)) != 0) {
+            HIP_TRY(hipDeviceSynchronize());  // a solve in flight may still read the old ones
+            HIP_TRY(hipMemcpy(h->d_ws, up, sizeof(up), hipMemcpyHostToDevice));
+            std::memcpy(h->ws_up, up, sizeof(up));
+            h->ws_up_valid = true;
+        }
+    }
     HIP_TRY(hipMemsetAsync(ws.counter, 0, 8 * sizeof(unsigned long long), st));
     HIP_TRY(hipMemsetAsync(ws.lvl, 0, (2 + kMaxBuckets) * (HVP_MAX_N + 1) * sizeof(unsigned long long), st));  // + claims, buckets
+    if (ws.dv_counter) HIP_TRY(hipMemsetAsync(ws.dv_counter, 0, 8 * sizeof(unsigned long long), st));
     HIP_TRY(hipEventRecord(h->ev0, st));
     HIP_TRY(hipEventRecord(h->evq0, st));
     const size_t lds = sizeof(double) * hvp::F_COUNT * N * BS;
@@ -2148,15 +2248,36 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
             hipLaunchKernelGGL((k_bnb_root<N, true>), dim3((B + BS - 1) / BS), dim3(BS), lds, st, B, h->d_sys, sys,
                                role, params, h->C, ws);
         } else {
-            // sigma-independent QP part once per instance, then the root kernel
+            // sigma-independent QP part + the root nodes once per instance
             hipLaunchKernelGGL(k_inst_prep<N>, dim3(grid_for(B)), dim3(kBlock), 0, st, B, h->d_sys, sys, role, params,
                                h->C, ws);
             HIP_TRY(hipGetLastError());
-            // (one lane per instance, 1 wave per SIMD: a persistent 2-wave root kernel -- root QP,
-            // dive, leaf QP per lane, generations of 64 -- spilled inside its active-set loop and
-            // measured 17 % slower on the whole step, profiles/r02f_*)
-            hipLaunchKernelGGL((k_bnb_root<N, false>), dim3((B + BS - 1) / BS), dim3(BS), lds, st, B, h->d_sys, sys,
-                               role, params, h->C, ws);
+            // The root level through the refill kernel (the root QPs as level-0 nodes, their
+            // children into level 1's buckets), then the greedy dives' leaves as a list of their own
+            // (k_bnb_dive_prep) through the same kernel at K = N, whose costs set the incumbents.
+            // The tree is k_bnb_root's: the root's children are never pruned (the root bound is <=
+            // every leaf), and the dives' incumbents are in place before level 1.  The refill kernel
+            // keeps every lane busy where k_bnb_root (one lane per instance, 1 wave per SIMD) waits
+            // for each wave's slowest root + dive.  HVP_ROOT_REFILL=0 selects k_bnb_root (A/B);
+            // so does a workspace whose bucket segment cannot hold the root level.
+            const char* rr = std::getenv("HVP_ROOT_REFILL");
+            const bool root_refill = !(rr && rr[0] == '0') && ws.dv_mem &&
+                                     ((unsigned long long)ws.cap >> ws.split_shift) >= (unsigned long long)B;
+            if (root_refill) {
+                const int g_root = (int)std::min<long long>((B + BS - 1) / BS, (long long)h->n_cu * kRefillBlocksPerCu);
+                hipLaunchKernelGGL(k_bnb_bound_refill<N>, dim3(g_root), dim3(BS), lds, st, 0, h->d_sys, sys, role,
+                                   params, h->C, h->d_ws, h->d_consts);
+                HIP_TRY(hipGetLastError());
+                hipLaunchKernelGGL(k_bnb_dive_prep<N>, dim3(grid_for(B)), dim3(kBlock), 0, st, B, h->d_sys, sys, params,
+                                   h->C, ws);
+                HIP_TRY(hipGetLastError());
+                hipLaunchKernelGGL(k_bnb_bound_refill<N>, dim3(g_root), dim3(BS), lds, st, N, h->d_sys, sys, role,
+                                   params, h->C, h->d_ws + 1, h->d_consts);
+            } else {
+                // (one lane per instance, 1 wave per SIMD)
+                hipLaunchKernelGGL((k_bnb_root<N, false>), dim3((B + BS - 1) / BS), dim3(BS), lds, st, B, h->d_sys,
+                                   sys, role, params, h->C, ws);
+            }
         }
     }
     HIP_TRY(hipGetLastError());
@@ -2185,7 +2306,7 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
                 const int g_refill = (int)std::min<long long>((h->ws.cap + BS - 1) / BS,
                                                               (long long)h->n_cu * kRefillBlocksPerCu);
                 hipLaunchKernelGGL(k_bnb_bound_refill<N>, dim3(g_refill), dim3(BS), lds, st, k, h->d_sys, sys, role,
-                                   params, h->C, ws);
+                                   params, h->C, h->d_ws, h->d_consts);
             }
         }
         HIP_TRY(hipGetLastError());

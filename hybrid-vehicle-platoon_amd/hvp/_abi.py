@@ -182,6 +182,21 @@ def load():
     return lib
 
 
+_lib_sha = None
+
+
+def lib_sha256() -> str:
+    """SHA-256 of the library file this process loads (LIB_PATH): the stamp profiles/ summaries
+    carry, so a roofline figure is only ever taken from a profile of the same binary."""
+    global _lib_sha
+    if _lib_sha is None:
+        import hashlib
+
+        with open(LIB_PATH, "rb") as f:
+            _lib_sha = hashlib.sha256(f.read()).hexdigest()
+    return _lib_sha
+
+
 def last_error() -> str:
     buf = ctypes.create_string_buffer(1024)
     load().hvp_last_error(buf, len(buf))

@@ -68,11 +68,15 @@ typedef struct hvp_system {
 typedef struct hvp_problem {
     int32_t N;              /* prediction horizon (2..HVP_MAX_N)                      */
     int32_t quadratic_cost; /* 1 = min_2_norm (MIQP); 0 = min_1_norm (MILP,
-                               fleet_decent_mld.py:73-76): HVP_FORM_DECENT, any N, by branch
-                               and bound over node LPs (AUTO / BNB) or enumeration (ENUMERATE,
-                               N <= HVP_MAX_N_ENUM); LPs of csrc/hvp_l1.h; an LP neither solved
-                               nor proven infeasible makes its instance HVP_MAXITER.  Other
-                               formulations: HVP_E_UNSUPPORTED */
+                               fleet_decent_mld.py:73-76, mpcs/cent_mld.py:58-61):
+                               HVP_FORM_DECENT, any N, by branch and bound over node LPs (AUTO /
+                               BNB) or enumeration (ENUMERATE, N <= HVP_MAX_N_ENUM), LPs of
+                               csrc/hvp_l1.h; HVP_FORM_CENT, the platoon LP inside the joint
+                               branch and bound (csrc/hvp_cent_l1.h; AUTO / BNB, or ENUMERATE =
+                               the exhaustive joint search).  Every LP ends solved, proven
+                               infeasible (excluded), or unresolved -- which makes its instance /
+                               platoon HVP_MAXITER while it is still in contention.
+                               HVP_FORM_ADMM, HVP_FORM_GADMM: HVP_E_UNSUPPORTED */
     double Qx[4];           /* 2x2 row-major state-tracking weight                     */
     double Qu;              /* control weight                                          */
     double Qdu;             /* control-variation weight                                */

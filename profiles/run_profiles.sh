@@ -16,6 +16,8 @@ shift || true
 if [ $# -gt 0 ]; then BENCH=(python3 bench.py "$@"); else BENCH=(python3 bench.py --platoons 16384 --steps 5 --warmup 1 --no-cpu --streams 1); fi
 mkdir -p "$OUT"
 echo "${BENCH[*]}" > "$OUT/cmd.txt"
+# the stamp bench.py matches against the library it loads (HVP_LIB, else the in-tree build)
+sha256sum "${HVP_LIB:-hybrid-vehicle-platoon_amd/lib/libhvpsolve.so}" | cut -d' ' -f1 > "$OUT/lib_sha256.txt"
 echo "profiling: ${BENCH[*]}"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -f csv -d "$OUT/trace" -o run -- "${BENCH[@]}" > "$OUT/trace.log" 2>&1
 echo trace done

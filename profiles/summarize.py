@@ -42,7 +42,8 @@ def short(name: str) -> str:
     for k in ("k_qp_gi", "k_qp_ipm", "k_enum", "k_cost", "k_select", "k_inst_prep", "k_bnb_root_coop", "k_bnb_root",
               "k_bnb_expand", "k_bnb_bound_refill", "k_bnb_bound_coop", "k_bnb_bound",
               "k_bnb_key", "k_bnb_write", "k_bnb_finish", "k_gadmm_qp_coop", "k_gadmm_qp", "k_gadmm_update",
-              "k_gadmm_rollout", "k_gadmm_switch", "k_admm_update"):
+              "k_gadmm_rollout", "k_gadmm_switch", "k_admm_update", "k_l1_root", "k_l1_bound", "k_qp_l1",
+              "k_cent_bnb", "k_cent_tasks", "k_cent_final", "k_cent_init", "k_env_step", "k_decent_params"):
         if k in name:
             return k
     return name[:48]
@@ -105,7 +106,9 @@ def main() -> None:
                     d[key] = d[c] / wc
             if d.get("GRBM_GUI_ACTIVE"):
                 d["waves_per_cu"] = 4.0 * wc / (d["GRBM_GUI_ACTIVE"] / 8.0) / 256.0
+    sha_path = os.path.join(src, "lib_sha256.txt")
     meta = {"round": rnd, "tag": tag, "source": "profiles/run_profiles.sh (rocprofv3 kernel trace + separate PMC passes)",
+            "lib_sha256": open(sha_path).read().strip() if os.path.exists(sha_path) else None,
             "workload": open(os.path.join(src, "cmd.txt")).read().strip() if os.path.exists(os.path.join(src, "cmd.txt")) else None,
             "kernels": out, "workloads": extra}
     with open(os.path.join(here, f"{rnd}_summary.json"), "w") as f:

@@ -72,3 +72,40 @@ def test_invalid_arguments_fail_loudly_without_touching_the_gpu():
     badq = tables.problem(5)
     badq.quadratic_cost = 2
     assert lib.hvp_create(ctypes.byref(h), ctypes.byref(badq), sysv, 1, 0) == -1
+
+
+def test_min_1_norm_acceptance_matches_integration_doc():
+    """INTEGRATION.md section 1 states which problems take quadratic_cost = 0 (min_1_norm,
+    fleet_decent_mld.py:73-76, mpcs/cent_mld.py:58-61): HVP_FORM_DECENT at every N <= 16 and
+    HVP_FORM_CENT are accepted, the ADMM forms return HVP_E_UNSUPPORTED.  hvp_create validates
+    before it touches a device, so on a CPU-only host an accepted problem fails at the device
+    step (HVP_E_HIP = -2) and a rejected one with HVP_E_UNSUPPORTED (-3)."""
+    import ctypes
+
+    from hvp import _abi, tables
+    from hvp.admm import admm_problem
+    from hvp.cent import cent_problem
+    from hvp.gadmm import gadmm_problem
+    from hvp.models import PwaGearVehicle
+
+    lib = _abi.load()
+    h = ctypes.c_void_p()
+    veh = PwaGearVehicle(800)
+    sysv = (_abi.HvpSystem * 1)(tables.system_from_dict(veh.get_discrete_system(1), tables.gears_of(veh)))
+
+    def rc(p):
+        r = lib.hvp_create(ctypes.byref(h), ctypes.byref(p), sysv, 1, 0)
+        if r == 0:
+            lib.hvp_destroy(h)
+        return r
+
+    for p in (tables.problem(10, quadratic_cost=False), cent_problem(5, quadratic_cost=False),
+              cent_problem(5, quadratic_cost=False, exhaustive=True)):
+        assert rc(p) in (0, -2), _abi.last_error()
+    g = gadmm_problem(10)
+    g.quadratic_cost = 0
+    for p in (admm_problem(10, 0.5, quadratic_cost=False), g):
+        assert rc(p) == -3
+        assert "min_1_norm" in _abi.last_error()
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    assert "HVP_FORM_CENT` accepts it" in doc and "solved by enumeration with" not in doc

@@ -359,3 +359,65 @@ def test_gadmm_warm_start_keeps_the_answers(gpu_available, monkeypatch):
         for a, b in zip(wr, cr):
             assert np.array_equal(a["seq"].cpu().numpy(), b["seq"].cpu().numpy())
             assert np.array_equal(a["platoon_rounds"].cpu().numpy(), b["platoon_rounds"].cpu().numpy())
+
+
+def _gadmm_local_call(solver, N, sysi, roles, params, seq):
+    """One hvp_gadmm_solve of B one-vehicle "platoons" on `solver`'s handle; host arrays out."""
+    import torch
+
+    from hvp import _abi
+
+    dev = torch.device("cuda", 0)
+    B = len(roles)
+    t = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a), dtype=dt, device=dev)  # noqa: E731
+    sysi, roles, params, seq = (t(sysi, torch.int32), t(roles, torch.int32), t(params, torch.float64),
+                                t(seq, torch.int8))
+    state = torch.ones(B, dtype=torch.int32, device=dev)
+    u = torch.zeros((B, N), dtype=torch.float64, device=dev)
+    x, xf, xb = (torch.zeros((B, 2, N + 1), dtype=torch.float64, device=dev) for _ in range(3))
+    cost = torch.zeros(B, dtype=torch.float64, device=dev)
+    st, edge = torch.zeros(B, dtype=torch.int32, device=dev), torch.zeros(B, dtype=torch.int32, device=dev)
+    p = lambda a: ctypes.c_void_p(a.data_ptr())  # noqa: E731
+    rc = solver._lib.hvp_gadmm_solve(solver._h, B, 1, 0, 1, p(sysi), p(roles), p(params), p(seq), p(state), p(u),
+                                     p(x), p(xf), p(xb), p(cost), p(st), p(edge), None,
+                                     ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
+    _abi.check(rc, "hvp_gadmm_solve")
+    torch.cuda.synchronize()
+    return {k: v.cpu().numpy() for k, v in dict(u=u, x=x, xf=xf, xb=xb, cost=cost, status=st, edge=edge).items()}
+
+
+@pytest.mark.gpu
+def test_gadmm_warm_records_never_start_another_qp(gpu_available):
+    """a handle's warm-start records (hvp_coop.h WarmQp) are keyed by region code,
+    hinge states AND (system index, role bits), so calling hvp_gadmm_solve again on the same
+    handle with another batch -- rows permuted, systems swapped -- gives the answers of a fresh
+    handle (cold start), never a solve from another QP's factors."""
+    from hvp import tables
+    from hvp.gadmm import gadmm_problem
+    from hvp.models import PwaGearVehicle
+    from hvp.solver import BatchSolver
+
+    N = 10
+    fx = load(f"gadmm_local_N{N}.npz")
+    B = len(fx["roles"])
+    heavy = PwaGearVehicle(950)
+    systems = [_system(), tables.system_from_dict(heavy.get_discrete_system(1), tables.gears_of(heavy))]
+    prob = gadmm_problem(N, float(fx["rho"]))
+    solver = BatchSolver(prob, systems)
+    first = _gadmm_local_call(solver, N, np.zeros(B), fx["roles"], fx["params"], fx["seq"])
+    _check_local(fx, first["u"], first["x"], first["xf"], first["xb"], first["cost"], first["status"],
+                 first["edge"].astype(np.uint32))
+    rng = np.random.default_rng(7)
+    perm = rng.permutation(B)
+    sys2 = (np.arange(B) % 2).astype(np.int32)
+    args = (sys2, fx["roles"][perm], fx["params"][perm], fx["seq"][perm])
+    again = _gadmm_local_call(solver, N, *args)
+    fresh = _gadmm_local_call(BatchSolver(prob, systems), N, *args)
+    assert np.array_equal(again["status"], fresh["status"])
+    ok = fresh["status"] == 0
+    assert ok.mean() > 0.9
+    assert np.abs(again["u"][ok] - fresh["u"][ok]).max() <= 1e-9
+    assert np.abs(again["x"][ok] - fresh["x"][ok]).max() <= 1e-7
+    c, cf = again["cost"][ok], fresh["cost"][ok]
+    assert np.all(np.abs(c - cf) <= 1e-10 * np.maximum(1.0, np.abs(cf)))
+    assert np.array_equal(again["edge"][ok], fresh["edge"][ok])
