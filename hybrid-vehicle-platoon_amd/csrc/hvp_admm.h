@@ -474,4 +474,46 @@ HVP_HD inline int solve_admm_lane(LaneQp<N, M>& q, const hvp_system& S, const Co
     return GI_FAIL_ITER;
 }
 
+// The interior-point fallback of the ADMM local QP (naive ADMM leaves, switching-ADMM local QPs):
+// the hinge-state iteration of solve_admm_lane with the Mehrotra interior point (hvp_ipm.h Solver)
+// in place of the active-set method, for the QPs the active-set method fails on (degenerate
+// vertices, its iteration cap).  The row set is setup_lane_admm's, so the optimum is the same QP's
+// -- what fleet_naive_admm.py:407-419 (Gurobi) and fleet_g_admm.py:162,195-205 (qpOASES) return for
+// it.  edge: the switching rule's bits (V rows active with multiplier > kEdgeMultTol, as
+// GiLane::verify reports them), from the interior point's multipliers.
+template <int N, class M>
+HVP_HD inline int solve_admm_ipm(LaneQp<N, M>& q, const hvp_system& S, const Consts& C, int role, const double* prm,
+                                 uint64_t code, int K, int& iters, uint32_t* edge = nullptr) {
+    uint64_t hs = 0;
+    iters = 0;
+    {
+        double y[N];
+#pragma unroll
+        for (int k = 0; k < N; ++k) y[k] = prm[1];
+        bool c;
+        hs = admm_classify<N>(C, role, prm, prm[0] + S.ts * prm[1], S.ts, y, 0, &c);
+    }
+    for (int round = 0; round < kHubRounds; ++round) {
+        setup_lane_admm<N>(q, S, C, role, prm, code, K, hs);
+        const QpOut o = Solver<N, true, M>::solve(q, C);
+        iters += o.iters;
+        if (o.status != 0) return GI_FAIL_ITER;
+        bool consistent;
+        hs = admm_classify<N>(C, role, prm, q.P1, q.ts, q.y, hs, &consistent);
+        if (consistent) {
+            if (edge) {
+                uint32_t m = 0;
+#pragma unroll
+                for (int j = 0; j < N; ++j) {
+                    if (q.llo[3 * j] > kEdgeMultTol) m |= 1u << (2 * j);
+                    if (q.lhi[3 * j] > kEdgeMultTol) m |= 1u << (2 * j + 1);
+                }
+                *edge = m;
+            }
+            return GI_OK;
+        }
+    }
+    return GI_FAIL_ITER;
+}
+
 }  // namespace hvp

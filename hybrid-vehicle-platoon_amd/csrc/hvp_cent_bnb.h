@@ -359,12 +359,41 @@ __device__ inline void bnb_platoon(Lane& L, const Lds& S, const Consts& C, const
         }
     };
     // split: the unexplored children of the open frames d .. d0 become tasks (deepest first;
-    // each vehicle's interval goes back to its parent's as the DFS backtrack does)
-    auto export_tasks = [&]() {
+    // each vehicle's interval goes back to its parent's as the DFS backtrack does).  The tasks'
+    // slots are reserved at once (compare-and-swap on the list size, never past its capacity):
+    // when the list cannot take them all, nothing is exported and the search goes on in this wave
+    // (returns false) -- a full task list costs parallelism, never a platoon (no HVP_OVERFLOW).
+    auto export_tasks = [&]() -> bool {
+        const double incp = shared_inc();
+        int want = 0;  // the tasks below, counted with the same incumbent
+        for (int j = d; j >= d0; --j) {
+            const int nch = bcu(st.f_n, j), cur = bcu(st.f_cur, j);
+            for (int c = cur; c < nch; ++c) {
+                const Child ch = load_child(frames + (size_t)j * nreg_max + c);
+                if (!(ch.lb < INF)) continue;
+                if (incp < INF && bnb_pruned(ch.lb, incp)) continue;
+                ++want;
+            }
+        }
+        unsigned long long base = 0;
+        int ok = 1;
+        if (t == 0) {
+            unsigned long long cur = __atomic_load_n(sp->out_count, __ATOMIC_RELAXED);
+            for (;;) {
+                if ((long long)(cur + (unsigned long long)want) > sp->out_cap) {
+                    ok = 0;
+                    break;
+                }
+                const unsigned long long prev = atomicCAS(sp->out_count, cur, cur + (unsigned long long)want);
+                if (prev == cur) break;
+                cur = prev;
+            }
+            base = cur;
+        }
+        if (!bcu(ok, 0)) return false;
+        base = bcu((uint64_t)base, 0);
         uint64_t vcode_w = st.vcode;
         double vlo_w = st.vlo, vhi_w = st.vhi;
-        bool over = false;
-        const double incp = shared_inc();
         for (int j = d; j >= d0; --j) {
             const int nch = bcu(st.f_n, j), cur = bcu(st.f_cur, j);
             const int i = j % n, k = j / n;
@@ -372,13 +401,7 @@ __device__ inline void bnb_platoon(Lane& L, const Lds& S, const Consts& C, const
                 const Child ch = load_child(frames + (size_t)j * nreg_max + c);
                 if (!(ch.lb < INF)) continue;
                 if (incp < INF && bnb_pruned(ch.lb, incp)) continue;
-                uint64_t slot = 0;
-                if (t == 0) slot = atomicAdd(sp->out_count, 1ull);
-                slot = bcu(slot, 0);
-                if ((long long)slot >= sp->out_cap) {
-                    over = true;
-                    continue;
-                }
+                const uint64_t slot = base++;
                 Task* tk = sp->out + slot;
                 if (t < n) {
                     tk->code[t] = t == i ? code_with(vcode_w, k, ch.r) : vcode_w;
@@ -397,8 +420,10 @@ __device__ inline void bnb_platoon(Lane& L, const Lds& S, const Consts& C, const
                 vhi_w = shi;
             }
         }
-        if (t == 0) atomicOr(&sp->rec->flags, REC_SPLIT | (over ? REC_TASK_OVER : 0));
+        if (t == 0) atomicOr(&sp->rec->flags, REC_SPLIT);
+        return true;
     };
+    int split_at = sp ? sp->budget : 0;  // QPs after which the search tries to split
 
     if (task && d0 >= D) {
         phase = LEAF;  // the task is one leaf
@@ -433,14 +458,16 @@ __device__ inline void bnb_platoon(Lane& L, const Lds& S, const Consts& C, const
                 pf.flush();
                 return;
             }
-            if (sp && d >= d0 && nodes >= sp->budget) {  // past the budget: split
-                export_tasks();
-                merge();
-                res.status = task ? kTaskDone : kSplit;
-                res.nodes = nodes;
-                res.iters = iters;
-                pf.flush();
-                return;
+            if (sp && d >= d0 && nodes >= split_at) {  // past the budget: split
+                if (export_tasks()) {
+                    merge();
+                    res.status = task ? kTaskDone : kSplit;
+                    res.nodes = nodes;
+                    res.iters = iters;
+                    pf.flush();
+                    return;
+                }
+                split_at = nodes + sp->budget;  // the task list is full: search on, try again later
             }
             if (d < 0) {  // search done
                 searched = nodes;

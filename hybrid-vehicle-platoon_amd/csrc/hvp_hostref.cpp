@@ -4,6 +4,7 @@
 // enumeration + per-lane IPM logic on a machine without a GPU) and by bench.py's extra
 // "same algorithm on the host cores" baseline.  The product entry points live in
 // libhvpsolve.so (hvp_kernels.hip) and never call into this library.
+#include <stdio.h>
 #include <string.h>
 
 #include <vector>
@@ -13,6 +14,16 @@
 #include "hvp_gi.h"
 #include "hvp_ipm.h"
 #include "hvp_l1.h"
+long long g_lp_why[5] = {0, 0, 0, 0, 0};
+#define HVP_LP_WHY(code) (__atomic_fetch_add(&g_lp_why[code], 1, __ATOMIC_RELAXED))
+int g_lp_trace = 0;
+#define HVP_LP_TRACE(it, lv, sd, dv, en, t, bl, yy)                                                             \
+    do {                                                                                                      \
+        if (g_lp_trace)                                                                                       \
+            fprintf(stderr, "[lp] it %d leave %d side %d D %.6e enter %d t %.6e bland %d y0 %.12f y1 %.12f\n", \
+                    (int)(it), (int)(lv), (int)(sd), (double)(dv), (int)(en), (double)(t), (int)(bl), (yy)[0], (yy)[1]); \
+    } while (0)
+#include "hvp_lp.h"
 
 namespace {
 
@@ -21,6 +32,37 @@ constexpr int kAutoEnumMaxNL1 = 0;
 
 // 0: interior point only; 1: Goldfarb-Idnani active set, interior point on failure
 int g_solver = 1;
+// min_1_norm LPs: 0 the interior point (hvp_l1.h l1_solve), 1 as the product: the simplex
+// (hvp_lp.h) up to N = 8, the interior point beyond (the device's wave kernels)
+int g_l1_solver = 1;
+long long g_lp_runs = 0, g_lp_iters = 0, g_lp_fail = 0;
+
+// one min_1_norm LP (node: K < N with the reachable interval [lo, hi] of v_K) by the selected solver
+template <int N>
+int l1_lp(const hvp_system& S, const hvp::Consts& C, int role, const double* prm, uint64_t code, int K, double lo,
+          double hi, double* y, int& it) {
+    if (g_l1_solver == 1 && N <= HVP_MAX_N_ENUM) {
+        hvp::LpData<N> D;
+        const int st = hvp::lp_solve_l1<N>(D, S, C, role, prm, code, K, lo, hi, C.max_iter, y, it);
+#pragma omp atomic
+        g_lp_runs += 1;
+#pragma omp atomic
+        g_lp_iters += it;
+        if (st == hvp::L1_FAIL) {
+#pragma omp atomic
+            g_lp_fail += 1;
+        }
+        return st;
+    }
+    hvp::L1Lp<N> lp;
+    hvp::l1_setup<N>(lp, S, C, role, prm, code, K, lo, hi);
+    for (int i = 0; i < N; ++i) lp.y[i] = prm[1];
+    const int st = hvp::l1_infeasible<N>(S, C, prm, code, K, lo, hi)
+                       ? hvp::L1_INFEASIBLE
+                       : hvp::l1_solve<N>(lp, prm[1], C.max_iter, it, S.vmin, S.vmax);
+    for (int i = 0; i < N; ++i) y[i] = lp.y[i];
+    return st;
+}
 long long g_gi_fail = 0, g_gi_iters = 0, g_gi_runs = 0, g_gi_code[4] = {0, 0, 0, 0};
 
 hvp::Consts make_consts(const hvp_problem& p) {
@@ -68,18 +110,12 @@ void solve_one(const hvp_system& S, const hvp::Consts& C, int role, const double
     if (ok) {
         n = hvp::enumerate_sequences(S, C, prm[1], [&](uint32_t code, int) {
             hvp::LaneQp<N> q;
-            if (C.l1) {  // min_1_norm: the fixed-sequence LP (hvp_l1.h)
-                hvp::L1Lp<N> lp;
-                hvp::l1_setup<N>(lp, S, C, role, prm, code);
+            if (C.l1) {  // min_1_norm: the fixed-sequence LP (hvp_l1.h / hvp_lp.h)
                 Cand c;
                 c.code = code;
                 c.iters = 0;
-                for (int i = 0; i < N; ++i) lp.y[i] = prm[1];
-                c.status = hvp::l1_infeasible<N>(S, C, prm, code, N, 0.0, -1.0)
-                               ? hvp::L1_INFEASIBLE
-                               : hvp::l1_solve<N>(lp, prm[1], C.max_iter, c.iters, S.vmin, S.vmax);
-                c.cost = c.status == 0 ? hvp::l1_direct_cost<N>(lp.y, S, C, role, prm, code) : 1e300;
-                for (int i = 0; i < N; ++i) c.y[i] = lp.y[i];
+                c.status = l1_lp<N>(S, C, role, prm, code, N, 0.0, -1.0, c.y, c.iters);
+                c.cost = c.status == 0 ? hvp::l1_direct_cost<N>(c.y, S, C, role, prm, code) : 1e300;
                 cands.push_back(c);
                 return;
             }
@@ -187,17 +223,14 @@ void solve_one_bnb(const hvp_system& S, const hvp::Consts& C, int role, const do
         hvp::LaneQp<N> q;
         int it = 0;
         if (C.l1) {  // min_1_norm: the node LP (relaxed after K steps), as k_l1_root / k_l1_bound
-            hvp::L1Lp<N> lp;
-            hvp::l1_setup<N>(lp, S, C, role, prm, code, K, lo, hi);
-            l1_st = hvp::l1_infeasible<N>(S, C, prm, code, K, lo, hi)
-                        ? hvp::L1_INFEASIBLE
-                        : hvp::l1_solve<N>(lp, prm[1], C.max_iter, it, S.vmin, S.vmax);
+            double yl[N];
+            l1_st = l1_lp<N>(S, C, role, prm, code, K, lo, hi, yl, it);
             ++nq;
             nit += it;
             if (l1_st != hvp::L1_OK) return false;
-            c = hvp::l1_direct_cost<N>(lp.y, S, C, role, prm, code, K, lo, hi);
+            c = hvp::l1_direct_cost<N>(yl, S, C, role, prm, code, K, lo, hi);
             if (y)
-                for (int i = 0; i < N; ++i) y[i] = lp.y[i];
+                for (int i = 0; i < N; ++i) y[i] = yl[i];
             return true;
         }
         if (C.form == HVP_FORM_ADMM) {
@@ -436,6 +469,15 @@ int hvp_hostref_gadmm_solve(const hvp_problem* P, const hvp_system* systems, int
 }
 
 void hvp_hostref_set_solver(int s) { g_solver = s; }
+void hvp_hostref_set_l1_solver(int s) { g_l1_solver = s; }
+void hvp_hostref_set_lp_trace(int s) { g_lp_trace = s; }
+void hvp_hostref_lp_stats(long long* out) {
+    out[0] = g_lp_runs;
+    out[1] = g_lp_iters;
+    out[2] = g_lp_fail;
+    for (int i = 1; i < 5; ++i) out[2 + i] = g_lp_why[i], g_lp_why[i] = 0;
+    g_lp_runs = g_lp_iters = g_lp_fail = 0;
+}
 void hvp_hostref_gi_stats(long long* out) {
     out[0] = g_gi_runs;
     out[1] = g_gi_fail;

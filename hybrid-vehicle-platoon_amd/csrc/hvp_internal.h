@@ -111,6 +111,8 @@ struct hvp_handle {
     void* gadmm_hs = nullptr;
     long long gadmm_hs_cap = 0;
     int gadmm_hs_valid = 0;
+    int32_t* gadmm_redo = nullptr;  // local QPs for the interior-point fallback (k_gadmm_ipm)
+    long long gadmm_redo_cap = 0;
     char* cent_split = nullptr;
     const int8_t* region_hint = nullptr;  // hvp_set_region_hint (copied into ws.hint per solve)
     // device copies of the workspace descriptors the refill kernel reads in its event code

@@ -728,6 +728,7 @@ void hvp_destroy(hvp_handle* h) {
     if (h->gadmm_hs) (void)hipFree(h->gadmm_hs);
     if (h->d_consts) (void)hipFree(h->d_consts);
     if (h->d_ws) (void)hipFree(h->d_ws);
+    if (h->gadmm_redo) (void)hipFree(h->gadmm_redo);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
     if (h->evq0) (void)hipEventDestroy(h->evq0);

@@ -19,6 +19,7 @@
 #include "hvp_internal.h"
 #include "hvp_admm.h"
 #include "hvp_bnb.h"
+#include "hvp_lp.h"
 #include "hvp_coop.h"
 #include "hvp_gi.h"
 #include "hvp_ipm.h"
@@ -733,10 +734,11 @@ __device__ inline double inc_of(const Workspace& ws, int inst) { return key_cost
 // QP path (both paths in one kernel pushed the lane kernels to 256 VGPRs + scratch spills)
 template <int N, int BS, bool ADMM>
 __device__ inline int bnb_qp(hvp::LaneQp<N, LdsMem<N, BS>>& q, const hvp_system& S, const hvp::Consts& C, int rl,
-                             const double* prm, uint64_t code, int K, double lo, double hi, double& cost) {
+                             const double* prm, uint64_t code, int K, double lo, double hi, double& cost,
+                             int cap = kGiMaxIter<N>) {
     int it = 0, st;
     if constexpr (ADMM) {
-        st = hvp::solve_admm_lane<N>(q, S, C, rl, prm, code, K, kGiMaxIter<N>, it);
+        st = hvp::solve_admm_lane<N>(q, S, C, rl, prm, code, K, cap, it);
         cost = st == hvp::GI_OK ? hvp::admm_direct_cost<N>(q, S, C, rl, prm, code, K) : 0.0;
     } else {
         hvp::setup_lane<N>(q, S, C, rl, prm, code, K, lo, hi);  // tail relaxed from v_K in [lo, hi]
@@ -1138,7 +1140,7 @@ __global__ __launch_bounds__(kCoopBlock) void k_bnb_bound_coop(int k, const hvp_
                     atomicMin(&ws.inc[inst], cost_key(c));
                 } else {
                     atomicOr(&ws.inst_flag[inst], 8);
-                    if (C.form == HVP_FORM_DECENT) {  // K_bnb_ipm re-solves it
+                    if (C.form == HVP_FORM_DECENT || C.form == HVP_FORM_ADMM) {  // K_bnb_ipm re-solves it
                         const unsigned long long r = atomicAdd(&ws.counter[2], 1ull);
                         if (r < (unsigned long long)ws.cap) ws.redo[r] = (int32_t)q;
                     }
@@ -1216,7 +1218,9 @@ __global__ __launch_bounds__(kBnbBlock<N>) HVP_LANE_OCC void k_bnb_bound(int k, 
         hvp::LaneQp<N, LdsMem<N, BS>> q;
         q.mem.lane = threadIdx.x;
         double c;
-        const int it = bnb_qp<N, BS, ADMM>(q, S, C, rl, prm, code, k, ws.nd_lo[dst][t], ws.nd_hi[dst][t], c);
+        // HVP_LEAF_GI_CAP (tests): the ADMM leaves' active-set cap, to send them through K_bnb_ipm
+        const int cap = ADMM && k == N && C.leaf_cap > 0 ? C.leaf_cap : kGiMaxIter<N>;
+        const int it = bnb_qp<N, BS, ADMM>(q, S, C, rl, prm, code, k, ws.nd_lo[dst][t], ws.nd_hi[dst][t], c, cap);
         const bool ok = it >= 0;
         const int its = ok ? it : -1 - it;
         iter_sum += (unsigned long long)its;
@@ -1238,7 +1242,7 @@ __global__ __launch_bounds__(kBnbBlock<N>) HVP_LANE_OCC void k_bnb_bound(int k, 
             } else {
                 ++fails;
                 atomicOr(&ws.inst_flag[inst], 8);  // a velocity-feasible sequence exists
-                if (C.form == HVP_FORM_DECENT) {  // K_bnb_ipm re-solves it
+                if (C.form == HVP_FORM_DECENT || C.form == HVP_FORM_ADMM) {  // K_bnb_ipm re-solves it
                     const unsigned long long r = atomicAdd(&ws.counter[2], 1ull);
                     if (r < (unsigned long long)ws.cap) ws.redo[r] = (int32_t)t;
                 }
@@ -1380,6 +1384,167 @@ __global__ __launch_bounds__(kL1BlockOf<N>) __attribute__((amdgpu_waves_per_eu(k
         }
     }
     if (lane == 0 && iter_sum) atomicAdd(&ws.counter[1], iter_sum);
+}
+
+// ---- min_1_norm by the per-lane simplex (hvp_lp.h), N <= 8: one node LP per LANE (64 per wave)
+// where k_l1_root / k_l1_bound spend a wavefront on each interior-point LP.  Same search, statuses
+// and bounds as those kernels (the LP optimum is the same; where it is a face the simplex returns
+// a vertex of it, the interior point a point inside -- equal costs).  The LP's per-step data live
+// in LDS (LdsMem rows, hvp_lp.h LF_*), its simplex state (vertex, basis inverse, basis ids) in
+// registers.
+template <int N>
+__device__ inline int lp_node(const hvp_system& S, const hvp::Consts& C, int rl, const double* prm, uint64_t code,
+                              int K, double rlo, double rhi, double* y, double& cost, int& it) {
+    constexpr int BS = kBnbBlock<N>;
+    hvp::LpData<N, LdsMem<N, BS>> D;
+    D.mem.lane = threadIdx.x;
+    const int st = hvp::lp_solve_l1<N>(D, S, C, rl, prm, code, K, rlo, rhi, C.max_iter, y, it);
+    cost = st == hvp::L1_OK ? hvp::l1_direct_cost<N>(y, S, C, rl, prm, code, K, rlo, rhi) : 0.0;
+    return st;
+}
+
+// the enumeration candidates' LPs, one per lane (k_cost prices them, as after k_qp_l1)
+template <int N>
+__global__ __launch_bounds__(kBnbBlock<N>) void k_qp_lp(const hvp_system* __restrict__ systems,
+                                                        const int32_t* __restrict__ sys,
+                                                        const int32_t* __restrict__ role,
+                                                        const double* __restrict__ params, hvp::Consts C,
+                                                        Workspace ws) {
+    constexpr int BS = kBnbBlock<N>;
+    const unsigned long long reserved = ws.counter[0];
+    const long long total = (long long)(reserved < (unsigned long long)ws.cap ? reserved : ws.cap);
+    unsigned long long iter_sum = 0;
+    for (long long t = (long long)blockIdx.x * BS + threadIdx.x; t < total; t += (long long)gridDim.x * BS) {
+        const int inst = ws.task_inst[t];
+        if (inst < 0) continue;  // dead slot of an overflowed instance
+        const hvp_system& S = systems[sys[inst]];
+        const double* prm = params + (size_t)inst * (2 + 6 * (N + 1));
+        hvp::LpData<N, LdsMem<N, BS>> D;
+        D.mem.lane = threadIdx.x;
+        double y[N];
+        int iters = 0;
+        const int status = hvp::lp_solve_l1<N>(D, S, C, role[inst], prm, ws.task_code[t], N, 0.0, -1.0, C.max_iter, y,
+                                               iters);
+        ws.task_stat[t] = status | (iters << 8);
+#pragma unroll
+        for (int k = 0; k < N; ++k) ws.task_y[t * N + k] = y[k];
+        iter_sum += (unsigned long long)iters;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) iter_sum += __shfl_down(iter_sum, off, 64);
+    if ((threadIdx.x & 63) == 0 && iter_sum) atomicAdd(&ws.counter[1], iter_sum);
+}
+
+template <int N>
+__global__ __launch_bounds__(kBnbBlock<N>) void k_lp_root(int B, const hvp_system* __restrict__ systems,
+                                                          const int32_t* __restrict__ sys,
+                                                          const int32_t* __restrict__ role,
+                                                          const double* __restrict__ params, hvp::Consts C,
+                                                          Workspace ws) {
+    constexpr int BS = kBnbBlock<N>;
+    const int i = blockIdx.x * BS + threadIdx.x;
+    if (i == 0) ws.lvl[0] = (unsigned long long)B;
+    if (i >= B) return;
+    const hvp_system& S = systems[sys[i]];
+    const int rl = role[i];
+    const double* prm = params + (size_t)i * C.stride;
+    const double v0 = prm[1], P1 = prm[0] + S.ts * v0;
+    const bool ok = P1 >= S.pmin - 1e-9 * (1.0 + fabs(S.pmin)) && P1 <= S.pmax + 1e-9 * (1.0 + fabs(S.pmax));
+    double inc = __longlong_as_double(0x7ff0000000000000ll);  // +inf: no incumbent
+    double lb = -1e300;
+    int nodes = 0, iters = 0;
+    // up to three LPs with ONE call site: 0 the root relaxation, 1 the greedy dive's leaf, 2 the
+    // hinted sequence's leaf
+    uint64_t code = 0, dive_code = 0;
+    int job = ok ? 0 : 3, K = 0;
+    double rlo = v0, rhi = v0;
+    bool dived = false;
+    while (job < 3) {
+        double y[N], c = 0.0;
+        int it = 0;
+        const int st = lp_node<N>(S, C, rl, prm, code, K, rlo, rhi, y, c, it);
+        ++nodes;
+        iters += it;
+        int next = 3;
+        if (job == 0) {
+            if (st == hvp::L1_INFEASIBLE) lb = 1e300;  // no completion is feasible
+            if (st == hvp::L1_OK) {
+                lb = c;
+                dived = hvp::bnb_dive<N>(S, C, v0, y, &dive_code);
+                next = dived ? 1 : 2;
+            }
+        } else {
+            if (st == hvp::L1_OK && !(c >= inc)) inc = c;
+            next = job + 1;
+        }
+        if (next == 1) code = dive_code;
+        if (next == 2) {
+            uint64_t hc = 0;
+            if (ws.hint && hint_code<N>(ws, i, S, C, v0, &hc) && !(dived && hc == dive_code)) code = hc;
+            else next = 3;
+        }
+        job = next;
+        K = N;
+        rlo = 0.0;
+        rhi = -1.0;
+    }
+    ws.key[i] = ~0ull;
+    ws.inst_flag[i] = ok ? 0 : 1;
+    ws.nd_inst[0][i] = ok ? i : -1;
+    ws.nd_code[0][i] = 0;
+    ws.nd_lo[0][i] = v0;
+    ws.nd_hi[0][i] = v0;
+    ws.nd_lb[0][i] = lb;
+    ws.inc[i] = cost_key(inc);
+    ws.nodes[i] = nodes;
+    ws.iters[i] = iters;
+    atomicAdd(&ws.counter[3], (unsigned long long)nodes);
+    atomicAdd(&ws.counter[1], (unsigned long long)iters);
+}
+
+template <int N>
+__global__ __launch_bounds__(kBnbBlock<N>) void k_lp_bound(int k, const hvp_system* __restrict__ systems,
+                                                           const int32_t* __restrict__ sys,
+                                                           const int32_t* __restrict__ role,
+                                                           const double* __restrict__ params, hvp::Consts C,
+                                                           Workspace ws) {
+    constexpr int BS = kBnbBlock<N>;
+    const int dst = k & 1;
+    const unsigned long long nn = ws.lvl[k];
+    const long long total = (long long)(nn < (unsigned long long)ws.cap ? nn : ws.cap);
+    unsigned long long iter_sum = 0;
+    for (long long t = (long long)blockIdx.x * BS + threadIdx.x; t < total; t += (long long)gridDim.x * BS) {
+        const int inst = ws.nd_inst[dst][t];
+        if (inst < 0) {  // dead slot of an overflowed reservation
+            if (k == N) ws.leaf_stat[t] = HVP_OVERFLOW;
+            else ws.nd_lb[dst][t] = 1e300;
+            continue;
+        }
+        const hvp_system& S = systems[sys[inst]];
+        const double* prm = params + (size_t)inst * C.stride;
+        double y[N], c = 0.0;
+        int it = 0;
+        const int st = lp_node<N>(S, C, role[inst], prm, ws.nd_code[dst][t], k, ws.nd_lo[dst][t], ws.nd_hi[dst][t],
+                                  y, c, it);
+        iter_sum += (unsigned long long)it;
+        atomicAdd(&ws.nodes[inst], 1);
+        atomicAdd(&ws.iters[inst], it);
+        if (k < N) {
+            // proven infeasible: the subtree holds no feasible completion; unresolved: prunes nothing
+            ws.nd_lb[dst][t] = st == hvp::L1_OK ? c : (st == hvp::L1_INFEASIBLE ? 1e300 : -1e300);
+            if (st == hvp::L1_FAIL) atomicAdd(&ws.counter[4], 1ull);
+        } else {
+            if (st == hvp::L1_OK) ws.nd_lb[dst][t] = c;  // an unresolved leaf keeps its parent's bound
+            ws.leaf_stat[t] = st == hvp::L1_OK ? 0 : (st == hvp::L1_INFEASIBLE ? HVP_INFEASIBLE : HVP_MAXITER);
+#pragma unroll
+            for (int j = 0; j < N; ++j) ws.task_y[t * N + j] = y[j];
+            if (st == hvp::L1_OK) atomicMin(&ws.inc[inst], cost_key(c));
+            if (st == hvp::L1_FAIL) atomicOr(&ws.inst_flag[inst], 8);  // a sequence exists, unresolved
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) iter_sum += __shfl_down(iter_sum, off, 64);
+    if ((threadIdx.x & 63) == 0 && iter_sum) atomicAdd(&ws.counter[1], iter_sum);
 }
 
 // ---- the same bound / leaf QPs, persistent waves (decentralised form, N <= 8)
@@ -1748,11 +1913,20 @@ __global__ __launch_bounds__(kBnbBlock<N>) void k_bnb_ipm(const hvp_system* __re
         const double* prm = params + (size_t)inst * C.stride;
         hvp::LaneQp<N, LdsMem<N, BS>> q;
         q.mem.lane = threadIdx.x;
-        hvp::setup_lane<N>(q, S, C, rl, prm, code);
-        const hvp::QpOut o = hvp::Solver<N, true, LdsMem<N, BS>>::solve(q, C);
-        atomicAdd(&ws.iters[inst], o.iters);
-        if (o.status != 0) continue;  // stays HVP_MAXITER with its parent's bound (K_key flags it)
-        const double c = hvp::direct_cost<N>(q, S, C, rl, prm, code);
+        double c;
+        if (C.form == HVP_FORM_ADMM) {  // the hinge-state iteration around the interior point
+            int its = 0;
+            const int st = hvp::solve_admm_ipm<N>(q, S, C, rl, prm, code, N, its);
+            atomicAdd(&ws.iters[inst], its);
+            if (st != hvp::GI_OK) continue;
+            c = hvp::admm_direct_cost<N>(q, S, C, rl, prm, code, N);
+        } else {
+            hvp::setup_lane<N>(q, S, C, rl, prm, code);
+            const hvp::QpOut o = hvp::Solver<N, true, LdsMem<N, BS>>::solve(q, C);
+            atomicAdd(&ws.iters[inst], o.iters);
+            if (o.status != 0) continue;  // stays HVP_MAXITER with its parent's bound (K_key flags it)
+            c = hvp::direct_cost<N>(q, S, C, rl, prm, code);
+        }
 #pragma unroll
         for (int j = 0; j < N; ++j) ws.task_y[t * N + j] = q.y[j];
         ws.nd_lb[src][t] = c;
@@ -1775,13 +1949,12 @@ __global__ __launch_bounds__(kBlock) void k_bnb_key(Workspace ws, int form, int 
         if (inst < 0) continue;
         const double best = inc_of(ws, inst);
         if (ws.leaf_stat[t] != 0) {
-            // A decentralised leaf that fails the active-set method AND the interior-point
-            // fallback (K_bnb_ipm, every N) is an infeasible QP (position box), excluded exactly as
-            // the enumeration path and the oracle exclude it.  The other forms have no fallback: a
-            // failed leaf still in contention makes the instance MAXITER rather than a possibly
-            // wrong answer.  The min_1_norm leaves are HVP_INFEASIBLE (certified, excluded) or
-            // HVP_MAXITER (unresolved).
-            const bool strict = form != HVP_FORM_DECENT || l1;
+            // A decentralised or naive-ADMM leaf that fails the active-set method AND the
+            // interior-point fallback (K_bnb_ipm, every N) is an infeasible QP (position box),
+            // excluded exactly as the enumeration path and the oracle exclude it.  The min_1_norm
+            // leaves are HVP_INFEASIBLE (certified, excluded) or HVP_MAXITER (unresolved: a leaf
+            // still in contention makes the instance MAXITER rather than a possibly wrong answer).
+            const bool strict = (form != HVP_FORM_DECENT && form != HVP_FORM_ADMM) || l1;
             if (ws.leaf_stat[t] == HVP_MAXITER && strict && !hvp::bnb_pruned(ws.nd_lb[src][t], best))
                 atomicOr(&ws.inst_flag[inst], 4);
             continue;
@@ -1981,6 +2154,14 @@ __device__ inline void gadmm_fail(int32_t* state, int p) {
     atomicAnd(&state[p], ~1);
 }
 
+// a local QP the active-set method failed on goes to k_gadmm_ipm (counter[3]: the list's size in
+// this launch; counter[2]: the fallbacks since the rollout, hvp_get_stats n_fallback)
+__device__ inline void gadmm_redo(int b, unsigned long long* counter, int32_t* redo) {
+    const unsigned long long r = atomicAdd(&counter[3], 1ull);
+    atomicAdd(&counter[2], 1ull);
+    redo[r] = b;  // r < P m: one entry per local QP and launch
+}
+
 // first region whose closed velocity band holds v (buf widens the lower edge: the [0, 1e-4]
 // buffer of PwaGearVehicle.find_region used by get_u_for_constant_vel, models.py:519-540)
 __device__ inline int gadmm_region(const hvp_system& S, double v, double buf) {
@@ -2100,7 +2281,8 @@ __global__ __launch_bounds__(kBnbBlock<N>) void k_gadmm_qp(int P, int n, int lo,
                                                            int32_t* __restrict__ status_out,
                                                            uint32_t* __restrict__ edge_out,
                                                            int32_t* __restrict__ iters_out,
-                                                           unsigned long long* __restrict__ counter) {
+                                                           unsigned long long* __restrict__ counter,
+                                                           int32_t* __restrict__ redo) {
     constexpr int BS = kBnbBlock<N>;
     const int b = blockIdx.x * BS + threadIdx.x;
     if (b >= P * m) return;
@@ -2114,7 +2296,8 @@ __global__ __launch_bounds__(kBnbBlock<N>) void k_gadmm_qp(int P, int n, int lo,
     q.mem.lane = threadIdx.x;
     int it = 0;
     uint32_t raw = 0;
-    const int st = hvp::solve_admm_lane<N>(q, S, C, rl, prm, code, N, kGiMaxIter<N>, it, &raw);
+    const int cap = C.leaf_cap > 0 ? C.leaf_cap : kGiMaxIter<N>;  // HVP_LEAF_GI_CAP: tests of k_gadmm_ipm
+    const int st = hvp::solve_admm_lane<N>(q, S, C, rl, prm, code, N, cap, it, &raw);
     if (iters_out) iters_out[b] = it;
     atomicAdd(&counter[1], (unsigned long long)it);
     if (st == hvp::GI_OK) {
@@ -2123,10 +2306,7 @@ __global__ __launch_bounds__(kBnbBlock<N>) void k_gadmm_qp(int P, int n, int lo,
         edge_out[b] = gadmm_edges<N>(S, code, raw);
         gadmm_write<N>(b, gadmm_slot(b, n, lo, m), S, C, rl, prm, code, q.y, u_out, x, xf, xb);
     } else {
-        cost_out[b] = 1e300;
-        status_out[b] = st == hvp::GI_FAIL_DUAL ? HVP_INFEASIBLE : HVP_MAXITER;
-        edge_out[b] = 0;
-        gadmm_fail(state, p);
+        gadmm_redo(b, counter, redo);
     }
 }
 
@@ -2145,7 +2325,8 @@ __global__ __launch_bounds__(kCoopBlock) void k_gadmm_qp_coop(int P, int n, int 
                                                               uint32_t* __restrict__ edge_out,
                                                               int32_t* __restrict__ iters_out,
                                                               unsigned long long* __restrict__ counter,
-                                                              hvp::coop::WarmQp* __restrict__ warm_ws, int warm) {
+                                                              hvp::coop::WarmQp* __restrict__ warm_ws, int warm,
+                                                              int32_t* __restrict__ redo) {
     __shared__ hvp::coop::GroupLds lds[kCoopGroups];
     const int g = threadIdx.x / hvp::coop::G, t = threadIdx.x % hvp::coop::G;
     const int b = blockIdx.x * kCoopGroups + g;
@@ -2160,7 +2341,8 @@ __global__ __launch_bounds__(kCoopBlock) void k_gadmm_qp_coop(int P, int n, int 
     double cost = 0.0;
     int it = 0;
     unsigned raw = 0;
-    const int st = hvp::coop::solve_qp<N>(L, lds[g], S, C, rl, prm, code, N, kGiMaxIter<N>, it, &cost, &raw, 0.0,
+    const int cap = C.leaf_cap > 0 ? C.leaf_cap : kGiMaxIter<N>;  // HVP_LEAF_GI_CAP: tests of k_gadmm_ipm
+    const int st = hvp::coop::solve_qp<N>(L, lds[g], S, C, rl, prm, code, N, cap, it, &cost, &raw, 0.0,
                                           -1.0, warm_ws ? warm_ws + b : nullptr, warm != 0,
                                           ((uint64_t)(uint32_t)sys[b] << 32) | (uint32_t)rl);
     if (st == hvp::GI_OK) {
@@ -2179,10 +2361,57 @@ __global__ __launch_bounds__(kCoopBlock) void k_gadmm_qp_coop(int P, int n, int 
         edge_out[b] = gadmm_edges<N>(S, code, raw);
         gadmm_write<N>(b, gadmm_slot(b, n, lo, m), S, C, rl, prm, code, y, u_out, x, xf, xb);
     } else {
-        cost_out[b] = 1e300;
-        status_out[b] = st == hvp::GI_FAIL_DUAL ? HVP_INFEASIBLE : HVP_MAXITER;
-        edge_out[b] = 0;
-        gadmm_fail(state, p);
+        gadmm_redo(b, counter, redo);
+    }
+}
+
+// Local QPs the active-set method failed on (k_gadmm_qp / _coop put them on the redo list):
+// re-solved by the interior point inside the hinge-state iteration (hvp_admm.h solve_admm_ipm),
+// one lane per QP.  Only a QP that fails here too fails its platoon (gadmm_fail), as a qpOASES
+// failure fails the reference's local solve (fleet_g_admm.py:162,195-205).  Normally an empty list.
+template <int N>
+__global__ __launch_bounds__(kBnbBlock<N>) void k_gadmm_ipm(int P, int n, int lo, int m,
+                                                            const hvp_system* __restrict__ systems,
+                                                            const int32_t* __restrict__ sys,
+                                                            const int32_t* __restrict__ role,
+                                                            const double* __restrict__ params, hvp::Consts C,
+                                                            const int8_t* __restrict__ seq,
+                                                            int32_t* __restrict__ state, double* __restrict__ u_out,
+                                                            double* __restrict__ x, double* __restrict__ xf,
+                                                            double* __restrict__ xb, double* __restrict__ cost_out,
+                                                            int32_t* __restrict__ status_out,
+                                                            uint32_t* __restrict__ edge_out,
+                                                            int32_t* __restrict__ iters_out,
+                                                            unsigned long long* __restrict__ counter,
+                                                            const int32_t* __restrict__ redo) {
+    constexpr int BS = kBnbBlock<N>;
+    const unsigned long long nr = counter[3];
+    const long long total = (long long)(nr < (unsigned long long)P * m ? nr : (unsigned long long)P * m);
+    for (long long i = (long long)blockIdx.x * BS + threadIdx.x; i < total; i += (long long)gridDim.x * BS) {
+        const int b = redo[i];
+        const int p = b / m;
+        const hvp_system& S = systems[sys[b]];
+        const int rl = role[b];
+        const double* prm = params + (size_t)b * C.stride;
+        const uint64_t code = gadmm_code<N>(seq, b);
+        hvp::LaneQp<N, LdsMem<N, BS>> q;
+        q.mem.lane = threadIdx.x;
+        int it = 0;
+        uint32_t raw = 0;
+        const int st = hvp::solve_admm_ipm<N>(q, S, C, rl, prm, code, N, it, &raw);
+        if (iters_out) iters_out[b] += it;
+        atomicAdd(&counter[1], (unsigned long long)it);
+        if (st == hvp::GI_OK) {
+            cost_out[b] = hvp::admm_direct_cost<N>(q, S, C, rl, prm, code, N);
+            status_out[b] = HVP_OPTIMAL;
+            edge_out[b] = gadmm_edges<N>(S, code, raw);
+            gadmm_write<N>(b, gadmm_slot(b, n, lo, m), S, C, rl, prm, code, q.y, u_out, x, xf, xb);
+        } else {
+            cost_out[b] = 1e300;
+            status_out[b] = HVP_MAXITER;
+            edge_out[b] = 0;
+            gadmm_fail(state, p);
+        }
     }
 }
 
@@ -2237,7 +2466,15 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
     const size_t lds = sizeof(double) * hvp::F_COUNT * N * BS;
     HIP_TRY(hipEventRecord(h->evb[0], st));
     const int g_l1 = std::max(1, h->n_cu) * (N <= HVP_MAX_N_ENUM ? 8 : 16);  // waves grid-stride over nodes
-    if (h->C.l1) {
+    // min_1_norm: the per-lane simplex up to N = 8 (HVP_L1_SIMPLEX=0: the wave interior point, A/B)
+    const char* lsx = std::getenv("HVP_L1_SIMPLEX");
+    const bool lp_lane = h->C.l1 && !kCoop<N> && !(lsx && lsx[0] == '0');
+    const size_t lds_lp = sizeof(double) * hvp::LF_COUNT * N * BS;
+    if (lp_lane) {
+        if constexpr (!kCoop<N>)
+            hipLaunchKernelGGL(k_lp_root<N>, dim3((B + BS - 1) / BS), dim3(BS), lds_lp, st, B, h->d_sys, sys, role,
+                               params, h->C, ws);
+    } else if (h->C.l1) {
         hipLaunchKernelGGL(k_l1_root<N>, dim3(g_l1), dim3(kL1BlockOf<N>), 0, st, B, h->d_sys, sys, role, params, h->C,
                            ws);
     } else if constexpr (kCoop<N>) {
@@ -2289,7 +2526,11 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
             hipLaunchKernelGGL(k_bnb_expand<N>, dim3(g_small), dim3(kBlock), 0, st, k, h->d_sys, sys, h->C, ws);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(h->evb[2 * k], st));
-        if (h->C.l1) {
+        if (lp_lane) {
+            if constexpr (!kCoop<N>)
+                hipLaunchKernelGGL(k_lp_bound<N>, dim3(g_qp), dim3(BS), lds_lp, st, k, h->d_sys, sys, role, params,
+                                   h->C, ws);
+        } else if (h->C.l1) {
             hipLaunchKernelGGL(k_l1_bound<N>, dim3(g_l1), dim3(kL1BlockOf<N>), 0, st, k, h->d_sys, sys, role, params,
                                h->C, ws);
         } else if constexpr (kCoop<N>) {
@@ -2313,7 +2554,7 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
         HIP_TRY(hipEventRecord(h->evb[2 * k + 1], st));
     }
     HIP_TRY(hipEventRecord(h->evq1, st));
-    if (h->C.form == HVP_FORM_DECENT && !h->C.l1) {  // failed leaves (normally none: reads a zero count)
+    if ((h->C.form == HVP_FORM_DECENT || h->C.form == HVP_FORM_ADMM) && !h->C.l1) {  // failed leaves (normally none: reads a zero count)
         hipLaunchKernelGGL(k_bnb_ipm<N>, dim3(std::max(1, h->n_cu)), dim3(BS), lds, st, h->d_sys, sys, role, params,
                            h->C, ws);
         HIP_TRY(hipGetLastError());
@@ -2362,8 +2603,18 @@ int launch_all(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
     const long long want = std::min<long long>(grid_for(h->ws.cap), (long long)h->n_cu * 8);
     HIP_TRY(hipEventRecord(h->evq0, st));
     const size_t lds = sizeof(double) * hvp::F_COUNT * N * kBlock;
-    if (h->C.l1) {
-        // min_1_norm: the fixed-sequence LPs, one per wavefront (wave grid-stride over the candidates)
+    const char* lsx = std::getenv("HVP_L1_SIMPLEX");
+    if (h->C.l1 && !(lsx && lsx[0] == '0')) {
+        // min_1_norm: the fixed-sequence LPs by the per-lane simplex (hvp_lp.h), one per lane
+        constexpr int BS = kBnbBlock<N>;
+        hipLaunchKernelGGL(k_qp_lp<N>, dim3((int)std::min<long long>((h->ws.cap + BS - 1) / BS, (long long)h->n_cu * 8)),
+                           dim3(BS), sizeof(double) * hvp::LF_COUNT * N * BS, st, h->d_sys, sys, role, params, h->C,
+                           ws);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(h->evq1, st));
+    } else if (h->C.l1) {
+        // min_1_norm: the fixed-sequence LPs, one per wavefront (wave grid-stride over the candidates;
+        // HVP_L1_SIMPLEX=0, A/B)
         hipLaunchKernelGGL(k_qp_l1<N>, dim3(std::max(1, h->n_cu) * 8), dim3(kL1Block), 0, st, h->d_sys, sys, role,
                            params, h->C, ws);
         HIP_TRY(hipGetLastError());
@@ -2395,6 +2646,16 @@ int launch_gadmm_qp(hvp_handle* h, int P, int n, int lo, int m, const int32_t* s
                            double* xf, double* xb, double* cost_out, int32_t* status_out, uint32_t* edge_out,
                            int32_t* iters_out, hipStream_t st) {
     const int B = P * m;
+    if (B > h->gadmm_redo_cap) {  // the interior-point fallback's list (k_gadmm_ipm)
+        HIP_TRY(hipDeviceSynchronize());
+        (void)hipFree(h->gadmm_redo);
+        h->gadmm_redo = nullptr;
+        h->gadmm_redo_cap = 0;
+        if (hipMalloc(&h->gadmm_redo, sizeof(int32_t) * (size_t)B) != hipSuccess)
+            return fail(HVP_E_NOMEM, "hvp_gadmm_solve: device allocation failed");
+        h->gadmm_redo_cap = B;
+    }
+    HIP_TRY(hipMemsetAsync(h->g_counter + 3, 0, sizeof(unsigned long long), st));
     HIP_TRY(hipEventRecord(h->evq0, st));
     if constexpr (kCoop<N>) {
         // each local QP's final hinge states, active set and factors, carried from one ADMM
@@ -2414,16 +2675,24 @@ int launch_gadmm_qp(hvp_handle* h, int P, int n, int lo, int m, const int32_t* s
         hipLaunchKernelGGL(k_gadmm_qp_coop<N>, dim3((B + kCoopGroups - 1) / kCoopGroups), dim3(kCoopBlock), 0, st, P, n,
                            lo, m, h->d_sys, sys, role, params, h->C, seq, state, u_out, x, xf, xb, cost_out,
                            status_out, edge_out, iters_out, h->g_counter,
-                           reinterpret_cast<hvp::coop::WarmQp*>(h->gadmm_hs), use);
+                           reinterpret_cast<hvp::coop::WarmQp*>(h->gadmm_hs), use, h->gadmm_redo);
         h->gadmm_hs_valid = 1;
     } else {
         constexpr int BS = kBnbBlock<N>;
         const size_t lds = sizeof(double) * hvp::F_COUNT * N * BS;
         hipLaunchKernelGGL(k_gadmm_qp<N>, dim3((B + BS - 1) / BS), dim3(BS), lds, st, P, n, lo, m, h->d_sys, sys, role,
                            params, h->C, seq, state, u_out, x, xf, xb, cost_out, status_out, edge_out, iters_out,
-                           h->g_counter);
+                           h->g_counter, h->gadmm_redo);
     }
     HIP_TRY(hipGetLastError());
+    {  // failed local QPs (normally none: reads a zero count)
+        constexpr int BS = kBnbBlock<N>;
+        const size_t lds = sizeof(double) * hvp::F_COUNT * N * BS;
+        hipLaunchKernelGGL(k_gadmm_ipm<N>, dim3(std::max(1, h->n_cu)), dim3(BS), lds, st, P, n, lo, m, h->d_sys, sys,
+                           role, params, h->C, seq, state, u_out, x, xf, xb, cost_out, status_out, edge_out, iters_out,
+                           h->g_counter, h->gadmm_redo);
+        HIP_TRY(hipGetLastError());
+    }
     HIP_TRY(hipEventRecord(h->evq1, st));
     h->last_stream = st;
     h->last_B = B;

@@ -179,6 +179,11 @@ typedef struct hvp_stats {
 
 int hvp_create(hvp_handle** out, const hvp_problem* problem, const hvp_system* systems,
                int n_systems, int device);
+/* Workspace for batches up to max_batch.  candidate_capacity (<= 0: a default per method) is, for
+ * branch and bound, the node capacity of ONE tree level pooled over the batch.  The decentralised
+ * min_2_norm lane path (N <= 8) keeps every level in 2 buckets (HVP_SPLIT_LEVELS: 1, 2 or 4) of
+ * capacity / buckets nodes each; an instance whose children do not fit its bucket is reported
+ * HVP_OVERFLOW (never truncated) and can be re-solved alone with a larger reserve. */
 int hvp_reserve(hvp_handle* h, int max_batch, int64_t candidate_capacity);
 /* Device-pointer entry point (async on stream).  Outputs may be NULL except cost/status. */
 int hvp_solve_batch(hvp_handle* h, int B, const int32_t* sys, const int32_t* role,

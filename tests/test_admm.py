@@ -347,3 +347,47 @@ def test_region_hint_is_checked(gpu_available):
     out = s.solve_device(t(np.zeros(B, np.int32)), t(roles), t(params))
     torch.cuda.synchronize()
     assert out["status"].shape == (B,)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N", [5, 10])
+def test_admm_leaf_fallback(gpu_available, monkeypatch, N):
+    """Naive-ADMM leaves whose active-set solve fails are re-solved by the interior point inside
+    the hinge-state iteration (K_bnb_ipm, hvp_admm.h solve_admm_ipm) instead of turning the
+    instance into HVP_MAXITER.  Forced by capping the leaves' active-set steps
+    (HVP_LEAF_GI_CAP=2, read at hvp_create): the lane path (N = 5) and the 16-lane path (N = 10)
+    still return the oracle's answers (fleet_naive_admm.py:407-419 gets them from Gurobi)."""
+    from hvp.admm import admm_problem
+    from hvp.solver import BatchSolver
+
+    monkeypatch.setenv("HVP_LEAF_GI_CAP", "2")
+    fx = load(f"admm_local_N{N}.npz")
+    s = BatchSolver(admm_problem(N, float(fx["rho"])), [_system()])
+    B = len(fx["roles"])
+    res = s.solve_admm(np.zeros(B, np.int32), fx["roles"], fx["params"])
+    assert s.stats().n_fallback > 0
+    _check(fx, res.u, res.x, res.region, res.cost, res.status, res.x_front, res.x_back)
+
+
+@pytest.mark.gpu
+def test_admm_coordinator_leaf_fallback(gpu_available, monkeypatch):
+    """configs[2] at its own size (n = 10, N = 10, 20 iterations) with every leaf forced through
+    the interior-point fallback: the coordinator's controls are still the oracle's."""
+    import torch
+
+    from hvp.admm import AdmmEngine, admm_problem
+    from instances import leader_window
+
+    monkeypatch.setenv("HVP_LEAF_GI_CAP", "2")
+    fx = load("admm_steps_n10_N10.npz")
+    n, N, iters = int(fx["n"]), int(fx["N"]), int(fx["iters"])
+    roles = [O.role_bits(i, n) for i in range(n)]
+    eng = AdmmEngine(admm_problem(N, float(fx["rho"])), [_system()], np.zeros(n, np.int32), roles, n, 1)
+    for t in range(len(fx["states"])):
+        eng.set_leader(leader_window(N, t))
+        o = eng.step(fx["states"][t][None], iters)
+        torch.cuda.synchronize()
+        assert (o["status"] == 0).all()
+        assert np.abs(o["u"].cpu().numpy() - fx["exp_u"][t][-1]).max() <= 1e-6, t
+        assert np.abs(o["x"].cpu().numpy() - fx["exp_x"][t][-1]).max() <= 1e-4, t
+    assert eng.solver.stats().n_fallback > 0

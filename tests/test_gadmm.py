@@ -421,3 +421,37 @@ def test_gadmm_warm_records_never_start_another_qp(gpu_available):
     c, cf = again["cost"][ok], fresh["cost"][ok]
     assert np.all(np.abs(c - cf) <= 1e-10 * np.maximum(1.0, np.abs(cf)))
     assert np.array_equal(again["edge"][ok], fresh["edge"][ok])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N", [5, 10])
+def test_gadmm_local_problem_ipm_fallback(gpu_available, monkeypatch, N):
+    """Switching-ADMM local QPs whose active-set solve fails go to k_gadmm_ipm (the interior point
+    inside the hinge-state iteration, hvp_admm.h solve_admm_ipm) instead of failing their
+    platoon.  Forced with HVP_LEAF_GI_CAP=2: the traced local problems still give the oracle's
+    u, trajectories, copies, costs and the switching rule's edge bits (fleet_g_admm.py:162,195-205
+    gets them from qpOASES)."""
+    from hvp.gadmm import gadmm_problem
+    from hvp.solver import BatchSolver
+
+    monkeypatch.setenv("HVP_LEAF_GI_CAP", "2")
+    fx = load(f"gadmm_local_N{N}.npz")
+    B = len(fx["roles"])
+    solver = BatchSolver(gadmm_problem(N, float(fx["rho"])), [_system()])
+    r = _gadmm_local_call(solver, N, np.zeros(B), fx["roles"], fx["params"], fx["seq"])
+    assert solver.stats().n_fallback > 0
+    _check_local(fx, r["u"], r["x"], r["xf"], r["xb"], r["cost"], r["status"], r["edge"].astype(np.uint32))
+
+
+@pytest.mark.gpu
+def test_gadmm_engine_ipm_fallback(gpu_available, monkeypatch):
+    """configs[3] at its own size (n = 20, N = 10, 100 ADMM iterations, 2 seeds x 2 steps) with the
+    local QPs forced through the interior-point fallback: the device coordinator still matches
+    the oracle coordinator (sequences, rounds, warm-start choices, controls, costs)."""
+    monkeypatch.setenv("HVP_LEAF_GI_CAP", "2")
+    fx = load("gadmm_steps_n20_N10.npz")
+    P = len(fx["states"]) // int(fx["steps"])
+    eng = _engine(fx, P)
+    outs = _run_steps(fx, [eng])
+    _check_steps(fx, [o[0] for o in outs])
+    assert eng.solver.stats().n_fallback > 0

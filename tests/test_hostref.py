@@ -160,3 +160,37 @@ def test_l1_branch_and_bound_matches_golden(hostref, name):
     assert np.abs(out["x"] - fx["exp_x"]).max() <= 1e-4
     if int(fx["N"]) >= 5 and int(fx.get("method", 0)) == 0:  # exp_nodes = sequences enumerated
         assert out["nodes"].mean() < fx["exp_nodes"].mean()
+
+
+@pytest.mark.parametrize("name", l1_fixture_names())
+def test_l1_simplex_matches_interior_point_and_golden(hostref, name):
+    """The per-lane simplex of the min_1_norm LPs (csrc/hvp_lp.h, the product's solver up to N = 8)
+    against the interior point (hvp_l1.h) on the same searches and against the oracle's fixtures:
+    statuses and regions exact, costs 1e-9 relative (both are the LP optimum), u 1e-6 (the fixtures'
+    LP optima are unique vertices).  No LP is left unresolved."""
+    import ctypes
+
+    fx = load(name)
+    N = int(fx["N"])
+    if N > 8:
+        pytest.skip("the simplex is the lane path (N <= 8); longer horizons keep the interior point")
+    stats = (ctypes.c_longlong * 7)()
+    for method in (1, 2):
+        prob, systems = product_problem(fx)
+        prob.method = method
+        res = {}
+        for solver in (0, 1):
+            hostref.hvp_hostref_set_l1_solver(solver)
+            res[solver] = run(hostref, prob, systems, fx)
+            hostref.hvp_hostref_lp_stats(stats)
+            if solver == 1:
+                assert stats[0] > 0 and stats[2] == 0, list(stats)  # LPs run, none unresolved
+        hostref.hvp_hostref_set_l1_solver(1)
+        a, b = res[0], res[1]
+        ok = fx["exp_status"] == 0
+        for r in (a, b):
+            assert np.array_equal(r["status"], fx["exp_status"])
+            assert np.array_equal(r["region"][ok], fx["exp_region"][ok])
+            ce = fx["exp_cost"][ok]
+            assert np.all(np.abs(r["cost"][ok] - ce) <= 1e-9 * np.maximum(1, np.abs(ce)))
+            assert np.abs(r["u"][ok] - fx["exp_u"][ok]).max() <= 1e-6
