@@ -276,6 +276,16 @@ void solve_one_bnb(const hvp_system& S, const hvp::Consts& C, int role, const do
             uint64_t code;
             double c1;
             if (hvp::bnb_dive<N>(S, C, v0, root.y, &code) && qp(code, N, 0.0, -1.0, c1, nullptr)) inc = c1;
+            if (C.l1 && g_l1_solver == 1 && N <= HVP_MAX_N_ENUM) {
+                // the simplex's root optimum is a vertex (an extreme point where the LP optimum is a
+                // face): a second dive towards the constant-velocity trajectory (k_lp_root)
+                double yt[N];
+                for (int i = 0; i < N; ++i) yt[i] = v0;
+                uint64_t code2;
+                double c2;
+                if (hvp::bnb_dive<N>(S, C, v0, yt, &code2) && code2 != code && qp(code2, N, 0.0, -1.0, c2, nullptr))
+                    inc = fmin(inc, c2);
+            }
         } else if (C.l1 && l1_st == hvp::L1_INFEASIBLE) {
             root.lb = 1e300;  // the root relaxation is infeasible: so is every sequence
         }
