@@ -348,7 +348,10 @@ int hvp_cent_solve_batch(hvp_handle* h, int P, int n, int leader_index, int real
     using hvp::cent::kTie;
     using hvp::cent::kTieG;
     const int waves = std::max(1, h->n_cu) * 3;  // LDS: three wave QPs per CU
-    const long long task_cap = std::max<long long>(1 << 16, 64LL * P);
+    // task list capacity; a search whose open frames do not fit searches on in its wave (hvp_cent_bnb.h
+    // export_tasks).  HVP_CENT_TASK_CAP (tests) shrinks it to exercise that path.
+    long long task_cap = std::max<long long>(1 << 16, 64LL * P);
+    if (const char* tc = std::getenv("HVP_CENT_TASK_CAP")) task_cap = std::max<long long>(1, std::atoll(tc));
     auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
     const size_t b_rec = al(sizeof(hvp::cent::PlatoonRec) * P), b_tg = al(sizeof(uint64_t) * P * kTieG * n),
                  b_tgc = al(sizeof(double) * P * kTieG), b_task = al(sizeof(hvp::cent::Task) * task_cap),

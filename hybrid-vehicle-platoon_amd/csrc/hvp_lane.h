@@ -1764,12 +1764,11 @@ __device__ inline const T* uniform_opaque(const T* p) {
 // into scratch.)
 template <int N>
 __global__ __launch_bounds__(kBnbBlock<N>) __attribute__((amdgpu_waves_per_eu(HVP_REFILL_WAVES)))
-void k_bnb_bound_refill(int k, const hvp_system* __restrict__ systems, const int32_t* __restrict__ sys,
+void k_bnb_bound_refill(int k_arg, const hvp_system* __restrict__ systems, const int32_t* __restrict__ sys,
                         const int32_t* __restrict__ role, const double* __restrict__ params, hvp::Consts C,
                         const Workspace* __restrict__ wsd, const hvp::Consts* __restrict__ cd) {
     constexpr int BS = kBnbBlock<N>;
     static_assert(N <= HVP_MAX_N_ENUM, "lane refill is the N <= 8 path");
-    const int dst = k & 1;
     const int lane = threadIdx.x & 63;
     hvp::LaneQp<N, LdsMem<N, BS>> q;
     q.mem.lane = threadIdx.x;
@@ -1806,6 +1805,11 @@ void k_bnb_bound_refill(int k, const hvp_system* __restrict__ systems, const int
             // ---- event: write the finished lanes' results, then refill every free lane
             const Workspace& ws = *uniform_opaque(wsd);
             const hvp::Consts& Ce = *uniform_opaque(cd);
+            // the level, opaque here: the per-step tests on it (k < K in the QP set-up and the
+            // direct cost) are evaluated inside the event, not hoisted as spilled lane masks
+            int k = k_arg;
+            asm volatile("" : "+s"(k));
+            const int dst = k & 1;
             unsigned cmask = 0;  // children of a finished bound node (k_bnb_expand's work, fused)
             double clb = 0.0;
             if (done) {

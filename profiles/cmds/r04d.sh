@@ -1,0 +1,15 @@
+# r04d: hash-stamped profiles of the current library (the five bench workloads: kernel trace + separate
+# PMC passes), summarised on the box so the bench lines that follow use them, then the bench lines
+set -o pipefail
+export TMPDIR=/tmp
+R=${1:-r04d}
+bash profiles/profile_all.sh gpurun_out/$R || exit 1
+mkdir -p gpurun_out/${R}_sum
+for w in decent_n10_N5_P16384 decent_n10_N5_l1_P16384 admm_n10_N10_P512 gadmm_n20_N10_P2048 cent_n10_N5_P4096; do
+  python profiles/summarize.py gpurun_out/$R/$w $R $w > /dev/null && cp profiles/${R}_${w}_* gpurun_out/${R}_sum/ || exit 1
+done
+timeout -k 10 400 python bench.py > gpurun_out/${R}_bench_default.jsonl 2> gpurun_out/${R}_bench_default.err || exit 2
+timeout -k 10 300 python bench.py --cost l1 --steps 5 --warmup 1 > gpurun_out/${R}_bench_l1.jsonl 2> gpurun_out/${R}_bench_l1.err || exit 3
+timeout -k 10 300 python bench.py --controller admm --n 10 --N 10 --platoons 1024 --steps 3 --warmup 1 > gpurun_out/${R}_bench_admm.jsonl 2> gpurun_out/${R}_bench_admm.err || exit 4
+timeout -k 10 300 python bench.py --controller gadmm --n 20 --N 10 --platoons 4096 --steps 3 --warmup 1 > gpurun_out/${R}_bench_gadmm.jsonl 2> gpurun_out/${R}_bench_gadmm.err || exit 5
+timeout -k 10 300 python bench.py --controller cent --n 10 --N 5 --platoons 4096 --steps 1 --warmup 0 > gpurun_out/${R}_bench_cent.jsonl 2> gpurun_out/${R}_bench_cent.err || exit 6

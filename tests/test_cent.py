@@ -437,3 +437,28 @@ def test_gpu_mpc_cent_l1_drop_in_and_simulate(gpu_available):
     X, U, R, agent, env = simulate(sim, seed=2)
     assert X.shape[0] == sim.ep_len + 1 and U.shape[0] == sim.ep_len
     assert np.all(agent.node_counts > 0) and np.all(np.isfinite(R))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["cent_n6_N5.npz", "cent_n8_N5.npz", "cent_l1_n4_N5.npz"])
+def test_gpu_full_task_list_declines_the_split(gpu_available, monkeypatch, name):
+    """the split-task list used to overflow (HVP_OVERFLOW) when heavy searches exported
+    more open frames than it holds.  Exports now reserve their slots at once or not at all: with a
+    4-task list and a split every 10 QPs most exports are declined and those searches go on in their
+    own wave -- no HVP_OVERFLOW, the oracle's answers."""
+    from hvp import _abi
+
+    monkeypatch.setenv("HVP_CENT_SPLIT", "10")
+    monkeypatch.setenv("HVP_CENT_TASK_BUDGET", "16")
+    monkeypatch.setenv("HVP_CENT_TASK_CAP", "4")
+    fx = load(name)
+    s, sys_idx = _product(fx)
+    for lead_idx, lsp in sorted({(int(a), int(b)) for a, b in zip(fx["leader_index"], fx["lsp"])}):
+        sel = np.flatnonzero((fx["leader_index"] == lead_idx) & (fx["lsp"] == lsp))
+        res = s.solve(sys_idx[sel], fx["x0"][sel], fx["leader_x"][sel], lead_idx, bool(lsp))
+        assert not (res.status == _abi.OVERFLOW).any(), res.status
+        for j, p in enumerate(sel):
+            assert res.status[j] == fx["exp_status"][p], (name, p, res.status[j])
+            if fx["exp_status"][p] == 0:
+                assert np.array_equal(res.region[j], fx["exp_region"][p]), (name, p)
+                assert abs(res.cost[j] - fx["exp_cost"][p]) <= 1e-9 * abs(fx["exp_cost"][p]), (name, p)
