@@ -322,11 +322,20 @@ HVP_HD inline int lp_simplex(const LpData<N, MEM>& D, const Consts& C, int max_i
     const double dtol = 1e-11 * wmax;  // edge derivatives within -dtol of zero count as >= 0
     int basis[N];
     double Bi[N][N];  // A_B^-1 (A_B y = -b_B)
+    // the basic terms' offsets and slopes (updated at each pivot: no lookup of basic terms per
+    // iteration; A_B^-1 by rank-1 updates, rebuilt from the normals every kLpRefresh pivots)
+    double bB[N], spB[N], smB[N];
+    constexpr int kLpRefresh = 12;
+    int since = 0;
     // start: the V rows nearest v0 (A_B = I)
 #pragma unroll
     for (int j = 0; j < N; ++j) {
-        const bool up = fabs(D.mem.get(LF_VHI, j) - D.v0) < fabs(D.v0 - D.mem.get(LF_VLO, j));
+        const double vlo = D.mem.get(LF_VLO, j), vhi = D.mem.get(LF_VHI, j);
+        const bool up = fabs(vhi - D.v0) < fabs(D.v0 - vlo);
         basis[j] = 6 * j + (up ? 1 : 0);
+        bB[j] = -(up ? vhi : vlo);
+        spB[j] = up ? D.M : 0.0;
+        smB[j] = up ? 0.0 : D.M;
 #pragma unroll
         for (int c = 0; c < N; ++c) Bi[j][c] = j == c ? 1.0 : 0.0;
     }
@@ -364,18 +373,11 @@ HVP_HD inline int lp_simplex(const LpData<N, MEM>& D, const Consts& C, int max_i
     bool bland = false;
     for (iters = 0; iters <= max_iter; ++iters) {
         // vertex: y = A_B^-1 (-b_B)
-        double bb[N];
-#pragma unroll
-        for (int r = 0; r < N; ++r) {
-            LpHyp h;
-            lp_hyp<N>(D, C, basis[r], h);
-            bb[r] = -h.b;
-        }
 #pragma unroll
         for (int i = 0; i < N; ++i) {
             double s = 0.0;
 #pragma unroll
-            for (int r = 0; r < N; ++r) s += Bi[i][r] * bb[r];
+            for (int r = 0; r < N; ++r) s -= Bi[i][r] * bB[r];
             y[i] = s;
         }
         double Y[N];
@@ -416,11 +418,9 @@ HVP_HD inline int lp_simplex(const LpData<N, MEM>& D, const Consts& C, int max_i
             double pk = 0.0;
 #pragma unroll
             for (int i = 0; i < N; ++i) pk += Bi[i][k] * g[i];
-            LpHyp h;
-            lp_hyp<N>(D, C, basis[k], h);
 #pragma unroll
             for (int sd = 0; sd < 2; ++sd) {
-                const double dv = sd == 0 ? pk + h.sp : -pk + h.sm;
+                const double dv = sd == 0 ? pk + spB[k] : -pk + smB[k];
                 const bool cand = dv < -dtol;
                 const bool take = cand && (bland ? (ek < 0 || basis[k] < eid) : dv < eD);
                 ek = take ? k : ek;
@@ -428,6 +428,15 @@ HVP_HD inline int lp_simplex(const LpData<N, MEM>& D, const Consts& C, int max_i
                 eid = take ? basis[k] : eid;
                 eD = take ? dv : eD;
             }
+        }
+        if (ek < 0 && since > 0) {  // optimal: confirm on a freshly built A_B^-1 (exact vertex)
+            if (!lp_invert<N>(D, C, basis, Bi)) {
+                HVP_LP_WHY(4);
+                return LP_FAIL;
+            }
+            since = 0;
+            --iters;
+            continue;
         }
         if (ek < 0) {  // optimal: every edge non-decreasing; the hard rows must hold
             bool viol = false;
@@ -499,16 +508,53 @@ HVP_HD inline int lp_simplex(const LpData<N, MEM>& D, const Consts& C, int max_i
             HVP_LP_WHY(3);
             return LP_FAIL;
         }
+        // the entering term (one lookup) replaces basic position ek
+        LpHyp he;
+        lp_hyp<N>(D, C, enter, he);
+        double ae[N];
+        lp_normal<N>(he, ae);
         int old = 0;
 #pragma unroll
         for (int k = 0; k < N; ++k) {
-            old = k == ek ? basis[k] : old;
-            basis[k] = k == ek ? enter : basis[k];
+            const bool at = k == ek;
+            old = at ? basis[k] : old;
+            basis[k] = at ? enter : basis[k];
+            bB[k] = at ? he.b : bB[k];
+            spB[k] = at ? he.sp : spB[k];
+            smB[k] = at ? he.sm : smB[k];
         }
         set_side(old, esd == 0 ? 1 : -1);  // the leaving term is on the side the edge took it to
-        if (!lp_invert<N>(D, C, basis, Bi)) {
-            HVP_LP_WHY(4);
-            return LP_FAIL;
+        // A_B^-1 with row ek replaced by a_e (Sherman-Morrison): with c = A_B^-1 e_ek (the edge's
+        // column) and w = a_e' A_B^-1, the new inverse is A_B^-1 - c (w - e_ek') / (a_e . c)
+        double cc[N], w[N];
+        double piv = 0.0;
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            double v = 0.0;
+#pragma unroll
+            for (int k = 0; k < N; ++k) v = k == ek ? Bi[i][k] : v;
+            cc[i] = v;
+            piv += ae[i] * v;
+        }
+#pragma unroll
+        for (int c = 0; c < N; ++c) {
+            double v = 0.0;
+#pragma unroll
+            for (int i = 0; i < N; ++i) v += ae[i] * Bi[i][c];
+            w[c] = v - (c == ek ? 1.0 : 0.0);
+        }
+        if (++since >= kLpRefresh || !(fabs(piv) > 1e-11)) {
+            if (!lp_invert<N>(D, C, basis, Bi)) {
+                HVP_LP_WHY(4);
+                return LP_FAIL;
+            }
+            since = 0;
+        } else {
+            const double ip = 1.0 / piv;
+#pragma unroll
+            for (int i = 0; i < N; ++i)
+#pragma unroll
+                for (int c = 0; c < N; ++c) Bi[i][c] -= cc[i] * w[c] * ip;
         }
         HVP_LP_TRACE(iters, old, esd, eD, enter, tstep, bland, y);
         if (!(tstep > 1e-13)) bland = true;  // a degenerate pivot: Bland's rule from here on
