@@ -70,8 +70,9 @@ typedef struct hvp_problem {
     int32_t quadratic_cost; /* 1 = min_2_norm (MIQP); 0 = min_1_norm (MILP,
                                fleet_decent_mld.py:73-76, mpcs/cent_mld.py:58-61):
                                HVP_FORM_DECENT, any N, by branch and bound over node LPs (AUTO /
-                               BNB) or enumeration (ENUMERATE, N <= HVP_MAX_N_ENUM), LPs of
-                               csrc/hvp_l1.h; HVP_FORM_CENT, the platoon LP inside the joint
+                               BNB) or enumeration (ENUMERATE, N <= HVP_MAX_N_ENUM), LPs by
+                               the per-lane simplex of csrc/hvp_lp.h (N <= 8) or the
+                               interior point of csrc/hvp_l1.h; HVP_FORM_CENT, the platoon LP inside the joint
                                branch and bound (csrc/hvp_cent_l1.h; AUTO / BNB, or ENUMERATE =
                                the exhaustive joint search).  Every LP ends solved, proven
                                infeasible (excluded), or unresolved -- which makes its instance /

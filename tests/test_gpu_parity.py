@@ -319,3 +319,27 @@ def test_position_box_long_horizon(gpu_available):
         obj, conv, _, _, _ = O.solve_qp(sysd, O.Cfg(), NL, int(roles[i]), res.region[i], x0, xf, xb, xl)
         assert conv and abs(res.cost[i] - obj) <= 1e-9 * max(1.0, abs(obj)), (i, res.cost[i], obj)
         assert res.x[i, 0].max() <= 10000 + 1e-6
+
+
+def test_root_refill_equals_root_kernel(gpu_available, monkeypatch):
+    """configs[1] at bench size: the root level solved by the refill kernel (k_inst_prep root nodes,
+    the dive list, round 4) against k_bnb_root (HVP_ROOT_REFILL=0): the same tree and the same QPs,
+    so every output -- sequences, costs, trajectories, QP and active-set step counts -- is equal."""
+    import torch
+
+    import bench
+
+    n, S = 10, 16384
+    params, roles = bench.make_inputs(range(S), n, N)
+    dev = torch.device("cuda", 0)
+    tp, tr = torch.from_numpy(params).to(dev), torch.from_numpy(roles).to(dev)
+    ts = torch.zeros(len(roles), dtype=torch.int32, device=dev)
+    s = _solver([_gear_system()])
+    a = {k: v.clone() for k, v in s.solve_device(ts, tr, tp).items()}
+    ca = s.stats().n_candidates
+    monkeypatch.setenv("HVP_ROOT_REFILL", "0")
+    b = s.solve_device(ts, tr, tp)
+    torch.cuda.synchronize()
+    assert s.stats().n_candidates == ca
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
