@@ -1035,13 +1035,14 @@ def main() -> None:
     qp_step_ms = float(np.mean(qp_ms))
     cand_per_step = cand / args.steps
     notional = cand_per_step * dense_qp_bytes(N) + B * instance_io_bytes(N)
+    simplex = N <= 8 and os.environ.get("HVP_L1_SIMPLEX", "1") != "0"  # min_1_norm LPs: per-lane simplex
     if bnb and not quadratic:
-        qk = [("k_l1_root", 1), ("k_l1_bound", N)]
+        qk = [("k_lp_root", 1), ("k_lp_bound", N)] if simplex else [("k_l1_root", 1), ("k_l1_bound", N)]
     elif bnb:
         qk = [("k_bnb_root_coop", 1), ("k_bnb_bound_coop", N)] if N > 8 else [("k_bnb_root", 1),
                                                                               ("k_bnb_bound_refill", N)]
     else:
-        qk = [("k_qp_gi", 1)] if quadratic else [("k_qp_l1", 1)]
+        qk = [("k_qp_gi", 1)] if quadratic else [("k_qp_lp" if simplex else "k_qp_l1", 1)]
     # the PMC figures are per launch over the WHOLE batch (the profile runs this workload with
     # --streams 1); qp_step_ms is the HIP-event time of those launches in the one-handle pass
     roofline = qp_roofline(qp_step_ms, qk, notional,

@@ -89,7 +89,8 @@ typedef struct hvp_problem {
     double spacing_d0;      /* spacing(x) = [-d0 - t0 * v, 0]                          */
     double spacing_t0;
     int32_t max_iter;       /* fallback IPM iteration cap per candidate (<=0: 60);
-                               min_1_norm: the LP interior point's cap (<=0: 120)       */
+                               min_1_norm: the LP solver's cap -- simplex pivots or
+                               interior-point iterations (<=0: 120)                   */
     int32_t method;         /* HVP_METHOD_*: how the region sequences are searched     */
     double tol;             /* fallback IPM relative tolerance (<=0: 1e-12)            */
     int32_t formulation;    /* HVP_FORM_*: which local MPC (parameter layout, cost)    */
