@@ -13,3 +13,6 @@ timeout -k 10 300 python bench.py --cost l1 --steps 5 --warmup 1 > gpurun_out/${
 timeout -k 10 300 python bench.py --controller admm --n 10 --N 10 --platoons 1024 --steps 3 --warmup 1 > gpurun_out/${R}_bench_admm.jsonl 2> gpurun_out/${R}_bench_admm.err || exit 4
 timeout -k 10 300 python bench.py --controller gadmm --n 20 --N 10 --platoons 4096 --steps 3 --warmup 1 > gpurun_out/${R}_bench_gadmm.jsonl 2> gpurun_out/${R}_bench_gadmm.err || exit 5
 timeout -k 10 300 python bench.py --controller cent --n 10 --N 5 --platoons 4096 --steps 1 --warmup 0 > gpurun_out/${R}_bench_cent.jsonl 2> gpurun_out/${R}_bench_cent.err || exit 6
+# seed 426 alone with a 30M QP cap: the split-task queue now declines exports when full instead of
+# overflowing, so the search should end (status 0) where r03s ended HVP_OVERFLOW at 22.1M QPs
+timeout -k 10 240 python profiles/cmds/diag_cent_heavy.py --seeds 426 --max-nodes 30000000 > gpurun_out/${R}_heavy_426.jsonl 2> gpurun_out/${R}_heavy_426.err || exit 7
