@@ -482,7 +482,7 @@ HVP_HD inline int solve_admm_lane(LaneQp<N, M>& q, const hvp_system& S, const Co
 // it.  edge: the switching rule's bits (V rows active with multiplier > kEdgeMultTol, as
 // GiLane::verify reports them), from the interior point's multipliers.
 template <int N, class M>
-HVP_HD inline int solve_admm_ipm(LaneQp<N, M>& q, const hvp_system& S, const Consts& C, int role, const double* prm,
+HVP_HD HVP_FORCEINLINE inline int solve_admm_ipm(LaneQp<N, M>& q, const hvp_system& S, const Consts& C, int role, const double* prm,
                                  uint64_t code, int K, int& iters, uint32_t* edge = nullptr) {
     uint64_t hs = 0;
     iters = 0;

@@ -15,6 +15,8 @@
 #include "hvp_ipm.h"
 #include "hvp_l1.h"
 long long g_lp_why[5] = {0, 0, 0, 0, 0};
+long long g_lp_pass = 0;  // ratio-test scans over the terms
+#define HVP_LP_PASS() (__atomic_fetch_add(&g_lp_pass, 1, __ATOMIC_RELAXED))
 #define HVP_LP_WHY(code) (__atomic_fetch_add(&g_lp_why[code], 1, __ATOMIC_RELAXED))
 int g_lp_trace = 0;
 #define HVP_LP_TRACE(it, lv, sd, dv, en, t, bl, yy)                                                             \
@@ -486,6 +488,8 @@ void hvp_hostref_lp_stats(long long* out) {
     out[1] = g_lp_iters;
     out[2] = g_lp_fail;
     for (int i = 1; i < 5; ++i) out[2 + i] = g_lp_why[i], g_lp_why[i] = 0;
+    out[7] = g_lp_pass;
+    g_lp_pass = 0;
     g_lp_runs = g_lp_iters = g_lp_fail = 0;
 }
 void hvp_hostref_gi_stats(long long* out) {

@@ -36,6 +36,13 @@
 #ifndef HVP_HD
 #define HVP_HD
 #endif
+// The solvers are inlined into every kernel that calls them.  Left to the compiler, a solver called
+// from several kernels of one unit becomes a real function (Solver<10>::solve, 204 KB, from the
+// three interior-point fallback kernels of N = 10), and that build's k_bnb_ipm<10> did not return
+// on MI355X (r04e/r04g: the same source inlined, commit 8abfabc, finishes the solve in 8 ms).
+#ifndef HVP_FORCEINLINE
+#define HVP_FORCEINLINE __attribute__((always_inline))
+#endif
 
 namespace hvp {
 
@@ -456,7 +463,7 @@ struct Solver {
         }
     }
 
-    HVP_HD static QpOut solve(LaneQp<N, M>& q, const Consts& C) {
+    HVP_HD HVP_FORCEINLINE static QpOut solve(LaneQp<N, M>& q, const Consts& C) {
         QpOut out{0.0, 2, 0};
         const double w = C.w;
         const int m = 2 * NPAIR_ACTIVE + (true ? 2 * NP : 0) + (true ? 2 * NP : 0);

@@ -1574,6 +1574,15 @@ __global__ __launch_bounds__(kBnbBlock<N>) void k_lp_bound(int k, const hvp_syst
 // done -> write 64 results) ran at 2.73M against this kernel's 4.87M (profiles/r02q_*): with two
 // trip-loop levels the compiler's allocation spills ~3x more scratch traffic inside the trips.
 // Same results per node as k_bnb_bound (the node -> lane mapping does not matter).
+// where the refill kernel's event reads the workspace descriptor and the problem constants
+// (A/B builds): 1 = the by-value kernel arguments, 0 = the handle's device copies through
+// uniform_opaque pointers (the level index laundered too)
+#ifndef HVP_REFILL_WS_ARG
+#define HVP_REFILL_WS_ARG 0
+#endif
+#ifndef HVP_REFILL_C_ARG
+#define HVP_REFILL_C_ARG 0
+#endif
 #ifndef HVP_REFILL_WAVES
 #define HVP_REFILL_WAVES 2
 #endif
@@ -1766,9 +1775,10 @@ template <int N>
 __global__ __launch_bounds__(kBnbBlock<N>) __attribute__((amdgpu_waves_per_eu(HVP_REFILL_WAVES)))
 void k_bnb_bound_refill(int k_arg, const hvp_system* __restrict__ systems, const int32_t* __restrict__ sys,
                         const int32_t* __restrict__ role, const double* __restrict__ params, hvp::Consts C,
-                        const Workspace* __restrict__ wsd, const hvp::Consts* __restrict__ cd) {
+                        const Workspace* __restrict__ wsd, const hvp::Consts* __restrict__ cd, Workspace wsv) {
     constexpr int BS = kBnbBlock<N>;
     static_assert(N <= HVP_MAX_N_ENUM, "lane refill is the N <= 8 path");
+    (void)wsd, (void)cd, (void)wsv;
     const int lane = threadIdx.x & 63;
     hvp::LaneQp<N, LdsMem<N, BS>> q;
     q.mem.lane = threadIdx.x;
@@ -1803,12 +1813,21 @@ void k_bnb_bound_refill(int k_arg, const hvp_system* __restrict__ systems, const
 #endif
         if (nfree >= kRefillMin || nfree == 64) {
             // ---- event: write the finished lanes' results, then refill every free lane
+#if HVP_REFILL_WS_ARG
+            const Workspace& ws = wsv;
+#else
             const Workspace& ws = *uniform_opaque(wsd);
+#endif
+#if HVP_REFILL_C_ARG
+            const hvp::Consts& Ce = C;
+            const int k = k_arg;
+#else
             const hvp::Consts& Ce = *uniform_opaque(cd);
             // the level, opaque here: the per-step tests on it (k < K in the QP set-up and the
             // direct cost) are evaluated inside the event, not hoisted as spilled lane masks
             int k = k_arg;
             asm volatile("" : "+s"(k));
+#endif
             const int dst = k & 1;
             unsigned cmask = 0;  // children of a finished bound node (k_bnb_expand's work, fused)
             double clb = 0.0;
@@ -1888,7 +1907,11 @@ void k_bnb_bound_refill(int k_arg, const hvp_system* __restrict__ systems, const
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) iter_sum += __shfl_down(iter_sum, off, 64);
+#if HVP_REFILL_WS_ARG
+    const Workspace& ws = wsv;
+#else
     const Workspace& ws = *uniform_opaque(wsd);
+#endif
     if (lane == 0 && iter_sum) atomicAdd(&ws.counter[1], (unsigned long long)iter_sum);
 #ifdef HVP_REFILL_PROF
     pf_all = __builtin_amdgcn_s_memtime() - pf_t0;
@@ -1908,8 +1931,11 @@ void k_bnb_bound_refill(int k_arg, const hvp_system* __restrict__ systems, const
 
 // Leaves whose active-set solve failed its verification (degenerate vertices, e.g. the
 // position box at p_max): re-solved by the interior-point method on the full row set
-// (hvp_ipm.h), as K_qp_ipm does for the enumeration path.  Normally an empty list.
-template <int N>
+// (hvp_ipm.h), as K_qp_ipm does for the enumeration path.  Normally an empty list.  ADMM: the
+// hinge-state iteration around the interior point (hvp_admm.h solve_admm_ipm).  The two forms are
+// separate kernels: with both bodies in one kernel the decentralised re-solve at N = 10 did not
+// finish on MI355X (r04e: k_bnb_ipm<10> never returned, the round-3 single-form kernel takes ms).
+template <int N, bool ADMM>
 __global__ __launch_bounds__(kBnbBlock<N>) void k_bnb_ipm(const hvp_system* __restrict__ systems,
                                                           const int32_t* __restrict__ sys,
                                                           const int32_t* __restrict__ role,
@@ -1929,7 +1955,7 @@ __global__ __launch_bounds__(kBnbBlock<N>) void k_bnb_ipm(const hvp_system* __re
         hvp::LaneQp<N, LdsMem<N, BS>> q;
         q.mem.lane = threadIdx.x;
         double c;
-        if (C.form == HVP_FORM_ADMM) {  // the hinge-state iteration around the interior point
+        if constexpr (ADMM) {
             int its = 0;
             const int st = hvp::solve_admm_ipm<N>(q, S, C, rl, prm, code, N, its);
             atomicAdd(&ws.iters[inst], its);
@@ -2518,13 +2544,13 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
             if (root_refill) {
                 const int g_root = (int)std::min<long long>((B + BS - 1) / BS, (long long)h->n_cu * kRefillBlocksPerCu);
                 hipLaunchKernelGGL(k_bnb_bound_refill<N>, dim3(g_root), dim3(BS), lds, st, 0, h->d_sys, sys, role,
-                                   params, h->C, h->d_ws, h->d_consts);
+                                   params, h->C, h->d_ws, h->d_consts, h->ws_up[0]);
                 HIP_TRY(hipGetLastError());
                 hipLaunchKernelGGL(k_bnb_dive_prep<N>, dim3(grid_for(B)), dim3(kBlock), 0, st, B, h->d_sys, sys, params,
                                    h->C, ws);
                 HIP_TRY(hipGetLastError());
                 hipLaunchKernelGGL(k_bnb_bound_refill<N>, dim3(g_root), dim3(BS), lds, st, N, h->d_sys, sys, role,
-                                   params, h->C, h->d_ws + 1, h->d_consts);
+                                   params, h->C, h->d_ws + 1, h->d_consts, h->ws_up[1]);
             } else {
                 // (one lane per instance, 1 wave per SIMD)
                 hipLaunchKernelGGL((k_bnb_root<N, false>), dim3((B + BS - 1) / BS), dim3(BS), lds, st, B, h->d_sys,
@@ -2562,16 +2588,21 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
                 const int g_refill = (int)std::min<long long>((h->ws.cap + BS - 1) / BS,
                                                               (long long)h->n_cu * kRefillBlocksPerCu);
                 hipLaunchKernelGGL(k_bnb_bound_refill<N>, dim3(g_refill), dim3(BS), lds, st, k, h->d_sys, sys, role,
-                                   params, h->C, h->d_ws, h->d_consts);
+                                   params, h->C, h->d_ws, h->d_consts, h->ws_up[0]);
             }
         }
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(h->evb[2 * k + 1], st));
     }
     HIP_TRY(hipEventRecord(h->evq1, st));
-    if ((h->C.form == HVP_FORM_DECENT || h->C.form == HVP_FORM_ADMM) && !h->C.l1) {  // failed leaves (normally none: reads a zero count)
-        hipLaunchKernelGGL(k_bnb_ipm<N>, dim3(std::max(1, h->n_cu)), dim3(BS), lds, st, h->d_sys, sys, role, params,
-                           h->C, ws);
+    if (!h->C.l1 && (h->C.form == HVP_FORM_DECENT || h->C.form == HVP_FORM_ADMM)) {
+        // failed leaves (normally none: reads a zero count)
+        if (h->C.form == HVP_FORM_ADMM)
+            hipLaunchKernelGGL((k_bnb_ipm<N, true>), dim3(std::max(1, h->n_cu)), dim3(BS), lds, st, h->d_sys, sys,
+                               role, params, h->C, ws);
+        else
+            hipLaunchKernelGGL((k_bnb_ipm<N, false>), dim3(std::max(1, h->n_cu)), dim3(BS), lds, st, h->d_sys, sys,
+                               role, params, h->C, ws);
         HIP_TRY(hipGetLastError());
     }
     hipLaunchKernelGGL(k_bnb_key<N>, dim3(g_small), dim3(kBlock), 0, st, ws, h->C.form, h->C.l1);

@@ -314,6 +314,20 @@ HVP_HD inline bool lp_invert(const LpData<N, MEM>& D, const Consts& C, const int
 #ifndef HVP_LP_TRACE
 #define HVP_LP_TRACE(...) (void)0
 #endif
+// The scans over the terms (uniform term id per wave): a rolled loop by default -- unrolled, the
+// 18N - 2 term bodies make the LP kernels ~100 KB of code, past the instruction cache; rolled,
+// each term is looked up at run time (uniform branches, LDS / global loads by address).
+#ifndef HVP_LP_UNROLL_TERMS
+#define HVP_LP_UNROLL_TERMS 0
+#endif
+#if HVP_LP_UNROLL_TERMS
+#define HVP_LP_TERM_LOOP _Pragma("unroll")
+#else
+#define HVP_LP_TERM_LOOP _Pragma("unroll 1")
+#endif
+#ifndef HVP_LP_PASS
+#define HVP_LP_PASS() (void)0
+#endif
 template <int N, class MEM>
 HVP_HD inline int lp_simplex(const LpData<N, MEM>& D, const Consts& C, int max_iter, double* y, int& iters) {
     constexpr int NT = kLpTerms<N>;
@@ -346,7 +360,7 @@ HVP_HD inline int lp_simplex(const LpData<N, MEM>& D, const Consts& C, int max_i
     uint64_t neg[NW];
 #pragma unroll
     for (int w = 0; w < NW; ++w) neg[w] = 0ull;
-#pragma unroll
+HVP_LP_TERM_LOOP
     for (int id = 0; id < NT; ++id) {
         LpHyp h;
         if (lp_hyp<N>(D, C, id, h) && h.sp > h.sm) neg[id >> 6] |= 1ull << (id & 63);
@@ -386,7 +400,7 @@ HVP_HD inline int lp_simplex(const LpData<N, MEM>& D, const Consts& C, int max_i
         double g[N], gpre[N];
 #pragma unroll
         for (int i = 0; i < N; ++i) g[i] = gpre[i] = 0.0;
-#pragma unroll
+HVP_LP_TERM_LOOP
         for (int id = 0; id < NT; ++id) {
             LpHyp h;
             if (!lp_hyp<N>(D, C, id, h) || is_basic(id)) continue;
@@ -440,7 +454,7 @@ HVP_HD inline int lp_simplex(const LpData<N, MEM>& D, const Consts& C, int max_i
         }
         if (ek < 0) {  // optimal: every edge non-decreasing; the hard rows must hold
             bool viol = false;
-#pragma unroll
+HVP_LP_TERM_LOOP
             for (int id = 0; id < 8 * N - 2; ++id) {
                 LpHyp h;
                 if (!lp_hyp<N>(D, C, id, h)) continue;
@@ -471,10 +485,11 @@ HVP_HD inline int lp_simplex(const LpData<N, MEM>& D, const Consts& C, int max_i
         int idprev = -1, enter = -1;
         double tstep = 0.0;
         for (int pass = 0; pass < NT; ++pass) {
+            HVP_LP_PASS();
             double tb = 1e300;
             int ib = -1, ibside = 1;
             double jump = 0.0;
-#pragma unroll
+HVP_LP_TERM_LOOP
             for (int id = 0; id < NT; ++id) {
                 LpHyp h;
                 if (!lp_hyp<N>(D, C, id, h) || is_basic(id)) continue;

@@ -174,7 +174,7 @@ def test_l1_simplex_matches_interior_point_and_golden(hostref, name):
     N = int(fx["N"])
     if N > 8:
         pytest.skip("the simplex is the lane path (N <= 8); longer horizons keep the interior point")
-    stats = (ctypes.c_longlong * 7)()
+    stats = (ctypes.c_longlong * 8)()
     for method in (1, 2):
         prob, systems = product_problem(fx)
         prob.method = method
