@@ -1392,10 +1392,9 @@ __global__ __launch_bounds__(kL1BlockOf<N>) __attribute__((amdgpu_waves_per_eu(k
 // a vertex of it, the interior point a point inside -- equal costs).  The LP's per-step data live
 // in LDS (LdsMem rows, hvp_lp.h LF_*), its simplex state (vertex, basis inverse, basis ids) in
 // registers.
-template <int N>
+template <int N, int BS = kBnbBlock<N>>
 __device__ inline int lp_node(const hvp_system& S, const hvp::Consts& C, int rl, const double* prm, uint64_t code,
                               int K, double rlo, double rhi, double* y, double& cost, int& it) {
-    constexpr int BS = kBnbBlock<N>;
     hvp::LpData<N, LdsMem<N, BS>> D;
     D.mem.lane = threadIdx.x;
     const int st = hvp::lp_solve_l1<N>(D, S, C, rl, prm, code, K, rlo, rhi, C.max_iter, y, it);
@@ -1435,13 +1434,16 @@ __global__ __launch_bounds__(kBnbBlock<N>) void k_qp_lp(const hvp_system* __rest
     if ((threadIdx.x & 63) == 0 && iter_sum) atomicAdd(&ws.counter[1], iter_sum);
 }
 
+// (one lane per instance: 64-lane blocks, so the B / 64 waves spread over every CU instead of
+// filling a quarter of them four waves deep)
+constexpr int kLpRootBlock = 64;
 template <int N>
-__global__ __launch_bounds__(kBnbBlock<N>) void k_lp_root(int B, const hvp_system* __restrict__ systems,
+__global__ __launch_bounds__(kLpRootBlock) void k_lp_root(int B, const hvp_system* __restrict__ systems,
                                                           const int32_t* __restrict__ sys,
                                                           const int32_t* __restrict__ role,
                                                           const double* __restrict__ params, hvp::Consts C,
                                                           Workspace ws) {
-    constexpr int BS = kBnbBlock<N>;
+    constexpr int BS = kLpRootBlock;
     const int i = blockIdx.x * BS + threadIdx.x;
     if (i == 0) ws.lvl[0] = (unsigned long long)B;
     if (i >= B) return;
@@ -1465,7 +1467,7 @@ __global__ __launch_bounds__(kBnbBlock<N>) void k_lp_root(int B, const hvp_syste
     while (job < 4) {
         double y[N], c = 0.0;
         int it = 0;
-        const int st = lp_node<N>(S, C, rl, prm, code, K, rlo, rhi, y, c, it);
+        const int st = lp_node<N, BS>(S, C, rl, prm, code, K, rlo, rhi, y, c, it);
         ++nodes;
         iters += it;
         int next = 4;
@@ -2513,8 +2515,9 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
     const size_t lds_lp = sizeof(double) * hvp::LF_COUNT * N * BS;
     if (lp_lane) {
         if constexpr (!kCoop<N>)
-            hipLaunchKernelGGL(k_lp_root<N>, dim3((B + BS - 1) / BS), dim3(BS), lds_lp, st, B, h->d_sys, sys, role,
-                               params, h->C, ws);
+            hipLaunchKernelGGL(k_lp_root<N>, dim3((B + kLpRootBlock - 1) / kLpRootBlock), dim3(kLpRootBlock),
+                               sizeof(double) * hvp::LF_COUNT * N * kLpRootBlock, st, B, h->d_sys, sys, role, params,
+                               h->C, ws);
     } else if (h->C.l1) {
         hipLaunchKernelGGL(k_l1_root<N>, dim3(g_l1), dim3(kL1BlockOf<N>), 0, st, B, h->d_sys, sys, role, params, h->C,
                            ws);
