@@ -38,6 +38,7 @@ int g_solver = 1;
 // (hvp_lp.h) up to N = 8, the interior point beyond (the device's wave kernels)
 int g_l1_solver = 1;
 long long g_lp_runs = 0, g_lp_iters = 0, g_lp_fail = 0;
+long long g_lp_hist[64] = {};  // LPs by pivot count (the lane-utilisation model of the LP kernels)
 
 // one min_1_norm LP (node: K < N with the reachable interval [lo, hi] of v_K) by the selected solver
 template <int N>
@@ -50,6 +51,8 @@ int l1_lp(const hvp_system& S, const hvp::Consts& C, int role, const double* prm
         g_lp_runs += 1;
 #pragma omp atomic
         g_lp_iters += it;
+#pragma omp atomic
+        g_lp_hist[it < 63 ? it : 63] += 1;
         if (st == hvp::L1_FAIL) {
 #pragma omp atomic
             g_lp_fail += 1;
@@ -483,6 +486,9 @@ int hvp_hostref_gadmm_solve(const hvp_problem* P, const hvp_system* systems, int
 void hvp_hostref_set_solver(int s) { g_solver = s; }
 void hvp_hostref_set_l1_solver(int s) { g_l1_solver = s; }
 void hvp_hostref_set_lp_trace(int s) { g_lp_trace = s; }
+void hvp_hostref_lp_hist(long long* out) {
+    for (int i = 0; i < 64; ++i) out[i] = g_lp_hist[i], g_lp_hist[i] = 0;
+}
 void hvp_hostref_lp_stats(long long* out) {
     out[0] = g_lp_runs;
     out[1] = g_lp_iters;

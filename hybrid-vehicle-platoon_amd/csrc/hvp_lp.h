@@ -249,6 +249,96 @@ HVP_HD inline void lp_normal(const LpHyp& h, double* a) {
         a[i] = (i <= h.m ? h.cp : 0.0) + (i == h.j ? h.c0 : 0.0) + (i + 1 == h.j ? h.c1 : 0.0) + (i + 2 == h.j ? h.c2 : 0.0);
 }
 
+// ---- the scans over the terms, step by step.  Every term of step j (its V, U, A rows, the P rows
+// of p_{j+1}, the tracking / safe terms of state j + 1, the input terms of step j: 18 per step, 16
+// at j = 0) is z = cp X_{j-1} + c0 x_j + c1 x_{j-1} + c2 x_{j-2} + b with coefficients whose
+// STRUCTURE is fixed per term type (lp_hyp's, term for term); a scan loops over the steps (uniform
+// j, rolled) and visits the 18 terms with that structure known at compile time -- a handful of
+// FMAs per term from four primitives of y (and of the direction), where a lookup by term id
+// (lp_hyp) costs a run-time decode and selects per term.  lp_hyp stays for the basis lookups.
+struct LpPrim {
+    double x0, x1, x2, p1;  // x_j, x_{j-1}, x_{j-2}, X_{j-1} (0 where the index is < 0)
+};
+template <int N>
+HVP_HD inline LpPrim lp_prim(const double* x, const double* X, int j) {
+    LpPrim r{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        r.x0 = i == j ? x[i] : r.x0;
+        r.x1 = i + 1 == j ? x[i] : r.x1;
+        r.x2 = i + 2 == j ? x[i] : r.x2;
+        r.p1 = i + 1 == j ? X[i] : r.p1;
+    }
+    return r;
+}
+struct LpTerm {
+    int id;
+    bool ok;  // present (lp_hyp's true)
+    double cp, c0, c1, c2, b, sp, sm;
+};
+// a . x in lp_dot's summation order (c2, c1, cp, c0)
+HVP_HD inline double lp_val(const LpTerm& t, const LpPrim& p) {
+    double s = t.c2 * p.x2;
+    s += t.c1 * p.x1;
+    s += t.cp * p.p1;
+    s += t.c0 * p.x0;
+    return s;
+}
+template <int N, class MEM, class F>
+HVP_HD inline void lp_step_terms(const LpData<N, MEM>& D, const Consts& C, int j, F&& f) {
+    const int k = j + 1, K1 = N + 1;
+    const double M = D.M;
+    const double aj = D.mem.get(LF_A, j), bj = D.mem.get(LF_B, j), ibj = D.mem.get(LF_IB, j);
+    const double cj = D.mem.get(LF_C, j);
+    const bool on = ((D.on >> j) & 1u) != 0;
+    // V, U, A rows of step j (hard)
+    f(LpTerm{6 * j + 0, true, 0.0, 1.0, 0.0, 0.0, -D.mem.get(LF_VLO, j), 0.0, M});
+    f(LpTerm{6 * j + 1, true, 0.0, 1.0, 0.0, 0.0, -D.mem.get(LF_VHI, j), M, 0.0});
+    const double cu = j == 0 ? aj * D.v0 : 0.0;
+    const double c1u = j ? -aj : 0.0;
+    f(LpTerm{6 * j + 2, on, 0.0, 1.0, c1u, 0.0, -(cj + bj * D.umin + cu), 0.0, M});
+    f(LpTerm{6 * j + 3, on, 0.0, 1.0, c1u, 0.0, -(cj + bj * D.umax + cu), M, 0.0});
+    const double ca = j == 0 ? D.v0 : 0.0;
+    const double c1a = j ? -1.0 : 0.0;
+    f(LpTerm{6 * j + 4, true, 0.0, 1.0, c1a, 0.0, -(D.mem.get(LF_DEC, j) + ca), 0.0, M});
+    f(LpTerm{6 * j + 5, true, 0.0, 1.0, c1a, 0.0, -(D.mem.get(LF_ACC, j) + ca), M, 0.0});
+    // P rows of p_{j+1} (prefix m = j - 1; none at j = 0)
+    const double cpj = j >= 1 ? D.ts : 0.0;
+    f(LpTerm{6 * N + 2 * (j - 1), j >= 1, cpj, 0.0, 0.0, 0.0, D.P1 - D.pmin, 0.0, M});
+    f(LpTerm{6 * N + 2 * (j - 1) + 1, j >= 1, cpj, 0.0, 0.0, 0.0, D.P1 - D.pmax, M, 0.0});
+    // tracking and safe terms of state k = j + 1
+    const double* xf = D.prm + 2;
+    const double* xb = D.prm + 2 + 2 * K1;
+    const double* xl = D.prm + 2 + 4 * K1;
+    const int role = D.role;
+    const bool tf = (role & HVP_ROLE_TRACK_FRONT) != 0, tb = (role & HVP_ROLE_TRACK_BACK) != 0;
+    const bool tl = (role & HVP_ROLE_TRACK_LEADER) != 0, lsp = (role & HVP_ROLE_LEADER_SPACING) != 0;
+    const bool qp = C.Qpp > 0.0, qv = C.Qvv > 0.0;
+    const double xfk = xf[k], xfv = xf[K1 + k], xbk = xb[k], xbv = xb[K1 + k], xlk = xl[k], xlv = xl[K1 + k];
+    const int base = 8 * N - 2 + 8 * j;
+    f(LpTerm{base + 0, tf && qp && (j >= 1 || C.t0 != 0.0), cpj, C.t0, 0.0, 0.0, D.P1 + C.d0 - xfk, C.Qpp, C.Qpp});
+    f(LpTerm{base + 1, tf && qv, 0.0, 1.0, 0.0, 0.0, -xfv, C.Qvv, C.Qvv});
+    f(LpTerm{base + 2, tb && qp && j >= 1, -cpj, 0.0, 0.0, 0.0, xbk + C.t0 * xbv + C.d0 - D.P1, C.Qpp, C.Qpp});
+    f(LpTerm{base + 3, tb && qv, 0.0, -1.0, 0.0, 0.0, xbv, C.Qvv, C.Qvv});
+    const double c0l = lsp ? C.t0 : 0.0;
+    f(LpTerm{base + 4, tl && qp && (j >= 1 || c0l != 0.0), cpj, c0l, 0.0, 0.0, D.P1 - xlk + (lsp ? C.d0 : 0.0),
+             C.Qpp, C.Qpp});
+    f(LpTerm{base + 5, tl && qv, 0.0, 1.0, 0.0, 0.0, -xlv, C.Qvv, C.Qvv});
+    const bool qw = C.w > 0.0;
+    f(LpTerm{base + 6, j >= 1 && qw && (role & HVP_ROLE_SAFE_FRONT) != 0, cpj, 0.0, 0.0, 0.0, D.P1 - xfk + C.d_safe,
+             C.w, 0.0});
+    f(LpTerm{base + 7, j >= 1 && qw && (role & HVP_ROLE_SAFE_BACK) != 0, -cpj, 0.0, 0.0, 0.0, xbk + C.d_safe - D.P1,
+             C.w, 0.0});
+    // input terms of step j: Q_u |u_j|, Q_du |u_j - u_{j-1}| (u_j = ubar_j + ib_j y_j - a_j ib_j y_{j-1})
+    const double ubar = -(cu + cj) * ibj;
+    f(LpTerm{16 * N - 2 + 2 * j, on && C.Qu > 0.0, 0.0, ibj, j ? -aj * ibj : 0.0, 0.0, ubar, C.Qu, C.Qu});
+    const int jp = j >= 1 ? j - 1 : 0;
+    const double ap = D.mem.get(LF_A, jp), ibp = D.mem.get(LF_IB, jp);
+    const double ubp = jp == 0 ? -(ap * D.v0 + D.mem.get(LF_C, 0)) * ibp : -D.mem.get(LF_C, jp) * ibp;
+    f(LpTerm{16 * N - 2 + 2 * j + 1, j >= 1 && j < D.K && C.Qdu > 0.0, 0.0, ibj, -aj * ibj - ibp,
+             j >= 2 ? ap * ibp : 0.0, ubar - ubp, C.Qdu, C.Qdu});
+}
+
 // inverse of the basis matrix (rows = basic normals) by Gauss-Jordan with partial pivoting, all
 // indices static (the pivot row is swapped in by selects); false if singular
 template <int N, class MEM>
@@ -314,17 +404,6 @@ HVP_HD inline bool lp_invert(const LpData<N, MEM>& D, const Consts& C, const int
 #ifndef HVP_LP_TRACE
 #define HVP_LP_TRACE(...) (void)0
 #endif
-// The scans over the terms (uniform term id per wave): a rolled loop by default -- unrolled, the
-// 18N - 2 term bodies make the LP kernels ~100 KB of code, past the instruction cache; rolled,
-// each term is looked up at run time (uniform branches, LDS / global loads by address).
-#ifndef HVP_LP_UNROLL_TERMS
-#define HVP_LP_UNROLL_TERMS 0
-#endif
-#if HVP_LP_UNROLL_TERMS
-#define HVP_LP_TERM_LOOP _Pragma("unroll")
-#else
-#define HVP_LP_TERM_LOOP _Pragma("unroll 1")
-#endif
 #ifndef HVP_LP_PASS
 #define HVP_LP_PASS() (void)0
 #endif
@@ -360,11 +439,13 @@ HVP_HD inline int lp_simplex(const LpData<N, MEM>& D, const Consts& C, int max_i
     uint64_t neg[NW];
 #pragma unroll
     for (int w = 0; w < NW; ++w) neg[w] = 0ull;
-HVP_LP_TERM_LOOP
-    for (int id = 0; id < NT; ++id) {
-        LpHyp h;
-        if (lp_hyp<N>(D, C, id, h) && h.sp > h.sm) neg[id >> 6] |= 1ull << (id & 63);
-    }
+#pragma unroll 1
+    for (int j = 0; j < N; ++j)
+        lp_step_terms<N>(D, C, j, [&](const LpTerm& t) {
+            if (!(t.ok && t.sp > t.sm)) return;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) neg[w] |= (t.id >> 6) == w ? 1ull << (t.id & 63) : 0ull;
+        });
     auto neg_bit = [&](int id) {
         uint64_t wd = 0;
 #pragma unroll
@@ -400,20 +481,27 @@ HVP_LP_TERM_LOOP
         double g[N], gpre[N];
 #pragma unroll
         for (int i = 0; i < N; ++i) g[i] = gpre[i] = 0.0;
-HVP_LP_TERM_LOOP
-        for (int id = 0; id < NT; ++id) {
-            LpHyp h;
-            if (!lp_hyp<N>(D, C, id, h) || is_basic(id)) continue;
-            const double z = lp_dot<N>(h, y, Y) + h.b;
-            const double zt = 1e-12 * (1.0 + fabs(h.b));
-            const bool pos = z > zt || (!(z < -zt) && !neg_bit(id));
-            const double s = pos ? h.sp : -h.sm;
+#pragma unroll 1
+        for (int j = 0; j < N; ++j) {
+            const LpPrim py = lp_prim<N>(y, Y, j);
+            double g0 = 0.0, g1 = 0.0, g2 = 0.0, gp = 0.0;
+            lp_step_terms<N>(D, C, j, [&](const LpTerm& t) {
+                if (!t.ok || is_basic(t.id)) return;
+                const double z = lp_val(t, py) + t.b;
+                const double zt = 1e-12 * (1.0 + fabs(t.b));
+                const bool pos = z > zt || (!(z < -zt) && !neg_bit(t.id));
+                const double sl = pos ? t.sp : -t.sm;
+                g0 += sl * t.c0;
+                g1 += sl * t.c1;
+                g2 += sl * t.c2;
+                gp += sl * t.cp;
+            });
 #pragma unroll
             for (int i = 0; i < N; ++i) {
-                g[i] += i == h.j ? s * h.c0 : 0.0;
-                g[i] += i + 1 == h.j ? s * h.c1 : 0.0;
-                g[i] += i + 2 == h.j ? s * h.c2 : 0.0;
-                gpre[i] += i == h.m ? s * h.cp : 0.0;
+                g[i] += i == j ? g0 : 0.0;
+                g[i] += i + 1 == j ? g1 : 0.0;
+                g[i] += i + 2 == j ? g2 : 0.0;
+                gpre[i] += i + 1 == j ? gp : 0.0;
             }
         }
         {
@@ -454,13 +542,15 @@ HVP_LP_TERM_LOOP
         }
         if (ek < 0) {  // optimal: every edge non-decreasing; the hard rows must hold
             bool viol = false;
-HVP_LP_TERM_LOOP
-            for (int id = 0; id < 8 * N - 2; ++id) {
-                LpHyp h;
-                if (!lp_hyp<N>(D, C, id, h)) continue;
-                const double z = lp_dot<N>(h, y, Y) + h.b;
-                const double tol = 1e-9 * (1.0 + fabs(h.b));
-                viol = viol || (h.sp > 0.0 && z > tol) || (h.sm > 0.0 && z < -tol);
+#pragma unroll 1
+            for (int j = 0; j < N; ++j) {
+                const LpPrim py = lp_prim<N>(y, Y, j);
+                lp_step_terms<N>(D, C, j, [&](const LpTerm& t) {
+                    if (!t.ok || t.id >= 8 * N - 2) return;  // the hard rows (V, U, A, P)
+                    const double z = lp_val(t, py) + t.b;
+                    const double tol = 1e-9 * (1.0 + fabs(t.b));
+                    viol = viol || (t.sp > 0.0 && z > tol) || (t.sm > 0.0 && z < -tol);
+                });
             }
             if (viol) HVP_LP_WHY(2);
             return viol ? LP_FAIL : LP_OK;
@@ -489,24 +579,27 @@ HVP_LP_TERM_LOOP
             double tb = 1e300;
             int ib = -1, ibside = 1;
             double jump = 0.0;
-HVP_LP_TERM_LOOP
-            for (int id = 0; id < NT; ++id) {
-                LpHyp h;
-                if (!lp_hyp<N>(D, C, id, h) || is_basic(id)) continue;
-                const double rd = lp_dot<N>(h, d, Dd);
-                const double an = fabs(h.cp) * (h.m + 1) + fabs(h.c0) + fabs(h.c1) + fabs(h.c2);
-                if (!(fabs(rd) > 1e-10 * an * dmax)) continue;
-                const double z = lp_dot<N>(h, y, Y) + h.b;
-                const double zt = 1e-12 * (1.0 + fabs(h.b));
-                const bool pos = z > zt || (!(z < -zt) && !neg_bit(id));
-                if (pos == (rd > 0.0)) continue;  // moving away from its kink
-                const double t = fmax(0.0, -z / rd);
-                const bool after = t > tprev || (t == tprev && id > idprev);
-                const bool better = after && (t < tb || (t == tb && id < ib));
-                tb = better ? t : tb;
-                ib = better ? id : ib;
-                ibside = better ? (pos ? -1 : 1) : ibside;
-                jump = better ? (h.sp + h.sm) * fabs(rd) : jump;
+#pragma unroll 1
+            for (int j = 0; j < N; ++j) {
+                const LpPrim py = lp_prim<N>(y, Y, j), pd = lp_prim<N>(d, Dd, j);
+                lp_step_terms<N>(D, C, j, [&](const LpTerm& t) {
+                    if (!t.ok || is_basic(t.id)) return;
+                    const int id = t.id;
+                    const double rd = lp_val(t, pd);
+                    const double an = fabs(t.cp) * j + fabs(t.c0) + fabs(t.c1) + fabs(t.c2);
+                    if (!(fabs(rd) > 1e-10 * an * dmax)) return;
+                    const double z = lp_val(t, py) + t.b;
+                    const double zt = 1e-12 * (1.0 + fabs(t.b));
+                    const bool pos = z > zt || (!(z < -zt) && !neg_bit(id));
+                    if (pos == (rd > 0.0)) return;  // moving away from its kink
+                    const double tt = fmax(0.0, -z / rd);
+                    const bool after = tt > tprev || (tt == tprev && id > idprev);
+                    const bool better = after && (tt < tb || (tt == tb && id < ib));
+                    tb = better ? tt : tb;
+                    ib = better ? id : ib;
+                    ibside = better ? (pos ? -1 : 1) : ibside;
+                    jump = better ? (t.sp + t.sm) * fabs(rd) : jump;
+                });
             }
             if (ib < 0) break;  // no breakpoint left: unbounded (cannot happen with the V walls)
             slope += jump;
