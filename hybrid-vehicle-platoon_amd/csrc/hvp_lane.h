@@ -1736,6 +1736,105 @@ __device__ inline int wave_rank(unsigned long long mask) {
     return __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
 }
 
+// The same node LPs through persistent waves: every lane keeps its LP's simplex state (hvp_lp.h
+// LpLane) in registers and runs one iteration per trip; when at least `refill_min` lanes of the
+// wave are free, their finished LPs are written (k_lp_bound's outputs, node for node) and every
+// free lane claims the level's next node (one atomic per wave).  A node LP takes 6.5 pivots on
+// average and a wave of 64 one-per-lane LPs waits for its slowest (~17 pivots, host histogram):
+// the grid-stride kernel idles ~60 % of its lanes.  HVP_LP_REFILL=<min free lanes> (0: k_lp_bound).
+template <int N>
+__global__ __launch_bounds__(kBnbBlock<N>) void k_lp_bound_refill(int k, const hvp_system* __restrict__ systems,
+                                                                   const int32_t* __restrict__ sys,
+                                                                   const int32_t* __restrict__ role,
+                                                                   const double* __restrict__ params, hvp::Consts C,
+                                                                   Workspace ws, int refill_min) {
+    constexpr int BS = kBnbBlock<N>;
+    enum { IDLE = 0, RUN = 1, DONE = 2 };
+    const int dst = k & 1;
+    const int lane = threadIdx.x & 63;
+    const unsigned long long nn = ws.lvl[k];
+    const long long total = (long long)(nn < (unsigned long long)ws.cap ? nn : ws.cap);
+    hvp::LpData<N, LdsMem<N, BS>> D;
+    D.mem.lane = threadIdx.x;
+    hvp::LpLane<N> L;
+    double y[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) y[j] = 0.0;
+    long long t = -1;
+    int inst = 0, stage = IDLE, st = 0;
+    bool exhausted = false;
+    unsigned long long iter_sum = 0;
+    for (;;) {
+        const unsigned long long free = __ballot(stage != RUN);
+        const int nfree = __popcll(free);
+        if (nfree >= refill_min || nfree == 64) {
+            if (stage == DONE) {
+                const hvp_system& S = systems[sys[inst]];
+                const double* prm = params + (size_t)inst * C.stride;
+                double c = 0.0;
+                if (st == hvp::L1_OK)
+                    c = hvp::l1_direct_cost<N>(y, S, C, role[inst], prm, ws.nd_code[dst][t], k, ws.nd_lo[dst][t],
+                                               ws.nd_hi[dst][t]);
+                const int it = L.iters;
+                iter_sum += (unsigned long long)it;
+                atomicAdd(&ws.nodes[inst], 1);
+                atomicAdd(&ws.iters[inst], it);
+                if (k < N) {
+                    ws.nd_lb[dst][t] = st == hvp::L1_OK ? c : (st == hvp::L1_INFEASIBLE ? 1e300 : -1e300);
+                    if (st == hvp::L1_FAIL) atomicAdd(&ws.counter[4], 1ull);
+                } else {
+                    if (st == hvp::L1_OK) ws.nd_lb[dst][t] = c;
+                    ws.leaf_stat[t] = st == hvp::L1_OK ? 0 : (st == hvp::L1_INFEASIBLE ? HVP_INFEASIBLE : HVP_MAXITER);
+#pragma unroll
+                    for (int j = 0; j < N; ++j) ws.task_y[t * N + j] = y[j];
+                    if (st == hvp::L1_OK) atomicMin(&ws.inc[inst], cost_key(c));
+                    if (st == hvp::L1_FAIL) atomicOr(&ws.inst_flag[inst], 8);
+                }
+                stage = IDLE;
+            }
+            if (exhausted && nfree == 64) break;
+            if (!exhausted) {
+                const unsigned long long base = wave_claim(ws.lvl + (HVP_MAX_N + 1) + k, free, nfree, lane);
+                if (base + nfree >= (unsigned long long)total) exhausted = true;
+                const long long mc = (long long)base + wave_rank(free);
+                if (stage == IDLE && mc < total) {
+                    const int in = ws.nd_inst[dst][mc];
+                    if (in < 0) {  // dead slot of an overflowed reservation
+                        if (k == N) ws.leaf_stat[mc] = HVP_OVERFLOW;
+                        else ws.nd_lb[dst][mc] = 1e300;
+                    } else {
+                        t = mc;
+                        inst = in;
+                        const hvp_system& S = systems[sys[inst]];
+                        const double* prm = params + (size_t)inst * C.stride;
+                        const uint64_t code = ws.nd_code[dst][mc];
+                        const double rlo = ws.nd_lo[dst][mc], rhi = ws.nd_hi[dst][mc];
+                        if (hvp::l1_infeasible<N>(S, C, prm, code, k, rlo, rhi)) {
+                            st = hvp::L1_INFEASIBLE;
+                            L.iters = 0;
+                            stage = DONE;
+                        } else {
+                            hvp::lp_data<N>(D, S, C, role[inst], prm, code, k, rlo, rhi);
+                            L.init(D, C);
+                            stage = RUN;
+                        }
+                    }
+                }
+            }
+        }
+        if (stage == RUN) {
+            const int r = L.trip(D, C, C.max_iter, y);
+            if (r != hvp::LP_RUN) {
+                st = r == hvp::LP_OK ? hvp::L1_OK : hvp::L1_FAIL;
+                stage = DONE;
+            }
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) iter_sum += __shfl_down(iter_sum, off, 64);
+    if (lane == 0 && iter_sum) atomicAdd(&ws.counter[1], iter_sum);
+}
+
 // lane stages of the refill kernels
 enum { RS_IDLE = 0, RS_SCAN = 1, RS_STEP = 2, RS_FAIL = 3, RS_OPT = 4 };
 
@@ -2513,6 +2612,11 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
     const char* lsx = std::getenv("HVP_L1_SIMPLEX");
     const bool lp_lane = h->C.l1 && !kCoop<N> && !(lsx && lsx[0] == '0');
     const size_t lds_lp = sizeof(double) * hvp::LF_COUNT * N * BS;
+    // the node LPs through persistent waves (k_lp_bound_refill, one 256-lane block per CU: the
+    // simplex kernels run one wave per SIMD), refilled when this many lanes are free
+    const char* lrf = std::getenv("HVP_LP_REFILL");
+    const int lp_refill = lrf && lrf[0] ? std::max(0, std::min(64, std::atoi(lrf))) : 32;
+    const int g_lp = (int)std::min<long long>((h->ws.cap + BS - 1) / BS, (long long)std::max(1, h->n_cu));
     if (lp_lane) {
         if constexpr (!kCoop<N>)
             hipLaunchKernelGGL(k_lp_root<N>, dim3((B + kLpRootBlock - 1) / kLpRootBlock), dim3(kLpRootBlock),
@@ -2571,9 +2675,14 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(h->evb[2 * k], st));
         if (lp_lane) {
-            if constexpr (!kCoop<N>)
-                hipLaunchKernelGGL(k_lp_bound<N>, dim3(g_qp), dim3(BS), lds_lp, st, k, h->d_sys, sys, role, params,
-                                   h->C, ws);
+            if constexpr (!kCoop<N>) {
+                if (lp_refill > 0)
+                    hipLaunchKernelGGL(k_lp_bound_refill<N>, dim3(g_lp), dim3(BS), lds_lp, st, k, h->d_sys, sys, role,
+                                       params, h->C, ws, lp_refill);
+                else
+                    hipLaunchKernelGGL(k_lp_bound<N>, dim3(g_qp), dim3(BS), lds_lp, st, k, h->d_sys, sys, role, params,
+                                       h->C, ws);
+            }
         } else if (h->C.l1) {
             hipLaunchKernelGGL(k_l1_bound<N>, dim3(g_l1), dim3(kL1BlockOf<N>), 0, st, k, h->d_sys, sys, role, params,
                                h->C, ws);

@@ -407,66 +407,82 @@ HVP_HD inline bool lp_invert(const LpData<N, MEM>& D, const Consts& C, const int
 #ifndef HVP_LP_PASS
 #define HVP_LP_PASS() (void)0
 #endif
-template <int N, class MEM>
-HVP_HD inline int lp_simplex(const LpData<N, MEM>& D, const Consts& C, int max_iter, double* y, int& iters) {
-    constexpr int NT = kLpTerms<N>;
-    constexpr int NW = (NT + 63) / 64;
-    const double wmax = fmax(fmax(C.Qpp, C.Qvv), fmax(fmax(C.Qu, C.Qdu), fmax(C.w, 1e-300)));
-    const double dtol = 1e-11 * wmax;  // edge derivatives within -dtol of zero count as >= 0
+// The simplex state of one LP (per lane): basis, A_B^-1 and the basic terms' data, the recorded
+// sides of the kink terms, counters.  init() sets the start vertex; every trip() is one iteration
+// -- a pivot, or the rebuild of A_B^-1 that confirms an optimum -- and returns LP_RUN until the LP
+// ends (LP_OK with the vertex in y, or LP_FAIL).  lp_simplex runs the trips back to back; the
+// refill kernel (hvp_lane.h k_lp_bound_refill) interleaves them with other lanes' new LPs.
+enum { LP_RUN = 1 };
+template <int N>
+struct LpLane {
+    static constexpr int NT = kLpTerms<N>;
+    static constexpr int NW = (NT + 63) / 64;
+    static constexpr int kLpRefresh = 12;  // pivots between rebuilds of A_B^-1 (rank-1 updates between)
     int basis[N];
     double Bi[N][N];  // A_B^-1 (A_B y = -b_B)
     // the basic terms' offsets and slopes (updated at each pivot: no lookup of basic terms per
-    // iteration; A_B^-1 by rank-1 updates, rebuilt from the normals every kLpRefresh pivots)
+    // iteration)
     double bB[N], spB[N], smB[N];
-    constexpr int kLpRefresh = 12;
-    int since = 0;
-    // start: the V rows nearest v0 (A_B = I)
-#pragma unroll
-    for (int j = 0; j < N; ++j) {
-        const double vlo = D.mem.get(LF_VLO, j), vhi = D.mem.get(LF_VHI, j);
-        const bool up = fabs(vhi - D.v0) < fabs(D.v0 - vlo);
-        basis[j] = 6 * j + (up ? 1 : 0);
-        bB[j] = -(up ? vhi : vlo);
-        spB[j] = up ? D.M : 0.0;
-        smB[j] = up ? 0.0 : D.M;
-#pragma unroll
-        for (int c = 0; c < N; ++c) Bi[j][c] = j == c ? 1.0 : 0.0;
-    }
     // side of every nonbasic term that sits on its kink (|z| <= its tolerance): bit set = the '-'
     // side.  A term keeps the side it was left on (a basic term leaving to one side, a breakpoint
     // crossed), so a degenerate vertex is priced consistently from pivot to pivot -- what makes
     // Bland's rule terminate.  Initially the cheaper side.  (Words selected by static index.)
     uint64_t neg[NW];
-#pragma unroll
-    for (int w = 0; w < NW; ++w) neg[w] = 0ull;
-#pragma unroll 1
-    for (int j = 0; j < N; ++j)
-        lp_step_terms<N>(D, C, j, [&](const LpTerm& t) {
-            if (!(t.ok && t.sp > t.sm)) return;
-#pragma unroll
-            for (int w = 0; w < NW; ++w) neg[w] |= (t.id >> 6) == w ? 1ull << (t.id & 63) : 0ull;
-        });
-    auto neg_bit = [&](int id) {
+    int since, iters;
+    bool bland;
+
+    HVP_HD bool neg_bit(int id) const {
         uint64_t wd = 0;
 #pragma unroll
         for (int w = 0; w < NW; ++w) wd = (id >> 6) == w ? neg[w] : wd;
         return ((wd >> (id & 63)) & 1ull) != 0;
-    };
-    auto set_side = [&](int id, int side) {
+    }
+    HVP_HD void set_side(int id, int side) {
 #pragma unroll
         for (int w = 0; w < NW; ++w) {
             const uint64_t bit = (id >> 6) == w ? 1ull << (id & 63) : 0ull;
             neg[w] = side < 0 ? (neg[w] | bit) : (neg[w] & ~bit);
         }
-    };
-    auto is_basic = [&](int id) {
+    }
+    HVP_HD bool is_basic(int id) const {
         bool b = false;
 #pragma unroll
         for (int r = 0; r < N; ++r) b = b || basis[r] == id;
         return b;
-    };
-    bool bland = false;
-    for (iters = 0; iters <= max_iter; ++iters) {
+    }
+
+    // start: the V rows nearest v0 (A_B = I)
+    template <class MEM>
+    HVP_HD HVP_FORCEINLINE void init(const LpData<N, MEM>& D, const Consts& C) {
+        since = 0;
+        iters = 0;
+        bland = false;
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            const double vlo = D.mem.get(LF_VLO, j), vhi = D.mem.get(LF_VHI, j);
+            const bool up = fabs(vhi - D.v0) < fabs(D.v0 - vlo);
+            basis[j] = 6 * j + (up ? 1 : 0);
+            bB[j] = -(up ? vhi : vlo);
+            spB[j] = up ? D.M : 0.0;
+            smB[j] = up ? 0.0 : D.M;
+#pragma unroll
+            for (int c = 0; c < N; ++c) Bi[j][c] = j == c ? 1.0 : 0.0;
+        }
+#pragma unroll
+        for (int w = 0; w < NW; ++w) neg[w] = 0ull;
+#pragma unroll 1
+        for (int j = 0; j < N; ++j)
+            lp_step_terms<N>(D, C, j, [&](const LpTerm& t) {
+                if (!(t.ok && t.sp > t.sm)) return;
+#pragma unroll
+                for (int w = 0; w < NW; ++w) neg[w] |= (t.id >> 6) == w ? 1ull << (t.id & 63) : 0ull;
+            });
+    }
+
+    template <class MEM>
+    HVP_HD HVP_FORCEINLINE int trip(const LpData<N, MEM>& D, const Consts& C, int max_iter, double* y) {
+        const double wmax = fmax(fmax(C.Qpp, C.Qvv), fmax(fmax(C.Qu, C.Qdu), fmax(C.w, 1e-300)));
+        const double dtol = 1e-11 * wmax;  // edge derivatives within -dtol of zero count as >= 0
         // vertex: y = A_B^-1 (-b_B)
 #pragma unroll
         for (int i = 0; i < N; ++i) {
@@ -537,8 +553,7 @@ HVP_HD inline int lp_simplex(const LpData<N, MEM>& D, const Consts& C, int max_i
                 return LP_FAIL;
             }
             since = 0;
-            --iters;
-            continue;
+            return LP_RUN;
         }
         if (ek < 0) {  // optimal: every edge non-decreasing; the hard rows must hold
             bool viol = false;
@@ -555,7 +570,10 @@ HVP_HD inline int lp_simplex(const LpData<N, MEM>& D, const Consts& C, int max_i
             if (viol) HVP_LP_WHY(2);
             return viol ? LP_FAIL : LP_OK;
         }
-        if (iters == max_iter) break;
+        if (iters == max_iter) {
+            HVP_LP_WHY(1);
+            return LP_FAIL;
+        }
         // direction d = +-A_B^-1 e_k (column ek selected by static index)
         const double sg = esd == 0 ? 1.0 : -1.0;
         double d[N], Dd[N];
@@ -666,9 +684,21 @@ HVP_HD inline int lp_simplex(const LpData<N, MEM>& D, const Consts& C, int max_i
         }
         HVP_LP_TRACE(iters, old, esd, eD, enter, tstep, bland, y);
         if (!(tstep > 1e-13)) bland = true;  // a degenerate pivot: Bland's rule from here on
+        ++iters;
+        return LP_RUN;
     }
-    HVP_LP_WHY(1);
-    return LP_FAIL;
+};
+
+template <int N, class MEM>
+HVP_HD inline int lp_simplex(const LpData<N, MEM>& D, const Consts& C, int max_iter, double* y, int& iters) {
+    LpLane<N> L;
+    L.init(D, C);
+    int st;
+    do {
+        st = L.trip(D, C, max_iter, y);
+    } while (st == LP_RUN);
+    iters = L.iters;
+    return st;
 }
 
 // The node LP (relaxed after K steps) or leaf LP (K = N) of l1_rows by the simplex: L1_OK with the

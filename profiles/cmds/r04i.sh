@@ -11,7 +11,12 @@ for r in a b; do
   done
   timeout -k 10 300 python bench.py --no-cpu > gpurun_out/r04i_bench_v00_$r.jsonl 2> gpurun_out/r04i_bench_v00_$r.err || exit 4
 done
+# L1: node LPs through the refill kernel (default, refill at 32 free lanes) on one and two streams,
+# its refill threshold, the grid-stride kernel (HVP_LP_REFILL=0), the wave interior point
 for s in 1 2; do
-  timeout -k 10 300 python bench.py --cost l1 --no-cpu --steps 3 --warmup 1 --streams $s > gpurun_out/r04i_bench_l1_rolled_s$s.jsonl 2> gpurun_out/r04i_bench_l1_rolled_s$s.err || exit 5
-  HVP_LIB=$L/libhvpsolve_lpu.so timeout -k 10 300 python bench.py --cost l1 --no-cpu --steps 3 --warmup 1 --streams $s > gpurun_out/r04i_bench_l1_unrolled_s$s.jsonl 2> gpurun_out/r04i_bench_l1_unrolled_s$s.err || exit 6
+  timeout -k 10 300 python bench.py --cost l1 --no-cpu --steps 3 --warmup 1 --streams $s > gpurun_out/r04i_bench_l1_refill32_s$s.jsonl 2> gpurun_out/r04i_bench_l1_refill32_s$s.err || exit 5
 done
+for m in 0 16 48; do
+  HVP_LP_REFILL=$m timeout -k 10 300 python bench.py --cost l1 --no-cpu --steps 3 --warmup 1 --streams 1 > gpurun_out/r04i_bench_l1_refill${m}_s1.jsonl 2> gpurun_out/r04i_bench_l1_refill${m}_s1.err || exit 6
+done
+HVP_L1_SIMPLEX=0 timeout -k 10 300 python bench.py --cost l1 --no-cpu --steps 3 --warmup 1 > gpurun_out/r04i_bench_l1_ipm_s2.jsonl 2> gpurun_out/r04i_bench_l1_ipm_s2.err || exit 7
