@@ -60,7 +60,8 @@ struct Workspace {
                                                  // instances (hvp_set_region_hint; ADMM form only)
     // the greedy dive's leaf of every instance (decentralised lane path, N <= 8): a node list of
     // its own, solved by the refill kernel after the root level (hvp_lane.h launch_bnb)
-    int32_t* dv_inst = nullptr;                  // [max_batch] instance (-1: no dive)
+    int32_t* dv_inst = nullptr;                  // [3 max_batch] instance (-1: no dive); the
+                                                 // min_1_norm search lists up to 3 per instance
     uint64_t* dv_code = nullptr;                 // [max_batch] the dive's sequence
     double* dv_lo = nullptr;                     // [max_batch] (unused at K = N: 0)
     double* dv_hi = nullptr;                     // [max_batch] (-1)

@@ -379,7 +379,7 @@ int hvp_reserve(hvp_handle* h, int max_batch, int64_t cap) {
         // the dive list of the lane path (hvp_lane.h launch_bnb): 8-byte fields first
         if (ok && N <= HVP_MAX_N_ENUM) {
             constexpr size_t M = HVP_MAX_N + 1;
-            const size_t mb = (size_t)max_batch;
+            const size_t mb = 3 * (size_t)max_batch;  // up to 3 dive leaves per instance (min_1_norm)
             const size_t bytes = 8 * (6 * M + 8) + mb * (8 * (4 + N) + 3 * 4);
             ok = hipMalloc(&w.dv_mem, bytes) == hipSuccess;
             if (ok) {

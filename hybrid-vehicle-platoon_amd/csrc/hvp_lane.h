@@ -1736,6 +1736,80 @@ __device__ inline int wave_rank(unsigned long long mask) {
     return __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
 }
 
+// min_1_norm root level through the LP refill kernel (HVP_LP_ROOT_REFILL, default on): the search
+// state and the root nodes (k_lp_root's, without its LPs) ...
+template <int N>
+__global__ __launch_bounds__(kBlock) void k_lp_root_init(int B, const hvp_system* __restrict__ systems,
+                                                         const int32_t* __restrict__ sys,
+                                                         const double* __restrict__ params, hvp::Consts C,
+                                                         Workspace ws) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) ws.lvl[0] = (unsigned long long)B;
+    if (i >= B) return;
+    const hvp_system& S = systems[sys[i]];
+    const double* prm = params + (size_t)i * C.stride;
+    const double v0 = prm[1], P1 = prm[0] + S.ts * v0;
+    const bool ok = P1 >= S.pmin - 1e-9 * (1.0 + fabs(S.pmin)) && P1 <= S.pmax + 1e-9 * (1.0 + fabs(S.pmax));
+    ws.key[i] = ~0ull;
+    ws.inst_flag[i] = ok ? 0 : 1;
+    ws.nd_inst[0][i] = ok ? i : -1;
+    ws.nd_code[0][i] = 0;
+    ws.nd_lo[0][i] = v0;
+    ws.nd_hi[0][i] = v0;
+    ws.nd_lb[0][i] = -1e300;
+    ws.inc[i] = cost_key(__longlong_as_double(0x7ff0000000000000ll));  // +inf: no incumbent
+    ws.nodes[i] = 0;
+    ws.iters[i] = 0;
+}
+
+// ... then, from each root optimum, k_lp_root's incumbent leaves -- the greedy dive, the dive
+// towards the constant-velocity trajectory, the hinted sequence (each skipped when it repeats an
+// earlier one) -- as a list of up to 3 leaves per instance (ws.dv_*), solved by the refill kernel
+// at K = N before level 1: only their costs are used (the incumbents), as in k_lp_root.
+template <int N>
+__global__ __launch_bounds__(kBlock) void k_lp_dive_prep(int B, const hvp_system* __restrict__ systems,
+                                                         const int32_t* __restrict__ sys,
+                                                         const double* __restrict__ params, hvp::Consts C,
+                                                         Workspace ws) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) {
+        ws.dv_lvl[N] = 3ull * (unsigned long long)B;
+        ws.dv_lvl[(HVP_MAX_N + 1) + N] = 0ull;  // claims
+    }
+    if (i >= B) return;
+    const hvp_system& S = systems[sys[i]];
+    const double v0 = params[(size_t)i * C.stride + 1];
+    const double lb = ws.nd_lb[0][i];
+    const bool root_ok = ws.nd_inst[0][i] >= 0 && lb > -1e300 && lb < 1e300;  // the root LP solved
+    uint64_t c1 = 0, c2 = 0, hc = 0;
+    bool d1 = false, d2 = false, dh = false;
+    if (root_ok) {
+        double y[N];
+#pragma unroll
+        for (int j = 0; j < N; ++j) y[j] = ws.task_y[(size_t)i * N + j];
+        d1 = hvp::bnb_dive<N>(S, C, v0, y, &c1);
+#pragma unroll
+        for (int j = 0; j < N; ++j) y[j] = v0;
+        d2 = hvp::bnb_dive<N>(S, C, v0, y, &c2) && !(d1 && c2 == c1);
+        dh = ws.hint && hint_code<N>(ws, i, S, C, v0, &hc) && !(d1 && hc == c1) && !(d2 && hc == c2);
+    }
+    const size_t o = 3 * (size_t)i;
+    ws.dv_inst[o] = d1 ? i : -1;
+    ws.dv_inst[o + 1] = d2 ? i : -1;
+    ws.dv_inst[o + 2] = dh ? i : -1;
+    ws.dv_code[o] = c1;
+    ws.dv_code[o + 1] = c2;
+    ws.dv_code[o + 2] = hc;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        ws.dv_lo[o + q] = 0.0;
+        ws.dv_hi[o + q] = -1.0;
+    }
+    // root + dive LPs (hvp_get_stats counts the levels' nodes from their lists)
+    const unsigned lps = (ws.nd_inst[0][i] >= 0 ? 1u : 0u) + (d1 ? 1u : 0u) + (d2 ? 1u : 0u) + (dh ? 1u : 0u);
+    if (lps) atomicAdd(&ws.counter[3], (unsigned long long)lps);
+}
+
 // The same node LPs through persistent waves: every lane keeps its LP's simplex state (hvp_lp.h
 // LpLane) in registers and runs one iteration per trip; when at least `refill_min` lanes of the
 // wave are free, their finished LPs are written (k_lp_bound's outputs, node for node) and every
@@ -1782,6 +1856,10 @@ __global__ __launch_bounds__(kBnbBlock<N>) void k_lp_bound_refill(int k, const h
                 if (k < N) {
                     ws.nd_lb[dst][t] = st == hvp::L1_OK ? c : (st == hvp::L1_INFEASIBLE ? 1e300 : -1e300);
                     if (st == hvp::L1_FAIL) atomicAdd(&ws.counter[4], 1ull);
+                    if (k == 0 && st == hvp::L1_OK) {  // the root optimum: the greedy dive's start
+#pragma unroll
+                        for (int j = 0; j < N; ++j) ws.task_y[t * N + j] = y[j];
+                    }
                 } else {
                     if (st == hvp::L1_OK) ws.nd_lb[dst][t] = c;
                     ws.leaf_stat[t] = st == hvp::L1_OK ? 0 : (st == hvp::L1_INFEASIBLE ? HVP_INFEASIBLE : HVP_MAXITER);
@@ -2618,10 +2696,41 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
     const int lp_refill = lrf && lrf[0] ? std::max(0, std::min(64, std::atoi(lrf))) : 32;
     const int g_lp = (int)std::min<long long>((h->ws.cap + BS - 1) / BS, (long long)std::max(1, h->n_cu));
     if (lp_lane) {
-        if constexpr (!kCoop<N>)
-            hipLaunchKernelGGL(k_lp_root<N>, dim3((B + kLpRootBlock - 1) / kLpRootBlock), dim3(kLpRootBlock),
-                               sizeof(double) * hvp::LF_COUNT * N * kLpRootBlock, st, B, h->d_sys, sys, role, params,
-                               h->C, ws);
+        if constexpr (!kCoop<N>) {
+            // root level and the incumbent dives through the LP refill kernel (k_lp_root solves
+            // root + up to 3 dive leaves one after another per lane: HVP_LP_ROOT_REFILL=0, A/B)
+            const char* lrr = std::getenv("HVP_LP_ROOT_REFILL");
+            const bool lp_root_refill = lp_refill > 0 && !(lrr && lrr[0] == '0') && ws.dv_mem;
+            if (lp_root_refill) {
+                Workspace wd = ws;  // the dive list in place of level N's (its leaf arrays, counts, claims)
+                wd.nd_inst[N & 1] = ws.dv_inst;
+                wd.nd_code[N & 1] = ws.dv_code;
+                wd.nd_lo[N & 1] = ws.dv_lo;
+                wd.nd_hi[N & 1] = ws.dv_hi;
+                wd.nd_lb[N & 1] = ws.dv_lb;
+                wd.leaf_stat = ws.dv_stat;
+                wd.task_y = ws.dv_y;
+                wd.redo = ws.dv_redo;
+                wd.lvl = ws.dv_lvl;
+                wd.counter = ws.dv_counter;
+                wd.cap = 3 * ws.max_batch;
+                hipLaunchKernelGGL(k_lp_root_init<N>, dim3(grid_for(B)), dim3(kBlock), 0, st, B, h->d_sys, sys, params,
+                                   h->C, ws);
+                HIP_TRY(hipGetLastError());
+                hipLaunchKernelGGL(k_lp_bound_refill<N>, dim3(g_lp), dim3(BS), lds_lp, st, 0, h->d_sys, sys, role,
+                                   params, h->C, ws, lp_refill);
+                HIP_TRY(hipGetLastError());
+                hipLaunchKernelGGL(k_lp_dive_prep<N>, dim3(grid_for(B)), dim3(kBlock), 0, st, B, h->d_sys, sys, params,
+                                   h->C, ws);
+                HIP_TRY(hipGetLastError());
+                hipLaunchKernelGGL(k_lp_bound_refill<N>, dim3(g_lp), dim3(BS), lds_lp, st, N, h->d_sys, sys, role,
+                                   params, h->C, wd, lp_refill);
+            } else {
+                hipLaunchKernelGGL(k_lp_root<N>, dim3((B + kLpRootBlock - 1) / kLpRootBlock), dim3(kLpRootBlock),
+                                   sizeof(double) * hvp::LF_COUNT * N * kLpRootBlock, st, B, h->d_sys, sys, role,
+                                   params, h->C, ws);
+            }
+        }
     } else if (h->C.l1) {
         hipLaunchKernelGGL(k_l1_root<N>, dim3(g_l1), dim3(kL1BlockOf<N>), 0, st, B, h->d_sys, sys, role, params, h->C,
                            ws);

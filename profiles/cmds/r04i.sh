@@ -19,4 +19,5 @@ done
 for m in 0 16 48; do
   HVP_LP_REFILL=$m timeout -k 10 300 python bench.py --cost l1 --no-cpu --steps 3 --warmup 1 --streams 1 > gpurun_out/r04i_bench_l1_refill${m}_s1.jsonl 2> gpurun_out/r04i_bench_l1_refill${m}_s1.err || exit 6
 done
+HVP_LP_ROOT_REFILL=0 timeout -k 10 300 python bench.py --cost l1 --no-cpu --steps 3 --warmup 1 --streams 1 > gpurun_out/r04i_bench_l1_rootkernel_s1.jsonl 2> gpurun_out/r04i_bench_l1_rootkernel_s1.err || exit 8
 HVP_L1_SIMPLEX=0 timeout -k 10 300 python bench.py --cost l1 --no-cpu --steps 3 --warmup 1 > gpurun_out/r04i_bench_l1_ipm_s2.jsonl 2> gpurun_out/r04i_bench_l1_ipm_s2.err || exit 7

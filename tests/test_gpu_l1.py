@@ -224,6 +224,41 @@ def test_l1_branch_and_bound_equals_enumeration_at_batch(gpu_available):
     assert b["nodes"].mean() < e["nodes"].mean()
 
 
+def test_l1_refill_kernels_equal_grid_stride_kernels(gpu_available, monkeypatch):
+    """4100 local MILPs (n = 10, N = 5): the node LPs through persistent waves (k_lp_bound_refill,
+    the root level and its dive leaves included) against the grid-stride kernels (k_lp_root +
+    k_lp_bound, HVP_LP_REFILL=0): the same LPs by the same simplex, so the same tree -- sequences,
+    statuses, LP counts -- and the same optima."""
+    import torch
+
+    from hvp import tables
+    from hvp.models import PwaGearVehicle
+    from hvp.solver import BatchSolver
+
+    n, N = 10, 5
+    veh = PwaGearVehicle(800.0)
+    table = tables.system_from_dict(veh.get_discrete_system(1), tables.gears_of(veh))
+    P, R = [], []
+    for seed in range(2000, 2410):
+        p, r = decent_instances(O.env_initial_state(n, seed), N, leader_window(N))
+        P.append(p)
+        R.append(r)
+    params, roles = np.concatenate(P), np.concatenate(R)
+    dev = torch.device("cuda", 0)
+    tp, tr = torch.from_numpy(params).to(dev), torch.from_numpy(roles).to(dev)
+    ts = torch.zeros(len(roles), dtype=torch.int32, device=dev)
+    s = BatchSolver(tables.problem(N, quadratic_cost=False), [table])
+    a = {k: v.cpu().numpy() for k, v in s.solve_device(ts, tr, tp).items()}
+    monkeypatch.setenv("HVP_LP_REFILL", "0")
+    b = {k: v.cpu().numpy() for k, v in s.solve_device(ts, tr, tp).items()}
+    assert (a["status"] == 0).all()
+    assert np.array_equal(a["status"], b["status"])
+    assert np.array_equal(a["region"], b["region"])
+    assert np.all(np.abs(a["cost"] - b["cost"]) <= 1e-12 * np.maximum(1, np.abs(b["cost"])))
+    assert np.abs(a["u"] - b["u"]).max() <= 1e-9
+    assert np.array_equal(a["nodes"], b["nodes"])
+
+
 @pytest.mark.parametrize("N,method", [(5, 1), (5, 2), (10, 2)])
 def test_l1_status_infeasible_and_unresolved(gpu_available, N, method):
     """Statuses of the min_1_norm search: a leader whose position box cannot be respected is
