@@ -15,7 +15,9 @@
 #include "hvp_ipm.h"
 #include "hvp_l1.h"
 long long g_lp_why[5] = {0, 0, 0, 0, 0};
-long long g_lp_pass = 0;  // ratio-test scans over the terms
+long long g_lp_pass = 0;
+int g_admm_leaf_ipm = 0;  // hvp_hostref_set_admm_leaf_ipm: 1 every ADMM leaf by the interior point, 2 the
+                          // device's HVP_LEAF_GI_CAP=2 (two active-set steps, then the interior point)  // ratio-test scans over the terms
 #define HVP_LP_PASS() (__atomic_fetch_add(&g_lp_pass, 1, __ATOMIC_RELAXED))
 #define HVP_LP_WHY(code) (__atomic_fetch_add(&g_lp_why[code], 1, __ATOMIC_RELAXED))
 int g_lp_trace = 0;
@@ -239,7 +241,18 @@ void solve_one_bnb(const hvp_system& S, const hvp::Consts& C, int role, const do
             return true;
         }
         if (C.form == HVP_FORM_ADMM) {
-            const int r = hvp::solve_admm_lane<N>(q, S, C, role, prm, code, K, 8 * hvp::GiConstraintSet<N>::NC, it);
+            // g_admm_leaf_ipm (tests): the leaves by the interior-point fallback (hvp_admm.h
+            // solve_admm_ipm), as HVP_LEAF_GI_CAP forces on the device
+            // (2: the leaves' active-set steps capped at 2, the interior point where that fails)
+            int r = g_admm_leaf_ipm == 1 && K == N
+                        ? hvp::solve_admm_ipm<N>(q, S, C, role, prm, code, K, it)
+                        : hvp::solve_admm_lane<N>(q, S, C, role, prm, code, K,
+                                                   g_admm_leaf_ipm == 2 && K == N ? 2 : 8 * hvp::GiConstraintSet<N>::NC, it);
+            if (r != hvp::GI_OK && g_admm_leaf_ipm == 2 && K == N) {
+                int it2 = 0;
+                r = hvp::solve_admm_ipm<N>(q, S, C, role, prm, code, K, it2);
+                it += it2;
+            }
             ++nq;
             nit += it;
             if (r != hvp::GI_OK) return false;
@@ -486,6 +499,7 @@ int hvp_hostref_gadmm_solve(const hvp_problem* P, const hvp_system* systems, int
 void hvp_hostref_set_solver(int s) { g_solver = s; }
 void hvp_hostref_set_l1_solver(int s) { g_l1_solver = s; }
 void hvp_hostref_set_lp_trace(int s) { g_lp_trace = s; }
+void hvp_hostref_set_admm_leaf_ipm(int s) { g_admm_leaf_ipm = s; }
 void hvp_hostref_lp_hist(long long* out) {
     for (int i = 0; i < 64; ++i) out[i] = g_lp_hist[i], g_lp_hist[i] = 0;
 }

@@ -2169,12 +2169,14 @@ __global__ __launch_bounds__(kBlock) void k_bnb_key(Workspace ws, int form, int 
         if (inst < 0) continue;
         const double best = inc_of(ws, inst);
         if (ws.leaf_stat[t] != 0) {
-            // A decentralised or naive-ADMM leaf that fails the active-set method AND the
-            // interior-point fallback (K_bnb_ipm, every N) is an infeasible QP (position box),
-            // excluded exactly as the enumeration path and the oracle exclude it.  The min_1_norm
-            // leaves are HVP_INFEASIBLE (certified, excluded) or HVP_MAXITER (unresolved: a leaf
-            // still in contention makes the instance MAXITER rather than a possibly wrong answer).
-            const bool strict = (form != HVP_FORM_DECENT && form != HVP_FORM_ADMM) || l1;
+            // A decentralised leaf that fails the active-set method AND the interior-point fallback
+            // (K_bnb_ipm, every N) is an infeasible QP (position box), excluded exactly as the
+            // enumeration path and the oracle exclude it.  A naive-ADMM leaf that fails both is not
+            // known to be infeasible (the interior point also fails on some feasible Huber-piece
+            // QPs): still in contention, it makes the instance MAXITER rather than a possibly wrong
+            // answer.  The min_1_norm leaves are HVP_INFEASIBLE (certified, excluded) or
+            // HVP_MAXITER (unresolved, treated the same way).
+            const bool strict = form != HVP_FORM_DECENT || l1;
             if (ws.leaf_stat[t] == HVP_MAXITER && strict && !hvp::bnb_pruned(ws.nd_lb[src][t], best))
                 atomicOr(&ws.inst_flag[inst], 4);
             continue;

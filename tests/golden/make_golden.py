@@ -525,7 +525,7 @@ def cent_fixtures(big: bool = False):
             ("cent_l1_gear_n2_N4.npz", 4, seeds_jobs(2, 4, range(2), model=1, quadratic=False), O.Cfg(), 1),
         ]
     elif big:
-        sets = [("cent_n10_N5.npz", 5, seeds_jobs(10, 5, range(2)), O.Cfg(), 0)]
+        sets = [("cent_n10_N5.npz", 5, seeds_jobs(10, 5, range(4)), O.Cfg(), 0)]  # ~1.5 min per platoon
     else:
         sets = [
             ("cent_n2_N5.npz", 5, seeds_jobs(2, 5, range(10)), O.Cfg(), 0),
