@@ -2925,6 +2925,7 @@ int launch_gadmm_qp(hvp_handle* h, int P, int n, int lo, int m, const int32_t* s
         h->gadmm_redo_cap = B;
     }
     HIP_TRY(hipMemsetAsync(h->g_counter + 3, 0, sizeof(unsigned long long), st));
+    HIP_TRY(hipEventRecord(h->ev0, st));  // (hvp_get_stats times ev0 -> ev1 of the last call)
     HIP_TRY(hipEventRecord(h->evq0, st));
     if constexpr (kCoop<N>) {
         // each local QP's final hinge states, active set and factors, carried from one ADMM
@@ -2963,6 +2964,7 @@ int launch_gadmm_qp(hvp_handle* h, int P, int n, int lo, int m, const int32_t* s
         HIP_TRY(hipGetLastError());
     }
     HIP_TRY(hipEventRecord(h->evq1, st));
+    HIP_TRY(hipEventRecord(h->ev1, st));
     h->last_stream = st;
     h->last_B = B;
     h->last_bnb = false;
