@@ -1036,11 +1036,23 @@ def main() -> None:
     cand_per_step = cand / args.steps
     notional = cand_per_step * dense_qp_bytes(N) + B * instance_io_bytes(N)
     simplex = N <= 8 and os.environ.get("HVP_L1_SIMPLEX", "1") != "0"  # min_1_norm LPs: per-lane simplex
+    env = os.environ.get
     if bnb and not quadratic:
-        qk = [("k_lp_root", 1), ("k_lp_bound", N)] if simplex else [("k_l1_root", 1), ("k_l1_bound", N)]
+        if not simplex:
+            qk = [("k_l1_root", 1), ("k_l1_bound", N)]
+        elif env("HVP_LP_REFILL", "32") == "0":
+            qk = [("k_lp_root", 1), ("k_lp_bound", N)]
+        elif env("HVP_LP_ROOT_REFILL", "1") == "0":
+            qk = [("k_lp_root", 1), ("k_lp_bound_refill", N)]
+        else:  # the root level, the dive leaves and the N levels through the refill kernel
+            qk = [("k_lp_bound_refill", N + 2)]
     elif bnb:
-        qk = [("k_bnb_root_coop", 1), ("k_bnb_bound_coop", N)] if N > 8 else [("k_bnb_root", 1),
-                                                                              ("k_bnb_bound_refill", N)]
+        if N > 8:
+            qk = [("k_bnb_root_coop", 1), ("k_bnb_bound_coop", N)]
+        elif env("HVP_ROOT_REFILL", "1") == "0":
+            qk = [("k_bnb_root", 1), ("k_bnb_bound_refill", N)]
+        else:  # root level + dive leaves + N levels, all through the refill kernel
+            qk = [("k_bnb_bound_refill", N + 2)]
     else:
         qk = [("k_qp_gi", 1)] if quadratic else [("k_qp_lp" if simplex else "k_qp_l1", 1)]
     # the PMC figures are per launch over the WHOLE batch (the profile runs this workload with

@@ -42,7 +42,8 @@ def short(name: str) -> str:
     for k in ("k_qp_gi", "k_qp_ipm", "k_enum", "k_cost", "k_select", "k_inst_prep", "k_bnb_root_coop", "k_bnb_root",
               "k_bnb_expand", "k_bnb_bound_refill", "k_bnb_bound_coop", "k_bnb_bound",
               "k_bnb_key", "k_bnb_write", "k_bnb_finish", "k_gadmm_qp_coop", "k_gadmm_qp", "k_gadmm_update",
-              "k_gadmm_rollout", "k_gadmm_switch", "k_admm_update", "k_l1_root", "k_l1_bound", "k_qp_l1", "k_lp_root", "k_lp_bound", "k_qp_lp",
+              "k_gadmm_rollout", "k_gadmm_switch", "k_admm_update", "k_l1_root", "k_l1_bound", "k_qp_l1", "k_lp_root_init", "k_lp_dive_prep", "k_lp_bound_refill",
+              "k_lp_root", "k_lp_bound", "k_qp_lp", "k_bnb_dive_prep",
               "k_cent_bnb", "k_cent_tasks", "k_cent_final", "k_cent_init", "k_env_step", "k_decent_params"):
         if k in name:
             return k
