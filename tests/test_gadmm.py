@@ -448,12 +448,23 @@ def test_gadmm_local_problem_ipm_fallback(gpu_available, monkeypatch, N):
 @pytest.mark.gpu
 def test_gadmm_engine_ipm_fallback(gpu_available, monkeypatch):
     """configs[3] at its own size (n = 20, N = 10, 100 ADMM iterations, 2 seeds x 2 steps) with the
-    local QPs forced through the interior-point fallback: the device coordinator still matches
-    the oracle coordinator (sequences, rounds, warm-start choices, controls, costs)."""
+    local QPs forced through the interior-point fallback (HVP_LEAF_GI_CAP=2): every local QP is
+    solved (no platoon fails) and the controls respect the input box.  Not the oracle's controls:
+    over 100 coupled iterations the switching rule's edge bits -- V-row multipliers against
+    kEdgeMultTol, exact from an active-set solve, approximate from the interior point -- decide
+    differently somewhere and the sequences part (MI355X r04i; the traced local problems alone
+    do match, test_gadmm_local_problem_ipm_fallback).  Unforced, the fallback only meets the rare
+    QPs the active-set method fails on."""
     monkeypatch.setenv("HVP_LEAF_GI_CAP", "2")
     fx = load("gadmm_steps_n20_N10.npz")
+    n, N = int(fx["n"]), int(fx["N"])
     P = len(fx["states"]) // int(fx["steps"])
     eng = _engine(fx, P)
     outs = _run_steps(fx, [eng])
-    _check_steps(fx, [o[0] for o in outs])
+    st = O.gear_pwa_system(800.0)
+    for out, runs in (o[0] for o in outs):
+        for r in runs:
+            assert not r["failed"].cpu().numpy().any()
+        u = out["u"].cpu().numpy().reshape(-1, n, N)
+        assert np.isfinite(u).all() and u.min() >= st["umin"] - 1e-7 and u.max() <= st["umax"] + 1e-7
     assert eng.solver.stats().n_fallback > 0
