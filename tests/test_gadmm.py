@@ -450,7 +450,8 @@ def test_gadmm_engine_ipm_fallback(gpu_available, monkeypatch):
     """configs[3] at its own size (n = 20, N = 10, 100 ADMM iterations, 2 seeds x 2 steps) with the
     local QPs forced through the interior-point fallback (HVP_LEAF_GI_CAP=2): the engine runs to
     the end, a platoon whose local QP fails both solvers is reported failed (never a silent
-    answer), and every other platoon's controls respect the input box.  Not the oracle's controls:
+    answer; on MI355X every platoon of this run fails somewhere), and every other platoon's controls
+    respect the input box.  Not the oracle's controls:
     over 100 coupled iterations the switching rule's edge bits -- V-row multipliers against
     kEdgeMultTol, exact from an active-set solve, approximate from the interior point -- decide
     differently somewhere, and the interior point fails on some of these QPs (MI355X r04i; the
@@ -468,5 +469,7 @@ def test_gadmm_engine_ipm_fallback(gpu_available, monkeypatch):
         for r in runs:
             ok |= ~r["failed"].cpu().numpy()
         u = out["u"].cpu().numpy().reshape(-1, n, N)[ok]
-        assert np.isfinite(u).all() and u.min() >= st["umin"] - 1e-7 and u.max() <= st["umax"] + 1e-7
+        assert np.isfinite(u).all()
+        if u.size:
+            assert u.min() >= st["umin"] - 1e-7 and u.max() <= st["umax"] + 1e-7
     assert eng.solver.stats().n_fallback > 0
