@@ -3,8 +3,6 @@
 set -o pipefail
 export TMPDIR=/tmp
 L=$PWD/hybrid-vehicle-platoon_amd/lib
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread > gpurun_out/r04i_tests.log 2>&1 || exit 1
-timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/r04i_smoke.log 2>&1 || exit 2
 for r in a b; do
   for v in v11 v10 v01 rr; do
     HVP_LIB=$L/libhvpsolve_$v.so timeout -k 10 300 python bench.py --no-cpu > gpurun_out/r04i_bench_${v}_$r.jsonl 2> gpurun_out/r04i_bench_${v}_$r.err || exit 3
@@ -21,3 +19,5 @@ for m in 0 16 48; do
 done
 HVP_LP_ROOT_REFILL=0 timeout -k 10 300 python bench.py --cost l1 --no-cpu --steps 3 --warmup 1 --streams 1 > gpurun_out/r04i_bench_l1_rootkernel_s1.jsonl 2> gpurun_out/r04i_bench_l1_rootkernel_s1.err || exit 8
 HVP_L1_SIMPLEX=0 timeout -k 10 300 python bench.py --cost l1 --no-cpu --steps 3 --warmup 1 > gpurun_out/r04i_bench_l1_ipm_s2.jsonl 2> gpurun_out/r04i_bench_l1_ipm_s2.err || exit 7
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread > gpurun_out/r04i_tests.log 2>&1 || exit 11
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/r04i_smoke.log 2>&1 || exit 12

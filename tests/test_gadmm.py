@@ -463,7 +463,7 @@ def test_gadmm_engine_ipm_fallback(gpu_available, monkeypatch):
     P = len(fx["states"]) // int(fx["steps"])
     eng = _engine(fx, P)
     outs = _run_steps(fx, [eng])
-    st = O.gear_pwa_system(800.0)
+    st = _system()
     for out, runs in (o[0] for o in outs):
         ok = np.zeros(P, bool)
         for r in runs:
@@ -471,5 +471,5 @@ def test_gadmm_engine_ipm_fallback(gpu_available, monkeypatch):
         u = out["u"].cpu().numpy().reshape(-1, n, N)[ok]
         assert np.isfinite(u).all()
         if u.size:
-            assert u.min() >= st["umin"] - 1e-7 and u.max() <= st["umax"] + 1e-7
+            assert u.min() >= st.umin - 1e-7 and u.max() <= st.umax + 1e-7
     assert eng.solver.stats().n_fallback > 0
