@@ -1579,6 +1579,15 @@ __global__ __launch_bounds__(kBnbBlock<N>) void k_lp_bound(int k, const hvp_syst
 // where the refill kernel's event reads the workspace descriptor and the problem constants
 // (A/B builds): 1 = the by-value kernel arguments, 0 = the handle's device copies through
 // uniform_opaque pointers (the level index laundered too)
+// HVP_REFILL_BYVAL: the kernel takes only the by-value descriptor (no device-copy pointers)
+#ifndef HVP_REFILL_BYVAL
+#define HVP_REFILL_BYVAL 0
+#endif
+#if HVP_REFILL_BYVAL
+#define HVP_REFILL_LAUNCH_ARGS(wsp, wsval) wsval
+#else
+#define HVP_REFILL_LAUNCH_ARGS(wsp, wsval) wsp, h->d_consts, wsval
+#endif
 #ifndef HVP_REFILL_WS_ARG
 #define HVP_REFILL_WS_ARG 0
 #endif
@@ -1950,14 +1959,155 @@ __device__ inline const T* uniform_opaque(const T* p) {
 // loaded inside the event through uniform_opaque pointers.  (With both structures as kernel
 // arguments live across the loop, 128 SGPRs spilled into two VGPRs' lanes and 35 dwords of VGPRs
 // into scratch.)
+#if HVP_REFILL_BYVAL
+// (round 3's kernel body: the descriptor and the constants as by-value kernel arguments, the
+// level list hoisted)
+template <int N>
+__global__ __launch_bounds__(kBnbBlock<N>) __attribute__((amdgpu_waves_per_eu(HVP_REFILL_WAVES)))
+void k_bnb_bound_refill(int k, const hvp_system* __restrict__ systems, const int32_t* __restrict__ sys,
+                        const int32_t* __restrict__ role, const double* __restrict__ params, hvp::Consts C,
+                        Workspace ws) {
+    constexpr int BS = kBnbBlock<N>;
+    static_assert(N <= HVP_MAX_N_ENUM, "lane refill is the N <= 8 path");
+    const int dst = k & 1;
+    const LevelList lvl = level_list(ws, k);
+    const long long total = lvl.count();
+    unsigned long long* claim = ws.lvl + (HVP_MAX_N + 1) + k;
+    const int lane = threadIdx.x & 63;
+    hvp::LaneQp<N, LdsMem<N, BS>> q;
+    q.mem.lane = threadIdx.x;
+    hvp::GiLane<N> g;
+    long long t = -1;  // node of the lane
+    int inst = 0, stage = RS_IDLE, fail = 0;
+    uint64_t code = 0;
+    bool exhausted = false;
+    unsigned long long iter_sum = 0;
+#ifdef HVP_REFILL_PROF  // diagnostics build: event / trip cycles and busy lane-trips per wave
+    unsigned long long pf_ev = 0, pf_all = 0, pf_busy = 0, pf_trips = 0, pf_wb = 0, pf_cl = 0, pf_dc = 0, pf_rs = 0;
+    const unsigned long long pf_t0 = __builtin_amdgcn_s_memtime();
+    int pf_mine = 0, pf_gen = 0;
+#endif
+    for (;;) {
+        const bool done = stage >= RS_FAIL;
+        const unsigned long long free = __ballot(stage == RS_IDLE || done);
+        const int nfree = __popcll(free);
+#ifdef HVP_REFILL_PROF
+        const unsigned long long pf_e0 = __builtin_amdgcn_s_memtime();
+        const bool pf_event = nfree >= kRefillMin || nfree == 64;
+        pf_busy += (unsigned long long)(64 - nfree);
+        pf_trips += 1;
+        if (pf_event) {
+            if (done) atomicAdd(&g_pf_hist[pf_mine < 63 ? pf_mine : 63], 1ull);
+            if (lane == 0) atomicAdd(&g_pf_hist[64 + (pf_gen < 63 ? pf_gen : 63)], 1ull);
+            pf_gen = 0;
+            pf_mine = 0;
+        }
+        ++pf_gen;
+        if (stage == RS_SCAN || stage == RS_STEP) ++pf_mine;
+#endif
+        if (nfree >= kRefillMin || nfree == 64) {
+            // ---- event: write the finished lanes' results, then refill every free lane
+            unsigned cmask = 0;  // children of a finished bound node (k_bnb_expand's work, fused)
+            double clb = 0.0;
+            if (done) {
+                const int st = stage == RS_OPT ? g.verify(C, nullptr) : fail;
+                const bool ok = st == hvp::GI_OK;
+                const double c = ok ? hvp::direct_cost<N>(q, systems[sys[inst]], C, role[inst],
+                                                          params + (size_t)inst * C.stride, code, k)
+                                    : 0.0;
+                iter_sum += (unsigned long long)g.iter;
+#ifdef HVP_REFILL_PROF
+                {
+                    const double cc = __builtin_amdgcn_readfirstlane(__double_as_longlong(c) & 0xffffffff);
+                    (void)cc;
+                    pf_dc += __builtin_amdgcn_s_memtime() - pf_e0;
+                }
+#endif
+                bnb_node_done<N>(k, t, inst, ok, g.iter, c, q.y, C, ws);
+                stage = RS_IDLE;
+                // the incumbent only changes at the leaves (level N): below N this pruning test
+                // sees the value a separate expand kernel would
+                clb = ok ? c : -1e300;
+                if (k < N && !(ws.inst_flag[inst] & 2) && !hvp::bnb_pruned(clb, inc_of(ws, inst)))
+                    cmask = bnb_children(systems[sys[inst]], C, k, ws.nd_lo[dst][t], ws.nd_hi[dst][t]);
+            }
+            if (k < N) {
+                unsigned long long limit;
+                const unsigned long long off =
+                    split_reserve(ws, k + 1, __popc(cmask), done ? g.iter : 0, lane, limit);
+                if (cmask)
+                    bnb_put_children(ws, k + 1, off, limit, cmask, inst, systems[sys[inst]], C, code,
+                                     ws.nd_lo[dst][t], ws.nd_hi[dst][t], clb);
+#ifdef HVP_REFILL_PROF
+                pf_rs += __builtin_amdgcn_s_memtime() - pf_e0;
+#endif
+            }
+            if (exhausted && nfree == 64) break;
+#ifdef HVP_REFILL_PROF
+            const unsigned long long pf_w1 = __builtin_amdgcn_s_memtime();
+            pf_wb += pf_w1 - pf_e0;
+#endif
+            if (!exhausted) {
+                const unsigned long long base = wave_claim(claim, free, nfree, lane);
+#ifdef HVP_REFILL_PROF
+                {
+                    const unsigned long long bb = __builtin_amdgcn_readfirstlane((unsigned)base);
+                    (void)bb;
+                    pf_cl += __builtin_amdgcn_s_memtime() - pf_w1;
+                }
+#endif
+                if (base + nfree >= (unsigned long long)total) exhausted = true;
+                const long long mc = (long long)base + wave_rank(free);
+                const long long mine = lvl.slot(mc);
+                if (stage == RS_IDLE && mc < total) {
+                    inst = ws.nd_inst[dst][mine];
+                    if (inst < 0) {  // dead slot of an overflowed reservation
+                        if (k == N) ws.leaf_stat[mine] = HVP_OVERFLOW;
+                        else ws.nd_lb[dst][mine] = 1e300;
+                    } else {
+                        t = mine;
+                        code = ws.nd_code[dst][mine];
+                        setup_node<N>(q, systems[sys[inst]], C, ws, inst, role[inst], params + (size_t)inst * C.stride,
+                                      code, k, ws.nd_lo[dst][mine], ws.nd_hi[dst][mine]);
+                        stage = g.init(q) == hvp::GI_OK ? RS_SCAN : RS_FAIL;
+                        fail = hvp::GI_FAIL_CHOL;
+                    }
+                }
+            }
+        }
+#ifdef HVP_REFILL_PROF
+        if (pf_event) pf_ev += __builtin_amdgcn_s_memtime() - pf_e0;
+#endif
+        if (stage == RS_SCAN || stage == RS_STEP) gi_trip<N>(q, g, C, stage, fail);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) iter_sum += __shfl_down(iter_sum, off, 64);
+    if (lane == 0 && iter_sum) atomicAdd(&ws.counter[1], iter_sum);
+#ifdef HVP_REFILL_PROF
+    pf_all = __builtin_amdgcn_s_memtime() - pf_t0;
+    if (lane == 0) {  // the claim slots of levels > N are free (prof builds need N <= 8)
+        unsigned long long* pf = ws.lvl + 2 * (HVP_MAX_N + 1) - 8;
+        atomicAdd(&pf[0], pf_ev);
+        atomicAdd(&pf[1], pf_all);
+        atomicAdd(&pf[2], pf_busy);
+        atomicAdd(&pf[3], pf_trips);
+        atomicAdd(&pf[4], pf_wb);
+        atomicAdd(&pf[5], pf_cl);
+        atomicAdd(&pf[6], pf_dc);
+        atomicAdd(&pf[7], pf_rs);
+    }
+#endif
+}
+#else
 template <int N>
 __global__ __launch_bounds__(kBnbBlock<N>) __attribute__((amdgpu_waves_per_eu(HVP_REFILL_WAVES)))
 void k_bnb_bound_refill(int k_arg, const hvp_system* __restrict__ systems, const int32_t* __restrict__ sys,
                         const int32_t* __restrict__ role, const double* __restrict__ params, hvp::Consts C,
                         const Workspace* __restrict__ wsd, const hvp::Consts* __restrict__ cd, Workspace wsv) {
+    (void)wsd, (void)cd;
     constexpr int BS = kBnbBlock<N>;
     static_assert(N <= HVP_MAX_N_ENUM, "lane refill is the N <= 8 path");
-    (void)wsd, (void)cd, (void)wsv;
+    (void)wsv;
     const int lane = threadIdx.x & 63;
     hvp::LaneQp<N, LdsMem<N, BS>> q;
     q.mem.lane = threadIdx.x;
@@ -2107,6 +2257,7 @@ void k_bnb_bound_refill(int k_arg, const hvp_system* __restrict__ systems, const
     }
 #endif
 }
+#endif
 
 // Leaves whose active-set solve failed its verification (degenerate vertices, e.g. the
 // position box at p_max): re-solved by the interior-point method on the full row set
@@ -2762,13 +2913,13 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
             if (root_refill) {
                 const int g_root = (int)std::min<long long>((B + BS - 1) / BS, (long long)h->n_cu * kRefillBlocksPerCu);
                 hipLaunchKernelGGL(k_bnb_bound_refill<N>, dim3(g_root), dim3(BS), lds, st, 0, h->d_sys, sys, role,
-                                   params, h->C, h->d_ws, h->d_consts, h->ws_up[0]);
+                                   params, h->C, HVP_REFILL_LAUNCH_ARGS(h->d_ws, h->ws_up[0]));
                 HIP_TRY(hipGetLastError());
                 hipLaunchKernelGGL(k_bnb_dive_prep<N>, dim3(grid_for(B)), dim3(kBlock), 0, st, B, h->d_sys, sys, params,
                                    h->C, ws);
                 HIP_TRY(hipGetLastError());
                 hipLaunchKernelGGL(k_bnb_bound_refill<N>, dim3(g_root), dim3(BS), lds, st, N, h->d_sys, sys, role,
-                                   params, h->C, h->d_ws + 1, h->d_consts, h->ws_up[1]);
+                                   params, h->C, HVP_REFILL_LAUNCH_ARGS(h->d_ws + 1, h->ws_up[1]));
             } else {
                 // (one lane per instance, 1 wave per SIMD)
                 hipLaunchKernelGGL((k_bnb_root<N, false>), dim3((B + BS - 1) / BS), dim3(BS), lds, st, B, h->d_sys,
@@ -2811,7 +2962,7 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
                 const int g_refill = (int)std::min<long long>((h->ws.cap + BS - 1) / BS,
                                                               (long long)h->n_cu * kRefillBlocksPerCu);
                 hipLaunchKernelGGL(k_bnb_bound_refill<N>, dim3(g_refill), dim3(BS), lds, st, k, h->d_sys, sys, role,
-                                   params, h->C, h->d_ws, h->d_consts, h->ws_up[0]);
+                                   params, h->C, HVP_REFILL_LAUNCH_ARGS(h->d_ws, h->ws_up[0]));
             }
         }
         HIP_TRY(hipGetLastError());
