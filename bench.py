@@ -893,9 +893,11 @@ def main() -> None:
                     help="decent: every step = neighbour predictions + local MIQPs + plant step, all on the device")
     ap.add_argument("--admm-iters", type=int, default=None, help="default 20 (admm) / 100 (gadmm)")
     ap.add_argument("--max-rounds", type=int, default=10, help="gadmm: switching rounds cap")
-    ap.add_argument("--streams", type=int, default=2,
+    ap.add_argument("--streams", type=int, default=None,
                     help="platoons split over this many handles / HIP streams (decent: one host thread; admm, "
-                         "gadmm replicas, cent: one host thread each); 2 measured best (DESIGN.md section 4)")
+                         "gadmm replicas, cent: one host thread each); default 2, measured best (DESIGN.md "
+                         "section 4) -- 1 for the min_1_norm simplex path, whose LP kernels fill the chip alone "
+                         "(231k vs 207k platoon-steps/s, profiles/r04i_bench_l1_*)")
     ap.add_argument("--no-warm-incumbent", action="store_true",
                     help="admm: do not try the previous iteration's sequences as incumbents (A/B)")
     ap.add_argument("--gadmm-layout", choices=["replicas", "vehicles"], default="replicas")
@@ -906,6 +908,10 @@ def main() -> None:
                     help="no GPU work: start the ranks (gloo), shard the seeds, run the timing protocol around an "
                          "empty step and print the line (tests the --gpus N launcher on a CPU)")
     args = ap.parse_args()
+    if args.streams is None:
+        simplex_l1 = (args.controller == "decent" and args.cost == "l1" and args.N <= 8
+                      and os.environ.get("HVP_L1_SIMPLEX", "1") != "0")
+        args.streams = 1 if simplex_l1 else 2
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(sys.argv[1:], args.gpus))
