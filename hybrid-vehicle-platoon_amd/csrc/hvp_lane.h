@@ -1579,9 +1579,11 @@ __global__ __launch_bounds__(kBnbBlock<N>) void k_lp_bound(int k, const hvp_syst
 // where the refill kernel's event reads the workspace descriptor and the problem constants
 // (A/B builds): 1 = the by-value kernel arguments, 0 = the handle's device copies through
 // uniform_opaque pointers (the level index laundered too)
-// HVP_REFILL_BYVAL: the kernel takes only the by-value descriptor (no device-copy pointers)
+// HVP_REFILL_BYVAL (default): round 3's kernel body -- the workspace descriptor and the problem
+// constants as by-value kernel arguments, the level list hoisted; 0: the variants below (measured
+// slower: 2.97-3.15 vs 2.68 ms of QP launches per C2 step, profiles/r04i_bench_*, r04j_bench_*)
 #ifndef HVP_REFILL_BYVAL
-#define HVP_REFILL_BYVAL 0
+#define HVP_REFILL_BYVAL 1
 #endif
 #if HVP_REFILL_BYVAL
 #define HVP_REFILL_LAUNCH_ARGS(wsp, wsval) wsval
