@@ -28,7 +28,12 @@ from .env import EpisodeMonitor, PlatoonEnv
 from .models import Platoon, Vehicle
 from .params import ConstantSpacingPolicy, Params, Sim, SpacingPolicy
 
-DEFAULT_MAX_NODES = 2_000_000
+DEFAULT_MAX_NODES = 2_000_000  # batched solves (bench.py names it in its metric)
+# The per-platoon drop-in (MpcMldCent.solve_mpc) searches to the optimum like the reference's
+# Gurobi call: the heaviest C2-size platoon found (seed 426) needs 27.8M QPs (84 s alone on one
+# MI355X, profiles/r04l_cent_heavy_426_cap30M.jsonl); past this cap the call raises as the
+# reference does on a non-optimal status.
+DROPIN_MAX_NODES = 64_000_000
 
 
 def cent_problem(N: int, spacing_policy: SpacingPolicy | None = None, quadratic_cost: bool = True,
@@ -173,7 +178,7 @@ class MpcMldCent:
         self.setup_cost_and_constraints(None, spacing_policy, leader_index, quadratic_cost, accel_cnstr_tightening,
                                         real_vehicle_as_reference)
         self.leader_traj = np.zeros((2, N + 1))
-        self.max_nodes = DEFAULT_MAX_NODES
+        self.max_nodes = DROPIN_MAX_NODES
         self.x_pred: np.ndarray | None = None
         self.u_pred: np.ndarray | None = None
         self.regions_pred: np.ndarray | None = None
