@@ -895,9 +895,10 @@ def main() -> None:
     ap.add_argument("--max-rounds", type=int, default=10, help="gadmm: switching rounds cap")
     ap.add_argument("--streams", type=int, default=None,
                     help="platoons split over this many handles / HIP streams (decent: one host thread; admm, "
-                         "gadmm replicas, cent: one host thread each); default 2, measured best (DESIGN.md "
-                         "section 4) -- 1 for the min_1_norm simplex path, whose LP kernels fill the chip alone "
-                         "(231k vs 207k platoon-steps/s, profiles/r04i_bench_l1_*)")
+                         "gadmm replicas, cent: one host thread each); default: 3 for decent min_2_norm "
+                         "(profiles/r04m_bench_*), 1 for the min_1_norm simplex path, whose LP kernels fill the "
+                         "chip alone (231k vs 207k platoon-steps/s, profiles/r04i_bench_l1_*), 2 otherwise "
+                         "(DESIGN.md section 4)")
     ap.add_argument("--no-warm-incumbent", action="store_true",
                     help="admm: do not try the previous iteration's sequences as incumbents (A/B)")
     ap.add_argument("--gadmm-layout", choices=["replicas", "vehicles"], default="replicas")
@@ -911,7 +912,10 @@ def main() -> None:
     if args.streams is None:
         simplex_l1 = (args.controller == "decent" and args.cost == "l1" and args.N <= 8
                       and os.environ.get("HVP_L1_SIMPLEX", "1") != "0")
-        args.streams = 1 if simplex_l1 else 2
+        # decent min_2_norm: 3 (the root level and the dive leaves occupy a quarter of the CUs for
+        # ~0.6 ms per solve; a third stream's levels fill the rest: 7.09-7.14M vs 6.74-6.98M on the
+        # same box, profiles/r04m_bench_*); min_1_norm simplex: 1; the ADMM forms, cent: 2
+        args.streams = 1 if simplex_l1 else (3 if args.controller == "decent" else 2)
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(sys.argv[1:], args.gpus))
