@@ -7,3 +7,5 @@ for r in a b; do
     timeout -k 10 300 python bench.py --no-cpu --streams $s > gpurun_out/r04n_bench_s${s}_$r.jsonl 2> gpurun_out/r04n_bench_s${s}_$r.err || exit 2
   done
 done
+# the default line of the shipped library and bench (three streams, CPU baselines)
+timeout -k 10 400 python bench.py > gpurun_out/r04n_bench_default.jsonl 2> gpurun_out/r04n_bench_default.err || exit 3
