@@ -497,19 +497,30 @@ HVP_HD HVP_FORCEINLINE inline int solve_admm_ipm(LaneQp<N, M>& q, const hvp_syst
         setup_lane_admm<N>(q, S, C, role, prm, code, K, hs);
         const QpOut o = Solver<N, true, M>::solve(q, C);
         iters += o.iters;
-        if (o.status != 0) return GI_FAIL_ITER;
+        // the interior point's own answer, kept for a polish that fails
+        double yi[N];
+        uint32_t mi = 0;
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            yi[j] = q.y[j];
+            if (q.llo[3 * j] > kEdgeMultTol) mi |= 1u << (2 * j);
+            if (q.lhi[3 * j] > kEdgeMultTol) mi |= 1u << (2 * j + 1);
+        }
+        // exact optimum and multipliers from the interior point's active set (hvp_gi.h gi_polish;
+        // tried from a non-converged iterate too: its active set may still be the right one)
+        int pit = 0;
+        uint32_t mp = 0;
+        const int pst = gi_polish<N>(q, C, 8 * GiConstraintSet<N>::NC, pit, &mp);
+        iters += pit;
+        if (pst != GI_OK) {
+            if (o.status != 0) return GI_FAIL_ITER;
+#pragma unroll
+            for (int j = 0; j < N; ++j) q.y[j] = yi[j];
+        }
         bool consistent;
         hs = admm_classify<N>(C, role, prm, q.P1, q.ts, q.y, hs, &consistent);
         if (consistent) {
-            if (edge) {
-                uint32_t m = 0;
-#pragma unroll
-                for (int j = 0; j < N; ++j) {
-                    if (q.llo[3 * j] > kEdgeMultTol) m |= 1u << (2 * j);
-                    if (q.lhi[3 * j] > kEdgeMultTol) m |= 1u << (2 * j + 1);
-                }
-                *edge = m;
-            }
+            if (edge) *edge = pst == GI_OK ? mp : mi;
             return GI_OK;
         }
     }

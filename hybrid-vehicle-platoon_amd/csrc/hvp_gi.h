@@ -526,13 +526,9 @@ struct GiLane {
     }
 };
 
-// One QP from start to finish.  Returns GI_OK with the optimum in q.y, or a GI_FAIL_* reason.
+// The scan / step loop of Goldfarb-Idnani from the lane's current state to the verified optimum.
 template <int N, class M>
-HVP_HD inline int solve_gi(LaneQp<N, M>& q, const Consts& C, int max_iter, int& iters, uint32_t* edge = nullptr) {
-    GiLane<N> g;
-    int st = g.init(q);
-    iters = 0;
-    if (st != GI_OK) return st;
+HVP_HD HVP_FORCEINLINE inline int gi_run(GiLane<N>& g, LaneQp<N, M>& q, const Consts& C, int max_iter, int& iters, uint32_t* edge) {
     for (;;) {
         q.mem.refresh();
         g.fence(q);
@@ -548,6 +544,106 @@ HVP_HD inline int solve_gi(LaneQp<N, M>& q, const Consts& C, int max_iter, int& 
     }
     iters = g.iter;
     return g.verify(C, edge);
+}
+
+// One QP from start to finish.  Returns GI_OK with the optimum in q.y, or a GI_FAIL_* reason.
+template <int N, class M>
+HVP_HD inline int solve_gi(LaneQp<N, M>& q, const Consts& C, int max_iter, int& iters, uint32_t* edge = nullptr) {
+    GiLane<N> g;
+    int st = g.init(q);
+    iters = 0;
+    if (st != GI_OK) return st;
+    return gi_run<N>(g, q, C, max_iter, iters, edge);
+}
+
+// Row `id` made active as an EQUALITY whatever its slack (the polish below): the step of
+// GiLane::step with the signed full length t = -slack / |v|^2 and no ratio test, so the
+// invariant (y optimal for the active rows at equality, u their multipliers, of any sign)
+// holds after it.  false (nothing changed) when the row depends on the active ones.
+template <int N, class M>
+HVP_HD HVP_FORCEINLINE inline bool gi_force_add(GiLane<N>& g, LaneQp<N, M>& q, const Consts& C, int id) {
+    double c[N], dp;
+    gi_row<N>(q, C, id, c, dp);
+    double d[N];
+    double dn = 0.0, d2n = 0.0;
+#pragma unroll
+    for (int col = 0; col < N; ++col) {
+        double s = 0.0;
+#pragma unroll
+        for (int i = 0; i < N; ++i) s -= g.J[i][col] * c[i];
+        d[col] = s;
+        dn += s * s;
+        d2n += col >= g.nact ? s * s : 0.0;
+    }
+    if (!(d2n > 1e-14 * dn) || g.nact >= N) return false;
+    double z[N], slack = dp;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        double s = 0.0;
+#pragma unroll
+        for (int col = 0; col < N; ++col) s += col >= g.nact ? g.J[i][col] * d[col] : 0.0;
+        z[i] = s;
+        slack -= c[i] * q.y[i];
+    }
+    double r[N];
+#pragma unroll
+    for (int i = N - 1; i >= 0; --i) {
+        double s = d[i];
+#pragma unroll
+        for (int j = i + 1; j < N; ++j) s -= g.R[rix(i, j)] * r[j];
+        r[i] = i < g.nact ? s * frcp(g.R[rix(i, i)]) : 0.0;
+    }
+    const double t = -slack / d2n;  // z.n = |v|^2
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        q.y[i] += t * z[i];
+        g.u[i] -= t * r[i];
+    }
+    g.unew = t;
+    g.p = id;
+    g.add(d, d2n);
+    return true;
+}
+
+// Active-set polish of an interior-point solution (the ADMM forms' fallback, hvp_admm.h
+// solve_admm_ipm).  The rows the interior point holds active (multiplier above slack: l t = mu
+// separates them from the inactive ones) are added as equalities from the unconstrained
+// minimiser, which gives the equality-constrained optimum on that set with its exact
+// multipliers; a row whose multiplier comes out negative leaves the set and the adds start over
+// (at most 4 times); from that dual-feasible state Goldfarb-Idnani runs to its verified optimum,
+// adding what the set missed.  So the answer, its multipliers and the switching rule's edge bits
+// are the active-set method's, not the interior point's approximations of them.  Only QPs
+// without soft rows (the ADMM forms: the safety lives in the copies' hinges); GI_OK with the
+// optimum in q.y, else a GI_FAIL_* code and q.y undefined.
+template <int N, class M>
+HVP_HD HVP_FORCEINLINE inline int gi_polish(LaneQp<N, M>& q, const Consts& C, int max_iter, int& iters, uint32_t* edge) {
+    iters = 0;
+    if (q.has_sf || q.has_sb) return GI_FAIL_VERIFY;
+    GiMask<N> cand;
+#pragma unroll
+    for (int p = 0; p < LaneQp<N, M>::NPAIR; ++p) {
+        const int id = p < 3 * N ? 6 * (p / 3) + 2 * (p % 3) : 6 * N + 4 * (p - 3 * N);
+        if (q.llo[p] > q.tlo[p]) cand.set(id, true);
+        if (q.lhi[p] > q.thi[p]) cand.set(id + 1, true);
+    }
+    GiLane<N> g;
+    bool dual_ok = false;
+    for (int attempt = 0; attempt < 4 && !dual_ok; ++attempt) {
+        if (g.init(q) != GI_OK) return GI_FAIL_CHOL;
+#pragma unroll 1
+        for (int id = 0; id < GiConstraintSet<N>::NC; ++id)
+            if (cand.get(id)) gi_force_add<N>(g, q, C, id);
+        dual_ok = true;
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            if (j < g.nact && g.u[j] < -1e-9 * C.w) {
+                cand.set(g.ids[j] & (GI_REV - 1), false);
+                dual_ok = false;
+            }
+        }
+    }
+    if (!dual_ok) return GI_FAIL_DUAL;
+    return gi_run<N>(g, q, C, max_iter, iters, edge);
 }
 
 }  // namespace hvp

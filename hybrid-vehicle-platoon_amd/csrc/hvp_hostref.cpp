@@ -431,7 +431,16 @@ void gadmm_one(const hvp_system& S, const hvp::Consts& C, int role, const double
     hvp::LaneQp<N> q;
     int it = 0;
     uint32_t raw = 0;
-    const int st = hvp::solve_admm_lane<N>(q, S, C, role, prm, code, N, 8 * hvp::GiConstraintSet<N>::NC, it, &raw);
+    // g_admm_leaf_ipm: 1 every local QP by the interior-point fallback, 2 the device's
+    // HVP_LEAF_GI_CAP=2 (two active-set steps, then k_gadmm_ipm's solve)
+    int st = g_admm_leaf_ipm == 1 ? hvp::GI_FAIL_ITER
+                                  : hvp::solve_admm_lane<N>(q, S, C, role, prm, code, N,
+                                                            g_admm_leaf_ipm == 2 ? 2 : 8 * hvp::GiConstraintSet<N>::NC,
+                                                            it, &raw);
+    if (st != hvp::GI_OK && g_admm_leaf_ipm) {
+        int it2 = 0;
+        st = hvp::solve_admm_ipm<N>(q, S, C, role, prm, code, N, it2, &raw);
+    }
     if (st != hvp::GI_OK) {
         *status = st == hvp::GI_FAIL_DUAL ? HVP_INFEASIBLE : HVP_MAXITER;
         *cost = 1e300;

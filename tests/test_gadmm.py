@@ -448,28 +448,34 @@ def test_gadmm_local_problem_ipm_fallback(gpu_available, monkeypatch, N):
 @pytest.mark.gpu
 def test_gadmm_engine_ipm_fallback(gpu_available, monkeypatch):
     """configs[3] at its own size (n = 20, N = 10, 100 ADMM iterations, 2 seeds x 2 steps) with the
-    local QPs forced through the interior-point fallback (HVP_LEAF_GI_CAP=2): the engine runs to
-    the end, a platoon whose local QP fails both solvers is reported failed (never a silent
-    answer; on MI355X every platoon of this run fails somewhere), and every other platoon's controls
-    respect the input box.  Not the oracle's controls:
-    over 100 coupled iterations the switching rule's edge bits -- V-row multipliers against
-    kEdgeMultTol, exact from an active-set solve, approximate from the interior point -- decide
-    differently somewhere, and the interior point fails on some of these QPs (MI355X r04i; the
-    traced local problems alone match, test_gadmm_local_problem_ipm_fallback).  Unforced, the
-    fallback only meets the rare QPs the active-set method fails on."""
+    local QPs forced through the interior-point fallback (HVP_LEAF_GI_CAP=2: two active-set
+    steps, then k_gadmm_ipm): the fallback polishes the interior point's active set into the
+    exact optimum and multipliers (hvp_gi.h gi_polish), so no platoon fails and every warm start's
+    sequences, rounds, costs and the winner's controls are the oracle coordinator's -- the same
+    bar as the unforced engine (test_gadmm_engine_matches_oracle_coordinator).  Round 4's fallback
+    (interior-point multipliers against kEdgeMultTol, hinge states classified at its approximate
+    optimum) failed every platoon of this run on MI355X (r04i); the host replay of the same
+    forcing, test_gadmm_forced_fallback_host_replay_matches_oracle, pins the algorithm on CPU."""
     monkeypatch.setenv("HVP_LEAF_GI_CAP", "2")
     fx = load("gadmm_steps_n20_N10.npz")
-    n, N = int(fx["n"]), int(fx["N"])
     P = len(fx["states"]) // int(fx["steps"])
     eng = _engine(fx, P)
     outs = _run_steps(fx, [eng])
-    st = _system()
     for out, runs in (o[0] for o in outs):
-        ok = np.zeros(P, bool)
         for r in runs:
-            ok |= ~r["failed"].cpu().numpy()
-        u = out["u"].cpu().numpy().reshape(-1, n, N)[ok]
-        assert np.isfinite(u).all()
-        if u.size:
-            assert u.min() >= st.umin - 1e-7 and u.max() <= st.umax + 1e-7
+            assert not r["failed"].cpu().numpy().any()
+    _check_steps(fx, [o[0] for o in outs])
     assert eng.solver.stats().n_fallback > 0
+
+
+def test_gadmm_forced_fallback_host_replay_matches_oracle():
+    """The oracle coordinator (oracle.py GAdmmCoordinator) on the product's local-QP algorithm
+    built for the host with every local QP through the fallback as HVP_LEAF_GI_CAP=2 forces it on
+    the device (two active-set steps, then hvp_admm.h solve_admm_ipm: interior point + active-set
+    polish): configs[3]'s first two coordinator calls (34,000 local QPs, both warm starts at
+    t = 1) give the fixture's controls, costs, sequences and rounds.  Without the polish, call 0
+    failed a local QP and call 1 moved u by 0.19 (tests/gadmm_replay.py, mode 2)."""
+    from gadmm_replay import replay
+
+    subprocess.run(["make", "-s", "-C", PKG, "lib/libhvp_hostref.so"], check=True)
+    assert replay(2, 2, verbose=False) == 0
