@@ -122,6 +122,42 @@ def qp_roofline(qp_step_ms: float, kernels: list, notional_bytes: float, tag: st
     return out
 
 
+def timed_roofline(kernels: list, K: int, qp_ms_handles: list, ms_per_step: float, tag: str) -> dict:
+    """Roofline of the configuration the headline times: K handles on K streams.  The PMC figures
+    come from the profile of the same command (workload `tag`, profile_streams = K); per step the
+    K handles run K x (launches per handle) launches.
+      frac_step     PMC FP64 FLOPs of one step's QP launches (masked lanes removed) / ms_per_step, the
+                    driver-visible time of the whole step (overlap and every other kernel included)
+      frac_kernel   FLOPs per launch / the average launch duration measured live in the timed region
+                    (each handle's HIP events around its launches in the last timed step; the K
+                    streams' launches overlap, so a launch takes longer than alone)"""
+    launches = sum(c for _, c in kernels)
+    out = {"profile_streams": K, "launches_per_step": K * launches, "ms_per_step": ms_per_step,
+           "qp_ms_per_handle": qp_ms_handles,
+           "kernel_avg_ms": sum(qp_ms_handles) / max(1, K * launches)}
+    flop = traffic = 0.0
+    srcs = set()
+    for name, count in kernels:
+        d, src = profiled(name, tag)
+        if not d or "f64_flop_active" not in d or "hbm_bytes" not in d:
+            out.update({"frac_step": None, "frac_kernel": None,
+                        "note": (src if not d else f"{src} lacks the PMC passes of {name}") +
+                                f": profiles/profile_all.sh OUT {tag} profiles this build"})
+            return out
+        flop += d["f64_flop_active"] * count * K
+        traffic += d["hbm_bytes"] * count * K
+        srcs.add(src)
+        out.setdefault("profile_avg_ms", {})[name] = d.get("avg_ms")
+    out.update({"flop_per_step": flop, "traffic": traffic, "profile": sorted(srcs),
+                "achieved_step": flop / (ms_per_step * 1e-3) / 1e12,
+                "frac_step": flop / (ms_per_step * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
+                "achieved_kernel": flop / (K * launches) / (out["kernel_avg_ms"] * 1e-3) / 1e12,
+                "hbm_step": {"achieved": traffic / (ms_per_step * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": traffic / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS}})
+    out["frac_kernel"] = out["achieved_kernel"] / FP64_PEAK_TFLOPS
+    return out
+
+
 def seed_range(rank: int, S: int) -> range:
     """The platoon seeds of one rank: a contiguous block of S, disjoint across ranks."""
     return range(rank * S, (rank + 1) * S)
@@ -410,31 +446,58 @@ def bench_admm(args, world: int, rank: int, local: int, dist) -> None:
         "not_optimal_total": int(notopt.item()), "plant_failures_total": int(bad.item()),
     }
     if rank == 0 and not args.no_cpu and args.cpu_budget > 0 and world == 1:
-        result["cpu_baseline"] = cpu_baseline_admm(n, N, iters, min(args.cpu_budget, 20.0))
+        result["cpu_baseline"] = cpu_baseline_admm(n, N, iters, min(args.cpu_budget, 20.0), cpu_threads())
+        result["cpu_baseline_1core"] = cpu_baseline_admm(n, N, iters, min(args.cpu_budget, 20.0) * 0.5, 1)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist:
         dist.destroy_process_group()
 
 
-def cpu_baseline_admm(n: int, N: int, iters: int, budget_s: float):
-    """The oracle coordinator (oracle.AdmmCoordinator: restated fleet_naive_admm get_control on
-    oracle local MIQPs), one platoon step at a time on one core."""
+def cpu_threads() -> int:
+    """Host cores a CPU baseline may use: the pool gives each GPU a 16-core share (OMP_NUM_THREADS=16
+    on the box; nproc shows the whole machine)."""
+    return min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16")), 16)
+
+
+def run_cpu_workers(worker, args: tuple, threads: int, budget_s: float, seed0: int) -> list:
+    """`threads` copies of a one-core baseline worker on disjoint seed ranges, as separate processes
+    (spawn: fresh interpreters that never touch the GPU; the coordinators are Python loops around
+    oracle calls, so threads would serialise on the GIL).  Each returns its own (done, seconds, ...)."""
+    if threads <= 1:
+        return [worker(*args, budget_s, seed0)]
+    import concurrent.futures as cf
+    import multiprocessing as mp
+
+    with cf.ProcessPoolExecutor(threads, mp_context=mp.get_context("spawn")) as ex:
+        futs = [ex.submit(worker, *args, budget_s, seed0 + 1_000_000 * k) for k in range(threads)]
+        return [f.result() for f in futs]
+
+
+def _admm_worker(n: int, N: int, iters: int, budget_s: float, seed0: int):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
 
     sysd = O.gear_pwa_system(800.0)
     lead = np.stack([3000.0 + 20.0 * np.arange(N + 1), np.full(N + 1, 20.0)])
-    done, seed, t0 = 0, 30_000_000, time.perf_counter()
+    done, seed, t0 = 0, seed0, time.perf_counter()
     while time.perf_counter() - t0 < budget_s:
         c = O.AdmmCoordinator(sysd, O.Cfg(), N, n)
         c.set_leader_x(lead)
         c.step(O.env_initial_state(n, seed).astype(float), iters)
         seed += 1
         done += 1
-    dt = time.perf_counter() - t0
-    return {"value": done / dt, "unit": "platoon-timesteps/s", "cores": 1, "kind": "port",
-            "sample": f"{done} platoon steps x {iters} ADMM iterations x {n} local MIQPs (N={N}), oracle, {dt:.1f} s"}
+    return done, time.perf_counter() - t0
+
+
+def cpu_baseline_admm(n: int, N: int, iters: int, budget_s: float, threads: int = 1):
+    """The oracle coordinator (oracle.AdmmCoordinator: restated fleet_naive_admm get_control on
+    oracle local MIQPs), one platoon step at a time per core, on `threads` cores."""
+    res = run_cpu_workers(_admm_worker, (n, N, iters), threads, budget_s, 30_000_000)
+    done = sum(r[0] for r in res)
+    return {"value": sum(r[0] / r[1] for r in res), "unit": "platoon-timesteps/s", "cores": threads, "kind": "port",
+            "sample": f"{done} platoon steps x {iters} ADMM iterations x {n} local MIQPs (N={N}), oracle, "
+                      f"{max(r[1] for r in res):.1f} s on {threads} core(s)"}
 
 
 def gadmm_qp_bytes(N: int) -> int:
@@ -577,22 +640,23 @@ def bench_gadmm(args, world: int, rank: int, local: int, dist) -> None:
     if ex is not None:
         result["halo_bytes_per_exchange"] = ex.bytes_per_call
     if rank == 0 and not args.no_cpu and args.cpu_budget > 0 and world == 1:
-        result["cpu_baseline"] = cpu_baseline_gadmm(n, N, iters, args.max_rounds, min(args.cpu_budget, 30.0))
+        result["cpu_baseline"] = cpu_baseline_gadmm(n, N, iters, args.max_rounds, min(args.cpu_budget, 30.0),
+                                                    cpu_threads())
+        result["cpu_baseline_1core"] = cpu_baseline_gadmm(n, N, iters, args.max_rounds,
+                                                          min(args.cpu_budget, 30.0) * 0.5, 1)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist:
         dist.destroy_process_group()
 
 
-def cpu_baseline_gadmm(n: int, N: int, iters: int, max_rounds: int, budget_s: float):
-    """The oracle coordinator (oracle.GAdmmCoordinator, full-space local QPs), one platoon's
-    g_admm_control at a time on one core, both warm starts (a preceding untimed call)."""
+def _gadmm_worker(n: int, N: int, iters: int, max_rounds: int, budget_s: float, seed0: int):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
 
     lead = np.stack([3000.0 + 20.0 * np.arange(N + 1), np.full(N + 1, 20.0)])
     systems = [O.gear_pwa_system(800.0)] * n
-    done, qps, seed, t_run = 0, 0, 40_000_000, 0.0
+    done, qps, seed, t_run = 0, 0, seed0, 0.0
     while t_run < budget_s:
         co = O.GAdmmCoordinator(systems, O.Cfg(), N, admm_iters=iters, max_rounds=max_rounds)
         co.set_leader_traj(lead)
@@ -605,9 +669,17 @@ def cpu_baseline_gadmm(n: int, N: int, iters: int, max_rounds: int, budget_s: fl
         qps += len(co.trace)
         seed += 1
         done += 1
-    return {"value": done / t_run, "unit": "platoon-timesteps/s", "cores": 1, "kind": "port",
+    return done, t_run, qps
+
+
+def cpu_baseline_gadmm(n: int, N: int, iters: int, max_rounds: int, budget_s: float, threads: int = 1):
+    """The oracle coordinator (oracle.GAdmmCoordinator, full-space local QPs), one platoon's
+    g_admm_control at a time per core (both warm starts: a preceding untimed call), `threads` cores."""
+    res = run_cpu_workers(_gadmm_worker, (n, N, iters, max_rounds), threads, budget_s, 40_000_000)
+    done, qps = sum(r[0] for r in res), sum(r[2] for r in res)
+    return {"value": sum(r[0] / r[1] for r in res), "unit": "platoon-timesteps/s", "cores": threads, "kind": "port",
             "sample": f"{done} g_admm_control calls (n={n}, N={N}, {iters} ADMM iterations, {qps} local QPs), "
-                      f"oracle, {t_run:.1f} s"}
+                      f"oracle, {max(r[1] for r in res):.1f} s on {threads} core(s)"}
 
 
 def bench_closed_loop(args, world: int, rank: int, local: int, dist) -> None:
@@ -824,7 +896,8 @@ def bench_cent(args, world: int, rank: int, local: int, dist) -> None:
                           "node_limit": int((status == 2).sum()), "overflow": int((status == 3).sum())},
     }
     if rank == 0 and not args.no_cpu and args.cpu_budget > 0 and world == 1:
-        result["cpu_baseline"] = cpu_baseline_cent(n, N, min(args.cpu_budget, 30.0), qps / S)
+        result["cpu_baseline"] = cpu_baseline_cent(n, N, min(args.cpu_budget, 30.0), qps / S, cpu_threads())
+        result["cpu_baseline_1core"] = cpu_baseline_cent(n, N, min(args.cpu_budget, 30.0) * 0.5, qps / S, 1)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist:
@@ -844,19 +917,14 @@ def cent_kernels(tag: str) -> list:
     return out
 
 
-def cpu_baseline_cent(n: int, N: int, budget_s: float, qps_per_platoon: float):
-    """The oracle's centralised MIQP (oracle_solve_cent: full-space dense IPM per QP, the same
-    joint branch and bound, so the same QPs per platoon) on one core.  Bounded sample: platoons
-    from seed 10^7 up, each search capped at 2000 QPs, until the budget is spent; the measured QP
-    rate is scaled to platoon-timesteps/s by the GPU run's mean QPs per platoon (same seeds'
-    distribution, same search order)."""
+def _cent_worker(n: int, N: int, budget_s: float, seed0: int):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
 
     systems = [O.gear_pwa_system(800.0)] * n
     lead = np.stack([3000.0 + 20.0 * np.arange(N + 1), np.full(N + 1, 20.0)])
     O.set_cent_cap(2000)
-    done, qps, seed = 0, 0, 10_000_000
+    done, qps, seed = 0, 0, seed0
     t0 = time.perf_counter()
     try:
         while time.perf_counter() - t0 < budget_s:
@@ -866,11 +934,22 @@ def cpu_baseline_cent(n: int, N: int, budget_s: float, qps_per_platoon: float):
             seed += 1
     finally:
         O.set_cent_cap(0)
-    dt = time.perf_counter() - t0
-    rate = qps / dt
-    return {"value": rate / max(qps_per_platoon, 1.0), "unit": "platoon-timesteps/s", "cores": 1, "kind": "port",
-            "sample": f"{qps} QPs of oracle_solve_cent in {dt:.1f} s ({done} platoons, search capped at 2000 QPs "
-                      f"each) = {rate:.1f} QPs/s, / {qps_per_platoon:.0f} QPs per platoon (GPU run mean)"}
+    return done, time.perf_counter() - t0, qps
+
+
+def cpu_baseline_cent(n: int, N: int, budget_s: float, qps_per_platoon: float, threads: int = 1):
+    """The oracle's centralised MIQP (oracle_solve_cent: full-space dense IPM per QP, the same
+    joint branch and bound, so the same QPs per platoon), one platoon at a time per core on
+    `threads` cores.  Bounded sample: platoons from seed 10^7 up, each search capped at 2000 QPs,
+    until the budget is spent; the measured QP rate is scaled to platoon-timesteps/s by the GPU
+    run's mean QPs per platoon (same seeds' distribution, same search order)."""
+    res = run_cpu_workers(_cent_worker, (n, N), threads, budget_s, 10_000_000)
+    done, qps = sum(r[0] for r in res), sum(r[2] for r in res)
+    rate = sum(r[2] / r[1] for r in res)
+    return {"value": rate / max(qps_per_platoon, 1.0), "unit": "platoon-timesteps/s", "cores": threads, "kind": "port",
+            "sample": f"{qps} QPs of oracle_solve_cent in {max(r[1] for r in res):.1f} s on {threads} core(s) "
+                      f"({done} platoons, search capped at 2000 QPs each) = {rate:.1f} QPs/s, / {qps_per_platoon:.0f} "
+                      f"QPs per platoon (GPU run mean)"}
 
 
 def main() -> None:
@@ -1010,6 +1089,9 @@ def main() -> None:
         dist.barrier()
     dt = time.perf_counter() - t0
     ok = all(bool((c[4]["status"] == 0).all().item()) for c in chunks)  # the timed steps' own results
+    # the QP launches of the LAST timed step as they ran in the timed configuration (K handles on K
+    # streams, overlapping): each handle's HIP events around its launches (read after the region)
+    timed_qp_ms = [float(c[0].stats().qp_ms) for c in chunks]
     if dist:
         tt = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -1071,6 +1153,14 @@ def main() -> None:
                            f"decent_n{n}_N{N}" + ("" if bnb else "_enum") + ("" if quadratic else "_l1") + f"_P{S}")
     roofline["time_basis"] = (f"HIP events around the QP launches of one handle over all {S} platoons (the timed "
                               f"region splits them over {K} streams, whose launches overlap)")
+    roofline["profile_streams"] = 1
+    if K > 1:
+        # the timed configuration itself: PMC figures of the same bench command with --streams K
+        # (workload tag ..._s<K>, per launch of one handle over S/K platoons) against (a) the
+        # driver-visible ms_per_step and (b) the live per-launch HIP-event time of the timed region
+        roofline["timed"] = timed_roofline(qk, K, timed_qp_ms, dt / args.steps * 1e3,
+                                           f"decent_n{n}_N{N}" + ("" if bnb else "_enum") + ("" if quadratic else "_l1")
+                                           + f"_P{S}_s{K}")
 
     result = {
         "metric": f"MPC timesteps/sec (whole platoon) at n={n} N={N} decent_mld" + ("" if quadratic else " min_1_norm"),
@@ -1101,7 +1191,7 @@ def main() -> None:
     if rank == 0 and not args.no_cpu and args.cpu_budget > 0 and world == 1:
         # every core this job may use: the pool gives each GPU a 16-core share (OMP_NUM_THREADS=16
         # on the box; nproc shows the whole machine), plus a 1-core run
-        threads = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16")), 16)
+        threads = cpu_threads()
         result["cpu_baseline"] = cpu_baseline(n, N, args.cpu_budget, threads, quadratic)
         result["cpu_baseline_1core"] = cpu_baseline(n, N, args.cpu_budget * 0.5, 1, quadratic)
         hr = hostref_baseline(n, N, min(args.cpu_budget, 10.0), threads, method, quadratic)
