@@ -249,7 +249,7 @@ __global__ __launch_bounds__(64) void k_cent_final(int P, int n, int N, int lead
     const int ntie = rec.tie_count < kTieG ? rec.tie_count : kTieG;
     const double fail_lb = kcost(rec.fail_key);
     if (rec.flags & REC_NODE_LIMIT) res.status = HVP_MAXITER;
-    else if (rec.flags & (REC_TIE_OVER | REC_TASK_OVER)) res.status = HVP_OVERFLOW;
+    else if (rec.flags & REC_TIE_OVER) res.status = HVP_OVERFLOW;
     else if (!(inc < __builtin_inf())) res.status = fail_lb < __builtin_inf() ? HVP_MAXITER : HVP_INFEASIBLE;
     else res.status = HVP_OPTIMAL;
     if (res.status == HVP_OPTIMAL) {
@@ -351,7 +351,14 @@ int hvp_cent_solve_batch(hvp_handle* h, int P, int n, int leader_index, int real
     // task list capacity; a search whose open frames do not fit searches on in its wave (hvp_cent_bnb.h
     // export_tasks).  HVP_CENT_TASK_CAP (tests) shrinks it to exercise that path.
     long long task_cap = std::max<long long>(1 << 16, 64LL * P);
-    if (const char* tc = std::getenv("HVP_CENT_TASK_CAP")) task_cap = std::max<long long>(1, std::atoll(tc));
+    if (const char* tc = std::getenv("HVP_CENT_TASK_CAP")) {
+        task_cap = std::max<long long>(1, std::atoll(tc));
+        static bool said = false;
+        if (!said) std::fprintf(stderr, "[hvp] HVP_CENT_TASK_CAP=%lld: the split-task queue holds %lld tasks "
+                                        "(test knob; answers unchanged, searches that do not fit stay in their wave)\n",
+                                task_cap, task_cap);
+        said = true;
+    }
     auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
     const size_t b_rec = al(sizeof(hvp::cent::PlatoonRec) * P), b_tg = al(sizeof(uint64_t) * P * kTieG * n),
                  b_tgc = al(sizeof(double) * P * kTieG), b_task = al(sizeof(hvp::cent::Task) * task_cap),

@@ -54,7 +54,8 @@ struct PlatoonRec {
     int tie_count;                // entries of the merged tie list
     int flags;                    // 1 split, 2 node limit, 4 tie list overflow, 8 task list overflow
 };
-enum { REC_SPLIT = 1, REC_NODE_LIMIT = 2, REC_TIE_OVER = 4, REC_TASK_OVER = 8 };
+// (bit 8, once REC_TASK_OVER, is free: a full task queue declines the split, export_tasks)
+enum { REC_SPLIT = 1, REC_NODE_LIMIT = 2, REC_TIE_OVER = 4 };
 
 __device__ inline unsigned long long ckey(double c) {
     const unsigned long long b = (unsigned long long)__double_as_longlong(c);

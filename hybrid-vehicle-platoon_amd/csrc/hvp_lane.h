@@ -1723,7 +1723,9 @@ __device__ inline void bnb_node_done(int k, long long t, int inst, bool ok, int 
         for (int j = 0; j < N; ++j) ws.task_y[t * N + j] = y[j];
         if (ok) {
             atomicMin(&ws.inc[inst], cost_key(c));
-        } else {
+        } else if (ws.lvl != ws.dv_lvl) {
+            // (a failed greedy-dive leaf -- the dive list's descriptor, launch_bnb -- only fails to set
+            // an incumbent, as in k_bnb_root: no flag, no interior-point re-solve)
             atomicOr(&ws.inst_flag[inst], 8);  // a velocity-feasible sequence exists
             if (C.form == HVP_FORM_DECENT) {  // K_bnb_ipm re-solves it
                 const unsigned long long r = atomicAdd(&ws.counter[2], 1ull);
@@ -1821,6 +1823,11 @@ __global__ __launch_bounds__(kBlock) void k_lp_dive_prep(int B, const hvp_system
     if (lps) atomicAdd(&ws.counter[3], (unsigned long long)lps);
 }
 
+#ifndef HVP_LP_INV_BATCH
+#define HVP_LP_INV_BATCH 12
+#endif
+constexpr int kLpInvBatch = HVP_LP_INV_BATCH;
+
 // The same node LPs through persistent waves: every lane keeps its LP's simplex state (hvp_lp.h
 // LpLane) in registers and runs one iteration per trip; when at least `refill_min` lanes of the
 // wave are free, their finished LPs are written (k_lp_bound's outputs, node for node) and every
@@ -1832,9 +1839,11 @@ __global__ __launch_bounds__(kBnbBlock<N>) void k_lp_bound_refill(int k, const h
                                                                    const int32_t* __restrict__ sys,
                                                                    const int32_t* __restrict__ role,
                                                                    const double* __restrict__ params, hvp::Consts C,
-                                                                   Workspace ws, int refill_min) {
+                                                                   Workspace ws, int refill_arg) {
     constexpr int BS = kBnbBlock<N>;
     enum { IDLE = 0, RUN = 1, DONE = 2 };
+    // refill_arg: the refill threshold (free lanes, bits 0-7) and the rebuild batch (bits 8-15)
+    const int refill_min = refill_arg & 255, inv_batch = (refill_arg >> 8) & 255;
     const int dst = k & 1;
     const int lane = threadIdx.x & 63;
     const unsigned long long nn = ws.lvl[k];
@@ -1877,7 +1886,8 @@ __global__ __launch_bounds__(kBnbBlock<N>) void k_lp_bound_refill(int k, const h
 #pragma unroll
                     for (int j = 0; j < N; ++j) ws.task_y[t * N + j] = y[j];
                     if (st == hvp::L1_OK) atomicMin(&ws.inc[inst], cost_key(c));
-                    if (st == hvp::L1_FAIL) atomicOr(&ws.inst_flag[inst], 8);
+                    // (an unresolved incumbent leaf of the dive list only sets no incumbent, as in k_lp_root)
+                    if (st == hvp::L1_FAIL && ws.lvl != ws.dv_lvl) atomicOr(&ws.inst_flag[inst], 8);
                 }
                 stage = IDLE;
             }
@@ -1911,8 +1921,16 @@ __global__ __launch_bounds__(kBnbBlock<N>) void k_lp_bound_refill(int k, const h
                 }
             }
         }
+        // every trip is one scan over the terms for every running lane (hvp_lp.h LpLane::trip); the
+        // lanes that wait for a rebuild of A_B^-1 (about one scan of work, taken by the whole wave
+        // whenever any lane runs it) are served together: when inv_batch of them wait, or a quarter
+        // of the running lanes
+        const unsigned long long run_m = __ballot(stage == RUN);
+        const unsigned long long inv_m = __ballot(stage == RUN && L.wants_inv());
+        const int ninv = __popcll(inv_m);
+        const bool do_inv = ninv > 0 && (ninv >= inv_batch || 4 * ninv >= __popcll(run_m));
         if (stage == RUN) {
-            const int r = L.trip(D, C, C.max_iter, y);
+            const int r = L.trip(D, C, C.max_iter, y, do_inv);
             if (r != hvp::LP_RUN) {
                 st = r == hvp::LP_OK ? hvp::L1_OK : hvp::L1_FAIL;
                 stage = DONE;
@@ -2848,7 +2866,11 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
     // the node LPs through persistent waves (k_lp_bound_refill, one 256-lane block per CU: the
     // simplex kernels run one wave per SIMD), refilled when this many lanes are free
     const char* lrf = std::getenv("HVP_LP_REFILL");
-    const int lp_refill = lrf && lrf[0] ? std::max(0, std::min(64, std::atoi(lrf))) : 32;
+    const int lp_refill_min = lrf && lrf[0] ? std::max(0, std::min(64, std::atoi(lrf))) : 32;
+    // lanes that wait for a rebuild of A_B^-1 before the wave runs one (k_lp_bound_refill)
+    const char* lib_ = std::getenv("HVP_LP_INV_BATCH");
+    const int lp_inv_batch = lib_ && lib_[0] ? std::max(1, std::min(64, std::atoi(lib_))) : kLpInvBatch;
+    const int lp_refill = lp_refill_min > 0 ? lp_refill_min | (lp_inv_batch << 8) : 0;
     const int g_lp = (int)std::min<long long>((h->ws.cap + BS - 1) / BS, (long long)std::max(1, h->n_cu));
     if (lp_lane) {
         if constexpr (!kCoop<N>) {

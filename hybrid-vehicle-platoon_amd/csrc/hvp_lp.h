@@ -408,11 +408,19 @@ HVP_HD inline bool lp_invert(const LpData<N, MEM>& D, const Consts& C, const int
 #define HVP_LP_PASS() (void)0
 #endif
 // The simplex state of one LP (per lane): basis, A_B^-1 and the basic terms' data, the recorded
-// sides of the kink terms, counters.  init() sets the start vertex; every trip() is one iteration
-// -- a pivot, or the rebuild of A_B^-1 that confirms an optimum -- and returns LP_RUN until the LP
-// ends (LP_OK with the vertex in y, or LP_FAIL).  lp_simplex runs the trips back to back; the
-// refill kernel (hvp_lane.h k_lp_bound_refill) interleaves them with other lanes' new LPs.
+// sides of the kink terms, counters, and the phase of the current pivot.  init() sets the start
+// vertex; every trip() runs ONE scan over the terms -- the gradient at the vertex (GRAD), one pass
+// of the ratio test along the chosen edge (RATIO), or the final check of the hard rows (CHECK) --
+// so that the lanes of a wavefront, whatever phase of whatever LP they are in, execute the same
+// scan together (one pivot used to be a gradient scan plus 1 to N+ ratio passes, and a wave ran as
+// many passes as its slowest lane: lane utilisation 0.22, profiles/r04k_decent_n10_N5_l1_*).  The
+// rebuild of A_B^-1 (every kLpRefresh pivots, and to confirm an optimum on an exact inverse) is a
+// phase of its own (INV), run when the caller says so (`do_inv`: the refill kernel batches the
+// lanes that wait for it, a rebuild costs about one scan; lp_simplex always).  Returns LP_RUN until
+// the LP ends (LP_OK with the vertex in y, or LP_FAIL).  The arithmetic and its order are the
+// one-pivot-per-call version's, so pivots, vertices and iteration counts are unchanged.
 enum { LP_RUN = 1 };
+enum { LPH_GRAD = 0, LPH_RATIO = 1, LPH_CHECK = 2, LPH_INV = 3 };
 template <int N>
 struct LpLane {
     static constexpr int NT = kLpTerms<N>;
@@ -430,6 +438,11 @@ struct LpLane {
     uint64_t neg[NW];
     int since, iters;
     bool bland;
+    // the pivot in progress: phase, the edge (basic position ek left to side esd, derivative eD),
+    // its direction d, and the ratio test's running slope / last breakpoint / passes
+    int phase, ek, esd, idprev, passes;
+    double eD, slope, tprev, dmax;
+    double d[N];
 
     HVP_HD bool neg_bit(int id) const {
         uint64_t wd = 0;
@@ -457,6 +470,10 @@ struct LpLane {
         since = 0;
         iters = 0;
         bland = false;
+        phase = LPH_GRAD;
+#pragma unroll
+        for (int j = 0; j < N; ++j) d[j] = 0.0;
+        dmax = 0.0;
 #pragma unroll
         for (int j = 0; j < N; ++j) {
             const double vlo = D.mem.get(LF_VLO, j), vhi = D.mem.get(LF_VHI, j);
@@ -479,38 +496,85 @@ struct LpLane {
             });
     }
 
+    // the LP is waiting for a rebuild of A_B^-1 (the caller's do_inv batches these)
+    HVP_HD bool wants_inv() const { return phase == LPH_INV; }
+
     template <class MEM>
-    HVP_HD HVP_FORCEINLINE int trip(const LpData<N, MEM>& D, const Consts& C, int max_iter, double* y) {
+    HVP_HD HVP_FORCEINLINE int trip(const LpData<N, MEM>& D, const Consts& C, int max_iter, double* y,
+                                    bool do_inv = true) {
         const double wmax = fmax(fmax(C.Qpp, C.Qvv), fmax(fmax(C.Qu, C.Qdu), fmax(C.w, 1e-300)));
         const double dtol = 1e-11 * wmax;  // edge derivatives within -dtol of zero count as >= 0
-        // vertex: y = A_B^-1 (-b_B)
-#pragma unroll
-        for (int i = 0; i < N; ++i) {
-            double s = 0.0;
-#pragma unroll
-            for (int r = 0; r < N; ++r) s -= Bi[i][r] * bB[r];
-            y[i] = s;
+        if (phase == LPH_INV) {
+            if (!do_inv) return LP_RUN;  // waits for the wave's batch
+            if (!lp_invert<N>(D, C, basis, Bi)) {
+                HVP_LP_WHY(4);
+                return LP_FAIL;
+            }
+            since = 0;
+            phase = LPH_GRAD;
         }
-        double Y[N];
+        if (phase == LPH_GRAD) {
+            // vertex: y = A_B^-1 (-b_B)
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                double s = 0.0;
+#pragma unroll
+                for (int r = 0; r < N; ++r) s -= Bi[i][r] * bB[r];
+                y[i] = s;
+            }
+        }
+        double Y[N], Dd[N];
         lp_prefix<N>(y, Y);
-        // gradient of the nonbasic terms (a term on its kink takes its recorded side)
+        lp_prefix<N>(d, Dd);
+        // ---- the scan: every term once, in the mode of the lane's phase
+        //   GRAD:  gradient of the nonbasic terms (a term on its kink takes its recorded side)
+        //   RATIO: the next breakpoint along d after (tprev, idprev) (a term whose value hardly moves
+        //          along d -- |a.d| at rounding level of |a| |d| -- is parallel to the edge)
+        //   CHECK: the hard rows (V, U, A, P) at the optimal vertex
+        const int ph = phase;
         double g[N], gpre[N];
 #pragma unroll
         for (int i = 0; i < N; ++i) g[i] = gpre[i] = 0.0;
+        double tb = 1e300, jump = 0.0;
+        int ib = -1, ibside = 1;
+        bool viol = false;
+        if (ph == LPH_RATIO) HVP_LP_PASS();
 #pragma unroll 1
         for (int j = 0; j < N; ++j) {
-            const LpPrim py = lp_prim<N>(y, Y, j);
+            const LpPrim py = lp_prim<N>(y, Y, j), pd = lp_prim<N>(d, Dd, j);
             double g0 = 0.0, g1 = 0.0, g2 = 0.0, gp = 0.0;
             lp_step_terms<N>(D, C, j, [&](const LpTerm& t) {
-                if (!t.ok || is_basic(t.id)) return;
+                if (!t.ok) return;
+                const int id = t.id;
                 const double z = lp_val(t, py) + t.b;
+                if (ph == LPH_CHECK) {
+                    if (id >= 8 * N - 2) return;
+                    const double tol = 1e-9 * (1.0 + fabs(t.b));
+                    viol = viol || (t.sp > 0.0 && z > tol) || (t.sm > 0.0 && z < -tol);
+                    return;
+                }
+                if (is_basic(id)) return;
                 const double zt = 1e-12 * (1.0 + fabs(t.b));
-                const bool pos = z > zt || (!(z < -zt) && !neg_bit(t.id));
-                const double sl = pos ? t.sp : -t.sm;
-                g0 += sl * t.c0;
-                g1 += sl * t.c1;
-                g2 += sl * t.c2;
-                gp += sl * t.cp;
+                const bool pos = z > zt || (!(z < -zt) && !neg_bit(id));
+                if (ph == LPH_GRAD) {
+                    const double sl = pos ? t.sp : -t.sm;
+                    g0 += sl * t.c0;
+                    g1 += sl * t.c1;
+                    g2 += sl * t.c2;
+                    gp += sl * t.cp;
+                    return;
+                }
+                const double rd = lp_val(t, pd);
+                const double an = fabs(t.cp) * j + fabs(t.c0) + fabs(t.c1) + fabs(t.c2);
+                if (!(fabs(rd) > 1e-10 * an * dmax)) return;
+                if (pos == (rd > 0.0)) return;  // moving away from its kink
+                const double tt = fmax(0.0, -z / rd);
+                const bool after = tt > tprev || (tt == tprev && id > idprev);
+                const bool better = after && (tt < tb || (tt == tb && id < ib));
+                tb = better ? tt : tb;
+                ib = better ? id : ib;
+                ibside = better ? (pos ? -1 : 1) : ibside;
+                jump = better ? (t.sp + t.sm) * fabs(rd) : jump;
             });
 #pragma unroll
             for (int i = 0; i < N; ++i) {
@@ -520,120 +584,87 @@ struct LpLane {
                 gpre[i] += i + 1 == j ? gp : 0.0;
             }
         }
-        {
-            double acc = 0.0;
-#pragma unroll
-            for (int i = N - 1; i >= 0; --i) {
-                acc += gpre[i];
-                g[i] += acc;
-            }
-        }
-        // edge derivatives: +-pi_k + s_k(side), pi = A_B^-T g
-        int ek = -1, esd = 0, eid = 0;
-        double eD = -dtol;
-#pragma unroll
-        for (int k = 0; k < N; ++k) {
-            double pk = 0.0;
-#pragma unroll
-            for (int i = 0; i < N; ++i) pk += Bi[i][k] * g[i];
-#pragma unroll
-            for (int sd = 0; sd < 2; ++sd) {
-                const double dv = sd == 0 ? pk + spB[k] : -pk + smB[k];
-                const bool cand = dv < -dtol;
-                const bool take = cand && (bland ? (ek < 0 || basis[k] < eid) : dv < eD);
-                ek = take ? k : ek;
-                esd = take ? sd : esd;
-                eid = take ? basis[k] : eid;
-                eD = take ? dv : eD;
-            }
-        }
-        if (ek < 0 && since > 0) {  // optimal: confirm on a freshly built A_B^-1 (exact vertex)
-            if (!lp_invert<N>(D, C, basis, Bi)) {
-                HVP_LP_WHY(4);
-                return LP_FAIL;
-            }
-            since = 0;
-            return LP_RUN;
-        }
-        if (ek < 0) {  // optimal: every edge non-decreasing; the hard rows must hold
-            bool viol = false;
-#pragma unroll 1
-            for (int j = 0; j < N; ++j) {
-                const LpPrim py = lp_prim<N>(y, Y, j);
-                lp_step_terms<N>(D, C, j, [&](const LpTerm& t) {
-                    if (!t.ok || t.id >= 8 * N - 2) return;  // the hard rows (V, U, A, P)
-                    const double z = lp_val(t, py) + t.b;
-                    const double tol = 1e-9 * (1.0 + fabs(t.b));
-                    viol = viol || (t.sp > 0.0 && z > tol) || (t.sm > 0.0 && z < -tol);
-                });
-            }
+        if (ph == LPH_CHECK) {  // optimal: every edge non-decreasing; the hard rows must hold
             if (viol) HVP_LP_WHY(2);
             return viol ? LP_FAIL : LP_OK;
         }
-        if (iters == max_iter) {
-            HVP_LP_WHY(1);
-            return LP_FAIL;
-        }
-        // direction d = +-A_B^-1 e_k (column ek selected by static index)
-        const double sg = esd == 0 ? 1.0 : -1.0;
-        double d[N], Dd[N];
-        double dmax = 0.0;
+        if (ph == LPH_GRAD) {
+            {
+                double acc = 0.0;
 #pragma unroll
-        for (int i = 0; i < N; ++i) {
-            double v = 0.0;
+                for (int i = N - 1; i >= 0; --i) {
+                    acc += gpre[i];
+                    g[i] += acc;
+                }
+            }
+            // edge derivatives: +-pi_k + s_k(side), pi = A_B^-T g
+            int k_ = -1, sd_ = 0, eid = 0;
+            double dv_ = -dtol;
 #pragma unroll
-            for (int k = 0; k < N; ++k) v = k == ek ? Bi[i][k] : v;
-            d[i] = sg * v;
-            dmax = fmax(dmax, fabs(v));
-        }
-        lp_prefix<N>(d, Dd);
-        // ratio test through the breakpoints in (t, id) order (a term whose value hardly moves along
-        // d -- |a.d| at rounding level of |a| |d| -- is parallel to the edge: no breakpoint)
-        double slope = eD, tprev = 0.0;
-        int idprev = -1, enter = -1;
-        double tstep = 0.0;
-        for (int pass = 0; pass < NT; ++pass) {
-            HVP_LP_PASS();
-            double tb = 1e300;
-            int ib = -1, ibside = 1;
-            double jump = 0.0;
-#pragma unroll 1
-            for (int j = 0; j < N; ++j) {
-                const LpPrim py = lp_prim<N>(y, Y, j), pd = lp_prim<N>(d, Dd, j);
-                lp_step_terms<N>(D, C, j, [&](const LpTerm& t) {
-                    if (!t.ok || is_basic(t.id)) return;
-                    const int id = t.id;
-                    const double rd = lp_val(t, pd);
-                    const double an = fabs(t.cp) * j + fabs(t.c0) + fabs(t.c1) + fabs(t.c2);
-                    if (!(fabs(rd) > 1e-10 * an * dmax)) return;
-                    const double z = lp_val(t, py) + t.b;
-                    const double zt = 1e-12 * (1.0 + fabs(t.b));
-                    const bool pos = z > zt || (!(z < -zt) && !neg_bit(id));
-                    if (pos == (rd > 0.0)) return;  // moving away from its kink
-                    const double tt = fmax(0.0, -z / rd);
-                    const bool after = tt > tprev || (tt == tprev && id > idprev);
-                    const bool better = after && (tt < tb || (tt == tb && id < ib));
-                    tb = better ? tt : tb;
-                    ib = better ? id : ib;
-                    ibside = better ? (pos ? -1 : 1) : ibside;
-                    jump = better ? (t.sp + t.sm) * fabs(rd) : jump;
-                });
+            for (int k = 0; k < N; ++k) {
+                double pk = 0.0;
+#pragma unroll
+                for (int i = 0; i < N; ++i) pk += Bi[i][k] * g[i];
+#pragma unroll
+                for (int sd = 0; sd < 2; ++sd) {
+                    const double dv = sd == 0 ? pk + spB[k] : -pk + smB[k];
+                    const bool cand = dv < -dtol;
+                    const bool take = cand && (bland ? (k_ < 0 || basis[k] < eid) : dv < dv_);
+                    k_ = take ? k : k_;
+                    sd_ = take ? sd : sd_;
+                    eid = take ? basis[k] : eid;
+                    dv_ = take ? dv : dv_;
+                }
             }
-            if (ib < 0) break;  // no breakpoint left: unbounded (cannot happen with the V walls)
-            slope += jump;
-            tprev = tb;
-            idprev = ib;
-            if (slope > -dtol || bland) {  // the function stops decreasing here (Bland: first breakpoint)
-                enter = ib;
-                tstep = tb;
-                break;
+            if (k_ < 0) {
+                // optimal: confirm on a freshly built A_B^-1 (exact vertex), then the hard rows
+                phase = since > 0 ? LPH_INV : LPH_CHECK;
+                return LP_RUN;
             }
-            set_side(ib, ibside);  // crossed: now on its far side
+            if (iters == max_iter) {
+                HVP_LP_WHY(1);
+                return LP_FAIL;
+            }
+            ek = k_;
+            esd = sd_;
+            eD = dv_;
+            // direction d = +-A_B^-1 e_k (column ek selected by static index)
+            const double sg = esd == 0 ? 1.0 : -1.0;
+            dmax = 0.0;
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                double v = 0.0;
+#pragma unroll
+                for (int k = 0; k < N; ++k) v = k == ek ? Bi[i][k] : v;
+                d[i] = sg * v;
+                dmax = fmax(dmax, fabs(v));
+            }
+            slope = eD;
+            tprev = 0.0;
+            idprev = -1;
+            passes = 0;
+            phase = LPH_RATIO;
+            return LP_RUN;
         }
-        if (enter < 0) {
+        // ---- RATIO: one pass of the ratio test through the breakpoints in (t, id) order
+        if (ib < 0) {  // no breakpoint left: unbounded (cannot happen with the V walls)
             HVP_LP_WHY(3);
             return LP_FAIL;
         }
+        slope += jump;
+        tprev = tb;
+        idprev = ib;
+        if (!(slope > -dtol || bland)) {  // still decreasing: crossed, now on its far side
+            set_side(ib, ibside);
+            if (++passes >= NT) {
+                HVP_LP_WHY(3);
+                return LP_FAIL;
+            }
+            return LP_RUN;
+        }
+        // the function stops decreasing here (Bland: first breakpoint): the term enters
+        const int enter = ib;
+        const double tstep = tb;
         // the entering term (one lookup) replaces basic position ek
         LpHyp he;
         lp_hyp<N>(D, C, enter, he);
@@ -670,17 +701,14 @@ struct LpLane {
             w[c] = v - (c == ek ? 1.0 : 0.0);
         }
         if (++since >= kLpRefresh || !(fabs(piv) > 1e-11)) {
-            if (!lp_invert<N>(D, C, basis, Bi)) {
-                HVP_LP_WHY(4);
-                return LP_FAIL;
-            }
-            since = 0;
+            phase = LPH_INV;  // rebuilt from the new basis before the next gradient
         } else {
             const double ip = 1.0 / piv;
 #pragma unroll
             for (int i = 0; i < N; ++i)
 #pragma unroll
                 for (int c = 0; c < N; ++c) Bi[i][c] -= cc[i] * w[c] * ip;
+            phase = LPH_GRAD;
         }
         HVP_LP_TRACE(iters, old, esd, eD, enter, tstep, bland, y);
         if (!(tstep > 1e-13)) bland = true;  // a degenerate pivot: Bland's rule from here on

@@ -32,7 +32,9 @@ DEFAULT_MAX_NODES = 2_000_000  # batched solves (bench.py names it in its metric
 # The per-platoon drop-in (MpcMldCent.solve_mpc) searches to the optimum like the reference's
 # Gurobi call: the heaviest C2-size platoon found (seed 426) needs 27.8M QPs (84 s alone on one
 # MI355X, profiles/r04l_cent_heavy_426_cap30M.jsonl); past this cap the call raises as the
-# reference does on a non-optimal status.
+# reference does on a non-optimal status.  Worst case at the default: ~3 QPs per 10 us on one
+# MI355X for a platoon that splits over the whole chip, i.e. about 3 minutes for one call that
+# exhausts 64M QPs; MpcMldCent(max_nodes=...) bounds it per controller.
 DROPIN_MAX_NODES = 64_000_000
 
 
@@ -168,7 +170,12 @@ class MpcMldCent:
 
     def __init__(self, n: int, N: int, pwa_systems: list[dict], spacing_policy: SpacingPolicy = ConstantSpacingPolicy(50),
                  leader_index: int = 0, quadratic_cost: bool = True, thread_limit: int | None = None,
-                 accel_cnstr_tightening: float = 0.0, real_vehicle_as_reference: bool = False, gears=None) -> None:
+                 accel_cnstr_tightening: float = 0.0, real_vehicle_as_reference: bool = False, gears=None,
+                 max_nodes: int = DROPIN_MAX_NODES) -> None:
+        """The reference's constructor arguments (mpcs/cent_mld.py:11-47), plus ``max_nodes``: the QPs
+        one solve_mpc call may search before it reports a non-optimal status (see DROPIN_MAX_NODES)."""
+        if max_nodes < 1:
+            raise ValueError("max_nodes must be >= 1")
         self.n, self.N = n, N
         self.thread_limit = thread_limit  # no CPU thread pool: kept for signature compatibility
         if len(pwa_systems) != n:
@@ -178,7 +185,7 @@ class MpcMldCent:
         self.setup_cost_and_constraints(None, spacing_policy, leader_index, quadratic_cost, accel_cnstr_tightening,
                                         real_vehicle_as_reference)
         self.leader_traj = np.zeros((2, N + 1))
-        self.max_nodes = DROPIN_MAX_NODES
+        self.max_nodes = int(max_nodes)
         self.x_pred: np.ndarray | None = None
         self.u_pred: np.ndarray | None = None
         self.regions_pred: np.ndarray | None = None
@@ -246,9 +253,10 @@ class MpcGearCent(MpcMldCent):
 
     def __init__(self, n: int, N: int, systems: list[dict], spacing_policy: SpacingPolicy = ConstantSpacingPolicy(50),
                  leader_index: int = 0, quadratic_cost: bool = True, thread_limit: int | None = None,
-                 accel_cnstr_tightening: float = 0.0, real_vehicle_as_reference: bool = False) -> None:
+                 accel_cnstr_tightening: float = 0.0, real_vehicle_as_reference: bool = False,
+                 max_nodes: int = DROPIN_MAX_NODES) -> None:
         super().__init__(n, N, systems, spacing_policy, leader_index, quadratic_cost, thread_limit,
-                         accel_cnstr_tightening, real_vehicle_as_reference)
+                         accel_cnstr_tightening, real_vehicle_as_reference, max_nodes=max_nodes)
         # delta (PWA regions) + sigma (gears) per vehicle and step
         self.num_bin_vars = sum(len(s["S"]) + len(Vehicle.b) for s in systems) * N
 

@@ -112,15 +112,49 @@ def test_l1_platoon_batch(gpu_available):
     rng = np.random.default_rng(1)
     idx = rng.choice(len(roles), 40, replace=False)
     ref = oracle_solve(g, O.Cfg(), N, params[idx], roles[idx], quadratic=False)
-    face = 0
+    face = []
     for j, r in zip(idx, ref):
         assert list(reg[j]) == list(r.sigma), j
         assert abs(cost[j] - r.cost) <= 1e-9 * max(1.0, abs(r.cost)), j
         # where the LP optimum is a face, the simplex (hvp_lp.h) returns a vertex of it and the
-        # oracle's interior point a point inside: both optimal -- the device's trajectory is
-        # feasible (above) and prices at the oracle's optimal cost (the line before)
-        face += int(np.abs(u[j] - r.u).max() > 1e-6)
-    assert face <= len(idx) // 4, face
+        # oracle's interior point a point inside: both optimal.  The device's (x, u) is priced by
+        # the ORACLE's own LP of that sequence (oracle_export_qp: its rows and objective, with the
+        # slack / epigraph variables re-optimised for the fixed trajectory) at the oracle's optimum
+        if np.abs(u[j] - r.u).max() > 1e-6:
+            face.append(int(j))
+            p = params[j]
+            K = 2 * (N + 1)
+            val = reprice_l1(g, O.Cfg(), N, int(roles[j]), reg[j], p[:2], p[2:2 + K].reshape(2, -1),
+                             p[2 + K:2 + 2 * K].reshape(2, -1), p[2 + 2 * K:].reshape(2, -1), x[j], u[j])
+            assert abs(val - r.cost) <= 1e-8 * max(1.0, abs(r.cost)), (j, val, r.cost)
+    # the sample is fixed (40 of the 4100 instances, rng seed 1) and so is the vertex the simplex
+    # returns: the face instances are pinned (MI355X r05b), so a change of the solver's vertex choice
+    # shows up here
+    assert face == L1_FACE_INSTANCES, face
+
+
+# instances of test_l1_platoon_batch's fixed sample where the LP optimum is a face and the device's
+# vertex differs from the oracle's interior point (the host build of the same simplex: none)
+L1_FACE_INSTANCES: list = []
+
+
+def reprice_l1(sysd, cfg, N, role, sigma, x0, xf, xb, xl, x, u):
+    """The oracle's min_1_norm objective (oracle_export_qp: the full (x, u, s, aux) LP of the fixed
+    sequence, fleet_decent_mld.py:73-208) at the trajectory (x, u): x_1..x_N and u fixed, the slack and
+    epigraph variables minimised (scipy HiGHS); every equality and inequality row must hold."""
+    from scipy.optimize import linprog
+
+    P, q, r0, A, b, G, h = O.export_qp(sysd, cfg, N, role, sigma, x0, xf, xb, xl, quadratic=False)
+    assert not P.any()
+    nz = len(q)
+    fixed = np.concatenate([np.asarray(x)[:, 1:].T.reshape(-1), np.asarray(u)])  # z = [x_1 .. x_N | u | ...]
+    lo = np.full(nz, -np.inf)
+    hi = np.full(nz, np.inf)
+    lo[:3 * N] = hi[:3 * N] = fixed
+    res = linprog(q, A_ub=G, b_ub=h, A_eq=A, b_eq=b, bounds=list(zip(lo, hi)),
+                  method="highs")
+    assert res.status == 0, res.message
+    return float(res.fun + r0)
 
 
 def test_l1_local_mpc_api(gpu_available):

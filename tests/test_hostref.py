@@ -194,3 +194,29 @@ def test_l1_simplex_matches_interior_point_and_golden(hostref, name):
             ce = fx["exp_cost"][ok]
             assert np.all(np.abs(r["cost"][ok] - ce) <= 1e-9 * np.maximum(1, np.abs(ce)))
             assert np.abs(r["u"][ok] - fx["exp_u"][ok]).max() <= 1e-6
+
+
+def test_l1_oracle_repricing_of_simplex_vertices(hostref):
+    """tests/test_gpu_l1.py prices the device's min_1_norm trajectories by the ORACLE's own LP of the
+    chosen sequence (reprice_l1: oracle_export_qp with x, u fixed, slacks / epigraph variables
+    re-optimised).  Pinned here on the host build of the same simplex: every L1 fixture instance's
+    vertex prices at the fixture's optimal cost to 1e-9."""
+    from test_gpu_l1 import reprice_l1
+
+    import oracle as O
+
+    fx = load("l1_decent_n10_N5.npz")
+    N = int(fx["N"])
+    prob, systems = product_problem(fx)
+    hostref.hvp_hostref_set_l1_solver(1)
+    r = run(hostref, prob, systems, fx)
+    K = 2 * (N + 1)
+    g = O.gear_pwa_system(800.0)
+    ok = np.flatnonzero(fx["exp_status"] == 0)
+    assert len(ok) >= 10
+    for j in ok[:10]:
+        p = fx["params"][j]
+        val = reprice_l1(g, O.Cfg(), N, int(fx["roles"][j]), r["region"][j], p[:2], p[2:2 + K].reshape(2, -1),
+                         p[2 + K:2 + 2 * K].reshape(2, -1), p[2 + 2 * K:].reshape(2, -1), r["x"][j], r["u"][j])
+        ce = float(fx["exp_cost"][j])
+        assert abs(val - ce) <= 1e-9 * max(1.0, abs(ce)), (j, val, ce)
