@@ -2866,7 +2866,7 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
     // the node LPs through persistent waves (k_lp_bound_refill, one 256-lane block per CU: the
     // simplex kernels run one wave per SIMD), refilled when this many lanes are free
     const char* lrf = std::getenv("HVP_LP_REFILL");
-    const int lp_refill_min = lrf && lrf[0] ? std::max(0, std::min(64, std::atoi(lrf))) : 32;
+    const int lp_refill_min = lrf && lrf[0] ? std::max(0, std::min(64, std::atoi(lrf))) : 12;  // (r05c sweep)
     // lanes that wait for a rebuild of A_B^-1 before the wave runs one (k_lp_bound_refill)
     const char* lib_ = std::getenv("HVP_LP_INV_BATCH");
     const int lp_inv_batch = lib_ && lib_[0] ? std::max(1, std::min(64, std::atoi(lib_))) : kLpInvBatch;
@@ -2998,9 +2998,11 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
         if (h->C.form == HVP_FORM_ADMM)
             hipLaunchKernelGGL((k_bnb_ipm<N, true>), dim3(std::max(1, h->n_cu)), dim3(BS), lds, st, h->d_sys, sys,
                                role, params, h->C, ws);
-        else
-            hipLaunchKernelGGL((k_bnb_ipm<N, false>), dim3(std::max(1, h->n_cu)), dim3(BS), lds, st, h->d_sys, sys,
-                               role, params, h->C, ws);
+        else  // (a small grid: the list is normally empty, and every resident wave of this 1-wave-per-SIMD
+              // kernel gets its scratch -- a full-chip grid cost 0.06 ms per solve for reading a zero count,
+              // profiles/r05c_decent_n10_N5_P16384_s3_summary.json)
+            hipLaunchKernelGGL((k_bnb_ipm<N, false>), dim3(std::max(1, std::min(h->n_cu, 16))), dim3(BS), lds, st,
+                               h->d_sys, sys, role, params, h->C, ws);
         HIP_TRY(hipGetLastError());
     }
     hipLaunchKernelGGL(k_bnb_key<N>, dim3(g_small), dim3(kBlock), 0, st, ws, h->C.form, h->C.l1);
