@@ -7,6 +7,8 @@ import os
 import re
 import subprocess
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "hybrid-vehicle-platoon_amd")
 
@@ -109,3 +111,22 @@ def test_min_1_norm_acceptance_matches_integration_doc():
         assert "min_1_norm" in _abi.last_error()
     doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
     assert "HVP_FORM_CENT` accepts it" in doc and "solved by enumeration with" not in doc
+
+
+def test_no_device_function_clobbers_its_return_address():
+    """Round 4's k_bnb_ipm<10> hang, root-caused in round 5 (tests/codeobj_audit.py, DESIGN.md
+    section 4): ROCm 7.2's branch relaxation routes out-of-range branches of a non-kernel function
+    through s[30:31], its return address, so the function never returns.  No function of the
+    built library may carry such a branch (the product force-inlines its solvers; the hung build's
+    Solver<9>/<10>::solve are caught by the same check, profiles/r05e_codeobj_audit.txt)."""
+    import shutil
+
+    from codeobj_audit import OBJDUMP, audit
+
+    from hvp import _abi
+
+    if not os.path.exists(_abi.LIB_PATH) or not shutil.which(OBJDUMP):
+        pytest.skip("needs the built library and llvm-objdump")
+    n, bad = audit(_abi.LIB_PATH)
+    assert n >= 18  # the 18 translation units' gfx950 code objects
+    assert not bad, bad
