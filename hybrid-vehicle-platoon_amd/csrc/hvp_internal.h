@@ -54,8 +54,8 @@ struct Workspace {
     int32_t* iters = nullptr;                    // [max_batch] active-set iterations
     unsigned long long* lvl = nullptr;           // [2 (HVP_MAX_N + 1)] nodes per level, then per-level
                                                  // claim counters of the refilling bound kernel
-    double* iq = nullptr;                        // [fields][max_batch] sigma-independent QP part per
-                                                 // instance (decentralised branch and bound, N <= 8)
+    double* iq = nullptr;                        // [max_batch][fields, padded to 16] sigma-independent QP
+                                                 // part per instance (decentralised branch and bound, N <= 8)
     const int8_t* hint = nullptr;                // [B][N] regions of a previous solve of the same
                                                  // instances (hvp_set_region_hint; ADMM form only)
     // the greedy dive's leaf of every instance (decentralised lane path, N <= 8): a node list of

@@ -373,9 +373,11 @@ int hvp_reserve(hvp_handle* h, int max_batch, int64_t cap) {
              hipMalloc(&w.nodes, sizeof(int32_t) * max_batch) == hipSuccess &&
              hipMalloc(&w.iters, sizeof(int32_t) * max_batch) == hipSuccess &&
              hipMalloc(&w.lvl, sizeof(unsigned long long) * 6 * (HVP_MAX_N + 1)) == hipSuccess;  // hvp_lane.h LevelList
-        // K_inst_prep's per-instance QP part: H (NT) + f (N) + hf, hb (N - 1 each)
+        // K_inst_prep's per-instance QP part: H (NT) + f (N) + hf, hb (N - 1 each), one row per instance
+        // padded to 16 doubles (hvp_lane.h kIqStride)
         if (ok && N <= HVP_MAX_N_ENUM)
-            ok = hipMalloc(&w.iq, sizeof(double) * (size_t)max_batch * (N * (N + 1) / 2 + 3 * N - 2)) == hipSuccess;
+            ok = hipMalloc(&w.iq, sizeof(double) * (size_t)max_batch * ((N * (N + 1) / 2 + 3 * N - 2 + 15) / 16 * 16)) ==
+                 hipSuccess;
         // the dive list of the lane path (hvp_lane.h launch_bnb): 8-byte fields first
         if (ok && N <= HVP_MAX_N_ENUM) {
             constexpr size_t M = HVP_MAX_N + 1;

@@ -1605,9 +1605,16 @@ __global__ __launch_bounds__(kBnbBlock<N>) void k_lp_bound(int k, const hvp_syst
 constexpr int kRefillMin = HVP_REFILL_MIN;
 constexpr int kRefillBlocksPerCu = HVP_REFILL_WAVES;
 
-// per-instance sigma-independent QP part (SoA: field f of instance i at iq[f * max_batch + i])
+// per-instance sigma-independent QP part, instance-major: instance i's fields at
+// iq[i * kIqStride + f], each row padded to whole 128-byte lines.  The refill kernel's event reads
+// the rows of ~20 distinct instances per 64-node generation; a field-major (SoA) layout made every
+// one of the 28 fields (N = 5) a separate line per instance -- about 1 KB of L2 misses per node,
+// most of the kernel's 304 MB of HBM traffic per launch (profiles/r04k, r05c) -- where a row is
+// two lines.
 template <int N>
 constexpr int kIqFields = N * (N + 1) / 2 + N + 2 * (N - 1);  // H, f, hf, hb
+template <int N>
+constexpr int kIqStride = (kIqFields<N> + 15) / 16 * 16;  // doubles per row (hvp_kernels.hip hvp_reserve)
 
 template <int N>
 __global__ __launch_bounds__(kBlock) void k_inst_prep(int B, const hvp_system* __restrict__ systems,
@@ -1636,16 +1643,15 @@ __global__ __launch_bounds__(kBlock) void k_inst_prep(int B, const hvp_system* _
     ws.inc[i] = cost_key(__longlong_as_double(0x7ff0000000000000ll));  // +inf: no incumbent
     ws.nodes[i] = 0;
     ws.iters[i] = 0;
-    const size_t mb = (size_t)ws.max_batch;
-    double* o = ws.iq + i;
+    double* o = ws.iq + (size_t)i * kIqStride<N>;
 #pragma unroll
-    for (int j = 0; j < NT; ++j) o[j * mb] = H[j];
+    for (int j = 0; j < NT; ++j) o[j] = H[j];
 #pragma unroll
-    for (int j = 0; j < N; ++j) o[(NT + j) * mb] = f[j];
+    for (int j = 0; j < N; ++j) o[NT + j] = f[j];
 #pragma unroll
     for (int j = 0; j < N - 1; ++j) {
-        o[(NT + N + j) * mb] = hf[j];
-        o[(NT + 2 * N - 1 + j) * mb] = hb[j];
+        o[NT + N + j] = hf[j];
+        o[NT + 2 * N - 1 + j] = hb[j];
     }
 }
 
@@ -1686,17 +1692,16 @@ template <int N, class Q>
 __device__ inline bool setup_node(Q& q, const hvp_system& S, const hvp::Consts& C, const Workspace& ws, int inst,
                                   int rl, const double* prm, uint64_t code, int K, double rlo, double rhi) {
     constexpr int NT = N * (N + 1) / 2;
-    const size_t mb = (size_t)ws.max_batch;
-    const double* o = ws.iq + inst;
+    const double* o = static_cast<const double*>(__builtin_assume_aligned(ws.iq + (size_t)inst * kIqStride<N>, 128));
     const bool ok = hvp::setup_scalars<N>(q, S, rl, prm[0], prm[1]);
 #pragma unroll
-    for (int j = 0; j < NT; ++j) q.H[j] = o[j * mb];
+    for (int j = 0; j < NT; ++j) q.H[j] = o[j];
 #pragma unroll
-    for (int j = 0; j < N; ++j) q.f[j] = o[(NT + j) * mb];
+    for (int j = 0; j < N; ++j) q.f[j] = o[NT + j];
 #pragma unroll
     for (int j = 0; j < N - 1; ++j) {
-        q.mem.set(hvp::F_HF, j, o[(NT + N + j) * mb]);
-        q.mem.set(hvp::F_HB, j, o[(NT + 2 * N - 1 + j) * mb]);
+        q.mem.set(hvp::F_HF, j, o[NT + N + j]);
+        q.mem.set(hvp::F_HB, j, o[NT + 2 * N - 1 + j]);
     }
     q.C0 = 0.0;  // not used by the active-set path (costs come from direct_cost)
     hvp::setup_input<N>(q, S, C, code, K, rlo, rhi);
