@@ -1828,6 +1828,12 @@ __global__ __launch_bounds__(kBlock) void k_lp_dive_prep(int B, const hvp_system
     if (lps) atomicAdd(&ws.counter[3], (unsigned long long)lps);
 }
 
+// occupancy of the LP refill kernel (A/B builds: -DHVP_LP_WAVES=2 asks for two waves per SIMD)
+#ifdef HVP_LP_WAVES
+#define HVP_LP_OCC __attribute__((amdgpu_waves_per_eu(HVP_LP_WAVES)))
+#else
+#define HVP_LP_OCC
+#endif
 #ifndef HVP_LP_INV_BATCH
 #define HVP_LP_INV_BATCH 12
 #endif
@@ -1840,7 +1846,7 @@ constexpr int kLpInvBatch = HVP_LP_INV_BATCH;
 // average and a wave of 64 one-per-lane LPs waits for its slowest (~17 pivots, host histogram):
 // the grid-stride kernel idles ~60 % of its lanes.  HVP_LP_REFILL=<min free lanes> (0: k_lp_bound).
 template <int N>
-__global__ __launch_bounds__(kBnbBlock<N>) void k_lp_bound_refill(int k, const hvp_system* __restrict__ systems,
+__global__ __launch_bounds__(kBnbBlock<N>) HVP_LP_OCC void k_lp_bound_refill(int k, const hvp_system* __restrict__ systems,
                                                                    const int32_t* __restrict__ sys,
                                                                    const int32_t* __restrict__ role,
                                                                    const double* __restrict__ params, hvp::Consts C,
