@@ -984,6 +984,9 @@ def main() -> None:
     ap.add_argument("--cost", choices=["quadratic", "l1"], default="quadratic",
                     help="decent: min_2_norm (default) or min_1_norm (the MILP variant; --method auto = branch and "
                          "bound, enum = exhaustive enumeration up to N = 8)")
+    ap.add_argument("--no-roofline-pass", action="store_true",
+                    help="decent: skip the untimed one-handle pass that times the QP launches for the roofline "
+                         "(profile runs of the multi-stream configuration, so the trace holds its launches only)")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU work: start the ranks (gloo), shard the seeds, run the timing protocol around an "
                          "empty step and print the line (tests the --gpus N launcher on a CPU)")
@@ -1101,7 +1104,11 @@ def main() -> None:
     # QP launches) and work counters: a second pass of the same steps, outside the timed region
     # (reading them synchronises the stream after every step), as ONE handle over the whole batch
     # -- the launch size of the committed profile (run_profiles.sh ... --streams 1)
-    if K == 1:
+    if args.no_roofline_pass:
+        # (profiling runs of the K-stream configuration: only its own launches in the trace; the work
+        # counters of the last timed step stand for every step)
+        ev = None
+    elif K == 1:
         ev = chunks[0]
     else:
         sv1 = BatchSolver(tables.problem(N, quadratic_cost=quadratic, method=method), [system], device=local)
@@ -1109,7 +1116,13 @@ def main() -> None:
         ev = (sv1, torch.zeros(B, dtype=torch.int32, device=dev), t_roles_all, t_params_all,
               sv1.alloc_outputs(B, dev), torch.cuda.current_stream(dev))
     qp_ms, cand, iters, fallback = [], 0, 0, 0
-    for _ in range(args.steps):
+    if ev is None:
+        sts = [c[0].stats() for c in chunks]
+        qp_ms = [sum(float(x.qp_ms) for x in sts)]
+        cand = args.steps * sum(x.n_candidates for x in sts)
+        iters = args.steps * sum(x.qp_iterations for x in sts)
+        fallback = args.steps * sum(x.n_fallback for x in sts)
+    for _ in range(args.steps if ev is not None else 0):
         sv, ts, tr, tp, o, stm = ev
         sv.solve_device(ts, tr, tp, o, stream=stm)
         s = sv.stats()

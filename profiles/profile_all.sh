@@ -12,7 +12,7 @@ for w in "${W[@]}"; do
   case $w in
     decent_n10_N5_P16384) bash profiles/run_profiles.sh "$O/$w" --platoons 16384 --steps 5 --warmup 1 --no-cpu --streams 1 ;;
     # the headline's own configuration: the default bench (three handles on three streams)
-    decent_n10_N5_P16384_s3) bash profiles/run_profiles.sh "$O/$w" --platoons 16384 --steps 5 --warmup 1 --no-cpu --streams 3 ;;
+    decent_n10_N5_P16384_s3) bash profiles/run_profiles.sh "$O/$w" --platoons 16384 --steps 5 --warmup 1 --no-cpu --streams 3 --no-roofline-pass ;;
     decent_n10_N5_l1_P16384) bash profiles/run_profiles.sh "$O/$w" --cost l1 --platoons 16384 --steps 2 --warmup 1 --no-cpu --streams 1 ;;
     admm_n10_N10_P512) bash profiles/run_profiles.sh "$O/$w" --controller admm --n 10 --N 10 --platoons 512 --steps 1 --warmup 1 --no-cpu --streams 1 ;;
     gadmm_n20_N10_P2048) bash profiles/run_profiles.sh "$O/$w" --controller gadmm --n 20 --N 10 --platoons 2048 --steps 1 --warmup 0 --no-cpu --streams 1 ;;
