@@ -448,13 +448,17 @@ HVP_HD inline double admm_direct_cost(const LaneQp<N, M>& q, const hvp_system& S
 // Returns GI_OK with the optimum in q.y, or a GI_FAIL_* code (GI_FAIL_ITER also when the hinge
 // states do not settle within kHubRounds).
 constexpr int kHubRounds = 12;
+constexpr uint64_t kHubNone = ~0ull;  // no starting hinge states given (two bits per hinge use 0..2)
 template <int N, class M>
 HVP_HD inline int solve_admm_lane(LaneQp<N, M>& q, const hvp_system& S, const Consts& C, int role, const double* prm,
-                                  uint64_t code, int K, int max_iter, int& iters, uint32_t* edge = nullptr) {
+                                  uint64_t code, int K, int max_iter, int& iters, uint32_t* edge = nullptr,
+                                  uint64_t* hs_io = nullptr, int* rounds = nullptr) {
     uint64_t hs = 0;
     iters = 0;
-    // initial states: those of the unconstrained copies at the constant-velocity trajectory
-    {
+    if (hs_io && *hs_io != kHubNone) {
+        hs = *hs_io;  // warm: the caller's starting states (a parent's, another iteration's)
+    } else {
+        // initial states: those of the unconstrained copies at the constant-velocity trajectory
         double y[N];
 #pragma unroll
         for (int k = 0; k < N; ++k) y[k] = prm[1];
@@ -466,10 +470,14 @@ HVP_HD inline int solve_admm_lane(LaneQp<N, M>& q, const hvp_system& S, const Co
         int it = 0;
         const int st = solve_gi<N>(q, C, max_iter, it, edge);
         iters += it;
+        if (rounds) *rounds = round + 1;
         if (st != GI_OK) return st;
         bool consistent;
         hs = admm_classify<N>(C, role, prm, q.P1, q.ts, q.y, hs, &consistent);
-        if (consistent) return GI_OK;
+        if (consistent) {
+            if (hs_io) *hs_io = hs;
+            return GI_OK;
+        }
     }
     return GI_FAIL_ITER;
 }

@@ -408,14 +408,19 @@ __device__ inline void row_owner(int id_in, int& lane, int& bit) {
 // same, and the equality-constrained optimum on the old active set is two triangular solves and
 // two N x N products away (warm_start below).  `key` names the rest of what the Hessian depends
 // on (system index, role bits): a record written for another QP -- a handle called again with a
-// different batch -- never starts this one.
-struct WarmQp {
+// different batch -- never starts this one.  RS: the row stride of the factors (G for the
+// switching ADMM's per-QP records; N for the naive ADMM's node records, hvp_lane.h NodeCache,
+// which are kept per tree node and so are many).
+template <int RS_>
+struct WarmRec {
+    static constexpr int RS = RS_;
     uint64_t code, hs, key;
     int32_t nact, valid;
-    int32_t ids[G];
-    double J[G * G];
-    double R[G * G];
+    int32_t ids[RS_];
+    double J[RS_ * RS_];
+    double R[RS_ * RS_];
 };
+using WarmQp = WarmRec<G>;
 
 // right-hand side dd of row p in the group's >= form (n = -c, slack dd + n.y): every lane
 // calls it with the same p; the owner lane computes the bound, the group receives it
@@ -450,27 +455,18 @@ __device__ inline double row_dd(const Lane<N>& L, int p) {
     return (rev ? -1.0 : 1.0) * bcast(dloc, ol);
 }
 
-// The equality-constrained optimum on the active set of the last solve (WarmQp), if it is dual
-// feasible: y = J1 R^-T b - J2 J2' f, u = R^-1 (R^-T b + J1' f) with b_j = -dd of active row j
-// (n_j.y = b_j).  On success J, R are in LDS, L.y, u, id, act, nact set, and the Goldfarb-Idnani
-// loop continues from there (it adds any row the new bounds violate); false leaves the LDS (H)
-// untouched for the cold start.  Multipliers down to -1e-9 w count as zero (clamped).
+// w (lane t: w1 = R^-T b at the active positions t < na, -s beyond) and u = R^-1 (w1 + s1) of the
+// active rows ids (lane j: row of position j) with the factors J, R at (Jp, Rp), row stride rs;
+// s = J' f, b_j = -dd of row j.  Every lane of the group calls it.
 template <int N>
-__device__ inline bool warm_start(Lane<N>& L, GroupLds& Sg, const Consts& C, const WarmQp* wq, double& u, int& id,
-                                  unsigned& act, int& nact) {
+__device__ inline void warm_solve(const Lane<N>& L, GroupLds& Sg, const double* Jp, const double* Rp, int rs, int na,
+                                  int myid, double& w, double& uu) {
     const int t = lane16();
-    const int na = wq->nact;
-    if (na < 0 || na > N) return false;
-    const double* Jg = wq->J;
-    const double* Rg = wq->R;
-    const int myid = t < na ? wq->ids[t] : -1;
-    // b_j = -dd of active row j, lane j
     double b = 0.0;
     for (int j = 0; j < na; ++j) {
         const double dd = row_dd<N>(L, bcast(myid, j));
         if (t == j) b = -dd;
     }
-    // s_c = (J' f)_c
     double* v = Sg.v;
     gsync();
     v[t] = t < N ? L.f : 0.0;
@@ -478,54 +474,154 @@ __device__ inline bool warm_start(Lane<N>& L, GroupLds& Sg, const Consts& C, con
     double s = 0.0;
     if (t < N) {
 #pragma unroll
-        for (int i = 0; i < N; ++i) s += Jg[i * G + t] * v[i];
+        for (int i = 0; i < N; ++i) s += Jp[i * rs + t] * v[i];
     }
-    // w1 = R^-T b (forward substitution over the active positions), w2 = -s
-    double w = t < N && t >= na ? -s : 0.0;
+    w = t < N && t >= na ? -s : 0.0;
     {
         double acc = t < na ? b : 0.0;
         for (int j = 0; j < na; ++j) {
             double wj = 0.0;
-            if (t == j) wj = acc / Rg[j * G + j];
+            if (t == j) wj = acc / Rp[j * rs + j];
             wj = bcast(wj, j);
             if (t == j) w = wj;
-            if (t > j && t < na) acc -= Rg[j * G + t] * wj;
+            if (t > j && t < na) acc -= Rp[j * rs + t] * wj;
         }
     }
-    // u = R^-1 (w1 + s1) (back substitution)
-    double uu = 0.0;
+    uu = 0.0;
     {
         double acc = t < na ? w + s : 0.0;
         for (int j = na - 1; j >= 0; --j) {
             double uj = 0.0;
-            if (t == j) uj = acc / Rg[j * G + j];
+            if (t == j) uj = acc / Rp[j * rs + j];
             uj = bcast(uj, j);
             if (t == j) uu = uj;
-            if (t < j) acc -= Rg[t * G + j] * uj;
+            if (t < j) acc -= Rp[t * rs + j] * uj;
         }
     }
+}
+
+enum { WARM_COLD = 0, WARM_OK = 1, WARM_LOST = 2 };
+constexpr int kWarmDrops = 4;
+
+// The equality-constrained optimum on the active set of the last solve (WarmQp), made dual
+// feasible: y = J1 R^-T b - J2 J2' f, u = R^-1 (R^-T b + J1' f) with b_j = -dd of active row j
+// (n_j.y = b_j).  When a multiplier is negative (the new linear term or bounds moved the optimum
+// off a row), the factors go to LDS and the most negative row leaves the set -- a column of R out,
+// Givens rotations back to triangular, J's columns rotated alike, as Goldfarb-Idnani's own drop --
+// up to kWarmDrops times (a row left out is added back by the loop if the new point violates it).
+// WARM_OK: J, R in LDS, L.y, u, id, act, nact set, and Goldfarb-Idnani continues from there.
+// WARM_COLD: nothing touched (H still in LDS).  WARM_LOST: still infeasible after the drops, and
+// the Hessian in LDS is overwritten -- the caller sets the QP up again for a cold start.
+// Multipliers down to -1e-9 w count as zero (clamped).
+template <int N, class W>
+__device__ inline int warm_start(Lane<N>& L, GroupLds& Sg, const Consts& C, const W* wq, double& u, int& id,
+                                 unsigned& act, int& nact) {
+    constexpr int RS = W::RS;
+    static_assert(RS >= N, "record rows shorter than the horizon");
+    const int t = lane16();
+    int na = wq->nact;
+    if (na < 0 || na > N) return WARM_COLD;
+    const double* Jg = wq->J;
+    const double* Rg = wq->R;
+    int myid = t < na ? wq->ids[t] : -1;
     const double wgt = C.w;
-    int bad = 0;
-    if (t < na) {
-        if (!(uu >= -1e-9 * wgt)) bad = 1;  // NaN-safe
-        if (gi_soft<N>(myid) && uu > wgt) bad = 1;
+    double w, uu;
+    warm_solve<N>(L, Sg, Jg, Rg, RS, na, myid, w, uu);
+    auto verdict = [&]() {  // 0 dual feasible, 1 a negative multiplier, 2 a soft row above w
+        int neg = 0, over = 0;
+        if (t < na) {
+            if (!(uu >= -1e-9 * wgt)) neg = 1;  // NaN-safe
+            if (gi_soft<N>(myid) && uu > wgt) over = 1;
+        }
+        return gor(over) ? 2 : (gor(neg) ? 1 : 0);
+    };
+    int vd = verdict();
+    if (vd == 2) return WARM_COLD;
+    const double* Jp = Jg;
+    int rs = RS;
+    if (vd == 1) {
+        // the factors into LDS (over H), then drop the most negative multiplier's row until the
+        // rest is dual feasible
+        gsync();
+        if (t < N) {
+#pragma unroll
+            for (int c = 0; c < N; ++c) {
+                Sg.J[t * LD + c] = Jg[t * RS + c];
+                Sg.R[t * LD + c] = Rg[t * RS + c];
+            }
+        }
+        gsync();
+        double* J = Sg.J;
+        double* R = Sg.R;
+        Jp = J;
+        rs = LD;
+        for (int drop_n = 0; vd == 1; ++drop_n) {
+            if (drop_n == kWarmDrops || na == 0) return WARM_LOST;
+            double key = t < na ? uu : 1e300;
+            int drop = t;
+            gargmin(key, drop);
+            const int id_n = __shfl_down(myid, 1, G);
+            if (t >= drop && t < na - 1) myid = id_n;
+            if (t == na - 1) myid = -1;
+            if (t < N) {
+#pragma unroll
+                for (int j = 0; j < N - 1; ++j)
+                    if (j >= drop && j < na - 1) R[t * LD + j] = R[t * LD + j + 1];
+#pragma unroll
+                for (int j = 0; j < N; ++j)
+                    if (j == na - 1) R[t * LD + j] = 0.0;
+            }
+            gsync();
+#pragma unroll
+            for (int i = 0; i < N - 1; ++i) {
+                if (i >= drop && i < na - 1) {
+                    double gc, gs;
+                    givens(R[i * LD + i], R[(i + 1) * LD + i], gc, gs);
+                    gsync();
+                    if (t >= i && t < na - 1) {
+                        const double a0 = R[i * LD + t], a1 = R[(i + 1) * LD + t];
+                        R[i * LD + t] = gc * a0 + gs * a1;
+                        R[(i + 1) * LD + t] = -gs * a0 + gc * a1;
+                    }
+                    if (t < N) {
+                        const double a0 = J[t * LD + i], a1 = J[t * LD + i + 1];
+                        J[t * LD + i] = gc * a0 + gs * a1;
+                        J[t * LD + i + 1] = -gs * a0 + gc * a1;
+                    }
+                    gsync();
+                }
+            }
+            // the subdiagonal entry the rotations zeroed (row i + 1, column i)
+            if (t < N) {
+#pragma unroll
+                for (int i = 0; i < N - 1; ++i)
+                    if (i >= drop && i < na - 1 && t == i + 1) R[t * LD + i] = 0.0;
+            }
+            --na;
+            gsync();
+            warm_solve<N>(L, Sg, J, R, LD, na, myid, w, uu);
+            vd = verdict();
+            if (vd == 2) return WARM_LOST;
+        }
     }
-    if (gor(bad)) return false;
     // y_t = sum_c J[t][c] w_c
+    double* v = Sg.v;
     gsync();
     v[t] = w;
     gsync();
     double y = 0.0;
     if (t < N) {
 #pragma unroll
-        for (int c = 0; c < N; ++c) y += Jg[t * G + c] * v[c];
+        for (int c = 0; c < N; ++c) y += Jp[t * rs + c] * v[c];
     }
-    // commit: factors into LDS, the GI state into the lanes
+    // commit: factors into LDS (when still in the record), the GI state into the lanes
     if (t < N) {
+        if (Jp == Jg) {
 #pragma unroll
-        for (int c = 0; c < N; ++c) {
-            Sg.J[t * LD + c] = Jg[t * G + c];
-            Sg.R[t * LD + c] = Rg[t * G + c];
+            for (int c = 0; c < N; ++c) {
+                Sg.J[t * LD + c] = Jg[t * RS + c];
+                Sg.R[t * LD + c] = Rg[t * RS + c];
+            }
         }
         L.y = y;
     }
@@ -539,16 +635,17 @@ __device__ inline bool warm_start(Lane<N>& L, GroupLds& Sg, const Consts& C, con
     }
     nact = na;
     gsync();
-    return true;
+    return WARM_OK;
 }
 
 // Cooperative Goldfarb-Idnani.  On GI_OK lane t < N holds y_t in L.y.
 // wq (optional): the QP's WarmQp record -- tried as the starting active set when it was written
 // for the same code and hinge states (wcode, whs) and wtry is set; rewritten on success.
-template <int N>
+template <int N, class W = WarmQp>
 __device__ inline int solve(Lane<N>& L, GroupLds& Sg, const Consts& C, int max_iter, int& iters,
-                            unsigned* edge = nullptr, WarmQp* wq = nullptr, uint64_t wcode = 0, uint64_t whs = 0,
+                            unsigned* edge = nullptr, W* wq = nullptr, uint64_t wcode = 0, uint64_t whs = 0,
                             bool wtry = false, uint64_t wkey = 0) {
+    constexpr int RS = W::RS;
     const int t = lane16();
     iters = 0;
     double* J = Sg.J;  // holds H on entry (row t written by lane t)
@@ -558,10 +655,14 @@ __device__ inline int solve(Lane<N>& L, GroupLds& Sg, const Consts& C, int max_i
     int nact = 0;
     unsigned act = 0;  // active bits of the rows lane t owns
     gsync();
-    bool warmed = false;
+    int warmed = WARM_COLD;
     if (wq && wtry && wq->valid && wq->code == wcode && wq->hs == whs && wq->key == wkey)  // group-uniform
-        warmed = warm_start<N>(L, Sg, C, wq, u, id, act, nact);
-    if (!warmed) {
+        warmed = warm_start<N, W>(L, Sg, C, wq, u, id, act, nact);
+    if (warmed == WARM_LOST) {
+        iters = 0;
+        return GI_WARM_LOST;
+    }
+    if (warmed == WARM_COLD) {
     // ---- Cholesky H = L L' into R area (lower, row-major), column by column
 #pragma unroll
     for (int j = 0; j < N; ++j) {
@@ -862,8 +963,8 @@ __device__ inline int solve(Lane<N>& L, GroupLds& Sg, const Consts& C, int max_i
         const bool keep = ok && gor((int)sat) == 0;  // saturated soft rows: not warm-startable
         if (t < N) {
             for (int c = 0; c < N; ++c) {
-                wq->J[t * G + c] = J[t * LD + c];
-                wq->R[t * G + c] = R[t * LD + c];
+                wq->J[t * RS + c] = J[t * LD + c];
+                wq->R[t * RS + c] = R[t * LD + c];
             }
             wq->ids[t] = t < nact ? id : -1;
         }
@@ -1028,14 +1129,17 @@ __device__ inline uint64_t admm_initial_states(Lane<N>& L, const Consts& C, int 
 // hinge states still change after kHubRounds), the QP is solved once more from the cold start
 // (constant-velocity states, Cholesky of H), so a warm start never fails a QP the cold start solves.
 // wkey: the record's owner key (system index, role bits; WarmQp).
-template <int N>
+template <int N, class W = WarmQp>
 __device__ inline int solve_qp(Lane<N>& L, GroupLds& Sg, const hvp_system& S, const Consts& C, int role,
                                const double* prm, uint64_t code, int K, int max_iter, int& iters, double* cost,
                                unsigned* edge = nullptr, double lo = 0.0, double hi = -1.0,
-                               WarmQp* wq = nullptr, bool warm = false, uint64_t wkey = 0) {
+                               W* wq = nullptr, bool warm = false, uint64_t wkey = 0) {
     iters = 0;
     if (C.form == HVP_FORM_ADMM || C.form == HVP_FORM_GADMM) {
-        bool w = wq && warm && wq->valid && wq->key == wkey;  // group-uniform (one address per group)
+        // group-uniform (one address per group).  A node record (RS < G: one table slot shared by
+        // the nodes that hash to it) starts only the node it was written for; the switching ADMM's
+        // per-QP record also lends its hinge states to the QP's next region sequence
+        bool w = wq && warm && wq->valid && wq->key == wkey && (W::RS == G || wq->code == code);
         int st = GI_FAIL_ITER;
         for (int attempt = 0; attempt < 2; ++attempt) {
             uint64_t hs;
@@ -1052,7 +1156,12 @@ __device__ inline int solve_qp(Lane<N>& L, GroupLds& Sg, const hvp_system& S, co
                 gsync();
                 setup<N>(L, Sg, S, C, role, prm, code, K, hs);
                 int it = 0;
-                st = solve<N>(L, Sg, C, max_iter, it, edge, wq, code, hs, w, wkey);
+                st = solve<N, W>(L, Sg, C, max_iter, it, edge, wq, code, hs, w, wkey);
+                if (st == GI_WARM_LOST) {  // the warm start overwrote the Hessian and failed: cold
+                    gsync();
+                    setup<N>(L, Sg, S, C, role, prm, code, K, hs);
+                    st = solve<N, W>(L, Sg, C, max_iter, it, edge, wq, code, hs, false, wkey);
+                }
                 iters += it;
                 if (st != GI_OK) break;
                 bool consistent;

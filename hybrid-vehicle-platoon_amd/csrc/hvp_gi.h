@@ -27,7 +27,8 @@
 namespace hvp {
 
 // GI_OK, or why the lane is handed to the interior-point fallback
-enum { GI_OK = 0, GI_FAIL_CHOL = 5, GI_FAIL_ITER = 6, GI_FAIL_DUAL = 7, GI_FAIL_VERIFY = 8 };
+enum { GI_OK = 0, GI_FAIL_CHOL = 5, GI_FAIL_ITER = 6, GI_FAIL_DUAL = 7, GI_FAIL_VERIFY = 8,
+       GI_WARM_LOST = 9 /* hvp_coop.h warm_start: set the QP up again, then solve cold */ };
 
 template <int N>
 struct GiConstraintSet {

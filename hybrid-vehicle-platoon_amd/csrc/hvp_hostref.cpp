@@ -7,6 +7,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <map>
 #include <vector>
 
 #include "hvp_admm.h"
@@ -21,6 +22,35 @@ int g_admm_leaf_ipm = 0;  // hvp_hostref_set_admm_leaf_ipm: 1 every ADMM leaf by
 #define HVP_LP_PASS() (__atomic_fetch_add(&g_lp_pass, 1, __ATOMIC_RELAXED))
 #define HVP_LP_WHY(code) (__atomic_fetch_add(&g_lp_why[code], 1, __ATOMIC_RELAXED))
 int g_lp_trace = 0;
+// hvp_hostref_set_admm_warm (diagnostics, profiles/diag_admm_warm.py): starting hinge states of the
+// naive-ADMM node QPs -- 0 constant-velocity (cold), 1 a child from its parent's final states,
+// 2 as 1 and the root from the previous call's root states of the same batch index,
+// 3 every node QP from the record of the same node (batch index, depth, region code) of the
+// previous call: its final hinge states and active set (forced in as equalities, negative
+// multipliers dropped), as a factor-carrying warm start would begin -- counted as one iteration
+int g_admm_warm = 0;
+struct WarmRec {
+    uint64_t hs;
+    int nact;
+    int ids[16];
+};
+std::map<std::pair<uint64_t, int>, WarmRec> g_admm_recs[4096];
+long long g_admm_rec_stats[4];  // lookups, hits, warm starts kept (dual feasible after the drops)
+// 4: as 3 through a direct-mapped table per (batch index, depth) of g_admm_slots records, slot =
+// hash(code); among a level's nodes that share a slot the smallest code owns it (reads and
+// writes it), the others start cold -- the device's deterministic claim
+int g_admm_slots = 64;
+struct SlotRec {
+    bool valid;
+    uint64_t code;
+    WarmRec rec;
+};
+std::vector<SlotRec> g_admm_tab[4096];
+inline int admm_slot(uint64_t code, int sd) {
+    return (int)((code * 0x9E3779B97F4A7C15ull) >> 40) & (sd - 1);
+}
+uint64_t g_admm_root_hs[4096];
+long long g_admm_warm_stats[4];  // QPs, hinge rounds, QPs consistent in one round, failed
 #define HVP_LP_TRACE(it, lv, sd, dv, en, t, bl, yy)                                                             \
     do {                                                                                                      \
         if (g_lp_trace)                                                                                       \
@@ -211,22 +241,89 @@ void solve_one(const hvp_system& S, const hvp::Consts& C, int role, const double
     }
 }
 
+// diagnostics (g_admm_warm == 3): the hinge-state iteration of hvp_admm.h solve_admm_lane started
+// from a record of the same node's previous solve
+template <int N>
+int admm_warm_solve(hvp::LaneQp<N>& q, const hvp_system& S, const hvp::Consts& C, int role, const double* prm,
+                    uint64_t code, int K, int max_iter, int& iters, int& rounds, WarmRec& rec, bool have) {
+    uint64_t hs;
+    iters = 0;
+    if (have) {
+        hs = rec.hs;
+    } else {
+        double y[N];
+        for (int k = 0; k < N; ++k) y[k] = prm[1];
+        bool c;
+        hs = hvp::admm_classify<N>(C, role, prm, prm[0] + S.ts * prm[1], S.ts, y, 0, &c);
+    }
+    for (int round = 0; round < hvp::kHubRounds; ++round) {
+        rounds = round + 1;
+        hvp::setup_lane_admm<N>(q, S, C, role, prm, code, K, hs);
+        hvp::GiLane<N> g;
+        if (g.init(q) != hvp::GI_OK) return hvp::GI_FAIL_CHOL;
+        if (round == 0 && have && rec.hs == hs) {
+            bool drop[16] = {};
+            bool dual_ok = false;
+            for (int attempt = 0; attempt < 4 && !dual_ok; ++attempt) {
+                if (attempt) g.init(q);
+                for (int j = 0; j < rec.nact; ++j)
+                    if (!drop[j]) hvp::gi_force_add<N>(g, q, C, rec.ids[j]);
+                dual_ok = true;
+                for (int j = 0; j < g.nact; ++j)
+                    if (g.u[j] < -1e-9 * C.w)
+                        for (int i = 0; i < rec.nact; ++i)
+                            if (rec.ids[i] == g.ids[j]) { drop[i] = true; dual_ok = false; }
+                if (attempt == 0 && dual_ok) {
+#pragma omp atomic
+                    g_admm_rec_stats[3] += 1;
+                }
+            }
+            iters += 1;  // the warm start itself
+            if (!dual_ok) g.init(q);
+#pragma omp atomic
+            g_admm_rec_stats[2] += dual_ok ? 1 : 0;
+        }
+        int it = 0;
+        const int st = hvp::gi_run<N>(g, q, C, max_iter, it, nullptr);
+        iters += it;
+        if (st != hvp::GI_OK) return st;
+        bool consistent;
+        const uint64_t hs2 = hvp::admm_classify<N>(C, role, prm, q.P1, q.ts, q.y, hs, &consistent);
+        if (consistent) {
+            rec.hs = hs;
+            rec.nact = g.nact;
+            for (int j = 0; j < g.nact && j < 16; ++j) rec.ids[j] = g.ids[j];
+            return hvp::GI_OK;
+        }
+        hs = hs2;
+    }
+    return hvp::GI_FAIL_ITER;
+}
+
 // Branch and bound (hvp_bnb.h) with the same level-synchronous order as the gfx950 kernels:
 // root bound + greedy dive, then per depth the children of the unpruned nodes, then the argmin
 // and tie rule over the leaves.
 template <int N>
 void solve_one_bnb(const hvp_system& S, const hvp::Consts& C, int role, const double* prm, double* u, double* x,
                    int8_t* region, double* cost, int32_t* status, int32_t* nodes, int32_t* iters,
-                   double* xf = nullptr, double* xb = nullptr) {
+                   double* xf = nullptr, double* xb = nullptr, int idx = -1) {
     struct Node {
         uint64_t code;
         double lo, hi, lb;
         int stat;
         double y[N];
+        uint64_t hs;
     };
     int nq = 0, nit = 0;
     int l1_st = 0;  // status of the last min_1_norm LP (hvp_l1.h L1_*)
-    auto qp = [&](uint64_t code, int K, double lo, double hi, double& c, double* y) {
+    const int SD = g_admm_slots;
+    std::vector<uint64_t> claim;  // g_admm_warm == 4: owner code per (depth, slot) of this solve
+    bool root_phase = true;
+    if (g_admm_warm == 4 && idx >= 0 && idx < 4096) {
+        claim.assign((size_t)(N + 1) * SD, ~0ull);
+        if (g_admm_tab[idx].size() != (size_t)(N + 1) * SD) g_admm_tab[idx].assign((size_t)(N + 1) * SD, SlotRec{});
+    }
+    auto qp = [&](uint64_t code, int K, double lo, double hi, double& c, double* y, uint64_t* hs = nullptr) {
         hvp::LaneQp<N> q;
         int it = 0;
         if (C.l1) {  // min_1_norm: the node LP (relaxed after K steps), as k_l1_root / k_l1_bound
@@ -244,10 +341,65 @@ void solve_one_bnb(const hvp_system& S, const hvp::Consts& C, int role, const do
             // g_admm_leaf_ipm (tests): the leaves by the interior-point fallback (hvp_admm.h
             // solve_admm_ipm), as HVP_LEAF_GI_CAP forces on the device
             // (2: the leaves' active-set steps capped at 2, the interior point where that fails)
+            int rounds = 0;
+            if ((g_admm_warm == 3 || g_admm_warm == 4) && idx >= 0 && idx < 4096 && !g_admm_leaf_ipm) {
+                auto& recs = g_admm_recs[idx];
+                const auto key = std::make_pair(code, K);
+                bool have;
+                WarmRec rec{};
+                SlotRec* sr = nullptr;
+                if (g_admm_warm == 3) {
+                    auto f = recs.find(key);
+                    have = f != recs.end();
+                    if (have) rec = f->second;
+                } else {
+                    const size_t si = (size_t)K * SD + admm_slot(code, SD);
+                    const bool owner = K == 0 || (K == N && root_phase) || claim[si] == code;
+                    sr = owner ? &g_admm_tab[idx][si] : nullptr;
+                    have = sr && sr->valid && sr->code == code;
+                    if (have) rec = sr->rec;
+                }
+#pragma omp atomic
+                g_admm_rec_stats[0] += 1;
+#pragma omp atomic
+                g_admm_rec_stats[1] += have ? 1 : 0;
+                const int r = admm_warm_solve<N>(q, S, C, role, prm, code, K, 8 * hvp::GiConstraintSet<N>::NC, it,
+                                                 rounds, rec, have);
+#pragma omp atomic
+                g_admm_warm_stats[0] += 1;
+#pragma omp atomic
+                g_admm_warm_stats[1] += rounds;
+                ++nq;
+                nit += it;
+                if (r != hvp::GI_OK) {
+#pragma omp atomic
+                    g_admm_warm_stats[3] += 1;
+                    return false;
+                }
+                if (g_admm_warm == 3) recs[key] = rec;
+                else if (sr) *sr = SlotRec{true, code, rec};
+                c = hvp::admm_direct_cost<N>(q, S, C, role, prm, code, K);
+                if (y)
+                    for (int i = 0; i < N; ++i) y[i] = q.y[i];
+                return true;
+            }
             int r = g_admm_leaf_ipm == 1 && K == N
                         ? hvp::solve_admm_ipm<N>(q, S, C, role, prm, code, K, it)
                         : hvp::solve_admm_lane<N>(q, S, C, role, prm, code, K,
-                                                   g_admm_leaf_ipm == 2 && K == N ? 2 : 8 * hvp::GiConstraintSet<N>::NC, it);
+                                                   g_admm_leaf_ipm == 2 && K == N ? 2 : 8 * hvp::GiConstraintSet<N>::NC, it,
+                                                   nullptr, g_admm_warm ? hs : nullptr, &rounds);
+#pragma omp atomic
+            g_admm_warm_stats[0] += 1;
+#pragma omp atomic
+            g_admm_warm_stats[1] += rounds;
+            if (r == hvp::GI_OK && rounds == 1) {
+#pragma omp atomic
+                g_admm_warm_stats[2] += 1;
+            }
+            if (r != hvp::GI_OK) {
+#pragma omp atomic
+                g_admm_warm_stats[3] += 1;
+            }
             if (r != hvp::GI_OK && g_admm_leaf_ipm == 2 && K == N) {
                 int it2 = 0;
                 r = hvp::solve_admm_ipm<N>(q, S, C, role, prm, code, K, it2);
@@ -288,12 +440,15 @@ void solve_one_bnb(const hvp_system& S, const hvp::Consts& C, int role, const do
         root.code = 0;
         root.lo = root.hi = v0;
         root.lb = -1e300;
+        root.hs = g_admm_warm == 2 && idx >= 0 && idx < 4096 ? g_admm_root_hs[idx] : hvp::kHubNone;
         double c0;
-        if (qp(0, 0, v0, v0, c0, root.y)) {
+        if (qp(0, 0, v0, v0, c0, root.y, &root.hs)) {
             root.lb = c0;
+            if (g_admm_warm == 2 && idx >= 0 && idx < 4096) g_admm_root_hs[idx] = root.hs;
             uint64_t code;
             double c1;
-            if (hvp::bnb_dive<N>(S, C, v0, root.y, &code) && qp(code, N, 0.0, -1.0, c1, nullptr)) inc = c1;
+            uint64_t dhs = root.hs;
+            if (hvp::bnb_dive<N>(S, C, v0, root.y, &code) && qp(code, N, 0.0, -1.0, c1, nullptr, &dhs)) inc = c1;
             if (C.l1 && g_l1_solver == 1 && N <= HVP_MAX_N_ENUM) {
                 // the simplex's root optimum is a vertex (an extreme point where the LP optimum is a
                 // face): a second dive towards the constant-velocity trajectory (k_lp_root)
@@ -318,14 +473,21 @@ void solve_one_bnb(const hvp_system& S, const hvp::Consts& C, int role, const do
                 if (!hvp::bnb_child(S, C, k - 1, p.lo, p.hi, r, &c.lo, &c.hi)) continue;
                 c.code = hvp::code_with(p.code, k - 1, r);
                 c.lb = p.lb;
+                c.hs = p.hs;
                 nxt.push_back(c);
             }
         }
         if (k == N) nleaves += (int)nxt.size();
+        root_phase = false;
+        if (!claim.empty())
+            for (const Node& c : nxt) {
+                uint64_t& w = claim[(size_t)k * SD + admm_slot(c.code, SD)];
+                w = c.code < w ? c.code : w;
+            }
         for (Node& c : nxt) {
             double lb;
             const double plb = c.lb;  // the parent's bound (min_1_norm: kept by an unresolved leaf)
-            const bool good = qp(c.code, k, c.lo, c.hi, lb, c.y);
+            const bool good = qp(c.code, k, c.lo, c.hi, lb, c.y, &c.hs);
             c.stat = good ? 0 : HVP_MAXITER;
             c.lb = good ? lb : (k < N ? -1e300 : 1e300);
             if (!good && C.l1) {
@@ -412,7 +574,7 @@ void solve_range(const hvp_problem& P, const hvp_system* systems, int B, const i
             solve_one_bnb<N>(systems[sys[i]], C, role[i], params + (size_t)i * stride, u + (size_t)i * N,
                              x + (size_t)i * 2 * (N + 1), region + (size_t)i * N, cost + i, status + i, nodes + i,
                              iters + i, xf ? xf + (size_t)i * 2 * (N + 1) : nullptr,
-                             xb ? xb + (size_t)i * 2 * (N + 1) : nullptr);
+                             xb ? xb + (size_t)i * 2 * (N + 1) : nullptr, i);
             continue;
         }
         if constexpr (N <= HVP_MAX_N_ENUM)
@@ -509,6 +671,19 @@ void hvp_hostref_set_solver(int s) { g_solver = s; }
 void hvp_hostref_set_l1_solver(int s) { g_l1_solver = s; }
 void hvp_hostref_set_lp_trace(int s) { g_lp_trace = s; }
 void hvp_hostref_set_admm_leaf_ipm(int s) { g_admm_leaf_ipm = s; }
+void hvp_hostref_set_admm_warm(int s) { g_admm_warm = s; }
+void hvp_hostref_set_admm_slots(int s) { g_admm_slots = s; }
+void hvp_hostref_reset_admm_warm() {
+    for (uint64_t& h : g_admm_root_hs) h = hvp::kHubNone;
+    for (auto& m : g_admm_recs) m.clear();
+    for (auto& m : g_admm_tab) m.clear();
+    for (long long& v : g_admm_rec_stats) v = 0;
+    for (long long& v : g_admm_warm_stats) v = 0;
+}
+void hvp_hostref_admm_warm_stats(long long* out) {
+    for (int i = 0; i < 4; ++i) out[i] = g_admm_warm_stats[i];
+    for (int i = 0; i < 4; ++i) out[4 + i] = g_admm_rec_stats[i];
+}
 void hvp_hostref_lp_hist(long long* out) {
     for (int i = 0; i < 64; ++i) out[i] = g_lp_hist[i], g_lp_hist[i] = 0;
 }

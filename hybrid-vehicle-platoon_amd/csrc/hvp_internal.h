@@ -75,6 +75,13 @@ struct Workspace {
     int split = 1;                               // buckets per level list (hvp_lane.h LevelList; > 1
                                                  // per launch for the decentralised lane path)
     int split_shift = 0;                         // log2(split): a bucket's segment is cap >> split_shift
+    // naive-ADMM node records (16-lane path, 8 < N <= 12; hvp_lane.h node_index): the final hinge
+    // states, active set and factors of every tree node's QP, for the same node in the next solve
+    void* nrec = nullptr;                        // [max_batch][N + 1][nslots] hvp::coop::WarmRec<N>
+    unsigned long long* nclaim = nullptr;        // [max_batch][N + 1][nslots] owner priority (node_prio)
+    int nslots = 0;                              // records per (instance, depth), a power of two; 0: none
+    int ndepth = 0;                              // N + 1
+    unsigned long long nepoch = 0;               // this solve's epoch << 48
 };
 
 
@@ -116,6 +123,12 @@ struct hvp_handle {
     long long gadmm_redo_cap = 0;
     char* cent_split = nullptr;
     const int8_t* region_hint = nullptr;  // hvp_set_region_hint (copied into ws.hint per solve)
+    // naive-ADMM node records (Workspace::nrec), allocated at the first solve for the reserve
+    void* nrec = nullptr;
+    unsigned long long* nclaim = nullptr;
+    long long nrec_batch = 0;
+    int nrec_slots = 0;
+    unsigned long long nrec_epoch = 0;
     // device copies of the workspace descriptors the refill kernel reads in its event code
     // (hvp_lane.h k_bnb_bound_refill): [0] the level lists, [1] the dive list; re-uploaded when
     // they change (a reserve, another bucket split)

@@ -646,6 +646,8 @@ int hvp_get_stats(hvp_handle* h, hvp_stats* out) {
     }
     out->qp_iterations = (int64_t)c[1];
     out->n_fallback = (int64_t)c[2];
+    const bool own_counter = h->prob.formulation != HVP_FORM_GADMM && h->prob.formulation != HVP_FORM_CENT;
+    out->n_spilled = own_counter ? (int64_t)c[5] : 0;  // ws.counter[5], hvp_lane.h bnb_put_children
 #ifdef HVP_REFILL_PROF
     {
         unsigned long long lv2[2 * (HVP_MAX_N + 1)];
@@ -728,6 +730,8 @@ void hvp_destroy(hvp_handle* h) {
     if (h->cent_ties) (void)hipFree(h->cent_ties);
     if (h->cent_split) (void)hipFree(h->cent_split);
     if (h->gadmm_hs) (void)hipFree(h->gadmm_hs);
+    if (h->nrec) (void)hipFree(h->nrec);
+    if (h->nclaim) (void)hipFree(h->nclaim);
     if (h->d_consts) (void)hipFree(h->d_consts);
     if (h->d_ws) (void)hipFree(h->d_ws);
     if (h->gadmm_redo) (void)hipFree(h->gadmm_redo);

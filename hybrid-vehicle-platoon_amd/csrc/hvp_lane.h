@@ -758,26 +758,74 @@ __device__ inline unsigned bnb_children(const hvp_system& S, const hvp::Consts& 
     return mask;
 }
 
+__device__ inline unsigned long long* bucket_count(const Workspace& ws, int b, int k);
+
+// Naive-ADMM node records (the 16-lane path at 8 < N <= 12, Workspace::nrec): ADMM iteration t + 1
+// meets most of iteration t's tree nodes again (same region prefix and depth, so the same Hessian
+// for the same hinge states -- only the linear term and the row bounds move with y, z), and a
+// node's QP can then start from the equality-constrained optimum on its previous active set with
+// its previous factors (hvp_coop.h warm_start) instead of a Cholesky and ~10 active-set steps.
+// One direct-mapped table of `nslots` records per (instance, depth); slot = hash of the code.  The
+// children of a level claim their slots when they are written (bnb_put_children): the largest
+// priority wins, i.e. this solve's epoch first and then the smallest code, so among the nodes of
+// one level that share a slot the same one owns it in every run (the answers do not depend on
+// scheduling); only the owner reads and rewrites the record.  The root owns depth 0, and the
+// dive / hint leaves of k_bnb_root_coop write depth N before any level-N claim exists.
+__device__ inline int node_slot(uint64_t code, int nslots) {
+    return (int)((code * 0x9E3779B97F4A7C15ull) >> 40) & (nslots - 1);
+}
+__device__ inline size_t node_index(const Workspace& ws, int inst, int depth, uint64_t code) {
+    return ((size_t)inst * ws.ndepth + depth) * ws.nslots + node_slot(code, ws.nslots);
+}
+__device__ inline unsigned long long node_prio(const Workspace& ws, uint64_t code) {
+    return ws.nepoch | (~code & 0xFFFFFFFFFFFFull);  // codes of N <= 12 steps fit 48 bits
+}
+
 // writes the children (regions in mask) of a level-(lv-1) node into level lv's list at slots
-// off.. (reserved by the caller) below `limit` (the end of the list's half, LevelList); past it
-// the instance is flagged HVP_OVERFLOW
+// off.. (reserved by the caller) below `limit` (the end of the reservation's bucket segment,
+// LevelList).  A reservation past its segment spills: the lane reserves its nc slots again in
+// each other bucket in turn (one atomic each; rare) and writes the children into the first
+// segment that holds them -- the bucket only orders the claims, so the tree is unchanged.  Only
+// when no segment has room is the instance flagged HVP_OVERFLOW (reported, never truncated).
+// The slots of a failed reservation below its segment's end are marked dead (-1), which the
+// next kernels sweep.
 __device__ inline void bnb_put_children(const Workspace& ws, int lv, unsigned long long off, unsigned long long limit,
                                         unsigned mask, int inst, const hvp_system& S, const hvp::Consts& C,
                                         uint64_t code, double lo, double hi, double plb) {
     const int nc = __popc(mask), d = lv & 1;
     if (off + nc > limit) {
-        atomicOr(&ws.inst_flag[inst], 2);  // overflow: reported, never truncated silently
-        // the slots of this reservation below the limit are swept by the next kernels
         for (unsigned long long t = off; t < limit && t < off + nc; ++t) ws.nd_inst[d][t] = -1;
-        return;
+        bool placed = false;
+        if (ws.split > 1) {
+            const unsigned long long cap = (unsigned long long)ws.cap, seg = cap >> ws.split_shift;
+            for (int j = 0; j < ws.split && !placed; ++j) {
+                const unsigned long long base = (unsigned long long)j * seg,
+                                         end = j + 1 < ws.split ? base + seg : cap;
+                if (end == limit) continue;  // the bucket that is full
+                const unsigned long long o = base + atomicAdd(bucket_count(ws, j, lv), (unsigned long long)nc);
+                if (o + nc <= end) {
+                    off = o;
+                    placed = true;
+                    atomicAdd(&ws.counter[5], 1ull);  // hvp_stats.n_spilled
+                } else {
+                    for (unsigned long long t = o; t < end; ++t) ws.nd_inst[d][t] = -1;
+                }
+            }
+        }
+        if (!placed) {
+            atomicOr(&ws.inst_flag[inst], 2);
+            return;
+        }
     }
     int j = 0;
     for (int r = 0; r < S.n_regions; ++r) {
         if (!((mask >> r) & 1u)) continue;
         double a, b;
         hvp::bnb_child(S, C, lv - 1, lo, hi, r, &a, &b);
+        const uint64_t cc = hvp::code_with(code, lv - 1, r);
         ws.nd_inst[d][off + j] = inst;
-        ws.nd_code[d][off + j] = hvp::code_with(code, lv - 1, r);
+        ws.nd_code[d][off + j] = cc;
+        if (ws.nclaim) atomicMax(&ws.nclaim[node_index(ws, inst, lv, cc)], node_prio(ws, cc));
         ws.nd_lo[d][off + j] = a;
         ws.nd_hi[d][off + j] = b;
         ws.nd_lb[d][off + j] = plb;  // inherited: kept by a leaf whose QP fails
@@ -1032,7 +1080,14 @@ __global__ __launch_bounds__(kCoopBlock) void k_bnb_root_coop(int B, const hvp_s
         hvp::coop::Lane<N> L;
         double c0 = 0.0;
         int it = 0;
-        int st = hvp::coop::solve_qp<N>(L, lds[g], S, C, rl, prm, 0, 0, kGiMaxIter<N>, it, &c0, nullptr, prm[1], prm[1]);
+        // naive-ADMM node records (node_index): the root owns depth 0, the dive / hint leaves write
+        // depth N before the level-N claims
+        using Rec = hvp::coop::WarmRec<N>;
+        Rec* recs = reinterpret_cast<Rec*>(ws.nrec);
+        const uint64_t wkey = ((uint64_t)(uint32_t)sys[i] << 32) | (uint32_t)rl;
+        Rec* w0 = ws.nclaim ? recs + node_index(ws, i, 0, 0) : nullptr;
+        int st = hvp::coop::solve_qp<N, Rec>(L, lds[g], S, C, rl, prm, 0, 0, kGiMaxIter<N>, it, &c0, nullptr, prm[1],
+                                             prm[1], w0, w0 != nullptr, wkey);
         ++nodes;
         iters += it;
         if (st == hvp::GI_OK) {
@@ -1053,7 +1108,9 @@ __global__ __launch_bounds__(kCoopBlock) void k_bnb_root_coop(int B, const hvp_s
             code = hvp::coop::bcast(code, 0);
             if (dive_ok) {
                 double c1 = 0.0;
-                st = hvp::coop::solve_qp<N>(L, lds[g], S, C, rl, prm, code, N, kGiMaxIter<N>, it, &c1);
+                Rec* w1 = ws.nclaim ? recs + node_index(ws, i, N, code) : nullptr;
+                st = hvp::coop::solve_qp<N, Rec>(L, lds[g], S, C, rl, prm, code, N, kGiMaxIter<N>, it, &c1, nullptr,
+                                                 0.0, -1.0, w1, w1 != nullptr, wkey);
                 ++nodes;
                 iters += it;
                 if (st == hvp::GI_OK) inc = c1;
@@ -1070,7 +1127,9 @@ __global__ __launch_bounds__(kCoopBlock) void k_bnb_root_coop(int B, const hvp_s
                 hc = hvp::coop::bcast(hc, 0);
                 if (hok) {
                     double c2 = 0.0;
-                    st = hvp::coop::solve_qp<N>(L, lds[g], S, C, rl, prm, hc, N, kGiMaxIter<N>, it, &c2);
+                    Rec* w2 = ws.nclaim ? recs + node_index(ws, i, N, hc) : nullptr;
+                    st = hvp::coop::solve_qp<N, Rec>(L, lds[g], S, C, rl, prm, hc, N, kGiMaxIter<N>, it, &c2, nullptr,
+                                                     0.0, -1.0, w2, w2 != nullptr, wkey);
                     ++nodes;
                     iters += it;
                     if (st == hvp::GI_OK && !(c2 >= inc)) inc = c2;
@@ -1122,8 +1181,15 @@ __global__ __launch_bounds__(kCoopBlock) void k_bnb_bound_coop(int k, const hvp_
         double c = 0.0;
         int it = 0;
         const int cap = k == N && C.leaf_cap > 0 ? C.leaf_cap : kGiMaxIter<N>;
-        const int st = hvp::coop::solve_qp<N>(L, lds[g], S, C, rl, prm, code, k, cap, it, &c, nullptr,
-                                              ws.nd_lo[dst][q], ws.nd_hi[dst][q]);
+        using Rec = hvp::coop::WarmRec<N>;
+        Rec* wq = nullptr;  // the node's record, when it owns the slot (node_index)
+        if (ws.nclaim) {
+            const size_t ni = node_index(ws, inst, k, code);
+            if (ws.nclaim[ni] == node_prio(ws, code)) wq = reinterpret_cast<Rec*>(ws.nrec) + ni;
+        }
+        const int st = hvp::coop::solve_qp<N, Rec>(L, lds[g], S, C, rl, prm, code, k, cap, it, &c, nullptr,
+                                                   ws.nd_lo[dst][q], ws.nd_hi[dst][q], wq, wq != nullptr,
+                                                   ((uint64_t)(uint32_t)sys[inst] << 32) | (uint32_t)rl);
         const bool ok = st == hvp::GI_OK;
         if (k == N && t < N) ws.task_y[q * N + t] = L.y;
         if (t == 0) {
@@ -2821,6 +2887,66 @@ __global__ __launch_bounds__(kBnbBlock<N>) void k_gadmm_ipm(int P, int n, int lo
 
 inline int grid_for(long long n) { return (int)std::max<long long>(1, (n + kBlock - 1) / kBlock); }
 
+// The naive-ADMM node records of the 16-lane path (node_index): HVP_ADMM_NODE_SLOTS records per
+// (instance, depth), a power of two (default 256; 0: none), allocated for the reserve's batch at
+// the first solve that needs them (hipMalloc outside any capture: the ADMM engine's first
+// iteration) and zeroed (no record valid, no claim).  Each solve takes the next epoch, so the claims
+// of the previous solve lose to every claim of this one; at the epoch counter's wrap the claims
+// are cleared.  An allocation failure only turns the records off (a cold start for every node).
+template <int N>
+hipError_t node_records(hvp_handle* h, int B, Workspace& ws) {
+    const char* e = std::getenv("HVP_ADMM_NODE_SLOTS");
+    int want = e && e[0] ? std::atoi(e) : 256;
+    int slots = 0;
+    if (want > 0) {
+        slots = 1;
+        while (slots < want && slots < (1 << 16)) slots <<= 1;
+    }
+    const long long batch = std::max<long long>(B, h->ws.max_batch);
+    if (slots != h->nrec_slots || (slots && batch > h->nrec_batch)) {
+        hipError_t err = hipDeviceSynchronize();
+        if (err != hipSuccess) return err;
+        (void)hipFree(h->nrec);
+        (void)hipFree(h->nclaim);
+        h->nrec = nullptr;
+        h->nclaim = nullptr;
+        h->nrec_batch = 0;
+        h->nrec_slots = slots;
+        h->nrec_epoch = 0;
+        if (slots) {
+            const size_t n = (size_t)batch * (N + 1) * slots;
+            if (hipMalloc(&h->nrec, n * sizeof(hvp::coop::WarmRec<N>)) == hipSuccess &&
+                hipMalloc(&h->nclaim, n * sizeof(unsigned long long)) == hipSuccess &&
+                hipMemset(h->nrec, 0, n * sizeof(hvp::coop::WarmRec<N>)) == hipSuccess &&
+                hipMemset(h->nclaim, 0, n * sizeof(unsigned long long)) == hipSuccess) {
+                h->nrec_batch = batch;
+            } else {
+                (void)hipGetLastError();
+                (void)hipFree(h->nrec);
+                (void)hipFree(h->nclaim);
+                h->nrec = nullptr;
+                h->nclaim = nullptr;
+                std::fprintf(stderr, "[hvp] naive-ADMM node records: %zu bytes not available, cold starts\n",
+                             n * (sizeof(hvp::coop::WarmRec<N>) + sizeof(unsigned long long)));
+            }
+        }
+    }
+    if (!h->nrec) return hipSuccess;
+    if (++h->nrec_epoch > 0xFFFFull) {
+        hipError_t err = hipDeviceSynchronize();  // (a solve in flight may still claim)
+        if (err != hipSuccess) return err;
+        err = hipMemset(h->nclaim, 0, (size_t)h->nrec_batch * (N + 1) * slots * sizeof(unsigned long long));
+        if (err != hipSuccess) return err;
+        h->nrec_epoch = 1;
+    }
+    ws.nrec = h->nrec;
+    ws.nclaim = h->nclaim;
+    ws.nslots = slots;
+    ws.ndepth = N + 1;
+    ws.nepoch = h->nrec_epoch << 48;
+    return hipSuccess;
+}
+
 template <int N>
 int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, const double* params, double* u_out,
                double* x_out, int8_t* region_out, int8_t* gear_out, double* cost_out, int32_t* status_out,
@@ -2832,6 +2958,9 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
     // kernel of the level above (fused expand) and keeps each level in two halves (LevelList);
     // the other paths run k_bnb_expand per level over one list
     const bool fused = !kCoop<N> && h->C.form == HVP_FORM_DECENT && !h->C.l1;
+    if constexpr (kCoop<N> && N <= 12) {
+        if (h->C.form == HVP_FORM_ADMM && !h->C.l1) HIP_TRY(node_records<N>(h, B, ws));
+    }
     const char* sp = std::getenv("HVP_SPLIT_LEVELS");  // buckets per level list: 1 (one list), 2, 4 (A/B runs)
     const int want = sp && sp[0] ? std::atoi(sp) : kDefaultBuckets;
     ws.split = fused ? (want >= 4 ? 4 : (want >= 2 ? 2 : 1)) : 1;

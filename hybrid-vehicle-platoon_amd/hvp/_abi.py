@@ -88,6 +88,7 @@ class HvpStats(ctypes.Structure):
         ("qp_ms", ctypes.c_double),
         ("n_fallback", ctypes.c_int64),
         ("n_failed_bounds", ctypes.c_int64),
+        ("n_spilled", ctypes.c_int64),
     ]
 
 

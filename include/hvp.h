@@ -177,6 +177,7 @@ typedef struct hvp_stats {
     double qp_ms;           /* device time of its QP kernel (K_qp), ms                 */
     int64_t n_fallback;     /* candidates re-solved by the interior-point fallback    */
     int64_t n_failed_bounds;/* B&B bound QPs that did not converge (they prune nothing) */
+    int64_t n_spilled;      /* B&B child reservations placed in another level bucket   */
 } hvp_stats;
 
 int hvp_create(hvp_handle** out, const hvp_problem* problem, const hvp_system* systems,
@@ -184,7 +185,8 @@ int hvp_create(hvp_handle** out, const hvp_problem* problem, const hvp_system* s
 /* Workspace for batches up to max_batch.  candidate_capacity (<= 0: a default per method) is, for
  * branch and bound, the node capacity of ONE tree level pooled over the batch.  The decentralised
  * min_2_norm lane path (N <= 8) keeps every level in 2 buckets (HVP_SPLIT_LEVELS: 1, 2 or 4) of
- * capacity / buckets nodes each; an instance whose children do not fit its bucket is reported
+ * capacity / buckets nodes each; children that do not fit their bucket spill into another
+ * bucket's free segment (hvp_stats.n_spilled).  An instance whose children fit nowhere is reported
  * HVP_OVERFLOW (never truncated) and can be re-solved alone with a larger reserve. */
 int hvp_reserve(hvp_handle* h, int max_batch, int64_t candidate_capacity);
 /* Device-pointer entry point (async on stream).  Outputs may be NULL except cost/status. */

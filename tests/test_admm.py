@@ -286,13 +286,17 @@ def test_admm_simulate_gear_model(gpu_available):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("N,P", [(5, 256), (10, 128)])
-def test_warm_incumbent_does_not_change_answers(gpu_available, N, P):
+def test_warm_incumbent_does_not_change_answers(gpu_available, monkeypatch, N, P):
     """hvp_set_region_hint (AdmmEngine warm_incumbent): the previous iteration's sequences tried as
     incumbents change how much of the tree is pruned, never the answer -- two closed-loop steps
-    with and without it give bit-identical controls, trajectories, copies, regions and costs."""
+    with and without it give bit-identical controls, trajectories, copies, regions and costs.
+    (Without the node records: those warm-start the nodes the previous tree held, so a different
+    tree rounds differently in the last bits -- test_node_records_keep_the_answers.)"""
     import torch
 
     from hvp.admm import AdmmEngine, admm_problem
+
+    monkeypatch.setenv("HVP_ADMM_NODE_SLOTS", "0")
 
     n = 10
     states = np.stack([O.env_initial_state(n, s).astype(float) for s in range(P)])
@@ -317,6 +321,51 @@ def test_warm_incumbent_does_not_change_answers(gpu_available, N, P):
             assert np.array_equal(a[k], b[k]), k
     if N > 8:  # the deep trees, where AdmmEngine uses it by default
         assert sum(o["nodes"].sum() for o in res[0]) < sum(o["nodes"].sum() for o in res[1])
+
+
+@pytest.mark.gpu
+def test_node_records_keep_the_answers(gpu_available, monkeypatch):
+    """configs[2] at its own size per platoon (n = 10, N = 10, 20 ADMM iterations, 2 closed-loop
+    steps, y carried), 64 platoons: the naive-ADMM node records (hvp_lane.h node_index -- each
+    tree node's QP started from its own final active set and factors of the previous iteration)
+    against cold starts (HVP_ADMM_NODE_SLOTS=0).  Every iteration's regions equal, controls,
+    trajectories and copies within 1e-9 (the warm start reaches the same optimum by another
+    sequence of floating-point operations), far fewer active-set iterations; and two runs with the
+    records are bit-identical (the slot owners do not depend on scheduling)."""
+    import torch
+
+    from hvp.admm import AdmmEngine, admm_problem
+
+    n, N, P, iters = 10, 10, 64, 20
+    states = np.stack([O.env_initial_state(n, s).astype(float) for s in range(P)])
+    roles = [O.role_bits(i, n) for i in range(n)] * P
+    lead = np.stack([3000.0 + 20.0 * np.arange(N + 1), np.full(N + 1, 20.0)])
+
+    def run(slots):
+        monkeypatch.setenv("HVP_ADMM_NODE_SLOTS", str(slots))
+        eng = AdmmEngine(admm_problem(N, 0.5), [_system()], np.zeros(P * n, np.int32), roles, n, P)
+        eng.set_leader(lead)
+        outs, its = [], []
+        st = states
+        for t in range(2):
+            o = eng.step(st, iters, on_solve=lambda s: its.append(s.stats().qp_iterations))
+            torch.cuda.synchronize()
+            outs.append({k: v.cpu().numpy().copy() for k, v in o.items()})
+            st = outs[-1]["x"][:, :, 1].reshape(P, 2 * n)  # (p_1, v_1) of every vehicle
+        return outs, sum(its)
+
+    cold, it_cold = run(0)
+    warm, it_warm = run(128)
+    again, _ = run(128)
+    for c, w, a in zip(cold, warm, again):
+        assert (w["status"] == 0).all()
+        assert np.array_equal(w["region"], c["region"])
+        for k in ("u", "x", "x_front", "x_back"):
+            if k in w:
+                assert np.abs(w[k] - c[k]).max() <= 1e-9, k
+        for k in w:
+            assert np.array_equal(w[k], a[k]), k
+    assert it_warm < 0.7 * it_cold, (it_warm, it_cold)
 
 
 @pytest.mark.gpu

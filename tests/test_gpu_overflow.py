@@ -81,3 +81,55 @@ def test_overflow_host_path(gpu_available):
     assert (out.status == _abi.OPTIMAL).all()
     assert (out.region == ref.region).all()
     assert np.abs(out.cost - ref.cost).max() <= 1e-12 * np.abs(ref.cost).max()
+
+
+@pytest.mark.parametrize("buckets", [2, 4])
+def test_full_bucket_spills_into_free_segment(gpu_available, monkeypatch, buckets):
+    """A level bucket that outgrows its segment (capacity / buckets) spills into another bucket's
+    free segment (hvp_lane.h bnb_put_children) instead of reporting HVP_OVERFLOW.  At the smallest
+    capacity at which ONE list per level fits (HVP_SPLIT_LEVELS=1, found by bisection), plus a few
+    slots for the reservations that straddle a segment end, the bucketed lists fit too: children
+    spill (n_spilled > 0), no instance overflows, and the answers and trees equal the default
+    solve's (the bucket only orders the refill kernel's claims)."""
+    import torch
+
+    import bench
+    from hvp import _abi
+
+    n, N, S = 10, 5, 512
+    params, roles = bench.make_inputs(range(S), n, N)
+    dev = torch.device("cuda", 0)
+    tp, tr = torch.from_numpy(params).to(dev), torch.from_numpy(roles).to(dev)
+    ts = torch.zeros(len(roles), dtype=torch.int32, device=dev)
+    B = len(roles)
+
+    ref = _solver(N).solve_device(ts, tr, tp, retry_overflow=True)
+    torch.cuda.synchronize()
+    assert (ref["status"] == _abi.OPTIMAL).all()
+
+    def solve(cap):  # a fresh handle per capacity (hvp_reserve only ever grows a workspace)
+        s = _solver(N)
+        s.reserve(B, cap)
+        out = s.solve_device(ts, tr, tp)
+        torch.cuda.synchronize()
+        return out, s
+
+    monkeypatch.setenv("HVP_SPLIT_LEVELS", "1")
+    lo, hi = B, 16 * B
+    assert not (solve(hi)[0]["status"] == _abi.OVERFLOW).any()
+    while hi - lo > 64:
+        mid = (lo + hi) // 2
+        if (solve(mid)[0]["status"] == _abi.OVERFLOW).any():
+            lo = mid
+        else:
+            hi = mid
+    monkeypatch.setenv("HVP_SPLIT_LEVELS", str(buckets))
+    cap = hi + 64 * buckets  # a straddling reservation leaves < 16 dead slots per bucket and attempt
+    out, s = solve(cap)
+    st = s.stats()
+    assert st.n_spilled > 0, "the bucketed levels must have needed the spill at this capacity"
+    assert (out["status"] == _abi.OPTIMAL).all()
+    assert torch.equal(out["region"], ref["region"])
+    assert torch.equal(out["gear"], ref["gear"])
+    assert torch.equal(out["nodes"], ref["nodes"])
+    assert (out["cost"] - ref["cost"]).abs().max().item() <= 1e-12 * ref["cost"].abs().max().item()
