@@ -506,12 +506,14 @@ constexpr int kWarmDrops = 4;
 // The equality-constrained optimum on the active set of the last solve (WarmQp), made dual
 // feasible: y = J1 R^-T b - J2 J2' f, u = R^-1 (R^-T b + J1' f) with b_j = -dd of active row j
 // (n_j.y = b_j).  When a multiplier is negative (the new linear term or bounds moved the optimum
-// off a row), the factors go to LDS and the most negative row leaves the set -- a column of R out,
+// off a row), the most negative row leaves the set -- a column of R out,
 // Givens rotations back to triangular, J's columns rotated alike, as Goldfarb-Idnani's own drop --
 // up to kWarmDrops times (a row left out is added back by the loop if the new point violates it).
-// WARM_OK: J, R in LDS, L.y, u, id, act, nact set, and Goldfarb-Idnani continues from there.
-// WARM_COLD: nothing touched (H still in LDS).  WARM_LOST: still infeasible after the drops, and
-// the Hessian in LDS is overwritten -- the caller sets the QP up again for a cold start.
+// The record's factors are read into LDS first (over H: independent loads, where the substitutions
+// would otherwise wait on global loads one after another).  WARM_OK: J, R in LDS, L.y, u, id, act,
+// nact set, and Goldfarb-Idnani continues from there.  WARM_COLD: an unusable record, nothing
+// touched.  WARM_LOST: still infeasible after the drops -- the Hessian in LDS is overwritten, and
+// the caller sets the QP up again for a cold start.
 // Multipliers down to -1e-9 w count as zero (clamped).
 template <int N, class W>
 __device__ inline int warm_start(Lane<N>& L, GroupLds& Sg, const Consts& C, const W* wq, double& u, int& id,
@@ -521,12 +523,21 @@ __device__ inline int warm_start(Lane<N>& L, GroupLds& Sg, const Consts& C, cons
     const int t = lane16();
     int na = wq->nact;
     if (na < 0 || na > N) return WARM_COLD;
-    const double* Jg = wq->J;
-    const double* Rg = wq->R;
     int myid = t < na ? wq->ids[t] : -1;
+    // the factors into LDS (over H): independent loads, one row per lane
+    double* J = Sg.J;
+    double* R = Sg.R;
+    if (t < N) {  // (lane t's own rows: nobody reads H in between)
+#pragma unroll
+        for (int c = 0; c < N; ++c) {
+            J[t * LD + c] = wq->J[t * RS + c];
+            R[t * LD + c] = wq->R[t * RS + c];
+        }
+    }
+    gsync();
     const double wgt = C.w;
     double w, uu;
-    warm_solve<N>(L, Sg, Jg, Rg, RS, na, myid, w, uu);
+    warm_solve<N>(L, Sg, J, R, LD, na, myid, w, uu);
     auto verdict = [&]() {  // 0 dual feasible, 1 a negative multiplier, 2 a soft row above w
         int neg = 0, over = 0;
         if (t < na) {
@@ -536,74 +547,48 @@ __device__ inline int warm_start(Lane<N>& L, GroupLds& Sg, const Consts& C, cons
         return gor(over) ? 2 : (gor(neg) ? 1 : 0);
     };
     int vd = verdict();
-    if (vd == 2) return WARM_COLD;
-    const double* Jp = Jg;
-    int rs = RS;
-    if (vd == 1) {
-        // the factors into LDS (over H), then drop the most negative multiplier's row until the
-        // rest is dual feasible
-        gsync();
+    // drop the most negative multiplier's row until the rest is dual feasible
+    for (int drop_n = 0; vd == 1; ++drop_n) {
+        if (drop_n == kWarmDrops || na == 0) return WARM_LOST;
+        double key = t < na ? uu : 1e300;
+        int drop = t;
+        gargmin(key, drop);
+        const int id_n = __shfl_down(myid, 1, G);
+        if (t >= drop && t < na - 1) myid = id_n;
+        if (t == na - 1) myid = -1;
         if (t < N) {
 #pragma unroll
-            for (int c = 0; c < N; ++c) {
-                Sg.J[t * LD + c] = Jg[t * RS + c];
-                Sg.R[t * LD + c] = Rg[t * RS + c];
-            }
+            for (int j = 0; j < N - 1; ++j)
+                if (j >= drop && j < na - 1) R[t * LD + j] = R[t * LD + j + 1];
+#pragma unroll
+            for (int j = 0; j < N; ++j)
+                if (j == na - 1) R[t * LD + j] = 0.0;
         }
         gsync();
-        double* J = Sg.J;
-        double* R = Sg.R;
-        Jp = J;
-        rs = LD;
-        for (int drop_n = 0; vd == 1; ++drop_n) {
-            if (drop_n == kWarmDrops || na == 0) return WARM_LOST;
-            double key = t < na ? uu : 1e300;
-            int drop = t;
-            gargmin(key, drop);
-            const int id_n = __shfl_down(myid, 1, G);
-            if (t >= drop && t < na - 1) myid = id_n;
-            if (t == na - 1) myid = -1;
-            if (t < N) {
 #pragma unroll
-                for (int j = 0; j < N - 1; ++j)
-                    if (j >= drop && j < na - 1) R[t * LD + j] = R[t * LD + j + 1];
-#pragma unroll
-                for (int j = 0; j < N; ++j)
-                    if (j == na - 1) R[t * LD + j] = 0.0;
-            }
-            gsync();
-#pragma unroll
-            for (int i = 0; i < N - 1; ++i) {
-                if (i >= drop && i < na - 1) {
-                    double gc, gs;
-                    givens(R[i * LD + i], R[(i + 1) * LD + i], gc, gs);
-                    gsync();
-                    if (t >= i && t < na - 1) {
-                        const double a0 = R[i * LD + t], a1 = R[(i + 1) * LD + t];
-                        R[i * LD + t] = gc * a0 + gs * a1;
-                        R[(i + 1) * LD + t] = -gs * a0 + gc * a1;
-                    }
-                    if (t < N) {
-                        const double a0 = J[t * LD + i], a1 = J[t * LD + i + 1];
-                        J[t * LD + i] = gc * a0 + gs * a1;
-                        J[t * LD + i + 1] = -gs * a0 + gc * a1;
-                    }
-                    gsync();
+        for (int i = 0; i < N - 1; ++i) {
+            if (i >= drop && i < na - 1) {
+                double gc, gs;
+                givens(R[i * LD + i], R[(i + 1) * LD + i], gc, gs);
+                gsync();
+                if (t >= i && t < na - 1) {
+                    const double a0 = R[i * LD + t], a1 = R[(i + 1) * LD + t];
+                    R[i * LD + t] = gc * a0 + gs * a1;
+                    R[(i + 1) * LD + t] = -gs * a0 + gc * a1;
                 }
+                if (t < N) {
+                    const double a0 = J[t * LD + i], a1 = J[t * LD + i + 1];
+                    J[t * LD + i] = gc * a0 + gs * a1;
+                    J[t * LD + i + 1] = -gs * a0 + gc * a1;
+                }
+                gsync();
             }
-            // the subdiagonal entry the rotations zeroed (row i + 1, column i)
-            if (t < N) {
-#pragma unroll
-                for (int i = 0; i < N - 1; ++i)
-                    if (i >= drop && i < na - 1 && t == i + 1) R[t * LD + i] = 0.0;
-            }
-            --na;
-            gsync();
-            warm_solve<N>(L, Sg, J, R, LD, na, myid, w, uu);
-            vd = verdict();
-            if (vd == 2) return WARM_LOST;
         }
+        --na;
+        warm_solve<N>(L, Sg, J, R, LD, na, myid, w, uu);
+        vd = verdict();
     }
+    if (vd == 2) return WARM_LOST;
     // y_t = sum_c J[t][c] w_c
     double* v = Sg.v;
     gsync();
@@ -612,17 +597,7 @@ __device__ inline int warm_start(Lane<N>& L, GroupLds& Sg, const Consts& C, cons
     double y = 0.0;
     if (t < N) {
 #pragma unroll
-        for (int c = 0; c < N; ++c) y += Jp[t * rs + c] * v[c];
-    }
-    // commit: factors into LDS (when still in the record), the GI state into the lanes
-    if (t < N) {
-        if (Jp == Jg) {
-#pragma unroll
-            for (int c = 0; c < N; ++c) {
-                Sg.J[t * LD + c] = Jg[t * RS + c];
-                Sg.R[t * LD + c] = Rg[t * RS + c];
-            }
-        }
+        for (int c = 0; c < N; ++c) y += J[t * LD + c] * v[c];
         L.y = y;
     }
     u = t < na ? fmax(uu, 0.0) : 0.0;
@@ -1146,9 +1121,11 @@ __device__ inline int solve_qp(Lane<N>& L, GroupLds& Sg, const hvp_system& S, co
             if (w) {
                 hs = wq->hs;
             } else {
-                // lane data for the classification helpers
+                // the lane data the classification reads (lane_state: v0, ts, P1 as setup sets them)
                 Lane<N> L0;
-                setup<N>(L0, Sg, S, C, role, prm, code, K, 0);
+                L0.v0 = prm[1];
+                L0.ts = S.ts;
+                L0.P1 = prm[0] + S.ts * prm[1];
                 hs = admm_initial_states<N>(L0, C, role, prm);
             }
             st = GI_FAIL_ITER;
