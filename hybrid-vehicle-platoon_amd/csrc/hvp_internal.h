@@ -82,6 +82,7 @@ struct Workspace {
     int nslots = 0;                              // records per (instance, depth), a power of two; 0: none
     int ndepth = 0;                              // N + 1
     unsigned long long nepoch = 0;               // this solve's epoch << 48
+    int norder = 0;                              // k_bnb_bound_coop takes the level in k_node_order's order
 };
 
 

@@ -1164,7 +1164,10 @@ __global__ __launch_bounds__(kCoopBlock) void k_bnb_bound_coop(int k, const hvp_
     const int dst = k & 1;
     const unsigned long long nn = ws.lvl[k];
     const long long total = (long long)(nn < (unsigned long long)ws.cap ? nn : ws.cap);
-    for (long long q = (long long)blockIdx.x * kCoopGroups + g; q < total; q += (long long)gridDim.x * kCoopGroups) {
+    for (long long q0 = (long long)blockIdx.x * kCoopGroups + g; q0 < total; q0 += (long long)gridDim.x * kCoopGroups) {
+        // with node records, the level in k_node_order's order: the warm-started nodes first, so
+        // the 4 groups of a wave mostly hold QPs of one kind (a wave lasts as long as its slowest)
+        const long long q = ws.norder ? (long long)ws.task_inst[q0] : q0;
         const int inst = ws.nd_inst[dst][q];
         if (inst < 0) {
             if (t == 0) {
@@ -1818,6 +1821,50 @@ __device__ inline unsigned long long wave_claim(unsigned long long* claim, unsig
 }
 __device__ inline int wave_rank(unsigned long long mask) {
     return __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
+}
+
+// The order in which k_bnb_bound_coop takes a level's nodes when the naive-ADMM node records are
+// on (node_index): the nodes whose slot they own and whose record is theirs (a warm start, ~2
+// active-set steps) from the front of ws.task_inst (unused by the branch and bound), the others
+// (a cold start, ~16) from the back.  Which group solves a node changes nothing in its result.
+// The two fill counters are level k's entries of ws.lvl's spare rows (5M + k: front, 2M + k: back,
+// M = HVP_MAX_N + 1; zeroed per solve, unused at split = 1).
+template <int N>
+__global__ __launch_bounds__(kBlock) void k_node_order(int k, Workspace ws) {
+    constexpr int M = HVP_MAX_N + 1;
+    using Rec = hvp::coop::WarmRec<N>;
+    const int dst = k & 1;
+    const unsigned long long nn = ws.lvl[k];
+    const long long total = (long long)(nn < (unsigned long long)ws.cap ? nn : ws.cap);
+    const int lane = threadIdx.x & 63;
+    const long long wave0 = (long long)blockIdx.x * blockDim.x + (threadIdx.x & ~63);
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    const Rec* recs = reinterpret_cast<const Rec*>(ws.nrec);
+    for (long long qw = wave0; qw < total; qw += stride) {  // wave-uniform loop
+        const long long q = qw + lane;
+        bool warm = false;
+        if (q < total) {
+            const int inst = ws.nd_inst[dst][q];
+            if (inst >= 0) {
+                const uint64_t code = ws.nd_code[dst][q];
+                const size_t ni = node_index(ws, inst, k, code);
+                warm = ws.nclaim[ni] == node_prio(ws, code) && recs[ni].valid && recs[ni].code == code;
+            }
+        }
+        const unsigned long long wm = __ballot(q < total && warm), cm = __ballot(q < total && !warm);
+        const int nw = __popcll(wm), nc = __popcll(cm);
+        unsigned long long bw = 0, bc = 0;
+        if (lane == 0) {
+            if (nw) bw = atomicAdd(&ws.lvl[5 * M + k], (unsigned long long)nw);
+            if (nc) bc = atomicAdd(&ws.lvl[2 * M + k], (unsigned long long)nc);
+        }
+        bw = __shfl((int)bw, 0, 64);  // (< 2^31: a level's node count)
+        bc = __shfl((int)bc, 0, 64);
+        if (q < total) {
+            const long long pos = warm ? (long long)(bw + wave_rank(wm)) : total - 1 - (long long)(bc + wave_rank(cm));
+            ws.task_inst[pos] = (int32_t)q;
+        }
+    }
 }
 
 // min_1_norm root level through the LP refill kernel (HVP_LP_ROOT_REFILL, default on): the search
@@ -2944,6 +2991,8 @@ hipError_t node_records(hvp_handle* h, int B, Workspace& ws) {
     ws.nslots = slots;
     ws.ndepth = N + 1;
     ws.nepoch = h->nrec_epoch << 48;
+    const char* no = std::getenv("HVP_ADMM_NODE_ORDER");  // 0: the list order (A/B)
+    ws.norder = !(no && no[0] == '0');
     return hipSuccess;
 }
 
@@ -3113,6 +3162,10 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
             hipLaunchKernelGGL(k_l1_bound<N>, dim3(g_l1), dim3(kL1BlockOf<N>), 0, st, k, h->d_sys, sys, role, params,
                                h->C, ws);
         } else if constexpr (kCoop<N>) {
+            if (ws.norder) {
+                hipLaunchKernelGGL(k_node_order<N>, dim3(g_small), dim3(kBlock), 0, st, k, ws);
+                HIP_TRY(hipGetLastError());
+            }
             const int g_coop = (int)std::min<long long>((h->ws.cap + kCoopGroups - 1) / kCoopGroups,
                                                         (long long)h->n_cu * 32);
             hipLaunchKernelGGL(k_bnb_bound_coop<N>, dim3(g_coop), dim3(kCoopBlock), 0, st, k, h->d_sys, sys, role,
