@@ -181,10 +181,12 @@ __device__ inline StepForm admm_form(const Consts& C, int role, const double* pr
 // Lane data + this lane's Hessian row (into LDS J area, row t) for region code / relaxation K;
 // [lo, hi] (lo <= hi) = exact interval of v_K: the decentralised tail relaxation of
 // hvp_ipm.h:relax_step (as setup_lane), each lane propagating it up to its own step.
+// need_h = false (group-uniform): the lane data and f only -- a warm start takes the factors of
+// the Hessian from its record (warm_start), so H is not assembled.
 template <int N>
 __device__ inline bool setup(Lane<N>& L, GroupLds& S_lds, const hvp_system& S, const Consts& C, int role,
                              const double* prm, uint64_t code, int K, uint64_t hs, double lo = 0.0,
-                             double hi = -1.0) {
+                             double hi = -1.0, bool need_h = true) {
     const int t = lane16();
     const bool admm = C.form == HVP_FORM_ADMM || C.form == HVP_FORM_GADMM;
     const double p0 = prm[0], v0 = prm[1], ts = S.ts;
@@ -271,23 +273,27 @@ __device__ inline bool setup(Lane<N>& L, GroupLds& S_lds, const hvp_system& S, c
     const double P1 = L.P1;
     StepForm F{0, 0, 0, 0, 0};
     if (t < N) F = admm ? admm_form<N>(C, role, prm, t + 1, hs) : decent_form<N>(C, role, prm, t + 1);
-    const double wpp = t < N ? 2.0 * F.Wpp * ts * ts : 0.0;
     const double wgp = t < N ? ts * 2.0 * (F.Wpp * P1 + F.lp) : 0.0;
     // suffix sums: total - inclusive prefix + own
-    const double pre_pp = gscan(wpp), pre_gp = gscan(wgp);
-    const double tot_pp = bcast(pre_pp, G - 1), tot_gp = bcast(pre_gp, G - 1);
-    const double suf_pp = tot_pp - pre_pp + wpp;  // Spp(t + 1) at lane t
+    const double pre_gp = gscan(wgp);
+    const double tot_gp = bcast(pre_gp, G - 1);
     const double suf_gp = tot_gp - pre_gp + wgp;
-    const double spp_next = __shfl_down(suf_pp, 1, G);  // Spp(t + 2)
     const double sgp_next = __shfl_down(suf_gp, 1, G);
-    const double spp2 = t + 1 < N ? spp_next : 0.0;
     const double sgp2 = t + 1 < N ? sgp_next : 0.0;
-    const double wpv2 = 2.0 * F.Wpv * ts;
-    const double colv = spp2 + wpv2;  // value of column t in the rows above it
+    if (need_h) {
+        const double wpp = t < N ? 2.0 * F.Wpp * ts * ts : 0.0;
+        const double pre_pp = gscan(wpp);
+        const double tot_pp = bcast(pre_pp, G - 1);
+        const double suf_pp = tot_pp - pre_pp + wpp;  // Spp(t + 1) at lane t
+        const double spp_next = __shfl_down(suf_pp, 1, G);  // Spp(t + 2)
+        const double spp2 = t + 1 < N ? spp_next : 0.0;
+        const double wpv2 = 2.0 * F.Wpv * ts;
+        const double colv = spp2 + wpv2;  // value of column t in the rows above it
 #pragma unroll
-    for (int c = 0; c < N; ++c) {
-        const double cv = bcast(colv, c);
-        if (t < N) Hrow[c] = c < t ? spp2 + wpv2 : (c > t ? cv : 2.0 * F.Wvv + spp2);
+        for (int c = 0; c < N; ++c) {
+            const double cv = bcast(colv, c);
+            if (t < N) Hrow[c] = c < t ? spp2 + wpv2 : (c > t ? cv : 2.0 * F.Wvv + spp2);
+        }
     }
     double f = 2.0 * (F.Wpv * P1 + F.lv) + sgp2;
     // input cost Qu u_k^2 (k < K) and variation Qdu (u_{k+1} - u_k)^2 (k + 1 < K)
@@ -304,16 +310,16 @@ __device__ inline bool setup(Lane<N>& L, GroupLds& S_lds, const hvp_system& S, c
         double ub, gk, gkm;
         ucoef(t, ub, gk, gkm);
         if (L.ucost) {
-            Hrow[t] += w2 * gk * gk;
+            if (need_h) Hrow[t] += w2 * gk * gk;
             f += w2 * ub * gk;
-            if (t >= 1) Hrow[t - 1] += w2 * gk * gkm;
+            if (need_h && t >= 1) Hrow[t - 1] += w2 * gk * gkm;
         }
         if (t + 1 < N && (t + 1 < K || virt1 >= 0)) {
             double ub1, gk1, gkm1;
             ucoef(t + 1, ub1, gk1, gkm1);
-            Hrow[t] += w2 * gkm1 * gkm1;
+            if (need_h) Hrow[t] += w2 * gkm1 * gkm1;
             f += w2 * ub1 * gkm1;
-            Hrow[t + 1] += w2 * gk1 * gkm1;
+            if (need_h) Hrow[t + 1] += w2 * gk1 * gkm1;
         }
         if (C.Qdu != 0.0) {
             const double wd = 2.0 * C.Qdu;
@@ -328,9 +334,11 @@ __device__ inline bool setup(Lane<N>& L, GroupLds& S_lds, const hvp_system& S, c
                 const double gt = t == k + 1 ? g_kp : (t == k ? g_k : (t == k - 1 ? g_km : 0.0));
                 if (gt == 0.0) continue;
                 f += wd * eb * gt;
-                Hrow[k + 1] += wd * gt * g_kp;
-                Hrow[k] += wd * gt * g_k;
-                if (k >= 1) Hrow[k - 1] += wd * gt * g_km;
+                if (need_h) {
+                    Hrow[k + 1] += wd * gt * g_kp;
+                    Hrow[k] += wd * gt * g_k;
+                    if (k >= 1) Hrow[k - 1] += wd * gt * g_km;
+                }
             }
         }
     }
@@ -616,10 +624,11 @@ __device__ inline int warm_start(Lane<N>& L, GroupLds& Sg, const Consts& C, cons
 // Cooperative Goldfarb-Idnani.  On GI_OK lane t < N holds y_t in L.y.
 // wq (optional): the QP's WarmQp record -- tried as the starting active set when it was written
 // for the same code and hinge states (wcode, whs) and wtry is set; rewritten on success.
+// no_h: the caller did not assemble H (setup need_h = false) -- any start but the record's is lost.
 template <int N, class W = WarmQp>
 __device__ inline int solve(Lane<N>& L, GroupLds& Sg, const Consts& C, int max_iter, int& iters,
                             unsigned* edge = nullptr, W* wq = nullptr, uint64_t wcode = 0, uint64_t whs = 0,
-                            bool wtry = false, uint64_t wkey = 0) {
+                            bool wtry = false, uint64_t wkey = 0, bool no_h = false) {
     constexpr int RS = W::RS;
     const int t = lane16();
     iters = 0;
@@ -633,7 +642,7 @@ __device__ inline int solve(Lane<N>& L, GroupLds& Sg, const Consts& C, int max_i
     int warmed = WARM_COLD;
     if (wq && wtry && wq->valid && wq->code == wcode && wq->hs == whs && wq->key == wkey)  // group-uniform
         warmed = warm_start<N, W>(L, Sg, C, wq, u, id, act, nact);
-    if (warmed == WARM_LOST) {
+    if (warmed == WARM_LOST || (no_h && warmed != WARM_OK)) {
         iters = 0;
         return GI_WARM_LOST;
     }
@@ -1131,9 +1140,11 @@ __device__ inline int solve_qp(Lane<N>& L, GroupLds& Sg, const hvp_system& S, co
             st = GI_FAIL_ITER;
             for (int round = 0; round < kHubRounds; ++round) {
                 gsync();
-                setup<N>(L, Sg, S, C, role, prm, code, K, hs);
+                // the record will start this round (solve's test): no Hessian to assemble
+                const bool from_rec = w && wq->code == code && wq->hs == hs && wq->key == wkey;
+                setup<N>(L, Sg, S, C, role, prm, code, K, hs, 0.0, -1.0, !from_rec);
                 int it = 0;
-                st = solve<N, W>(L, Sg, C, max_iter, it, edge, wq, code, hs, w, wkey);
+                st = solve<N, W>(L, Sg, C, max_iter, it, edge, wq, code, hs, w, wkey, from_rec);
                 if (st == GI_WARM_LOST) {  // the warm start overwrote the Hessian and failed: cold
                     gsync();
                     setup<N>(L, Sg, S, C, role, prm, code, K, hs);
