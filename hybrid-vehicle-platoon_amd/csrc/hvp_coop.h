@@ -463,6 +463,38 @@ __device__ inline double row_dd(const Lane<N>& L, int p) {
     return (rev ? -1.0 : 1.0) * bcast(dloc, ol);
 }
 
+// row_dd of every lane's own row p (lanes with p < 0 get 0): the owner lanes' bounds gathered all
+// at once (independent cross-lane reads) where row_dd takes two dependent broadcasts per row
+template <int N>
+__device__ inline double own_row_dd(const Lane<N>& L, int p) {
+    const int t = lane16();
+    int ol = t, ob = 0;
+    if (p >= 0) row_owner<N>(p, ol, ob);
+    const double am = __shfl(L.am, ol, G), vlo = __shfl(L.vlo, ol, G), vhi = __shfl(L.vhi, ol, G);
+    const double ulo = __shfl(L.ulo, ol, G), uhi = __shfl(L.uhi, ol, G);
+    const double dec = __shfl(L.dec, ol, G), acc = __shfl(L.acc, ol, G);
+    const double hf = __shfl(L.hf, ol, G), hb = __shfl(L.hb, ol, G);
+    if (p < 0) return 0.0;
+    const int base = p & (GI_REV - 1);
+    const bool rev = (p & GI_REV) != 0;
+    double dloc;
+    if (base < 6 * N) {
+        const int rj = base / 6, r = base % 6, pair = r / 2;
+        const double a = pair == 1 ? am : (pair == 2 ? 1.0 : 0.0);
+        const double lo = pair == 0 ? vlo : (pair == 1 ? ulo : dec);
+        const double hi = pair == 0 ? vhi : (pair == 1 ? uhi : acc);
+        const double cst = rj == 0 ? -a * L.v0 : 0.0;
+        dloc = (r & 1) ? hi - cst : -(lo - cst);
+    } else {
+        const int r = (base - 6 * N) % 4;
+        if (r == 0) dloc = L.P1 - L.pmin;
+        else if (r == 1) dloc = L.pmax - L.P1;
+        else if (r == 2) dloc = hf - L.P1;
+        else dloc = L.P1 - hb;
+    }
+    return (rev ? -1.0 : 1.0) * dloc;
+}
+
 // w (lane t: w1 = R^-T b at the active positions t < na, -s beyond) and u = R^-1 (w1 + s1) of the
 // active rows ids (lane j: row of position j) with the factors J, R at (Jp, Rp), row stride rs;
 // s = J' f, b_j = -dd of row j.  Every lane of the group calls it.
@@ -470,11 +502,7 @@ template <int N>
 __device__ inline void warm_solve(const Lane<N>& L, GroupLds& Sg, const double* Jp, const double* Rp, int rs, int na,
                                   int myid, double& w, double& uu) {
     const int t = lane16();
-    double b = 0.0;
-    for (int j = 0; j < na; ++j) {
-        const double dd = row_dd<N>(L, bcast(myid, j));
-        if (t == j) b = -dd;
-    }
+    const double b = -own_row_dd<N>(L, t < na ? myid : -1);
     double* v = Sg.v;
     gsync();
     v[t] = t < N ? L.f : 0.0;
