@@ -1055,10 +1055,16 @@ __global__ __launch_bounds__(kBnbBlock<N>) HVP_LANE_OCC void k_bnb_root(int B, c
 template <int N>
 constexpr bool kCoop = N > HVP_MAX_N_ENUM;
 constexpr int kCoopBlock = 64;
+// waves per SIMD of the 16-lane group kernels (A/B builds: -DHVP_COOP_WAVES=2 caps them at 256 VGPRs)
+#ifdef HVP_COOP_WAVES
+#define HVP_COOP_OCC __attribute__((amdgpu_waves_per_eu(HVP_COOP_WAVES)))
+#else
+#define HVP_COOP_OCC
+#endif
 constexpr int kCoopGroups = kCoopBlock / hvp::coop::G;
 
 template <int N>
-__global__ __launch_bounds__(kCoopBlock) void k_bnb_root_coop(int B, const hvp_system* __restrict__ systems,
+__global__ __launch_bounds__(kCoopBlock) HVP_COOP_OCC void k_bnb_root_coop(int B, const hvp_system* __restrict__ systems,
                                                               const int32_t* __restrict__ sys,
                                                               const int32_t* __restrict__ role,
                                                               const double* __restrict__ params, hvp::Consts C,
@@ -1154,7 +1160,7 @@ __global__ __launch_bounds__(kCoopBlock) void k_bnb_root_coop(int B, const hvp_s
 }
 
 template <int N>
-__global__ __launch_bounds__(kCoopBlock) void k_bnb_bound_coop(int k, const hvp_system* __restrict__ systems,
+__global__ __launch_bounds__(kCoopBlock) HVP_COOP_OCC void k_bnb_bound_coop(int k, const hvp_system* __restrict__ systems,
                                                                const int32_t* __restrict__ sys,
                                                                const int32_t* __restrict__ role,
                                                                const double* __restrict__ params, hvp::Consts C,
@@ -2829,7 +2835,7 @@ __global__ __launch_bounds__(kBnbBlock<N>) void k_gadmm_qp(int P, int n, int lo,
 
 // x-update, one 16-lane group per local QP (long horizons, hvp_coop.h)
 template <int N>
-__global__ __launch_bounds__(kCoopBlock) void k_gadmm_qp_coop(int P, int n, int lo, int m,
+__global__ __launch_bounds__(kCoopBlock) HVP_COOP_OCC void k_gadmm_qp_coop(int P, int n, int lo, int m,
                                                               const hvp_system* __restrict__ systems,
                                                               const int32_t* __restrict__ sys,
                                                               const int32_t* __restrict__ role,
