@@ -987,6 +987,11 @@ __device__ inline int solve(Lane<N>& L, GroupLds& Sg, const Consts& C, int max_i
             wq->nact = nact;
             wq->valid = keep ? 1 : 0;
         }
+        // the record may be read again by this wave before the kernel ends (the next hinge round,
+        // the hint leaf after the dive leaf on one slot): its stores must be complete and seen by
+        // every lane first, not a mix of old and new rows
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        gsync();
     }
     return ok ? GI_OK : GI_FAIL_VERIFY;
 }

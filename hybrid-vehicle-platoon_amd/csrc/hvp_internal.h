@@ -130,6 +130,7 @@ struct hvp_handle {
     long long nrec_batch = 0;
     int nrec_slots = 0;
     unsigned long long nrec_epoch = 0;
+    bool nrec_enable = true;  // hvp_set_node_records
     // device copies of the workspace descriptors the refill kernel reads in its event code
     // (hvp_lane.h k_bnb_bound_refill): [0] the level lists, [1] the dive list; re-uploaded when
     // they change (a reserve, another bucket split)

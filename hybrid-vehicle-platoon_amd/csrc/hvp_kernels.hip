@@ -437,6 +437,12 @@ int hvp_set_region_hint(hvp_handle* h, const int8_t* region_hint) {
     return 0;
 }
 
+int hvp_set_node_records(hvp_handle* h, int enable) {
+    if (!h) return fail(HVP_E_ARG, "hvp_set_node_records: null handle");
+    h->nrec_enable = enable != 0;
+    return 0;
+}
+
 static int solve_impl(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, const double* params,
                       double* u_out, double* x_out, int8_t* region_out, int8_t* gear_out, double* cost_out,
                       int32_t* status_out, int32_t* nodes_out, int32_t* iters_out, void* stream, double* xf_out,

@@ -2599,6 +2599,13 @@ __global__ __launch_bounds__(kBlock) void k_bnb_finish(int B, const hvp_system* 
     if (status_out) status_out[i] = status;
     if (nodes_out) nodes_out[i] = ws.nodes[i];
     if (iters_out) iters_out[i] = ws.iters[i];
+    if (ws.nclaim && (flag & 2)) {
+        // an overflowed search wrote some of its node records in an order that depends on the
+        // scheduling (which reservation ran out first): none of them starts a later solve
+        hvp::coop::WarmRec<N>* recs = reinterpret_cast<hvp::coop::WarmRec<N>*>(ws.nrec);
+        const size_t nr = (size_t)ws.ndepth * ws.nslots;
+        for (size_t r = 0; r < nr; ++r) recs[(size_t)i * nr + r].valid = 0;
+    }
     if (!win || status != HVP_OPTIMAL) {
         if (cost_out) cost_out[i] = 1e300;
         const double* prm = params + (size_t)i * C.stride;
@@ -2984,7 +2991,7 @@ hipError_t node_records(hvp_handle* h, int B, Workspace& ws) {
             }
         }
     }
-    if (!h->nrec) return hipSuccess;
+    if (!h->nrec || !h->nrec_enable) return hipSuccess;
     if (++h->nrec_epoch > 0xFFFFull) {
         hipError_t err = hipDeviceSynchronize();  // (a solve in flight may still claim)
         if (err != hipSuccess) return err;

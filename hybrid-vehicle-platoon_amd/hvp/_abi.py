@@ -120,6 +120,7 @@ EXPORTS = {
     "hvp_evaluate_batch": ([_P, ctypes.c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
     "hvp_solve_admm_batch": ([_P, ctypes.c_int] + [_P] * 14, ctypes.c_int),
     "hvp_set_region_hint": ([_P, _P], ctypes.c_int),
+    "hvp_set_node_records": ([_P, ctypes.c_int], ctypes.c_int),
     "hvp_admm_update": ([_P, ctypes.c_int, ctypes.c_int] + [_P] * 8, ctypes.c_int),
     "hvp_gadmm_rollout": ([_P] + [ctypes.c_int] * 4 + [_P, _P, ctypes.c_int] + [_P] * 6, ctypes.c_int),
     "hvp_gadmm_solve": ([_P] + [ctypes.c_int] * 4 + [_P] * 14, ctypes.c_int),

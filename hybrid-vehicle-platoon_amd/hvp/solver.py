@@ -267,12 +267,16 @@ class BatchSolver:
 
     @contextlib.contextmanager
     def _hint_cleared(self):
+        """For a solve of a subset of the batch: the region hint and the naive-ADMM node records
+        (hvp_set_node_records) are indexed by the full batch's positions, so neither is used."""
         hint = getattr(self, "_hint", None)
         if hint is not None:
             self.set_region_hint(None)
+        _abi.check(self._lib.hvp_set_node_records(self._h, 0), "hvp_set_node_records")
         try:
             yield
         finally:
+            _abi.check(self._lib.hvp_set_node_records(self._h, 1), "hvp_set_node_records")
             if hint is not None:
                 self.set_region_hint(hint)
 

@@ -216,6 +216,16 @@ int hvp_solve_admm_batch(hvp_handle* h, int B, const int32_t* sys, const int32_t
  * nodes_out counts its QP.  The pointer must stay valid while solves may read it. */
 int hvp_set_region_hint(hvp_handle* h, const int8_t* region_hint);
 
+/* Naive-ADMM node records (HVP_FORM_ADMM, 8 < N <= 12): every branch-and-bound node
+ * QP of instance i keeps its final active set and factors for the same node of instance i in the
+ * next solve of this handle, which warm-starts from them (same answers to rounding; repeated runs
+ * bit-identical).  On by default (HVP_ADMM_NODE_SLOTS records per instance and depth, 0: off).
+ * The records are indexed by batch position like the region hint: a caller that re-solves a
+ * subset of its batch (an overflow retry) turns them off for that solve (enable = 0), so the
+ * subset neither reads nor overwrites the batch's records.  An instance whose search overflows
+ * leaves no record behind. */
+int hvp_set_node_records(hvp_handle* h, int enable);
+
 /* ADMM z- and y-update of ADMMCoordinator.get_control (fleet_naive_admm.py:421-468) for P
  * platoons of n vehicles (instance p*n + i), device pointers, async on stream:
  *   z_i = mean of x_i, vehicle (i+1)'s front copy and vehicle (i-1)'s back copy;

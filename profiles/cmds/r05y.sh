@@ -1,8 +1,8 @@
-# r05v: the bench lines of the round's library with their CPU baselines (every host core + one),
-# rooflines from the committed r05t / r05u summaries: C2 default, min_1_norm, C3, C4, centralised
+# r05y: the bench lines of the round's library with their CPU baselines (every host core + one),
+# rooflines from the committed r05w / r05x summaries: C2 default, min_1_norm, C3, C4, centralised
 set -o pipefail
 export TMPDIR=/tmp
-R=r05v
+R=r05y
 timeout -k 10 400 python bench.py > gpurun_out/${R}_bench_default.jsonl 2> gpurun_out/${R}_bench_default.err || exit 1
 timeout -k 10 300 python bench.py --cost l1 --steps 5 --warmup 1 > gpurun_out/${R}_bench_l1.jsonl 2> gpurun_out/${R}_bench_l1.err || exit 2
 timeout -k 10 300 python bench.py --controller admm --n 10 --N 10 --platoons 1024 --steps 3 --warmup 1 > gpurun_out/${R}_bench_admm.jsonl 2> gpurun_out/${R}_bench_admm.err || exit 3

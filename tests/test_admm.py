@@ -369,6 +369,41 @@ def test_node_records_keep_the_answers(gpu_available, monkeypatch):
 
 
 @pytest.mark.gpu
+def test_node_records_repeatable_at_scale(gpu_available):
+    """Half of C3's bench size (512 platoons of n = 10, N = 10, 20 ADMM iterations, 2 closed-loop
+    steps) twice on fresh engines: every iteration's QP count and the final outputs bit-identical.
+    (The hint leaf can share a table slot with the dive leaf solved just before it in the same
+    wave: the record write-back is fenced, hvp_coop.h solve.)"""
+    import torch
+
+    from hvp.admm import AdmmEngine, admm_problem
+
+    n, N, P, iters = 10, 10, 512, 20
+    states = np.stack([O.env_initial_state(n, s).astype(float) for s in range(P)])
+    roles = [O.role_bits(i, n) for i in range(n)] * P
+    lead = np.stack([3000.0 + 20.0 * np.arange(N + 1), np.full(N + 1, 20.0)])
+
+    def run():
+        eng = AdmmEngine(admm_problem(N, 0.5), [_system()], np.zeros(P * n, np.int32), roles, n, P)
+        eng.set_leader(lead)
+        qps, outs, st = [], [], states
+        for t in range(2):
+            o = eng.step(st, iters, on_solve=lambda s: qps.append(int(s.stats().n_candidates)))
+            torch.cuda.synchronize()
+            outs.append({k: v.cpu().numpy().copy() for k, v in o.items()})
+            st = outs[-1]["x"][:, :, 1].reshape(P, 2 * n)
+        return qps, outs
+
+    qa, a = run()
+    qb, b = run()
+    assert qa == qb
+    for x, y in zip(a, b):
+        assert (x["status"] == 0).all()
+        for k in x:
+            assert np.array_equal(x[k], y[k]), k
+
+
+@pytest.mark.gpu
 def test_region_hint_is_checked(gpu_available):
     """set_region_hint takes a contiguous CUDA (B, N) int8 tensor; a solve over more instances
     than the hint holds rows is refused before any launch (the kernels read hint[i * N + k])."""
