@@ -789,6 +789,8 @@ __device__ inline unsigned long long node_prio(const Workspace& ws, uint64_t cod
 // when no segment has room is the instance flagged HVP_OVERFLOW (reported, never truncated).
 // The slots of a failed reservation below its segment's end are marked dead (-1), which the
 // next kernels sweep.
+// CLAIM: the 16-lane path's k_bnb_expand, the only writer whose levels can have node records
+template <bool CLAIM = false>
 __device__ inline void bnb_put_children(const Workspace& ws, int lv, unsigned long long off, unsigned long long limit,
                                         unsigned mask, int inst, const hvp_system& S, const hvp::Consts& C,
                                         uint64_t code, double lo, double hi, double plb) {
@@ -796,7 +798,10 @@ __device__ inline void bnb_put_children(const Workspace& ws, int lv, unsigned lo
     if (off + nc > limit) {
         for (unsigned long long t = off; t < limit && t < off + nc; ++t) ws.nd_inst[d][t] = -1;
         bool placed = false;
-        if (ws.split > 1) {
+#ifndef HVP_SPILL
+#define HVP_SPILL 1
+#endif
+        if (HVP_SPILL && ws.split > 1) {
             const unsigned long long cap = (unsigned long long)ws.cap, seg = cap >> ws.split_shift;
             for (int j = 0; j < ws.split && !placed; ++j) {
                 const unsigned long long base = (unsigned long long)j * seg,
@@ -825,7 +830,7 @@ __device__ inline void bnb_put_children(const Workspace& ws, int lv, unsigned lo
         const uint64_t cc = hvp::code_with(code, lv - 1, r);
         ws.nd_inst[d][off + j] = inst;
         ws.nd_code[d][off + j] = cc;
-        if (ws.nclaim) atomicMax(&ws.nclaim[node_index(ws, inst, lv, cc)], node_prio(ws, cc));
+        if (CLAIM && ws.nclaim) atomicMax(&ws.nclaim[node_index(ws, inst, lv, cc)], node_prio(ws, cc));
         ws.nd_lo[d][off + j] = a;
         ws.nd_hi[d][off + j] = b;
         ws.nd_lb[d][off + j] = plb;  // inherited: kept by a leaf whose QP fails
@@ -1263,7 +1268,8 @@ __global__ __launch_bounds__(kBlock) void k_bnb_expand(int k, const hvp_system* 
         bool any;
         const unsigned long long off = wave_reserve(&ws.lvl[k], __popc(mask), lane, any);
         if (!any || !mask) continue;
-        bnb_put_children(ws, k, off, (unsigned long long)ws.cap, mask, inst, systems[sys[inst]], C, code, lo, hi, plb);
+        bnb_put_children<kCoop<N>>(ws, k, off, (unsigned long long)ws.cap, mask, inst, systems[sys[inst]], C, code, lo,
+                                   hi, plb);
     }
 }
 
