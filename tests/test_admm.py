@@ -404,6 +404,53 @@ def test_node_records_repeatable_at_scale(gpu_available):
 
 
 @pytest.mark.gpu
+def test_node_records_with_overflow_retries(gpu_available, monkeypatch):
+    """configs[2]'s local problems (64 platoons, 2 closed-loop steps x 20 ADMM iterations) on a
+    workspace small enough that some searches overflow every iteration: the overflowed instances
+    invalidate their node records (k_bnb_finish) and are re-solved alone with the records off
+    (hvp_set_node_records, BatchSolver._hint_cleared); every answer still equals the cold,
+    unconstrained run to rounding (regions exact, controls / trajectories / copies 1e-9)."""
+    import torch
+
+    from hvp.admm import AdmmEngine, admm_problem
+    from hvp.solver import BatchSolver
+
+    n, N, P, iters = 10, 10, 64, 20
+    states = np.stack([O.env_initial_state(n, s).astype(float) for s in range(P)])
+    roles = [O.role_bits(i, n) for i in range(n)] * P
+    lead = np.stack([3000.0 + 20.0 * np.arange(N + 1), np.full(N + 1, 20.0)])
+    orig_reserve, orig_launch = BatchSolver.reserve, BatchSolver._launch_admm
+    launches = []
+
+    def run(slots, tiny):
+        monkeypatch.setenv("HVP_ADMM_NODE_SLOTS", str(slots))
+        if tiny:  # the engine's own reserve: 6 nodes per instance and level (retries grow it)
+            monkeypatch.setattr(BatchSolver, "reserve", lambda self, b, c=0: orig_reserve(self, b, c or 6 * b))
+            monkeypatch.setattr(BatchSolver, "_launch_admm",
+                                lambda self, *a, **k: (launches.append(1), orig_launch(self, *a, **k))[1])
+        eng = AdmmEngine(admm_problem(N, 0.5), [_system()], np.zeros(P * n, np.int32), roles, n, P)
+        monkeypatch.setattr(BatchSolver, "reserve", orig_reserve)
+        eng.set_leader(lead)
+        outs, st = [], states
+        for t in range(2):
+            o = eng.step(st, iters)
+            torch.cuda.synchronize()
+            outs.append({k: v.cpu().numpy().copy() for k, v in o.items()})
+            st = outs[-1]["x"][:, :, 1].reshape(P, 2 * n)
+        monkeypatch.setattr(BatchSolver, "_launch_admm", orig_launch)
+        return outs
+
+    ref = run(0, False)
+    out = run(256, True)
+    assert len(launches) > 2 * iters, "the small workspace must have overflowed (retry launches)"
+    for c, w in zip(ref, out):
+        assert (w["status"] == 0).all()
+        assert np.array_equal(w["region"], c["region"])
+        for k in ("u", "x", "x_front", "x_back"):
+            assert np.abs(w[k] - c[k]).max() <= 1e-9, k
+
+
+@pytest.mark.gpu
 def test_region_hint_is_checked(gpu_available):
     """set_region_hint takes a contiguous CUDA (B, N) int8 tensor; a solve over more instances
     than the hint holds rows is refused before any launch (the kernels read hint[i * N + k])."""
