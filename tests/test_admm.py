@@ -73,6 +73,63 @@ def test_admm_local_problem_host_build_matches_oracle(hostref, N):
     _check(fx, u, x, reg, cost, st, xf, xb)
 
 
+def test_node_record_warm_starts_keep_the_answers_on_the_host(hostref):
+    """The node-record warm start on the host build (hvp_hostref_set_admm_warm 4:
+    each node QP from its own final hinge states and active set of the previous call, through a
+    direct-mapped table per (vehicle, depth) whose slots the smallest code of a level owns, negative
+    multipliers dropped): the oracle coordinator's local problems over 4 ADMM iterations of a
+    4-vehicle N = 10 platoon give the cold start's regions, costs to 1e-9 and controls to 1e-9,
+    with fewer active-set iterations."""
+    from hvp import _abi
+    from hvp.admm import admm_problem
+    from instances import leader_window
+
+    n, N, iters = 4, 10, 4
+    calls = []
+    orig = O.solve_admm_miqp
+
+    def rec(sysd, cfg, N_, role, rho, params, maxit=200):
+        calls.append((role, np.array(params, dtype=np.float64)))
+        return orig(sysd, cfg, N_, role, rho, params, maxit)
+
+    O.solve_admm_miqp = rec
+    try:
+        coord = O.AdmmCoordinator(O.gear_pwa_system(800.0), O.Cfg(), N, n)
+        coord.set_leader_x(leader_window(N, 0))
+        coord.step(O.env_initial_state(n, 0).astype(float), iters)
+    finally:
+        O.solve_admm_miqp = orig
+    roles = np.array([c[0] for c in calls], np.int32).reshape(iters, n)
+    params = np.stack([c[1] for c in calls]).reshape(iters, n, -1)
+    S = (_abi.HvpSystem * 1)(_system())
+    prob = admm_problem(N, 0.5)
+    f = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    res = {}
+    for mode in (0, 4):
+        hostref.hvp_hostref_set_admm_warm(mode)
+        hostref.hvp_hostref_set_admm_slots(16)
+        hostref.hvp_hostref_reset_admm_warm()
+        outs, total_it = [], 0
+        for it in range(iters):
+            u, x, reg = np.zeros((n, N)), np.zeros((n, 2, N + 1)), np.zeros((n, N), np.int8)
+            cost, st, nodes, its = np.zeros(n), np.zeros(n, np.int32), np.zeros(n, np.int32), np.zeros(n, np.int32)
+            xf, xb = np.zeros((n, 2, N + 1)), np.zeros((n, 2, N + 1))
+            rc = hostref.hvp_hostref_solve_admm_batch(ctypes.byref(prob), S, n, f(np.zeros(n, np.int32)),
+                                                      f(np.ascontiguousarray(roles[it])),
+                                                      f(np.ascontiguousarray(params[it])), f(u), f(x), f(reg),
+                                                      f(cost), f(st), f(nodes), f(its), f(xf), f(xb), 1)
+            assert rc == 0 and (st == 0).all()
+            outs.append((u, reg, cost))
+            total_it += int(its.sum())
+        res[mode] = (outs, total_it)
+    hostref.hvp_hostref_set_admm_warm(0)
+    for (uc, rc_, cc), (uw, rw, cw) in zip(res[0][0], res[4][0]):
+        assert np.array_equal(rc_, rw)
+        assert np.abs(cw - cc).max() <= 1e-9 * np.abs(cc).max()
+        assert np.abs(uw - uc).max() <= 1e-9
+    assert res[4][1] < res[0][1]
+
+
 def test_copy_elimination_is_exact_on_the_huber_pieces():
     """The closed-form copy (csrc/hvp_admm.h) in all three hinge regimes against a brute-force
     minimisation of the copy's terms (tracking + ADMM + w max(0, .)) on a fine grid."""
