@@ -536,7 +536,7 @@ __device__ inline void warm_solve(const Lane<N>& L, GroupLds& Sg, const double* 
     }
 }
 
-enum { WARM_COLD = 0, WARM_OK = 1, WARM_LOST = 2 };
+enum { WARM_COLD = 0, WARM_OK = 1, WARM_LOST = 2, WARM_DROPPED = 3 };
 constexpr int kWarmDrops = 4;
 
 // The equality-constrained optimum on the active set of the last solve (WarmQp), made dual
@@ -547,7 +547,8 @@ constexpr int kWarmDrops = 4;
 // up to kWarmDrops times (a row left out is added back by the loop if the new point violates it).
 // The record's factors are read into LDS first (over H: independent loads, where the substitutions
 // would otherwise wait on global loads one after another).  WARM_OK: J, R in LDS, L.y, u, id, act,
-// nact set, and Goldfarb-Idnani continues from there.  WARM_COLD: an unusable record, nothing
+// nact set, and Goldfarb-Idnani continues from there (WARM_DROPPED: the same after drops, so the
+// factors in LDS no longer equal the record's).  WARM_COLD: an unusable record, nothing
 // touched.  WARM_LOST: still infeasible after the drops -- the Hessian in LDS is overwritten, and
 // the caller sets the QP up again for a cold start.
 // Multipliers down to -1e-9 w count as zero (clamped).
@@ -584,9 +585,12 @@ __device__ inline int warm_start(Lane<N>& L, GroupLds& Sg, const Consts& C, cons
     };
     int vd = verdict();
     // drop the most negative multiplier's row until the rest is dual feasible
-    for (int drop_n = 0; vd == 1; ++drop_n) {
+    int drop_n = 0;
+    for (; vd == 1; ++drop_n) {
         if (drop_n == kWarmDrops || na == 0) return WARM_LOST;
-        double key = t < na ? uu : 1e300;
+        // NaN-safe key: a NaN multiplier (flagged negative by verdict) is the most negative, so
+        // the xor butterfly compares ordered values only and every lane agrees on `drop`
+        double key = t < na ? (uu == uu ? uu : -1e300) : 1e300;
         int drop = t;
         gargmin(key, drop);
         const int id_n = __shfl_down(myid, 1, G);
@@ -646,7 +650,7 @@ __device__ inline int warm_start(Lane<N>& L, GroupLds& Sg, const Consts& C, cons
     }
     nact = na;
     gsync();
-    return WARM_OK;
+    return drop_n ? WARM_DROPPED : WARM_OK;
 }
 
 // Cooperative Goldfarb-Idnani.  On GI_OK lane t < N holds y_t in L.y.
@@ -670,7 +674,8 @@ __device__ inline int solve(Lane<N>& L, GroupLds& Sg, const Consts& C, int max_i
     int warmed = WARM_COLD;
     if (wq && wtry && wq->valid && wq->code == wcode && wq->hs == whs && wq->key == wkey)  // group-uniform
         warmed = warm_start<N, W>(L, Sg, C, wq, u, id, act, nact);
-    if (warmed == WARM_LOST || (no_h && warmed != WARM_OK)) {
+    const bool warm_ok = warmed == WARM_OK || warmed == WARM_DROPPED;
+    if (warmed == WARM_LOST || (no_h && !warm_ok)) {
         iters = 0;
         return GI_WARM_LOST;
     }
@@ -973,25 +978,34 @@ __device__ inline int solve(Lane<N>& L, GroupLds& Sg, const Consts& C, int max_i
     const bool ok = gor(bad) == 0;
     if (wq) {  // the final active set and factors for the next ADMM iteration
         const bool keep = ok && gor((int)sat) == 0;  // saturated soft rows: not warm-startable
-        if (t < N) {
-            for (int c = 0; c < N; ++c) {
-                wq->J[t * RS + c] = J[t * LD + c];
-                wq->R[t * RS + c] = R[t * LD + c];
+        // started from this very record (same code, hinge states and key, no drop) and no add or
+        // drop since: active set and factors are the record's, so only a lost `valid` is written
+        const bool same = warmed == WARM_OK && iter == 0;
+        if (!same) {
+            if (t < N) {
+                for (int c = 0; c < N; ++c) {
+                    wq->J[t * RS + c] = J[t * LD + c];
+                    wq->R[t * RS + c] = R[t * LD + c];
+                }
+                wq->ids[t] = t < nact ? id : -1;
             }
-            wq->ids[t] = t < nact ? id : -1;
+            if (t == 0) {
+                wq->code = wcode;
+                wq->hs = whs;
+                wq->key = wkey;
+                wq->nact = nact;
+                wq->valid = keep ? 1 : 0;
+            }
+        } else if (!keep && t == 0) {
+            wq->valid = 0;
         }
-        if (t == 0) {
-            wq->code = wcode;
-            wq->hs = whs;
-            wq->key = wkey;
-            wq->nact = nact;
-            wq->valid = keep ? 1 : 0;
+        if (!same || !keep) {
+            // the record may be read again by this wave before the kernel ends (the next hinge
+            // round, the hint leaf after the dive leaf on one slot): its stores must be complete and
+            // seen by every lane first, not a mix of old and new rows
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            gsync();
         }
-        // the record may be read again by this wave before the kernel ends (the next hinge round,
-        // the hint leaf after the dive leaf on one slot): its stores must be complete and seen by
-        // every lane first, not a mix of old and new rows
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-        gsync();
     }
     return ok ? GI_OK : GI_FAIL_VERIFY;
 }

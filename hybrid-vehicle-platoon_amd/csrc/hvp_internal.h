@@ -127,8 +127,10 @@ struct hvp_handle {
     // naive-ADMM node records (Workspace::nrec), allocated at the first solve for the reserve
     void* nrec = nullptr;
     unsigned long long* nclaim = nullptr;
-    long long nrec_batch = 0;
-    int nrec_slots = 0;
+    long long nrec_batch = 0;   // batch the records were sized for (also set after a failed
+                                // allocation, so the next solve does not try again)
+    int nrec_want = 0;          // slots requested (HVP_ADMM_NODE_SLOTS, rounded to a power of two)
+    int nrec_slots = 0;         // slots allocated (nrec_want, halved until it fits the free HBM)
     unsigned long long nrec_epoch = 0;
     bool nrec_enable = true;  // hvp_set_node_records
     // device copies of the workspace descriptors the refill kernel reads in its event code

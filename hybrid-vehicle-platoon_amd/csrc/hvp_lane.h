@@ -2958,45 +2958,57 @@ inline int grid_for(long long n) { return (int)std::max<long long>(1, (n + kBloc
 // the first solve that needs them (hipMalloc outside any capture: the ADMM engine's first
 // iteration) and zeroed (no record valid, no claim).  Each solve takes the next epoch, so the claims
 // of the previous solve lose to every claim of this one; at the epoch counter's wrap the claims
-// are cleared.  An allocation failure only turns the records off (a cold start for every node).
+// are cleared.  The slot count is halved (down to 16) until the table fits in half of the free HBM;
+// an allocation that still fails only turns the records off (a cold start for every node) and is
+// not tried again until the slot request or the batch grows.
 template <int N>
 hipError_t node_records(hvp_handle* h, int B, Workspace& ws) {
     const char* e = std::getenv("HVP_ADMM_NODE_SLOTS");
     int want = e && e[0] ? std::atoi(e) : 256;
-    int slots = 0;
+    int req = 0;
     if (want > 0) {
-        slots = 1;
-        while (slots < want && slots < (1 << 16)) slots <<= 1;
+        req = 1;
+        while (req < want && req < (1 << 16)) req <<= 1;
     }
     const long long batch = std::max<long long>(B, h->ws.max_batch);
-    if (slots != h->nrec_slots || (slots && batch > h->nrec_batch)) {
+    if (req != h->nrec_want || (req && batch > h->nrec_batch)) {
         hipError_t err = hipDeviceSynchronize();
         if (err != hipSuccess) return err;
         (void)hipFree(h->nrec);
         (void)hipFree(h->nclaim);
         h->nrec = nullptr;
         h->nclaim = nullptr;
-        h->nrec_batch = 0;
-        h->nrec_slots = slots;
+        h->nrec_want = req;
+        h->nrec_batch = req ? batch : 0;  // also on failure: one attempt per request / batch size
         h->nrec_epoch = 0;
+        constexpr size_t per = sizeof(hvp::coop::WarmRec<N>) + sizeof(unsigned long long);
+        int slots = req;
+        size_t free_b = 0, total_b = 0;
+        if (slots && hipMemGetInfo(&free_b, &total_b) == hipSuccess)
+            while (slots > 16 && (size_t)batch * (N + 1) * slots * per > free_b / 2) slots >>= 1;
+        h->nrec_slots = slots;
         if (slots) {
             const size_t n = (size_t)batch * (N + 1) * slots;
             if (hipMalloc(&h->nrec, n * sizeof(hvp::coop::WarmRec<N>)) == hipSuccess &&
                 hipMalloc(&h->nclaim, n * sizeof(unsigned long long)) == hipSuccess &&
                 hipMemset(h->nrec, 0, n * sizeof(hvp::coop::WarmRec<N>)) == hipSuccess &&
                 hipMemset(h->nclaim, 0, n * sizeof(unsigned long long)) == hipSuccess) {
-                h->nrec_batch = batch;
+                if (slots < req)
+                    std::fprintf(stderr, "[hvp] naive-ADMM node records: %d of %d slots per node fit the free HBM\n",
+                                 slots, req);
             } else {
                 (void)hipGetLastError();
                 (void)hipFree(h->nrec);
                 (void)hipFree(h->nclaim);
                 h->nrec = nullptr;
                 h->nclaim = nullptr;
+                h->nrec_slots = 0;
                 std::fprintf(stderr, "[hvp] naive-ADMM node records: %zu bytes not available, cold starts\n",
-                             n * (sizeof(hvp::coop::WarmRec<N>) + sizeof(unsigned long long)));
+                             n * per);
             }
         }
     }
+    const int slots = h->nrec_slots;
     if (!h->nrec || !h->nrec_enable) return hipSuccess;
     if (++h->nrec_epoch > 0xFFFFull) {
         hipError_t err = hipDeviceSynchronize();  // (a solve in flight may still claim)

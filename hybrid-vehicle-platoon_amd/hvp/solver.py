@@ -102,7 +102,8 @@ class BatchSolver:
             if attempt:
                 self.reserve(max(B, 1), 4 * self.stats().capacity)
             sub = BatchResult(**{k: v[over].copy() for k, v in out.__dict__.items()})
-            self._solve_host(sys_idx[over], roles[over], np.ascontiguousarray(params[over]), sub)
+            with self._hint_cleared():  # hint rows and node records are indexed by the full batch
+                self._solve_host(sys_idx[over], roles[over], np.ascontiguousarray(params[over]), sub)
             for k, v in sub.__dict__.items():
                 getattr(out, k)[over] = v
         return out

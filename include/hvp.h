@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define HVP_ABI_VERSION 4
+#define HVP_ABI_VERSION 5
 #define HVP_MAX_REGIONS 16
 #define HVP_MAX_N 16     /* longest horizon (branch-and-bound path)            */
 #define HVP_MAX_N_ENUM 8 /* longest horizon of the exhaustive-enumeration path */

@@ -1229,7 +1229,10 @@ int oracle_solve_miqp(int N, int nreg, int nsr, const double* S, const double* R
 
 /* Naive-ADMM local MIQP (LocalMpcADMM, fleet_naive_admm.py:24-253), by branch and bound.
  * p = [x0 (2) | y_front | z_front | y_back | z_back | leader_x] (each (2, N+1)), as
- * hvp_params_stride_admm.  Outputs as oracle_solve_miqp plus the copies xf_out / xb_out. */
+ * hvp_params_stride_admm.  Outputs as oracle_solve_miqp plus the copies xf_out / xb_out.
+ * role bit 17: min_1_norm (LocalMpcADMM(quadratic_cost=False), fleet_naive_admm.py:74-77): every
+ * tracking / input term priced sum_i Q_ii |e_i| through add_norm's epigraph variables, the ADMM
+ * terms y'(c - z) + rho/2 |c - z|^2 of the copies (:172-198) unchanged -- a QP with L1 terms. */
 int oracle_solve_admm_miqp(int N, int nreg, int nsr, const double* S, const double* R, const double* T,
                            const double* A, const double* B, const double* c, int nd, const double* D, const double* E,
                            int nf, const double* F, const double* G, const double* cfgp, int role, double rho,
@@ -1239,7 +1242,9 @@ int oracle_solve_admm_miqp(int N, int nreg, int nsr, const double* S, const doub
     or_cfg cf;
     or_vmodel vm;
     if (N > OR_MAX_N || unpack_model(&md, nreg, nsr, S, R, T, A, B, c, nd, D, E, nf, F, G)) return -1;
-    unpack_cfg(&cf, N, 1, role, cfgp);
+    const int quadratic = !((role >> 17) & 1);
+    role &= 0xffff;
+    unpack_cfg(&cf, N, quadratic, role, cfgp);
     const int K1 = 2 * (N + 1);
     cf.admm = 1;
     cf.rho = rho;

@@ -404,9 +404,12 @@ def admm_params(x0, y_front, z_front, y_back, z_back, leader_x) -> np.ndarray:
     return np.concatenate([np.asarray(x0, dtype=np.float64).reshape(-1)[:2]] + blocks)
 
 
-def solve_admm_miqp(sysd: dict, cfg: Cfg, N: int, role: int, rho: float, params, maxit: int = 200) -> AdmmResult:
+def solve_admm_miqp(sysd: dict, cfg: Cfg, N: int, role: int, rho: float, params, maxit: int = 200,
+                    quadratic: bool = True) -> AdmmResult:
     """LocalMpcADMM's MIQP (fleet_naive_admm.py:24-253) in the full (x, u, s, copies) space,
-    branch and bound over the region sequences; see hvp_oracle.c oracle_solve_admm_miqp."""
+    branch and bound over the region sequences; see hvp_oracle.c oracle_solve_admm_miqp.
+    quadratic=False: min_1_norm (LocalMpcADMM(quadratic_cost=False), :74-77) -- L1 tracking and
+    input terms next to the quadratic ADMM terms of the copies."""
     L = lib()
     args, keep = _model_args(sysd)
     cv = cfg.vector()
@@ -415,7 +418,8 @@ def solve_admm_miqp(sysd: dict, cfg: Cfg, N: int, role: int, rho: float, params,
     x_out, u_out = np.zeros((2, N + 1)), np.zeros(N)
     sig, info = np.zeros(N, dtype=np.int32), np.zeros(7)
     xf, xb = np.zeros((2, N + 1)), np.zeros((2, N + 1))
-    rc = L.oracle_solve_admm_miqp(N, *args, _d(cv), int(role), float(rho), _d(p), maxit, _d(x_out), _d(u_out), _i(sig),
+    rl = int(role) | (0 if quadratic else 1 << 17)
+    rc = L.oracle_solve_admm_miqp(N, *args, _d(cv), rl, float(rho), _d(p), maxit, _d(x_out), _d(u_out), _i(sig),
                                   _d(info), _d(xf), _d(xb))
     del keep
     if rc != 0:
@@ -536,9 +540,11 @@ class AdmmCoordinator:
     State carried across time steps as in the reference: y_front / y_back (never reset), the
     parameter blocks each local MPC was last given, and the last local solutions (warm start)."""
 
-    def __init__(self, sysd: dict, cfg: Cfg, N: int, n: int, rho: float = 0.5, leader_index: int = 0):
+    def __init__(self, sysd: dict, cfg: Cfg, N: int, n: int, rho: float = 0.5, leader_index: int = 0,
+                 quadratic: bool = True):
         self.sysd, self.cfg, self.N, self.n, self.rho = sysd, cfg, N, n, rho
         self.leader_index = leader_index
+        self.quadratic = quadratic  # False: LocalMpcADMM(quadratic_cost=False), fleet_naive_admm.py:74-77
         K = (2, N + 1)
         self.y_front = [np.zeros(K) for _ in range(n)]
         self.y_back = [np.zeros(K) for _ in range(n)]
@@ -551,7 +557,10 @@ class AdmmCoordinator:
     def set_leader_x(self, xl) -> None:
         self.blocks[self.leader_index]["xl"] = np.asarray(xl, dtype=float)
 
-    def step(self, state, admm_iters: int):
+    def step(self, state, admm_iters: int, pool=None):
+        """One time step (admm_iters ADMM iterations).  pool: an optional process pool
+        (multiprocessing, spawn context) that runs the n local solves of an iteration in parallel
+        -- the same solves, the same answers (fixture generation at configs[2]'s size)."""
         n, N, rho = self.n, self.N, self.rho
         x = np.asarray(state, dtype=float).reshape(n, 2)
         for i in range(n):  # warm start (:392-402)
@@ -565,14 +574,15 @@ class AdmmCoordinator:
                 self.blocks[i]["zb"] = np.hstack((xp[:, 1:], xp[:, [-1]]))
         history = []
         for _ in range(admm_iters):
-            res = []
+            args = []
             for i in range(n):  # x-update (:407-419)
                 b = self.blocks[i]
                 p = admm_params(x[i], b["yf"], b["zf"], b["yb"], b["zb"], b["xl"])
-                r = solve_admm_miqp(self.sysd, self.cfg, N, self.roles[i], rho, p)
+                args.append((self.sysd, self.cfg, N, self.roles[i], rho, p, 200, self.quadratic))
+            res = pool.starmap(solve_admm_miqp, args) if pool is not None else [solve_admm_miqp(*a) for a in args]
+            for i, r in enumerate(res):
                 if r.status != 0:
                     raise RuntimeError(f"oracle ADMM local MIQP {i} status {r.status}")
-                res.append(r)
             history.append(res)
             for i in range(n):  # z- and y-update (:421-447)
                 if i == 0:

@@ -51,13 +51,27 @@ def device_code_objects(path: str) -> list[bytes]:
         pos = i + 1
 
 
+def _kernels(syms: str) -> set[str]:
+    """Kernel entry symbols of a code object: the names that have a ``<name>.kd`` descriptor."""
+    out = set()
+    for line in syms.splitlines():
+        name = line.split()[-1] if line.strip() else ""
+        if name.endswith(".kd"):
+            out.add(name[:-3])
+    return out
+
+
 def _scan(code: bytes) -> dict:
-    """{function: (long branches through s[30:31], s_setpc_b64 s[30:31])} of one code object."""
+    """{function: (long branches through s[30:31], s_setpc_b64 s[30:31])} of one code object's
+    NON-kernel functions (in a kernel s[30:31] is an ordinary register pair, so a kernel's long
+    branch through it is harmless and not reported)."""
     with tempfile.NamedTemporaryFile(suffix=".o") as f:
         f.write(code)
         f.flush()
         dis = subprocess.run([OBJDUMP, "-d", "--mcpu=gfx950", f.name], capture_output=True, text=True,
                              check=True).stdout
+        kernels = _kernels(subprocess.run([OBJDUMP, "--syms", f.name], capture_output=True, text=True,
+                                          check=True).stdout)
     cur, funcs = None, {}
     for line in dis.splitlines():
         m = re.match(r"^[0-9a-f]+ <([^>]+)>:", line)
@@ -69,7 +83,7 @@ def _scan(code: bytes) -> dict:
                 funcs[cur][0] += 1
             elif "s_setpc_b64 s[30:31]" in line:
                 funcs[cur][1] += 1
-    return {k: tuple(v) for k, v in funcs.items() if v[0]}
+    return {k: tuple(v) for k, v in funcs.items() if v[0] and k not in kernels}
 
 
 def audit(path: str) -> tuple[int, dict]:

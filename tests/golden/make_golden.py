@@ -47,7 +47,10 @@ Files (numpy .npz, no pickles):
                       the gear model (MpcGearCent)
   l1_long_*_N{9,10}.npz  min_1_norm at the MILP-vs-MIQP study's longer horizons (oracle branch
                       and bound, "method" = 1, "quadratic" = 0): t = 0 states, Q_du, a rollout
-Run:  python tests/golden/make_golden.py [sweep | gear | admm | admm_gear | gadmm | cent [n10 | l1] | configs admm|gadmm
+  admm_l1_*.npz       naive ADMM with min_1_norm (LocalMpcADMM(quadratic_cost=False)): local problems
+                      (incl. ConstantTime spacing), 3 closed-loop steps at n = 4, N = 5, and configs[2]'s
+                      size (n = 10, N = 10, 20 iterations, 2 steps; "admm_l1 n10")
+Run:  python tests/golden/make_golden.py [sweep | gear | admm | admm_l1 [n10] | admm_gear | gadmm | cent [n10 | l1] | configs admm|gadmm
                                           | l1 | l1_rollout | l1_long]
 """
 
@@ -313,6 +316,83 @@ def admm_fixtures():
     print("admm_steps_n4_N5.npz written")
 
 
+def admm_l1_fixtures(big: bool = False):
+    """Naive ADMM with min_1_norm (LocalMpcADMM(quadratic_cost=False), fleet_naive_admm.py:74-77):
+    L1 tracking / input terms next to the quadratic ADMM terms of the copies, from the oracle
+    (full (x, u, s, copies) space, branch and bound, KKT-certified QPs).
+      admm_l1_local_N{5,10}.npz    local problems as admm_local_* (random y, z; seed 0: y = z = 0)
+      admm_l1_local_ct_N5.npz      the same with ConstantTime(10, 3) spacing (t0 != 0: the back
+                                   copy's position error involves its velocity, task_2's policy)
+      admm_l1_steps_n4_N5.npz      3 closed-loop time steps x 4 ADMM iterations (oracle coordinator)
+      admm_l1_steps_n10_N10.npz    (big) configs[2]'s size: n = 10, N = 10, 20 iterations, 2 steps"""
+    import multiprocessing as mp
+
+    sysd = O.gear_pwa_system(800.0)
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(min(8, os.cpu_count() or 1)) as pool:
+        if big:
+            n, N, iters = 10, 10, 20
+            coord = O.AdmmCoordinator(sysd, O.Cfg(), N, n, quadratic=False)
+            st = O.env_initial_state(n, 0).astype(float)
+            states, us, xs = [], [], []
+            for t in range(2):
+                coord.set_leader_x(leader_window(N, t))
+                u, hist = coord.step(st, iters, pool=pool)
+                states.append(st.copy()); us.append(np.array([[r.u for r in res] for res in hist]))
+                xs.append(np.array([[r.x for r in res] for res in hist]))
+                st = np.concatenate([r.x[:, 1] for r in hist[-1]])
+                print(f"admm l1 step {t} done", flush=True)
+            np.savez_compressed(os.path.join(HERE, f"admm_l1_steps_n{n}_N{N}.npz"), N=N, n=n, iters=iters, rho=0.5,
+                                quadratic=0, states=np.array(states), exp_u=np.array(us), exp_x=np.array(xs),
+                                exp_region=np.array([[r.sigma for r in hist[-1]]]))
+            print(f"admm_l1_steps_n{n}_N{N}.npz written")
+            return
+        rng = np.random.default_rng(17)
+        for name, N, seeds, cfg in (("admm_l1_local_N5", 5, range(4), O.Cfg()),
+                                    ("admm_l1_local_N10", 10, range(2), O.Cfg()),
+                                    ("admm_l1_local_ct_N5", 5, range(1, 3), O.Cfg(d0=10.0, t0=3.0))):
+            P, R = [], []
+            for seed in seeds:
+                n = 4
+                st = O.env_initial_state(n, seed).astype(float)
+                for i in range(n):
+                    pred = lambda j: O.constant_velocity_prediction(st[2 * j], st[2 * j + 1], N)  # noqa: E731
+                    zf = pred(i - 1) + rng.normal(0, 3, (2, N + 1)) if i > 0 else np.zeros((2, N + 1))
+                    zb = pred(i + 1) + rng.normal(0, 3, (2, N + 1)) if i < n - 1 else np.zeros((2, N + 1))
+                    yf = rng.normal(0, 2, (2, N + 1)) if i > 0 else np.zeros((2, N + 1))
+                    yb = rng.normal(0, 2, (2, N + 1)) if i < n - 1 else np.zeros((2, N + 1))
+                    if seed == 0:  # the first time step of the reference: y = z = 0
+                        yf, zf, yb, zb = (np.zeros((2, N + 1)),) * 4
+                    xl = leader_window(N) if i == 0 else np.zeros((2, N + 1))
+                    P.append(O.admm_params(st[2 * i:2 * i + 2], yf, zf, yb, zb, xl))
+                    R.append(O.role_bits(i, n))
+            res = pool.starmap(O.solve_admm_miqp, [(sysd, cfg, N, r, 0.5, p, 200, False) for r, p in zip(R, P)])
+            np.savez_compressed(os.path.join(HERE, f"{name}.npz"), N=N, rho=0.5, quadratic=0, cfg=cfg.vector(),
+                                params=np.array(P), roles=np.array(R, np.int32),
+                                exp_x=np.array([r.x for r in res]), exp_u=np.array([r.u for r in res]),
+                                exp_xf=np.array([r.x_front for r in res]), exp_xb=np.array([r.x_back for r in res]),
+                                exp_cost=np.array([r.cost for r in res]),
+                                exp_status=np.array([r.status for r in res], np.int32),
+                                exp_cert=np.array([r.certified for r in res]),
+                                exp_region=np.array([r.sigma for r in res], np.int32))
+            print(f"{name}.npz: {len(R)} instances", flush=True)
+        n, N, iters = 4, 5, 4
+        coord = O.AdmmCoordinator(sysd, O.Cfg(), N, n, quadratic=False)
+        st = O.env_initial_state(n, 3).astype(float)
+        states, us, xs, regs = [], [], [], []
+        for t in range(3):
+            coord.set_leader_x(leader_window(N, t))
+            u, hist = coord.step(st, iters, pool=pool)
+            states.append(st.copy()); us.append(np.array([[r.u for r in res] for res in hist]))
+            xs.append(np.array([[r.x for r in res] for res in hist]))
+            regs.append(np.array([[r.sigma for r in res] for res in hist]))
+            st = np.concatenate([r.x[:, 1] for r in hist[-1]])
+        np.savez_compressed(os.path.join(HERE, "admm_l1_steps_n4_N5.npz"), N=N, n=n, iters=iters, rho=0.5,
+                            quadratic=0, states=np.array(states), exp_u=np.array(us), exp_x=np.array(xs),
+                            exp_region=np.array(regs, np.int32))
+        print("admm_l1_steps_n4_N5.npz written")
+
+
 def admm_gear_fixtures():
     """Naive ADMM with LocalMpcGear (fleet_naive_admm.py:261-288, selected for pwa_friction at
     :632-633): the local problem's modes are (gear, friction region) pairs (oracle
@@ -562,6 +642,9 @@ def main():
         return
     if len(sys.argv) > 1 and sys.argv[1] == "admm":
         admm_fixtures()
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == "admm_l1":
+        admm_l1_fixtures(big=len(sys.argv) > 2 and sys.argv[2] == "n10")
         return
     if len(sys.argv) > 1 and sys.argv[1] == "admm_gear":
         admm_gear_fixtures()

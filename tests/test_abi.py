@@ -20,6 +20,51 @@ def header_functions() -> set[str]:
         "hvp_params_stride"}
 
 
+def abi_digest() -> str:
+    """SHA-256 over include/hvp.h's declarations with comments and whitespace runs removed: the
+    struct definitions, enums, inline helpers and every prototype.  Any change of a field, a
+    signature or an export changes it; comment edits do not."""
+    import hashlib
+
+    src = open(os.path.join(ROOT, "include", "hvp.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    src = re.sub(r"//[^\n]*", "", src)
+    src = src.replace("#define HVP_ABI_VERSION", "#define HVP_ABI_VERSION_")  # the version is the key
+    src = re.sub(r"#define HVP_ABI_VERSION_\s+\d+", "", src)
+    return hashlib.sha256(" ".join(src.split()).encode()).hexdigest()
+
+
+# One entry per released ABI version: (sizeof hvp_system, hvp_problem, hvp_stats) and abi_digest().
+# A header change without a version bump fails test_abi_change_bumps_the_version; when the change is
+# deliberate, bump HVP_ABI_VERSION (include/hvp.h, hvp/_abi.py), add the new entry here and note the
+# change in INTEGRATION.md's ABI history.
+ABI_MANIFEST = {
+    5: ((768, 152, 72), "039ded6e2bca5fd6408117c0885b6e007dedd7d49a60bfa8b8714821c85f9606"),
+}
+
+
+def test_abi_change_bumps_the_version():
+    """hvp_stats grew (n_spilled) and hvp_set_node_records was added in round 5
+    under ABI 4, so a round-4 caller would have passed a 64-byte hvp_stats that the library
+    overran by 8 bytes.  The layout and the declarations are pinned per version."""
+    import ctypes
+
+    from hvp import _abi
+
+    lib = _abi.load()
+    assert lib.hvp_abi_version() == _abi.ABI_VERSION
+    sizes = (ctypes.c_int32 * 3)()
+    lib.hvp_abi_sizes(sizes)
+    assert _abi.ABI_VERSION in ABI_MANIFEST, "a new ABI version needs its ABI_MANIFEST entry"
+    want_sizes, want_digest = ABI_MANIFEST[_abi.ABI_VERSION]
+    assert tuple(sizes) == want_sizes, ("struct sizes changed: bump HVP_ABI_VERSION", tuple(sizes))
+    assert abi_digest() == want_digest, ("include/hvp.h declarations changed: bump HVP_ABI_VERSION",
+                                         abi_digest())
+    for old in ABI_MANIFEST:
+        if old != _abi.ABI_VERSION:
+            assert ABI_MANIFEST[old][1] != want_digest, f"ABI {_abi.ABI_VERSION} equals ABI {old}"
+
+
 def test_library_builds_and_exports_the_header():
     from hvp import _abi
 
