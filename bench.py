@@ -76,6 +76,29 @@ def profiled(kernel: str, tag: str):
     return None, why
 
 
+def step_traffic(tag: str, per_solve: str = "k_bnb_finish") -> dict | None:
+    """HBM bytes of EVERY product kernel of one solve: sum over the kernels of
+    the hash-matched profile of hbm_bytes x launches, divided by the launches of `per_solve` (one per
+    solve), with the per-kernel split.  None without a matching profile."""
+    import glob
+
+    sha = loaded_lib_sha()
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{tag}_summary.json")), reverse=True):
+        with open(path) as f:
+            meta = json.load(f)
+        if meta.get("lib_sha256") != sha:
+            continue
+        ks = meta["kernels"]
+        solves = (ks.get(per_solve) or {}).get("calls")
+        if not solves:
+            return None
+        per = {k: d["hbm_bytes"] * d["calls"] / solves for k, d in ks.items()
+               if k.startswith("k_") and "hbm_bytes" in d and d.get("calls")}
+        return {"bytes_per_solve": sum(per.values()), "by_kernel": per, "solves_profiled": solves,
+                "profile": os.path.relpath(path, ROOT)}
+    return None
+
+
 def qp_roofline(qp_step_ms: float, kernels: list, notional_bytes: float, tag: str) -> dict:
     """Roofline of the QP kernels of one step, from the live HIP-event time of their launches
     (qp_step_ms) and the per-launch PMC figures of profiles/ (the same bench workload):
@@ -331,6 +354,9 @@ def bench_admm(args, world: int, rank: int, local: int, dist) -> None:
     from hvp.models import PwaGearVehicle
 
     n, N, S, iters = args.n, args.N, args.platoons, args.admm_iters
+    # --cost l1: LocalMpcADMM(quadratic_cost=False) (fleet_naive_admm.py:74-77), the node QPs by the
+    # wave interior point with the copies as variables
+    quadratic = args.cost == "quadratic"
     veh = PwaGearVehicle(800)
     system = tables.system_from_dict(veh.get_discrete_system(1), tables.gears_of(veh))
     seeds = seed_range(rank, S)
@@ -349,7 +375,8 @@ def bench_admm(args, world: int, rank: int, local: int, dist) -> None:
         a, b = S * j // K, S * (j + 1) // K
         P = b - a
         roles = [tables.role_bits(i == 0, i == n - 1, i == 0) for i in range(n)] * P
-        eng = AdmmEngine(admm_problem(N, 0.5), [system], np.zeros(n * P, np.int32), roles, n, P, device=local,
+        eng = AdmmEngine(admm_problem(N, 0.5, quadratic_cost=quadratic), [system], np.zeros(n * P, np.int32), roles,
+                         n, P, device=local,
                          warm_incumbent=False if args.no_warm_incumbent else None)
         groups.append({"eng": eng, "P": P, "env": DeviceEnv(eng.solver, torch.full((P, n), 800.0, dtype=torch.float64,
                                                                                   device=dev)),
@@ -428,10 +455,12 @@ def bench_admm(args, world: int, rank: int, local: int, dist) -> None:
     notional = acc["qps"] * dense_qp_bytes(N) + iters * n * S * instance_io_bytes(N)
     # per-launch PMC figures of one engine's launches (profile: --streams 1 --platoons S/K); the
     # event pass above ran the K engines one after the other, so acc["qp_ms"] is their summed time
-    qk = ([("k_bnb_root_coop", iters * K), ("k_bnb_bound_coop", iters * N * K)] if N > 8
+    qk = ([("k_l1_root", iters * K), ("k_l1_bound", iters * N * K)] if not quadratic
+          else [("k_bnb_root_coop", iters * K), ("k_bnb_bound_coop", iters * N * K)] if N > 8
           else [("k_bnb_root", iters * K), ("k_bnb_bound", iters * N * K)])
     result = {
-        "metric": f"MPC timesteps/sec (whole platoon) at n={n} N={N} naive_admm ({iters} ADMM iterations)",
+        "metric": f"MPC timesteps/sec (whole platoon) at n={n} N={N} naive_admm ({iters} ADMM iterations)"
+                  + ("" if quadratic else " min_1_norm"),
         "value": value, "unit": "platoon-timesteps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "f64",
@@ -439,13 +468,15 @@ def bench_admm(args, world: int, rank: int, local: int, dist) -> None:
                 "on the device (ADMM control + plant step), y and the warm starts carried across steps",
         "config": {"workload": f"fleet_naive_admm n={n} N={N} pwa_gear closed loop (configs[2])", "n_vehicles": n,
                    "horizon": N, "admm_iters": iters, "rho": 0.5, "platoons_per_gpu": S,
+                   "cost": "min_2_norm" if quadratic else "min_1_norm",
                    "local_miqps_per_step": iters * n * S * world, "warm_incumbent": N > 8 and not args.no_warm_incumbent,
                    "streams_per_gpu": K, "parallelism": f"seeds-sharded x{world}"},
-        "roofline": qp_roofline(acc["qp_ms"], qk, notional, f"admm_n{n}_N{N}_P{S // K}"),
+        "roofline": qp_roofline(acc["qp_ms"], qk, notional, f"admm_n{n}_N{N}" + ("" if quadratic else "_l1")
+                                + f"_P{S // K}"),
         "qps_per_step": acc["qps"], "qp_iters_per_qp": acc["it"] / max(acc["qps"], 1),
         "not_optimal_total": int(notopt.item()), "plant_failures_total": int(bad.item()),
     }
-    if rank == 0 and not args.no_cpu and args.cpu_budget > 0 and world == 1:
+    if rank == 0 and not args.no_cpu and args.cpu_budget > 0 and world == 1 and quadratic:
         result["cpu_baseline"] = cpu_baseline_admm(n, N, iters, min(args.cpu_budget, 20.0), cpu_threads())
         result["cpu_baseline_1core"] = cpu_baseline_admm(n, N, iters, min(args.cpu_budget, 20.0) * 0.5, 1)
     if rank == 0:
@@ -1162,8 +1193,15 @@ def main() -> None:
         qk = [("k_qp_gi", 1)] if quadratic else [("k_qp_lp" if simplex else "k_qp_l1", 1)]
     # the PMC figures are per launch over the WHOLE batch (the profile runs this workload with
     # --streams 1); qp_step_ms is the HIP-event time of those launches in the one-handle pass
-    roofline = qp_roofline(qp_step_ms, qk, notional,
-                           f"decent_n{n}_N{N}" + ("" if bnb else "_enum") + ("" if quadratic else "_l1") + f"_P{S}")
+    prof_tag = f"decent_n{n}_N{N}" + ("" if bnb else "_enum") + ("" if quadratic else "_l1") + f"_P{S}"
+    roofline = qp_roofline(qp_step_ms, qk, notional, prof_tag)
+    # every launch of the step (instance prep, levels, tie rule, outputs): bytes per solve of the
+    # whole batch against the instance I/O (SURVEY 8(d)'s per-instance bytes x B)
+    st = step_traffic(prof_tag) if bnb else None
+    if st:
+        st["instance_io_bytes"] = B * instance_io_bytes(N)
+        st["x_instance_io"] = st["bytes_per_solve"] / st["instance_io_bytes"]
+    roofline["traffic_step"] = st
     roofline["time_basis"] = (f"HIP events around the QP launches of one handle over all {S} platoons (the timed "
                               f"region splits them over {K} streams, whose launches overlap)")
     roofline["profile_streams"] = 1

@@ -417,7 +417,7 @@ __device__ inline void row_owner(int id_in, int& lane, int& bit) {
 // two N x N products away (warm_start below).  `key` names the rest of what the Hessian depends
 // on (system index, role bits): a record written for another QP -- a handle called again with a
 // different batch -- never starts this one.  RS: the row stride of the factors (G for the
-// switching ADMM's per-QP records; N for the naive ADMM's node records, hvp_lane.h NodeCache,
+// switching ADMM's per-QP records; N for the naive ADMM's node records, hvp_lane.h node_index,
 // which are kept per tree node and so are many).
 template <int RS_>
 struct WarmRec {

@@ -52,8 +52,14 @@ struct Workspace {
     unsigned long long* key = nullptr;           // [max_batch] lexicographic key of the winner
     int32_t* nodes = nullptr;                    // [max_batch] QPs solved for the instance
     int32_t* iters = nullptr;                    // [max_batch] active-set iterations
-    unsigned long long* lvl = nullptr;           // [2 (HVP_MAX_N + 1)] nodes per level, then per-level
-                                                 // claim counters of the refilling bound kernel
+    unsigned long long* lvl = nullptr;           // [6 (HVP_MAX_N + 1)], M = HVP_MAX_N + 1 rows per block:
+                                                 // [0, M) nodes per level (bucket 0's count), [M, 2M)
+                                                 // the refill kernels' per-level claim counters, [2M, 5M)
+                                                 // buckets 1..3's counts (hvp_lane.h LevelList), [5M, 6M)
+                                                 // free.  k_node_order (16-lane naive ADMM) keeps its
+                                                 // per-level counters at rows 2M and 5M: bucket 1's
+                                                 // count row, unused there because that path runs at
+                                                 // split = 1 (launch_bnb: split > 1 only when fused)
     double* iq = nullptr;                        // [max_batch][fields, padded to 16] sigma-independent QP
                                                  // part per instance (decentralised branch and bound, N <= 8)
     const int8_t* hint = nullptr;                // [B][N] regions of a previous solve of the same
@@ -83,6 +89,9 @@ struct Workspace {
     int ndepth = 0;                              // N + 1
     unsigned long long nepoch = 0;               // this solve's epoch << 48
     int norder = 0;                              // k_bnb_bound_coop takes the level in k_node_order's order
+    int32_t* win = nullptr;                      // [max_batch] the winning leaf's slot in level N's list
+                                                 // (k_bnb_write), read by k_bnb_finish, which writes
+                                                 // every per-instance output in instance order
 };
 
 

@@ -227,6 +227,7 @@ void free_ws(Workspace& w) {
     (void)hipFree(w.lvl);
     (void)hipFree(w.iq);
     (void)hipFree(w.dv_mem);
+    (void)hipFree(w.win);
     w = Workspace{};
 }
 
@@ -305,9 +306,9 @@ int hvp_create(hvp_handle** out, const hvp_problem* problem, const hvp_system* s
         return fail(HVP_E_ARG, "hvp_create: the ADMM formulation needs rho > 0");
     if (problem->quadratic_cost != 1 && problem->quadratic_cost != 0)
         return fail(HVP_E_ARG, "hvp_create: quadratic_cost must be 1 (min_2_norm) or 0 (min_1_norm)");
-    if (problem->quadratic_cost == 0 && problem->formulation != HVP_FORM_DECENT && problem->formulation != HVP_FORM_CENT)
-        return fail(HVP_E_UNSUPPORTED, "hvp_create: the min_1_norm cost runs for the HVP_FORM_DECENT and HVP_FORM_CENT "
-                                       "problems");
+    if (problem->quadratic_cost == 0 && problem->formulation == HVP_FORM_GADMM)
+        return fail(HVP_E_UNSUPPORTED, "hvp_create: the min_1_norm cost runs for the HVP_FORM_DECENT, HVP_FORM_ADMM and "
+                                       "HVP_FORM_CENT problems (fleet_g_admm.LocalMpc is quadratic)");
     for (int i = 0; i < n_systems; ++i) {
         std::string why;
         if (!valid_system(systems[i], &why)) return fail(HVP_E_ARG, "hvp_create: system " + std::to_string(i) + ": " + why);
@@ -372,6 +373,7 @@ int hvp_reserve(hvp_handle* h, int max_batch, int64_t cap) {
              hipMalloc(&w.key, sizeof(unsigned long long) * max_batch) == hipSuccess &&
              hipMalloc(&w.nodes, sizeof(int32_t) * max_batch) == hipSuccess &&
              hipMalloc(&w.iters, sizeof(int32_t) * max_batch) == hipSuccess &&
+             hipMalloc(&w.win, sizeof(int32_t) * max_batch) == hipSuccess &&
              hipMalloc(&w.lvl, sizeof(unsigned long long) * 6 * (HVP_MAX_N + 1)) == hipSuccess;  // hvp_lane.h LevelList
         // K_inst_prep's per-instance QP part: H (NT) + f (N) + hf, hb (N - 1 each), one row per instance
         // padded to 16 doubles (hvp_lane.h kIqStride)

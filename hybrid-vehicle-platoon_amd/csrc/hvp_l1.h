@@ -173,13 +173,16 @@ HVP_HD inline void l1_steps(const hvp_system& S, const Consts& C, uint64_t code,
 // every lane: the per-lane host solver stores them all (l1_setup), the wave-cooperative kernels
 // (hvp_lane.h) keep the rows whose index maps to their lane.  Returns (mh, mp) through the
 // counters and false when the constant row p_1 in [pmin, pmax] is violated.
+// xl_blk: the leader window's offset in the params row in units of N + 1 (4: HVP_FORM_DECENT; the
+// naive-ADMM form's own rows (l1_admm_*) pass 8 with every role bit but HVP_ROLE_TRACK_LEADER
+// cleared, so xf / xb are never read).
 template <int N, class FH, class FP>
 HVP_HD inline bool l1_rows(const hvp_system& S, const Consts& C, int role, const double* prm, uint64_t code, int K,
-                           double rlo, double rhi, int& mh, int& mp, FH&& hard_cb, FP&& pair_cb) {
+                           double rlo, double rhi, int& mh, int& mp, FH&& hard_cb, FP&& pair_cb, int xl_blk = 4) {
     const double p0 = prm[0], v0 = prm[1];
     const double* xf = prm + 2;
     const double* xb = prm + 2 + 2 * (N + 1);
-    const double* xl = prm + 2 + 4 * (N + 1);
+    const double* xl = prm + 2 + xl_blk * (N + 1);
     const int K1 = N + 1;
     const double ts = S.ts, P1 = p0 + ts * v0;
     mh = 0;
@@ -609,10 +612,10 @@ HVP_HD inline int l1_solve(L1Lp<N>& L, double v0, int max_iter, int& iters, doub
 // between decided steps) -- the branch-and-bound bound.
 template <int N>
 HVP_HD inline double l1_direct_cost(const double* y, const hvp_system& S, const Consts& C, int role, const double* prm,
-                                    uint64_t code, int K = N, double rlo = 0.0, double rhi = -1.0) {
+                                    uint64_t code, int K = N, double rlo = 0.0, double rhi = -1.0, int xl_blk = 4) {
     const double* xf = prm + 2;
     const double* xb = prm + 2 + 2 * (N + 1);
-    const double* xl = prm + 2 + 4 * (N + 1);
+    const double* xl = prm + 2 + xl_blk * (N + 1);
     const int K1 = N + 1;
     const bool tf = (role & HVP_ROLE_TRACK_FRONT) != 0, tb = (role & HVP_ROLE_TRACK_BACK) != 0;
     const bool tl = (role & HVP_ROLE_TRACK_LEADER) != 0, lsp = (role & HVP_ROLE_LEADER_SPACING) != 0;
@@ -638,6 +641,104 @@ HVP_HD inline double l1_direct_cost(const double* y, const hvp_system& S, const 
         }
     }
     return J;
+}
+
+// ---- naive ADMM with min_1_norm: the exact copies of a trajectory
+// A copy group (side, step k) of LocalMpcADMM(quadratic_cost=False) (fleet_naive_admm.py:74-77)
+// given the own state (p_k, v_k): c = (c_p, c_v) minimises rho/2 |c - m|^2 (the ADMM terms,
+// :172-198, m = z - y / rho) + sum_j w+_j max(e_j, 0) + w-_j max(-e_j, 0), e_j = a_j . c + b_j (the
+// copy's L1 tracking terms, :110-133, and its soft safe row, :205-236).  The interior point leaves c
+// ~1e-9 off the safe row's kink, where w = 1e4 turns that into ~1e-5 of objective; the exact
+// minimiser is the stationary point of one kink pattern (each term > 0, < 0 or at its kink), so the
+// patterns' points are compared by the objective and the best taken.  l1_admm_node_lp prices the
+// trajectory and returns the copies with it.
+struct CopyTerms {
+    int nt;
+    double a[3][2], b[3], wp[3], wn[3];
+};
+
+HVP_HD inline double copy_objective(const CopyTerms& T, double rho, const double* m, double c0, double c1) {
+    double f = 0.5 * rho * ((c0 - m[0]) * (c0 - m[0]) + (c1 - m[1]) * (c1 - m[1]));
+    for (int j = 0; j < T.nt; ++j) {
+        const double e = T.a[j][0] * c0 + T.a[j][1] * c1 + T.b[j];
+        f += e > 0.0 ? T.wp[j] * e : -T.wn[j] * e;
+    }
+    return f;
+}
+
+HVP_HD inline void copy_exact(const CopyTerms& T, double rho, const double* m, double* c) {
+    double best = 1e308;
+    c[0] = m[0];
+    c[1] = m[1];
+    int npat = 1;
+    for (int j = 0; j < T.nt; ++j) npat *= 3;
+    for (int pat = 0; pat < npat; ++pat) {
+        int kink[2] = {-1, -1}, nk = 0, r = pat;
+        double g0 = 0.0, g1 = 0.0;
+        for (int j = 0; j < T.nt; ++j, r /= 3) {
+            const int s = r % 3;  // 0 kink, 1 e > 0, 2 e < 0
+            if (s == 0) {
+                if (nk < 2) kink[nk] = j;
+                ++nk;
+            } else {
+                const double sl = s == 1 ? T.wp[j] : -T.wn[j];
+                g0 += sl * T.a[j][0];
+                g1 += sl * T.a[j][1];
+            }
+        }
+        if (nk > 2) continue;
+        const double f0 = m[0] - g0 / rho, f1 = m[1] - g1 / rho;
+        double x0 = f0, x1 = f1;
+        if (nk == 1) {
+            const double* a = T.a[kink[0]];
+            const double aa = a[0] * a[0] + a[1] * a[1];
+            if (!(aa > 0.0)) continue;
+            const double mu = (a[0] * f0 + a[1] * f1 + T.b[kink[0]]) / aa;  // lambda / rho
+            x0 = f0 - a[0] * mu;
+            x1 = f1 - a[1] * mu;
+        } else if (nk == 2) {
+            const double *a = T.a[kink[0]], *d = T.a[kink[1]];
+            const double m00 = a[0] * a[0] + a[1] * a[1], m01 = a[0] * d[0] + a[1] * d[1], m11 = d[0] * d[0] + d[1] * d[1];
+            const double det = m00 * m11 - m01 * m01;
+            if (!(fabs(det) > 1e-12 * (m00 * m11 + 1e-300))) continue;
+            const double r0 = a[0] * f0 + a[1] * f1 + T.b[kink[0]], r1 = d[0] * f0 + d[1] * f1 + T.b[kink[1]];
+            const double u0 = (m11 * r0 - m01 * r1) / det, u1 = (m00 * r1 - m01 * r0) / det;
+            x0 = f0 - a[0] * u0 - d[0] * u1;
+            x1 = f1 - a[1] * u0 - d[1] * u1;
+        }
+        const double f = copy_objective(T, rho, m, x0, x1);
+        if (f < best) {
+            best = f;
+            c[0] = x0;
+            c[1] = x1;
+        }
+    }
+}
+
+// the terms of copy group (side, k) at own state (p, v) (roles: HVP_ROLE_SAFE_* = the copy exists,
+// HVP_ROLE_TRACK_* = its tracking terms)
+HVP_HD inline CopyTerms copy_terms(const Consts& C, int role, int side, double p, double v) {
+    CopyTerms T;
+    T.nt = 0;
+    const bool tr = (role & (side == 0 ? HVP_ROLE_TRACK_FRONT : HVP_ROLE_TRACK_BACK)) != 0;
+    auto add = [&](double a0, double a1, double b, double wp, double wn) {
+        T.a[T.nt][0] = a0;
+        T.a[T.nt][1] = a1;
+        T.b[T.nt] = b;
+        T.wp[T.nt] = wp;
+        T.wn[T.nt] = wn;
+        ++T.nt;
+    };
+    if (tr && side == 0) {  // p + t0 v + d0 - c_p ; v - c_v
+        add(-1.0, 0.0, p + C.t0 * v + C.d0, C.Qpp, C.Qpp);
+        add(0.0, -1.0, v, C.Qvv, C.Qvv);
+    } else if (tr) {  // c_p + t0 c_v + d0 - p ; c_v - v
+        add(1.0, C.t0, C.d0 - p, C.Qpp, C.Qpp);
+        add(0.0, 1.0, -v, C.Qvv, C.Qvv);
+    }
+    if (side == 0) add(-1.0, 0.0, p + C.d_safe, C.w, 0.0);  // w max(0, p - c_p + d_safe)
+    else add(1.0, 0.0, C.d_safe - p, C.w, 0.0);            // w max(0, c_p + d_safe - p)
+    return T;
 }
 
 }  // namespace hvp

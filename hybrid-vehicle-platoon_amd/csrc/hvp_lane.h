@@ -287,7 +287,7 @@ struct L1Wave {
     // the rows of the LP of (prm, code) relaxed after K steps (hvp_l1.h l1_rows) that map to this
     // lane; false when the constant p_1 row is violated
     __device__ bool load(const hvp_system& S, const hvp::Consts& C, int rl, const double* prm, uint64_t code, int K,
-                         double rlo, double rhi, int lane, int& mh, int& mp) {
+                         double rlo, double rhi, int lane, int& mh, int& mp, int xl_blk = 4) {
         clear();
         return hvp::l1_rows<N>(
             S, C, rl, prm, code, K, rlo, rhi, mh, mp,
@@ -314,7 +314,8 @@ struct L1Wave {
                         pal[q] = alpha;
                     }
                 }
-            });
+            },
+            xl_blk);
     }
 
     // this lane's share of: residuals (gap, obj, rd_y, max |rp|, max |rd_t|) when res, and the
@@ -565,6 +566,453 @@ __device__ int l1_node_lp(const hvp_system& S, const hvp::Consts& C, int rl, con
     W.load(S, C, rl, prm, code, K, rlo, rhi, lane, mh, mp);
     const int st = l1_wave_solve<N>(W, y, prm[1], mh, mp, C.max_iter, iters, red, lane, S.vmin, S.vmax);
     cost = COST && st == hvp::L1_OK ? hvp::l1_direct_cost<N>(y, S, C, rl, prm, code, K, rlo, rhi) : 0.0;
+    return st;
+}
+
+// ---- naive ADMM with min_1_norm (LocalMpcADMM(quadratic_cost=False), fleet_naive_admm.py:74-77)
+// The local problem keeps the neighbour COPIES (x_front / x_back, (2, N+1) each, :84-102) as
+// variables: their L1 tracking terms (:110-133 under min_1_norm), the soft safe rows on their
+// positions (:205-236, slack eliminated: w max(0, .)) and the quadratic ADMM terms
+// y'(c - z) + rho/2 |c - z|^2 (:172-198).  With sigma fixed it is a QP whose only curvature is the
+// copies' rho -- neither the velocity-space active-set solvers (no curvature in y) nor the simplex
+// take it.  Solved by the wave interior point above with the copies as extra variables: lane
+// l < 2(N+1) owns the copy GROUP (side = l / (N+1), step k = l % (N+1)), i.e. the two copies
+// (position, velocity) of that side and step and the up to three pairs that touch them (the two
+// tracking terms, the safe hinge), each the row g.y + h.c + e0 around its epigraph variable.  Each
+// group's 2 x 2 block rho I + sum ce h h' is eliminated into the N x N Newton matrix (Schur
+// complement) and recovered after the solve (dc = A^-1 (rc - A_cy dy)), so the system stays N x N;
+// hard rows and the own pairs (leader tracking, Q_u |u|, Q_du |du|) are L1Wave's.  Primal and dual
+// take one common step (the copies' dual residual rho c + q + sum (l1 - al l2) h couples both).
+template <int N>
+struct L1AdmmWave {
+    static constexpr int NQ = 3;  // pairs of a copy group: position tracking, velocity tracking, safe hinge
+    L1Wave<N> W;
+    bool gon;
+    double rho, c[2], q[2], dc[2];  // the group's copies (p, v) and linear terms y - rho z
+    bool qon[NQ];
+    double qg[NQ][N], qh[NQ][2], qe0[NQ], qw[NQ], qal[NQ], qt[NQ], qs1[NQ], qs2[NQ], ql1[NQ], ql2[NQ];
+    double qds1[NQ], qdl1[NQ], qds2[NQ], qdl2[NQ], qdt[NQ];
+
+    // the own rows (hard rows, leader tracking, inputs: l1_rows with the ADMM params layout) and this
+    // lane's copy group; mg = pairs of every group of the wave
+    __device__ bool load(const hvp_system& S, const hvp::Consts& C, int rl, const double* prm, uint64_t code, int K,
+                         double rlo, double rhi, int lane, int& mh, int& mp, int& mg) {
+        const bool ok = W.load(S, C, rl & HVP_ROLE_TRACK_LEADER, prm, code, K, rlo, rhi, lane, mh, mp, 8);
+        constexpr int K1 = N + 1;
+        const int side = lane / K1, k = lane % K1;
+        gon = lane < 2 * K1 && (rl & (side == 0 ? HVP_ROLE_SAFE_FRONT : HVP_ROLE_SAFE_BACK)) != 0;
+        rho = C.rho;
+        int cnt = 0;
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) {
+            qon[j] = false;
+            qe0[j] = qw[j] = qal[j] = qt[j] = ql1[j] = ql2[j] = 0.0;
+            qs1[j] = qs2[j] = 1.0;
+            qds1[j] = qdl1[j] = qds2[j] = qdl2[j] = qdt[j] = 0.0;
+            qh[j][0] = qh[j][1] = 0.0;
+#pragma unroll
+            for (int a = 0; a < N; ++a) qg[j][a] = 0.0;
+        }
+        c[0] = c[1] = q[0] = q[1] = dc[0] = dc[1] = 0.0;
+        if (gon) {
+            const double* yy = hvp::admm_y(prm, side, N);
+            const double* zz = hvp::admm_z(prm, side, N);
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                c[i] = zz[i * K1 + k] - yy[i * K1 + k] / rho;  // the ADMM term's own minimiser
+                q[i] = yy[i * K1 + k] - rho * zz[i * K1 + k];
+            }
+            const bool tr = (rl & (side == 0 ? HVP_ROLE_TRACK_FRONT : HVP_ROLE_TRACK_BACK)) != 0;
+            const double ts = S.ts, P1 = prm[0] + ts * prm[1];
+            const double pc = k == 0 ? prm[0] : P1, vc = k == 0 ? prm[1] : 0.0;  // constant parts of p_k, v_k
+            const double sg = side == 0 ? 1.0 : -1.0;  // front: own - copy (:110-121), back: copy - own (:122-133)
+            // pair 0: position tracking (front: p + t0 v + d0 - c_p; back: c_p + t0 c_v + d0 - p)
+            if (tr && C.Qpp > 0.0) {
+                qon[0] = true;
+#pragma unroll
+                for (int a = 0; a < N; ++a) {
+                    const double gp = (k >= 2 && a <= k - 2) ? ts : 0.0, gv = (k >= 1 && a == k - 1) ? 1.0 : 0.0;
+                    qg[0][a] = side == 0 ? gp + C.t0 * gv : -gp;
+                }
+                qh[0][0] = -sg;
+                qh[0][1] = side == 0 ? 0.0 : C.t0;
+                qe0[0] = side == 0 ? pc + C.t0 * vc + C.d0 : C.d0 - pc;
+                qw[0] = C.Qpp;
+                qal[0] = 1.0;
+            }
+            // pair 1: velocity tracking (front: v - c_v; back: c_v - v)
+            if (tr && C.Qvv > 0.0) {
+                qon[1] = true;
+#pragma unroll
+                for (int a = 0; a < N; ++a) qg[1][a] = (k >= 1 && a == k - 1) ? sg : 0.0;
+                qh[1][1] = -sg;
+                qe0[1] = sg * vc;
+                qw[1] = C.Qvv;
+                qal[1] = 1.0;
+            }
+            // pair 2: the soft safe row, w max(0, p - c_p + d_safe) (front) / w max(0, c_p + d_safe - p) (back)
+            if (C.w > 0.0) {
+                qon[2] = true;
+#pragma unroll
+                for (int a = 0; a < N; ++a) qg[2][a] = (k >= 2 && a <= k - 2) ? sg * ts : 0.0;
+                qh[2][0] = -sg;
+                qe0[2] = side == 0 ? pc + C.d_safe : C.d_safe - pc;
+                qw[2] = C.w;
+                qal[2] = 0.0;
+            }
+            cnt = (int)qon[0] + (int)qon[1] + (int)qon[2];
+        }
+        double cs = (double)cnt;
+        mg = (int)wave_sum(cs);
+        return ok;
+    }
+
+    __device__ double hc(int j, const double* cc) const { return qh[j][0] * cc[0] + qh[j][1] * cc[1]; }
+
+    // the per-pair terms of contrib / directions (hvp_l1.h l1_direction) at the pair's row value gy
+    struct PairTerms {
+        double rp1, rp2, D1, D2, rho1, rho2, rdt, rhst, mt, m, ce, coef;
+    };
+    __device__ PairTerms pair_terms(int j, double gy, bool corr, double sigmu) const {
+        PairTerms P;
+        const double al = qal[j];
+        P.rp1 = gy - qt[j] + qs1[j] + qe0[j];
+        P.rp2 = -al * gy - qt[j] + qs2[j] - al * qe0[j];
+        P.D1 = ql1[j] / qs1[j];
+        P.D2 = ql2[j] / qs2[j];
+        const double rc1 = qs1[j] * ql1[j] + (corr ? qds1[j] * qdl1[j] : 0.0) - sigmu;
+        const double rc2 = qs2[j] * ql2[j] + (corr ? qds2[j] * qdl2[j] : 0.0) - sigmu;
+        P.rho1 = (ql1[j] * P.rp1 - rc1) / qs1[j];
+        P.rho2 = (ql2[j] * P.rp2 - rc2) / qs2[j];
+        P.rdt = qw[j] - ql1[j] - ql2[j];
+        P.rhst = -P.rdt + P.rho1 + P.rho2;
+        P.mt = P.D1 + P.D2;
+        P.m = al * P.D2 - P.D1;
+        P.ce = P.D1 * P.D2 * (1.0 + al) * (1.0 + al) / P.mt;
+        P.coef = -(ql1[j] - al * ql2[j]) - (P.rho1 - al * P.rho2) - P.m * P.rhst / P.mt;
+        return P;
+    }
+
+    // the group's copy block A = rho I + sum ce h h' (inverse), A_cy dy (when dy), and rc = -(rho c + q)
+    // + sum coef h; also adds the group's pair terms to K / rhs / residuals when acc
+    __device__ void group_block(const double* y, const double* dy, bool corr, double sigmu, bool withK, double* K,
+                                double* rhs, double& gap, double& obj, double* rdy, double& rpm, double& rdm, bool acc,
+                                double& i00, double& i01, double& i11, double& rc0, double& rc1, double& ad0,
+                                double& ad1) const {
+        double a00 = rho, a01 = 0.0, a11 = rho;
+        rc0 = -(rho * c[0] + q[0]);
+        rc1 = -(rho * c[1] + q[1]);
+        double rd0 = -rc0, rd1 = -rc1;
+        ad0 = ad1 = 0.0;
+        double acy[2][N];
+#pragma unroll
+        for (int a = 0; a < N; ++a) acy[0][a] = acy[1][a] = 0.0;
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) {
+            if (!qon[j]) continue;
+            const double gy = hvp::l1_dot<N>(qg[j], y) + hc(j, c);
+            const PairTerms P = pair_terms(j, gy, corr, sigmu);
+            const double h0 = qh[j][0], h1 = qh[j][1], lm = ql1[j] - qal[j] * ql2[j];
+            a00 += P.ce * h0 * h0;
+            a01 += P.ce * h0 * h1;
+            a11 += P.ce * h1 * h1;
+            rc0 += P.coef * h0;
+            rc1 += P.coef * h1;
+            rd0 += lm * h0;
+            rd1 += lm * h1;
+            if (dy) {
+                const double gd = hvp::l1_dot<N>(qg[j], dy);
+                ad0 += P.ce * h0 * gd;
+                ad1 += P.ce * h1 * gd;
+            }
+            if (acc) {
+                gap += qs1[j] * ql1[j] + qs2[j] * ql2[j];
+                obj += qw[j] * qt[j];
+                rpm = fmax(rpm, fmax(fabs(P.rp1), fabs(P.rp2)));
+                rdm = fmax(rdm, fabs(P.rdt));
+#pragma unroll
+                for (int a = 0; a < N; ++a) {
+                    rdy[a] += lm * qg[j][a];
+                    rhs[a] += P.coef * qg[j][a];
+                    acy[0][a] += P.ce * h0 * qg[j][a];
+                    acy[1][a] += P.ce * h1 * qg[j][a];
+                    if (withK) {
+#pragma unroll
+                        for (int b = 0; b <= a; ++b) K[hvp::tri(a, b)] += P.ce * qg[j][a] * qg[j][b];
+                    }
+                }
+            }
+        }
+        const double det = a00 * a11 - a01 * a01;
+        i00 = a11 / det;
+        i01 = -a01 / det;
+        i11 = a00 / det;
+        if (acc) {
+            rdm = fmax(rdm, fmax(fabs(rd0), fabs(rd1)));
+            obj += fabs(0.5 * rho * (c[0] * c[0] + c[1] * c[1]) + q[0] * c[0] + q[1] * c[1]);
+            // Schur complement of the copy block: K -= A_yc A^-1 A_cy, rhs -= A_yc A^-1 rc
+            const double w0 = i00 * rc0 + i01 * rc1, w1 = i01 * rc0 + i11 * rc1;
+#pragma unroll
+            for (int a = 0; a < N; ++a) {
+                rhs[a] -= acy[0][a] * w0 + acy[1][a] * w1;
+                if (withK) {
+                    const double u0 = i00 * acy[0][a] + i01 * acy[1][a], u1 = i01 * acy[0][a] + i11 * acy[1][a];
+#pragma unroll
+                    for (int b = 0; b <= a; ++b) K[hvp::tri(a, b)] -= u0 * acy[0][b] + u1 * acy[1][b];
+                }
+            }
+        }
+    }
+
+    __device__ void contrib(const double* y, bool corr, double sigmu, bool withK, double* K, double* rhs, double& gap,
+                            double& obj, double* rdy, double& rpm, double& rdm) const {
+        W.contrib(y, corr, sigmu, withK, K, rhs, gap, obj, rdy, rpm, rdm);
+        if (!gon) return;
+        double i00, i01, i11, rc0, rc1, ad0, ad1;
+        group_block(y, nullptr, corr, sigmu, withK, K, rhs, gap, obj, rdy, rpm, rdm, true, i00, i01, i11, rc0, rc1, ad0,
+                    ad1);
+    }
+
+    __device__ void directions(const double* y, const double* dy, bool corr, double sigmu, double& ap, double& ad) {
+        W.directions(y, dy, corr, sigmu, ap, ad);
+        if (!gon) return;
+        double i00, i01, i11, rc0, rc1, ad0, ad1, dum = 0.0;
+        group_block(y, dy, corr, sigmu, false, nullptr, nullptr, dum, dum, nullptr, dum, dum, false, i00, i01, i11, rc0,
+                    rc1, ad0, ad1);
+        dc[0] = i00 * (rc0 - ad0) + i01 * (rc1 - ad1);
+        dc[1] = i01 * (rc0 - ad0) + i11 * (rc1 - ad1);
+        // every pair's terms from the stored (predictor) directions first, then the new directions
+        PairTerms P[NQ];
+        double gys[NQ];
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) {
+            gys[j] = hvp::l1_dot<N>(qg[j], y) + hc(j, c);
+            P[j] = pair_terms(j, gys[j], corr, sigmu);
+        }
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) {
+            if (!qon[j]) continue;
+            const double al = qal[j];
+            const double gd = hvp::l1_dot<N>(qg[j], dy) + hc(j, dc);
+            qdt[j] = (P[j].rhst - P[j].m * gd) / P[j].mt;
+            const double a1 = gd - qdt[j], a2 = -al * gd - qdt[j];
+            qds1[j] = -P[j].rp1 - a1;
+            qds2[j] = -P[j].rp2 - a2;
+            const bool big1 = P[j].D1 >= P[j].D2;
+            const double dls = big1 ? P[j].D2 * a2 + P[j].rho2 : P[j].D1 * a1 + P[j].rho1;
+            qdl1[j] = big1 ? P[j].rdt - dls : dls;
+            qdl2[j] = big1 ? dls : P[j].rdt - dls;
+            hvp::l1_ratio(ap, qs1[j], qds1[j]);
+            hvp::l1_ratio(ap, qs2[j], qds2[j]);
+            hvp::l1_ratio(ad, ql1[j], qdl1[j]);
+            hvp::l1_ratio(ad, ql2[j], qdl2[j]);
+        }
+    }
+
+    // the group's copies at their exact minimisers given the own trajectory y (hvp_l1.h copy_exact)
+    // and its objective term by term: ADMM terms and the pairs' w |e| / w max(0, e)
+    __device__ double group_cost(const double* y, const hvp_system& S, const hvp::Consts& C, int rl, const double* prm,
+                                 int lane) {
+        if (!gon) return 0.0;
+        constexpr int K1 = N + 1;
+        const int side = lane / K1, k = lane % K1;
+        const double* yy = hvp::admm_y(prm, side, N);
+        const double* zz = hvp::admm_z(prm, side, N);
+        double p = prm[0], v = prm[1];  // own state at step k
+        if (k >= 1) {
+            p = prm[0] + S.ts * prm[1];
+#pragma unroll
+            for (int a = 0; a < N; ++a)
+                if (a <= k - 2) p += S.ts * y[a];
+#pragma unroll
+            for (int a = 0; a < N; ++a)
+                if (a == k - 1) v = y[a];
+        }
+        const double m[2] = {zz[k] - yy[k] / rho, zz[K1 + k] - yy[K1 + k] / rho};
+        hvp::copy_exact(hvp::copy_terms(C, rl, side, p, v), rho, m, c);
+        double J = 0.0;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const double d = c[i] - zz[i * K1 + k];
+            J += yy[i * K1 + k] * d + 0.5 * rho * d * d;
+        }
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) {
+            if (!qon[j]) continue;
+            const double e = hvp::l1_dot<N>(qg[j], y) + hc(j, c) + qe0[j];
+            J += qw[j] * (qal[j] > 0.0 ? fabs(e) : fmax(e, 0.0));
+        }
+        return J;
+    }
+};
+
+// Mehrotra predictor-corrector of l1_wave_solve with the copy groups (L1AdmmWave).
+template <int N>
+__device__ int l1_admm_wave_solve(L1AdmmWave<N>& A, double* y, double v0, int mh, int mp, int mg, int max_iter,
+                                  int& iters, double* red, int lane, double ylo, double yhi) {
+    constexpr int NPS = L1Wave<N>::NPS, NHS = L1Wave<N>::NHS, NQ = L1AdmmWave<N>::NQ;
+    L1Wave<N>& W = A.W;
+    const int mtot = mh + 2 * mp + 2 * mg;
+#pragma unroll
+    for (int i = 0; i < N; ++i) y[i] = v0;
+    double hsc = 1.0, wmx = 1.0;
+#pragma unroll
+    for (int q = 0; q < NHS; ++q) {
+        if (!W.hon[q]) continue;
+        W.hs[q] = fmax(W.hh[q] - hvp::l1_dot<N>(W.hg[q], y), 1.0);
+        W.hl[q] = 1.0;
+        hsc = fmax(hsc, fabs(W.hh[q]));
+    }
+#pragma unroll
+    for (int q = 0; q < NPS; ++q) {
+        if (!W.pon[q]) continue;
+        const double e = hvp::l1_dot<N>(W.pg[q], y) + W.pe0[q];
+        W.pt[q] = (W.pal[q] > 0.0 ? fabs(e) : fmax(e, 0.0)) + 1.0;
+        W.ps1[q] = W.pt[q] - e;
+        W.ps2[q] = W.pt[q] + W.pal[q] * e;
+        W.pl1[q] = 0.5 * W.pw[q];
+        W.pl2[q] = 0.5 * W.pw[q];
+        wmx = fmax(wmx, W.pw[q]);
+        hsc = fmax(hsc, fabs(W.pe0[q]));
+    }
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) {
+        if (!A.qon[j]) continue;
+        const double e = hvp::l1_dot<N>(A.qg[j], y) + A.hc(j, A.c) + A.qe0[j];
+        A.qt[j] = (A.qal[j] > 0.0 ? fabs(e) : fmax(e, 0.0)) + 1.0;
+        A.qs1[j] = A.qt[j] - e;
+        A.qs2[j] = A.qt[j] + A.qal[j] * e;
+        A.ql1[j] = 0.5 * A.qw[j];
+        A.ql2[j] = 0.5 * A.qw[j];
+        wmx = fmax(wmx, A.qw[j]);
+        hsc = fmax(hsc, fabs(A.qe0[j]));
+    }
+    if (A.gon) wmx = fmax(wmx, fmax(fabs(A.q[0]), fabs(A.q[1])));
+    hsc = wave_max(hsc);
+    wmx = wave_max(wmx);
+    for (iters = 0; iters < max_iter; ++iters) {
+        double acc[kL1Red<N>];
+#pragma unroll
+        for (int i = 0; i < kL1Red<N>; ++i) acc[i] = 0.0;
+        double* rdy = acc + 2;
+        double* rhs = acc + 2 + N;
+        double* K = acc + 2 + 2 * N;
+        double rpm = 0.0, rdm = 0.0;
+        A.contrib(y, false, 0.0, true, K, rhs, acc[0], acc[1], rdy, rpm, rdm);
+        wave_sum_lds<kL1Red<N>>(acc, red, lane);
+        const double gap = acc[0], obj = acc[1];
+        rpm = wave_max(rpm);
+        rdm = wave_max(rdm);
+#pragma unroll
+        for (int i = 0; i < N; ++i) rdm = fmax(rdm, fabs(rdy[i]));
+        if (rpm <= 1e-10 * hsc && rdm <= 1e-10 * wmx && gap <= 1e-12 * fmax(1.0, fabs(obj))) return hvp::L1_OK;
+        const double mu = gap / mtot;
+        hvp::cholesky_l1<N>(K);
+        double dy[N];
+        hvp::chol_solve<N>(K, rhs, dy);
+        double ap = 1.0, ad = 1.0;
+        A.directions(y, dy, false, 0.0, ap, ad);
+        ap = wave_min(fmin(ap, ad));
+        ad = ap;
+        double gaff = 0.0;
+#pragma unroll
+        for (int q = 0; q < NHS; ++q)
+            if (W.hon[q]) gaff += (W.hs[q] + ap * W.hds[q]) * (W.hl[q] + ad * W.hdl[q]);
+#pragma unroll
+        for (int q = 0; q < NPS; ++q)
+            if (W.pon[q])
+                gaff += (W.ps1[q] + ap * W.pds1[q]) * (W.pl1[q] + ad * W.pdl1[q]) +
+                        (W.ps2[q] + ap * W.pds2[q]) * (W.pl2[q] + ad * W.pdl2[q]);
+#pragma unroll
+        for (int j = 0; j < NQ; ++j)
+            if (A.qon[j])
+                gaff += (A.qs1[j] + ap * A.qds1[j]) * (A.ql1[j] + ad * A.qdl1[j]) +
+                        (A.qs2[j] + ap * A.qds2[j]) * (A.ql2[j] + ad * A.qdl2[j]);
+        gaff = wave_sum(gaff);
+        const double ratio = gaff / gap;
+        const double sigmu = ratio * ratio * ratio * mu;
+        for (int pass = 0; pass < 2; ++pass) {
+            const bool corr = pass == 0;
+            const double sm = corr ? sigmu : hvp::kL1Centre * mu;
+            double rhs2[N], dum[N];
+#pragma unroll
+            for (int i = 0; i < N; ++i) rhs2[i] = dum[i] = 0.0;
+            double g2 = 0.0, o2 = 0.0, r2 = 0.0, d2 = 0.0;
+            A.contrib(y, corr, sm, false, K, rhs2, g2, o2, dum, r2, d2);
+            wave_sum_lds<N>(rhs2, red, lane);
+            hvp::chol_solve<N>(K, rhs2, dy);
+            ap = 1.0 / 0.995;
+            ad = 1.0 / 0.995;
+            A.directions(y, dy, corr, sm, ap, ad);
+            ap = wave_min(fmin(ap, ad));
+            ad = ap;
+            if (ap >= hvp::kL1Short) break;
+        }
+        ap *= 0.995;
+        ad *= 0.995;
+#pragma unroll
+        for (int a = 0; a < N; ++a) y[a] += ap * dy[a];
+        A.c[0] += ap * A.dc[0];
+        A.c[1] += ap * A.dc[1];
+#pragma unroll
+        for (int q = 0; q < NHS; ++q) {
+            if (!W.hon[q]) continue;
+            W.hs[q] += ap * W.hds[q];
+            W.hl[q] += ad * W.hdl[q];
+        }
+#pragma unroll
+        for (int q = 0; q < NPS; ++q) {
+            if (!W.pon[q]) continue;
+            W.pt[q] += ap * W.pdt[q];
+            W.ps1[q] += ap * W.pds1[q];
+            W.ps2[q] += ap * W.pds2[q];
+            W.pl1[q] += ad * W.pdl1[q];
+            W.pl2[q] += ad * W.pdl2[q];
+        }
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) {
+            if (!A.qon[j]) continue;
+            A.qt[j] += ap * A.qdt[j];
+            A.qs1[j] += ap * A.qds1[j];
+            A.qs2[j] += ap * A.qds2[j];
+            A.ql1[j] += ad * A.qdl1[j];
+            A.ql2[j] += ad * A.qdl2[j];
+        }
+    }
+    return l1_wave_cert<N>(W, red, lane, ylo, yhi);
+}
+
+// one (node) LP of the naive-ADMM min_1_norm form, as l1_node_lp; xf_o / xb_o (optional, the
+// instance's (2, N+1) rows): the optimal copies, written by the lanes that own them
+template <int N>
+__device__ int l1_admm_node_lp(const hvp_system& S, const hvp::Consts& C, int rl, const double* prm, uint64_t code,
+                               int K, double rlo, double rhi, double* y, double& cost, int& iters, double* red, int lane,
+                               double* xf_o = nullptr, double* xb_o = nullptr) {
+    if (hvp::l1_infeasible<N>(S, C, prm, code, K, rlo, rhi)) {  // the hard rows do not involve the copies
+        iters = 0;
+        cost = 0.0;
+#pragma unroll
+        for (int i = 0; i < N; ++i) y[i] = prm[1];
+        return hvp::L1_INFEASIBLE;
+    }
+    L1AdmmWave<N> A;
+    int mh = 0, mp = 0, mg = 0;
+    A.load(S, C, rl, prm, code, K, rlo, rhi, lane, mh, mp, mg);
+    const int st = l1_admm_wave_solve<N>(A, y, prm[1], mh, mp, mg, C.max_iter, iters, red, lane, S.vmin, S.vmax);
+    cost = 0.0;
+    if (st == hvp::L1_OK) {
+        const double own = hvp::l1_direct_cost<N>(y, S, C, rl & HVP_ROLE_TRACK_LEADER, prm, code, K, rlo, rhi, 8);
+        cost = own + wave_sum(A.group_cost(y, S, C, rl, prm, lane));
+    }
+    constexpr int K1 = N + 1;
+    if (lane < 2 * K1) {
+        double* o = lane < K1 ? xf_o : xb_o;
+        const int k = lane % K1;
+        if (o) {
+            o[k] = st == hvp::L1_OK && A.gon ? A.c[0] : 0.0;
+            o[K1 + k] = st == hvp::L1_OK && A.gon ? A.c[1] : 0.0;
+        }
+    }
     return st;
 }
 
@@ -1057,8 +1505,13 @@ __global__ __launch_bounds__(kBnbBlock<N>) HVP_LANE_OCC void k_bnb_root(int B, c
 }
 
 // ---- long horizons: one QP per 16-lane group (hvp_coop.h), 4 groups per 64-lane block
+// (HVP_COOP_MIN_N: the shortest horizon on the 16-lane path; an A/B build with -DHVP_COOP_MIN_N=5
+// runs configs[1] there)
+#ifndef HVP_COOP_MIN_N
+#define HVP_COOP_MIN_N (HVP_MAX_N_ENUM + 1)
+#endif
 template <int N>
-constexpr bool kCoop = N > HVP_MAX_N_ENUM;
+constexpr bool kCoop = N >= HVP_COOP_MIN_N;
 constexpr int kCoopBlock = 64;
 // waves per SIMD of the 16-lane group kernels (A/B builds: -DHVP_COOP_WAVES=2 caps them at 256 VGPRs)
 #ifdef HVP_COOP_WAVES
@@ -1343,11 +1796,23 @@ __global__ __launch_bounds__(kBnbBlock<N>) HVP_LANE_OCC void k_bnb_bound(int k, 
 // drops its leaf; an unresolved LP prunes nothing (bound -inf) and, at a leaf still in contention,
 // makes the instance HVP_MAXITER (k_bnb_key).  Children: k_bnb_expand per level.
 // 2 waves per SIMD up to N = 8 (the wave solver fits 256 registers; at 1 wave the LP rate halves)
+// (the naive-ADMM form's copy groups need the registers of one wave per SIMD)
 template <int N>
 constexpr int kL1Waves = N <= HVP_MAX_N_ENUM ? 2 : 1;
+template <int N, bool ADMM>
+constexpr int kL1WavesOf = ADMM ? 1 : kL1Waves<N>;
 
-template <int N>
-__global__ __launch_bounds__(kL1BlockOf<N>) __attribute__((amdgpu_waves_per_eu(kL1Waves<N>))) void k_l1_root(int B, const hvp_system* __restrict__ systems,
+// the node LP of either form (ADMM: the naive-ADMM min_1_norm local problem, l1_admm_node_lp)
+template <int N, bool ADMM>
+__device__ inline int l1_any_node_lp(const hvp_system& S, const hvp::Consts& C, int rl, const double* prm,
+                                     uint64_t code, int K, double rlo, double rhi, double* y, double& cost, int& iters,
+                                     double* red, int lane) {
+    if constexpr (ADMM) return l1_admm_node_lp<N>(S, C, rl, prm, code, K, rlo, rhi, y, cost, iters, red, lane);
+    else return l1_node_lp<N>(S, C, rl, prm, code, K, rlo, rhi, y, cost, iters, red, lane);
+}
+
+template <int N, bool ADMM>
+__global__ __launch_bounds__(kL1BlockOf<N>) __attribute__((amdgpu_waves_per_eu(kL1WavesOf<N, ADMM>))) void k_l1_root(int B, const hvp_system* __restrict__ systems,
                                                            const int32_t* __restrict__ sys,
                                                            const int32_t* __restrict__ role,
                                                            const double* __restrict__ params, hvp::Consts C,
@@ -1375,7 +1840,7 @@ __global__ __launch_bounds__(kL1BlockOf<N>) __attribute__((amdgpu_waves_per_eu(k
         while (job < 3) {
             double y[N], c = 0.0;
             int it = 0;
-            const int st = l1_node_lp<N>(S, C, rl, prm, code, K, rlo, rhi, y, c, it, red, lane);
+            const int st = l1_any_node_lp<N, ADMM>(S, C, rl, prm, code, K, rlo, rhi, y, c, it, red, lane);
             ++nodes;
             iters += it;
             int next = 3;
@@ -1418,8 +1883,8 @@ __global__ __launch_bounds__(kL1BlockOf<N>) __attribute__((amdgpu_waves_per_eu(k
     }
 }
 
-template <int N>
-__global__ __launch_bounds__(kL1BlockOf<N>) __attribute__((amdgpu_waves_per_eu(kL1Waves<N>))) void k_l1_bound(int k, const hvp_system* __restrict__ systems,
+template <int N, bool ADMM>
+__global__ __launch_bounds__(kL1BlockOf<N>) __attribute__((amdgpu_waves_per_eu(kL1WavesOf<N, ADMM>))) void k_l1_bound(int k, const hvp_system* __restrict__ systems,
                                                             const int32_t* __restrict__ sys,
                                                             const int32_t* __restrict__ role,
                                                             const double* __restrict__ params, hvp::Consts C,
@@ -1445,8 +1910,8 @@ __global__ __launch_bounds__(kL1BlockOf<N>) __attribute__((amdgpu_waves_per_eu(k
         const double* prm = params + (size_t)inst * C.stride;
         double y[N], c = 0.0;
         int it = 0;
-        const int st = l1_node_lp<N>(S, C, role[inst], prm, ws.nd_code[dst][t], k, ws.nd_lo[dst][t],
-                                     ws.nd_hi[dst][t], y, c, it, red, lane);
+        const int st = l1_any_node_lp<N, ADMM>(S, C, role[inst], prm, ws.nd_code[dst][t], k, ws.nd_lo[dst][t],
+                                               ws.nd_hi[dst][t], y, c, it, red, lane);
         iter_sum += (unsigned long long)it;
         if (lane != 0) continue;
         atomicAdd(&ws.nodes[inst], 1);
@@ -1465,6 +1930,37 @@ __global__ __launch_bounds__(kL1BlockOf<N>) __attribute__((amdgpu_waves_per_eu(k
         }
     }
     if (lane == 0 && iter_sum) atomicAdd(&ws.counter[1], iter_sum);
+}
+
+// The optimal copies (mpc.x_front.X / x_back.X, fleet_naive_admm.py:413-446) of the naive-ADMM
+// min_1_norm winners: one wave per instance re-solves the winning sequence's LP (the same LP as its
+// leaf, the same iterate) and the lanes that own the copy groups write them.  After k_bnb_finish
+// (which zeroes the copies of instances without an optimal answer).
+template <int N>
+__global__ __launch_bounds__(kL1BlockOf<N>) __attribute__((amdgpu_waves_per_eu(1))) void k_l1_admm_write(int B, const hvp_system* __restrict__ systems,
+                                                                 const int32_t* __restrict__ sys,
+                                                                 const int32_t* __restrict__ role,
+                                                                 const double* __restrict__ params, hvp::Consts C,
+                                                                 Workspace ws, double* __restrict__ xf_out,
+                                                                 double* __restrict__ xb_out) {
+    __shared__ double s_red[kL1BlockOf<N> / 64][kRedRows<kL1Red<N>> * 65];
+    double* red = s_red[threadIdx.x >> 6];
+    const int lane = threadIdx.x & 63;
+    const long long nwaves = ((long long)gridDim.x * blockDim.x) >> 6;
+    for (long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6; i < B; i += nwaves) {
+        const unsigned long long key = ws.key[i];
+        const int flag = ws.inst_flag[i];
+        if (key == ~0ull || (flag & 7)) continue;  // not HVP_OPTIMAL (k_bnb_finish)
+        uint64_t code = 0;
+#pragma unroll
+        for (int k = 0; k < N; ++k)
+            code = hvp::code_with(code, k, (int)((key >> (hvp::kCodeBits * (N - 1 - k))) & ((1u << hvp::kCodeBits) - 1)));
+        double y[N], c = 0.0;
+        int it = 0;
+        const size_t o = (size_t)i * 2 * (N + 1);
+        l1_admm_node_lp<N>(systems[sys[i]], C, role[i], params + (size_t)i * C.stride, code, N, 0.0, -1.0, y, c, it,
+                           red, lane, xf_out ? xf_out + o : nullptr, xb_out ? xb_out + o : nullptr);
+    }
 }
 
 // ---- min_1_norm by the per-lane simplex (hvp_lp.h), N <= 8: one node LP per LANE (64 per wave)
@@ -1734,6 +2230,8 @@ __global__ __launch_bounds__(kBlock) void k_inst_prep(int B, const hvp_system* _
         o[NT + N + j] = hf[j];
         o[NT + 2 * N - 1 + j] = hb[j];
     }
+#pragma unroll
+    for (int j = kIqFields<N>; j < kIqStride<N>; ++j) o[j] = 0.0;  // whole lines: no partial-line write-back
 }
 
 // The greedy dive of every instance whose root QP (level 0, solved by the refill kernel) succeeded:
@@ -2548,15 +3046,14 @@ __device__ inline void write_copies(int i, const hvp_system& S, const hvp::Const
     }
 }
 
+// The winning leaf of every instance (its lexicographic key equals the instance's key, k_bnb_key):
+// only its slot is recorded here (4 bytes, scattered in leaf order); k_bnb_finish writes the
+// outputs in instance order, so every output line is written whole by one wave.  (Writing u, x,
+// regions, gears and cost here, in leaf order, scattered 150 B per instance over lines that other
+// waves -- on other XCDs -- complete: 116 MB of HBM writes per C2 solve for ~25 MB of outputs,
+// profiles/r05zc.)
 template <int N>
-__global__ __launch_bounds__(kBlock) void k_bnb_write(const hvp_system* __restrict__ systems,
-                                                      const int32_t* __restrict__ sys,
-                                                      const int32_t* __restrict__ role,
-                                                      const double* __restrict__ params, hvp::Consts C, Workspace ws,
-                                                      double* __restrict__ u_out, double* __restrict__ x_out,
-                                                      int8_t* __restrict__ region_out, int8_t* __restrict__ gear_out,
-                                                      double* __restrict__ cost_out, double* __restrict__ xf_out,
-                                                      double* __restrict__ xb_out) {
+__global__ __launch_bounds__(kBlock) void k_bnb_write(Workspace ws) {
     const int src = N & 1;
     const LevelList lvl = level_list(ws, N);
 #pragma unroll
@@ -2567,16 +3064,8 @@ __global__ __launch_bounds__(kBlock) void k_bnb_write(const hvp_system* __restri
         if (ws.leaf_stat[t] != 0) continue;
         const int inst = ws.nd_inst[src][t];
         if (inst < 0) continue;
-        const uint64_t code = ws.nd_code[src][t];
-        if (hvp::bnb_lexkey(code, N) != ws.key[inst]) continue;
-        const hvp_system& S = systems[sys[inst]];
-        double y[N];
-#pragma unroll
-        for (int j = 0; j < N; ++j) y[j] = ws.task_y[t * N + j];
-        const double* prm = params + (size_t)inst * C.stride;
-        write_solution<N>(inst, S, prm, true, code, y, u_out, x_out, region_out, gear_out);
-        if (C.form == HVP_FORM_ADMM) write_copies<N>(inst, S, C, role[inst], prm, true, y, xf_out, xb_out);
-        if (cost_out) cost_out[inst] = ws.nd_lb[src][t];
+        if (hvp::bnb_lexkey(ws.nd_code[src][t], N) != ws.key[inst]) continue;
+        ws.win[inst] = (int32_t)t;
     }
 }
 
@@ -2612,12 +3101,25 @@ __global__ __launch_bounds__(kBlock) void k_bnb_finish(int B, const hvp_system* 
         const size_t nr = (size_t)ws.ndepth * ws.nslots;
         for (size_t r = 0; r < nr; ++r) recs[(size_t)i * nr + r].valid = 0;
     }
+    const double* prm = params + (size_t)i * C.stride;
+    const hvp_system& S = systems[sys[i]];
     if (!win || status != HVP_OPTIMAL) {
         if (cost_out) cost_out[i] = 1e300;
-        const double* prm = params + (size_t)i * C.stride;
-        write_solution<N>(i, systems[sys[i]], prm, false, 0, nullptr, u_out, x_out, region_out, gear_out);
-        if (C.form == HVP_FORM_ADMM) write_copies<N>(i, systems[sys[i]], C, role[i], prm, false, nullptr, xf_out, xb_out);
+        write_solution<N>(i, S, prm, false, 0, nullptr, u_out, x_out, region_out, gear_out);
+        if (C.form == HVP_FORM_ADMM) write_copies<N>(i, S, C, role[i], prm, false, nullptr, xf_out, xb_out);
+        return;
     }
+    // the winner recorded by k_bnb_write
+    const int src = N & 1;
+    const long long t = ws.win[i];
+    const uint64_t code = ws.nd_code[src][t];
+    double y[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) y[j] = ws.task_y[t * N + j];
+    write_solution<N>(i, S, prm, true, code, y, u_out, x_out, region_out, gear_out);
+    // (the min_1_norm copies come from the winner's LP: k_l1_admm_write)
+    if (C.form == HVP_FORM_ADMM && !C.l1) write_copies<N>(i, S, C, role[i], prm, true, y, xf_out, xb_out);
+    if (cost_out) cost_out[i] = ws.nd_lb[src][t];
 }
 
 // ================================================================== fixed-control evaluation
@@ -3081,7 +3583,8 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
     const int g_l1 = std::max(1, h->n_cu) * (N <= HVP_MAX_N_ENUM ? 8 : 16);  // waves grid-stride over nodes
     // min_1_norm: the per-lane simplex up to N = 8 (HVP_L1_SIMPLEX=0: the wave interior point, A/B)
     const char* lsx = std::getenv("HVP_L1_SIMPLEX");
-    const bool lp_lane = h->C.l1 && !kCoop<N> && !(lsx && lsx[0] == '0');
+    const bool lp_lane = h->C.l1 && h->C.form == HVP_FORM_DECENT && !kCoop<N> && !(lsx && lsx[0] == '0');
+    const bool l1_admm = h->C.l1 && h->C.form == HVP_FORM_ADMM;  // copies in the wave interior point
     const size_t lds_lp = sizeof(double) * hvp::LF_COUNT * N * BS;
     // the node LPs through persistent waves (k_lp_bound_refill, one 256-lane block per CU: the
     // simplex kernels run one wave per SIMD), refilled when this many lanes are free
@@ -3129,8 +3632,12 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
             }
         }
     } else if (h->C.l1) {
-        hipLaunchKernelGGL(k_l1_root<N>, dim3(g_l1), dim3(kL1BlockOf<N>), 0, st, B, h->d_sys, sys, role, params, h->C,
-                           ws);
+        if (l1_admm)
+            hipLaunchKernelGGL((k_l1_root<N, true>), dim3(g_l1), dim3(kL1BlockOf<N>), 0, st, B, h->d_sys, sys, role, params,
+                               h->C, ws);
+        else
+            hipLaunchKernelGGL((k_l1_root<N, false>), dim3(g_l1), dim3(kL1BlockOf<N>), 0, st, B, h->d_sys, sys, role,
+                               params, h->C, ws);
     } else if constexpr (kCoop<N>) {
         hipLaunchKernelGGL(k_bnb_root_coop<N>, dim3((B + kCoopGroups - 1) / kCoopGroups), dim3(kCoopBlock), 0, st, B,
                            h->d_sys, sys, role, params, h->C, ws);
@@ -3190,10 +3697,16 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
                                        h->C, ws);
             }
         } else if (h->C.l1) {
-            hipLaunchKernelGGL(k_l1_bound<N>, dim3(g_l1), dim3(kL1BlockOf<N>), 0, st, k, h->d_sys, sys, role, params,
-                               h->C, ws);
+            if (l1_admm)
+                hipLaunchKernelGGL((k_l1_bound<N, true>), dim3(g_l1), dim3(kL1BlockOf<N>), 0, st, k, h->d_sys, sys, role,
+                                   params, h->C, ws);
+            else
+                hipLaunchKernelGGL((k_l1_bound<N, false>), dim3(g_l1), dim3(kL1BlockOf<N>), 0, st, k, h->d_sys, sys, role,
+                                   params, h->C, ws);
         } else if constexpr (kCoop<N>) {
             if (ws.norder) {
+                // its counters live in rows 2M and 5M of ws.lvl, bucket 1's count row (hvp_internal.h)
+                if (ws.split != 1) return fail(HVP_E_ARG, "k_node_order needs one bucket per level list");
                 hipLaunchKernelGGL(k_node_order<N>, dim3(g_small), dim3(kBlock), 0, st, k, ws);
                 HIP_TRY(hipGetLastError());
             }
@@ -3231,13 +3744,17 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
     }
     hipLaunchKernelGGL(k_bnb_key<N>, dim3(g_small), dim3(kBlock), 0, st, ws, h->C.form, h->C.l1);
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_bnb_write<N>, dim3(g_small), dim3(kBlock), 0, st, h->d_sys, sys, role, params, h->C, ws,
-                       u_out, x_out, region_out, gear_out, cost_out, xf_out, xb_out);
+    hipLaunchKernelGGL(k_bnb_write<N>, dim3(g_small), dim3(kBlock), 0, st, ws);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_bnb_finish<N>, dim3(grid_for(B)), dim3(kBlock), 0, st, B, h->d_sys, sys, role, params, h->C,
                        ws, u_out, x_out, region_out, gear_out, cost_out, status_out, nodes_out, iters_out, xf_out,
                        xb_out);
     HIP_TRY(hipGetLastError());
+    if (l1_admm && (xf_out || xb_out)) {
+        hipLaunchKernelGGL(k_l1_admm_write<N>, dim3(std::max(1, std::min((B + 1) / 2, h->n_cu * 4))),
+                           dim3(kL1BlockOf<N>), 0, st, B, h->d_sys, sys, role, params, h->C, ws, xf_out, xb_out);
+        HIP_TRY(hipGetLastError());
+    }
     HIP_TRY(hipEventRecord(h->ev1, st));
     h->last_stream = st;
     h->last_B = B;

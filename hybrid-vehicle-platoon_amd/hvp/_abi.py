@@ -12,7 +12,7 @@ import os
 MAX_REGIONS = 16
 MAX_N = 16
 MAX_N_ENUM = 8
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 METHOD_AUTO, METHOD_ENUMERATE, METHOD_BNB = 0, 1, 2
 FORM_DECENT, FORM_ADMM, FORM_GADMM, FORM_CENT = 0, 1, 2, 3

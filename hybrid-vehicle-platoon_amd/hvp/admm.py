@@ -67,8 +67,10 @@ class LocalMpcADMM:
                  quadratic_cost: bool = True, is_front: bool = False, is_leader: bool = False,
                  is_trailer: bool = False, thread_limit: int | None = None, accel_cnstr_tightening: float = 0.0,
                  gears=None) -> None:
-        if not quadratic_cost:
-            raise NotImplementedError("the GPU path implements the quadratic cost (min_2_norm) only")
+        # quadratic_cost=False (min_1_norm, :74-77): L1 tracking / input terms next to the quadratic
+        # ADMM terms of the copies, solved by the device's wave interior point with the copies as
+        # variables (csrc/hvp_lane.h L1AdmmWave)
+        self.quadratic_cost = quadratic_cost
         self.N = N
         self.rho = rho
         self.system = pwa_system

@@ -77,7 +77,11 @@ typedef struct hvp_problem {
                                the exhaustive joint search).  Every LP ends solved, proven
                                infeasible (excluded), or unresolved -- which makes its instance /
                                platoon HVP_MAXITER while it is still in contention.
-                               HVP_FORM_ADMM, HVP_FORM_GADMM: HVP_E_UNSUPPORTED */
+                               HVP_FORM_ADMM (LocalMpcADMM(quadratic_cost=False),
+                               fleet_naive_admm.py:74-77): L1 terms next to the quadratic ADMM
+                               terms of the copies -- the node QPs by the wave interior point with
+                               the copies as variables (csrc/hvp_lane.h L1AdmmWave), branch and
+                               bound.  HVP_FORM_GADMM: HVP_E_UNSUPPORTED */
     double Qx[4];           /* 2x2 row-major state-tracking weight                     */
     double Qu;              /* control weight                                          */
     double Qdu;             /* control-variation weight                                */

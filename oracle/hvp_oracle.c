@@ -725,6 +725,97 @@ static or_result ipm_solve(const or_qp* qp, or_work* w, int maxit) {
     return res;
 }
 
+/* Exact copies of the min_1_norm naive-ADMM local problem for a given own trajectory (TEST
+ * INFRASTRUCTURE restatement).  Each (side, step) copy c = (c_p, c_v) minimises
+ *   rho/2 |c - m|^2 + sum_j phi_j(a_j . c + b_j),  m = z - y/rho  (y'(c - z) + rho/2 |c - z|^2, :172-198),
+ * phi_j(e) = wp_j max(e, 0) + wn_j max(-e, 0): the L1 tracking terms Q_ii |e_i| of the copy
+ * (:110-133) and the soft safe row w max(0, .) on its position (:205-236).  The interior point's copy
+ * stops ~1e-9 away from a kink of the w = 1e4 safe row, which moves the priced objective by ~1e-5;
+ * the exact minimiser is one of the stationary points of the 3^3 kink patterns (each term strictly
+ * positive, strictly negative or at its kink), so every pattern's point is evaluated and the best
+ * kept.  Used for the objective and the returned copies of the L1 form only. */
+static double prox_obj(double rho, const double* m, int nt, const double (*a)[2], const double* b, const double* wp,
+                       const double* wn, const double* c) {
+    double f = 0.5 * rho * ((c[0] - m[0]) * (c[0] - m[0]) + (c[1] - m[1]) * (c[1] - m[1]));
+    for (int j = 0; j < nt; ++j) {
+        double e = a[j][0] * c[0] + a[j][1] * c[1] + b[j];
+        f += e > 0.0 ? wp[j] * e : -wn[j] * e;
+    }
+    return f;
+}
+
+static void copy_prox(double rho, const double* m, int nt, const double (*a)[2], const double* b, const double* wp,
+                      const double* wn, double* c) {
+    int npat = 1;
+    for (int j = 0; j < nt; ++j) npat *= 3;
+    double best = INFINITY;
+    c[0] = m[0]; c[1] = m[1];
+    for (int pat = 0; pat < npat; ++pat) {
+        int st[3], zs[3], nz = 0, q = pat;
+        double g[2] = {0.0, 0.0};
+        for (int j = 0; j < nt; ++j) {
+            st[j] = q % 3; q /= 3; /* 0: at the kink, 1: e > 0, 2: e < 0 */
+            if (st[j] == 0) zs[nz++] = j;
+            else { double s = st[j] == 1 ? wp[j] : -wn[j]; g[0] += s * a[j][0]; g[1] += s * a[j][1]; }
+        }
+        if (nz > 2) continue;
+        double c0[2] = {m[0] - g[0] / rho, m[1] - g[1] / rho}, cc[2] = {c0[0], c0[1]};
+        if (nz == 1) {
+            const double* aj = a[zs[0]];
+            double aa = aj[0] * aj[0] + aj[1] * aj[1];
+            if (!(aa > 0.0)) continue;
+            double lam = rho * (aj[0] * c0[0] + aj[1] * c0[1] + b[zs[0]]) / aa;
+            cc[0] = c0[0] - aj[0] * lam / rho; cc[1] = c0[1] - aj[1] * lam / rho;
+        } else if (nz == 2) {
+            const double *aj = a[zs[0]], *ak = a[zs[1]];
+            double A00 = aj[0] * aj[0] + aj[1] * aj[1], A01 = aj[0] * ak[0] + aj[1] * ak[1];
+            double A11 = ak[0] * ak[0] + ak[1] * ak[1], det = A00 * A11 - A01 * A01;
+            if (!(fabs(det) > 1e-12 * (A00 * A11 + 1e-300))) continue;
+            double r0 = rho * (aj[0] * c0[0] + aj[1] * c0[1] + b[zs[0]]), r1 = rho * (ak[0] * c0[0] + ak[1] * c0[1] + b[zs[1]]);
+            double l0 = (A11 * r0 - A01 * r1) / det, l1 = (A00 * r1 - A01 * r0) / det;
+            cc[0] = c0[0] - (aj[0] * l0 + ak[0] * l1) / rho; cc[1] = c0[1] - (aj[1] * l0 + ak[1] * l1) / rho;
+        }
+        double f = prox_obj(rho, m, nt, a, b, wp, wn, cc);
+        if (f < best) { best = f; c[0] = cc[0]; c[1] = cc[1]; }
+    }
+}
+
+/* overwrite the copies of the solution z (layout of build_qp_k) by their exact minimisers given
+ * the own trajectory in z (naive ADMM, min_1_norm) */
+static void admm_l1_exact_copies(const or_cfg* cf, const double* x0, double* z) {
+    const int N = cf->N;
+    int idx = 3 * N + ((cf->role & R_SF) ? N + 1 : 0) + ((cf->role & R_SB) ? N + 1 : 0);
+    const double rho = cf->rho;
+    for (int side = 0; side < 2; ++side) {
+        if (!(cf->role & (side == 0 ? R_SF : R_SB))) continue;
+        const int tr = (cf->role & (side == 0 ? R_TF : R_TB)) != 0;
+        const double* yy = side == 0 ? cf->yf : cf->yb;
+        const double* zz = side == 0 ? cf->zf : cf->zb;
+        for (int k = 0; k <= N; ++k) {
+            double p = k == 0 ? x0[0] : z[2 * (k - 1)], v = k == 0 ? x0[1] : z[2 * (k - 1) + 1];
+            double a[3][2], b[3], wp[3], wn[3];
+            int nt = 0;
+            if (tr) {
+                if (side == 0) { /* p + t0 v + d0 - c_p, v - c_v */
+                    a[nt][0] = -1.0; a[nt][1] = 0.0; b[nt] = p + cf->t0 * v + cf->d0; wp[nt] = wn[nt] = fabs(cf->Qx[0][0]); nt++;
+                    a[nt][0] = 0.0; a[nt][1] = -1.0; b[nt] = v; wp[nt] = wn[nt] = fabs(cf->Qx[1][1]); nt++;
+                } else { /* c_p + t0 c_v + d0 - p, c_v - v */
+                    a[nt][0] = 1.0; a[nt][1] = cf->t0; b[nt] = cf->d0 - p; wp[nt] = wn[nt] = fabs(cf->Qx[0][0]); nt++;
+                    a[nt][0] = 0.0; a[nt][1] = 1.0; b[nt] = -v; wp[nt] = wn[nt] = fabs(cf->Qx[1][1]); nt++;
+                }
+            }
+            /* w max(0, p - c_p + d_safe) (front) / w max(0, c_p + d_safe - p) (back) */
+            a[nt][0] = side == 0 ? -1.0 : 1.0; a[nt][1] = 0.0; b[nt] = side == 0 ? p + cf->d_safe : cf->d_safe - p;
+            wp[nt] = cf->w; wn[nt] = 0.0; nt++;
+            double m[2] = {par(zz, N, 0, k) - par(yy, N, 0, k) / rho, par(zz, N, 1, k) - par(yy, N, 1, k) / rho}, c[2];
+            copy_prox(rho, m, nt, (const double(*)[2])a, b, wp, wn, c);
+            z[idx + k] = c[0];
+            z[idx + N + 1 + k] = c[1];
+        }
+        idx += 2 * (N + 1);
+    }
+}
+
 /* Objective evaluated term by term on the trajectory (the form of fleet_decent_mld.py:107-169):
  * sums of squared tracking errors, control terms and w * slack with the slacks at their optimal
  * value max(0, .).  Avoids the cancellation of 1/2 z'Pz + q'z + r0 (positions ~3e3). */
@@ -1021,6 +1112,7 @@ static double bnb_qp(or_ctx* C, const int* sigma, int K, int* cert) {
     C->iters += r.iters;
     if (!r.converged) return K < C->cf->N ? -INFINITY : INFINITY; /* an unsolved bound prunes nothing */
     *cert = r.certified;
+    if (C->cf->admm && !C->cf->quadratic && !C->cf->gadmm) admm_l1_exact_copies(C->cf, C->x0, C->w->z);
     return direct_objective_k(C->cf, C->x0, C->xf, C->xb, C->xl, C->w->z, K);
 }
 
@@ -1284,6 +1376,7 @@ int oracle_solve_admm_miqp(int N, int nreg, int nsr, const double* S, const doub
         const int* ws = C.sig + (size_t)win * N;
         build_qp(qp, &md, &cf, ws, p, zero, zero, xl);
         or_result r = ipm_solve(qp, w, C.maxit);
+        if (!quadratic) admm_l1_exact_copies(&cf, p, w->z);
         best_obj = direct_objective(&cf, p, zero, zero, xl, w->z);
         best_cert = r.certified;
         for (int i = 0; i < 2; ++i) x_out[i * (N + 1)] = p[i];

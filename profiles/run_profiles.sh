@@ -31,4 +31,9 @@ echo f64 done
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU \
     SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE \
     -T -f csv -d "$OUT/occ" -o run -- "${BENCH[@]}" > "$OUT/occ.log" 2>&1
+# memory instructions and L2 write-back transaction sizes (the byte budget of DESIGN.md section 4):
+# vector memory instructions issued (incl. scratch), scalar loads, and the L2's write requests to
+# the fabric in total and as whole 64-byte transactions (the rest are 32-byte partial lines)
+timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum \
+    -T -f csv -d "$OUT/mem" -o run -- "${BENCH[@]}" > "$OUT/mem.log" 2>&1
 echo profiles done

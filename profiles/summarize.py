@@ -17,6 +17,9 @@ which bench.py looks up for its roofline):
   valu_issue_frac        SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES (share of wave lifetime issuing VALU)
   wait_frac, stall_frac  SQ_WAIT_ANY, SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES (parked on waitcnt / issue-stalled)
   waves_per_cu           mean resident waves per CU: 4 SQ_WAVE_CYCLES (quad-cycles) / (GRBM_GUI_ACTIVE / 8 XCDs) / 256 CUs
+  SQ_INSTS_VMEM_RD/_WR   vector memory instructions (scratch included) per launch, SQ_INSTS_SMEM scalar loads;
+  TCC_EA0_WRREQ_sum      L2-to-fabric write requests, TCC_EA0_WRREQ_64B_sum those that are whole 64-byte
+                         transactions (the rest 32 B: partial lines), "mem" pass (round 6)
 bench.py reads hbm_bytes of its dominant kernel from here as roofline.traffic.
 """
 
@@ -73,7 +76,7 @@ def main() -> None:
         with open(p) as f:
             extra[name] = {short(r["Name"]): {"avg_ms": float(r["AverageNs"]) / 1e6, "calls": int(r["Calls"])}
                            for r in csv.DictReader(f)}
-    for sub in ("fetch", "write", "f64", "occ"):
+    for sub in ("fetch", "write", "f64", "occ", "mem"):
         p = os.path.join(src, sub, "run_counter_collection.csv")
         if not os.path.exists(p):
             continue

@@ -114,8 +114,11 @@ def test_invalid_arguments_fail_loudly_without_touching_the_gpu():
             lib.hvp_destroy(h)
     from hvp.admm import admm_problem
 
-    l1a = admm_problem(5, 0.5, quadratic_cost=False)
-    assert lib.hvp_create(ctypes.byref(h), ctypes.byref(l1a), sysv, 1, 0) == -3
+    l1a = admm_problem(5, 0.5, quadratic_cost=False)  # naive-ADMM min_1_norm: accepted (round 6)
+    rc = lib.hvp_create(ctypes.byref(h), ctypes.byref(l1a), sysv, 1, 0)
+    assert rc in (0, -2), (rc, _abi.last_error())
+    if rc == 0:
+        lib.hvp_destroy(h)
     badq = tables.problem(5)
     badq.quadratic_cost = 2
     assert lib.hvp_create(ctypes.byref(h), ctypes.byref(badq), sysv, 1, 0) == -1
@@ -123,10 +126,11 @@ def test_invalid_arguments_fail_loudly_without_touching_the_gpu():
 
 def test_min_1_norm_acceptance_matches_integration_doc():
     """INTEGRATION.md section 1 states which problems take quadratic_cost = 0 (min_1_norm,
-    fleet_decent_mld.py:73-76, mpcs/cent_mld.py:58-61): HVP_FORM_DECENT at every N <= 16 and
-    HVP_FORM_CENT are accepted, the ADMM forms return HVP_E_UNSUPPORTED.  hvp_create validates
-    before it touches a device, so on a CPU-only host an accepted problem fails at the device
-    step (HVP_E_HIP = -2) and a rejected one with HVP_E_UNSUPPORTED (-3)."""
+    fleet_decent_mld.py:73-76, fleet_naive_admm.py:74-77, mpcs/cent_mld.py:58-61): HVP_FORM_DECENT
+    at every N <= 16, HVP_FORM_ADMM and HVP_FORM_CENT are accepted, the switching-ADMM form returns
+    HVP_E_UNSUPPORTED.  hvp_create validates before it touches a device, so on a CPU-only host an
+    accepted problem fails at the device step (HVP_E_HIP = -2) and a rejected one with
+    HVP_E_UNSUPPORTED (-3)."""
     import ctypes
 
     from hvp import _abi, tables
@@ -147,15 +151,16 @@ def test_min_1_norm_acceptance_matches_integration_doc():
         return r
 
     for p in (tables.problem(10, quadratic_cost=False), cent_problem(5, quadratic_cost=False),
-              cent_problem(5, quadratic_cost=False, exhaustive=True)):
+              cent_problem(5, quadratic_cost=False, exhaustive=True), admm_problem(10, 0.5, quadratic_cost=False),
+              admm_problem(5, 0.5, quadratic_cost=False)):
         assert rc(p) in (0, -2), _abi.last_error()
     g = gadmm_problem(10)
     g.quadratic_cost = 0
-    for p in (admm_problem(10, 0.5, quadratic_cost=False), g):
-        assert rc(p) == -3
-        assert "min_1_norm" in _abi.last_error()
+    assert rc(g) == -3
+    assert "min_1_norm" in _abi.last_error()
     doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
     assert "HVP_FORM_CENT` accepts it" in doc and "solved by enumeration with" not in doc
+    assert "`HVP_FORM_ADMM` accepts it" in doc and "`HVP_FORM_GADMM` with `quadratic_cost = 0` returns" in doc
 
 
 def test_no_device_function_clobbers_its_return_address():

@@ -88,9 +88,9 @@ def test_node_record_warm_starts_keep_the_answers_on_the_host(hostref):
     calls = []
     orig = O.solve_admm_miqp
 
-    def rec(sysd, cfg, N_, role, rho, params, maxit=200):
+    def rec(sysd, cfg, N_, role, rho, params, maxit=200, quadratic=True):
         calls.append((role, np.array(params, dtype=np.float64)))
-        return orig(sysd, cfg, N_, role, rho, params, maxit)
+        return orig(sysd, cfg, N_, role, rho, params, maxit, quadratic)
 
     O.solve_admm_miqp = rec
     try:
