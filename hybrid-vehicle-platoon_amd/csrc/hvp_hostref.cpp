@@ -71,6 +71,8 @@ int g_solver = 1;
 int g_l1_solver = 1;
 long long g_lp_runs = 0, g_lp_iters = 0, g_lp_fail = 0;
 long long g_lp_hist[64] = {};  // LPs by pivot count (the lane-utilisation model of the LP kernels)
+long long g_lp_pc[32][32] = {};  // branch-and-bound node LPs by (parent's pivots, own pivots), capped at 31
+long long g_bnb_nch[17][8] = {};  // unpruned branch-and-bound nodes by depth and number of children (7 = 7+)
 
 // one min_1_norm LP (node: K < N with the reachable interval [lo, hi] of v_K) by the selected solver
 template <int N>
@@ -313,8 +315,9 @@ void solve_one_bnb(const hvp_system& S, const hvp::Consts& C, int role, const do
         int stat;
         double y[N];
         uint64_t hs;
+        int pit;  // min_1_norm: pivots of this node's LP (g_lp_pc, the parent / child correlation)
     };
-    int nq = 0, nit = 0;
+    int nq = 0, nit = 0, last_it = 0;
     int l1_st = 0;  // status of the last min_1_norm LP (hvp_l1.h L1_*)
     const int SD = g_admm_slots;
     std::vector<uint64_t> claim;  // g_admm_warm == 4: owner code per (depth, slot) of this solve
@@ -331,6 +334,7 @@ void solve_one_bnb(const hvp_system& S, const hvp::Consts& C, int role, const do
             l1_st = l1_lp<N>(S, C, role, prm, code, K, lo, hi, yl, it);
             ++nq;
             nit += it;
+            last_it = it;
             if (l1_st != hvp::L1_OK) return false;
             c = hvp::l1_direct_cost<N>(yl, S, C, role, prm, code, K, lo, hi);
             if (y)
@@ -442,7 +446,9 @@ void solve_one_bnb(const hvp_system& S, const hvp::Consts& C, int role, const do
         root.lb = -1e300;
         root.hs = g_admm_warm == 2 && idx >= 0 && idx < 4096 ? g_admm_root_hs[idx] : hvp::kHubNone;
         double c0;
-        if (qp(0, 0, v0, v0, c0, root.y, &root.hs)) {
+        const bool root_ok = qp(0, 0, v0, v0, c0, root.y, &root.hs);
+        root.pit = last_it;
+        if (root_ok) {
             root.lb = c0;
             if (g_admm_warm == 2 && idx >= 0 && idx < 4096) g_admm_root_hs[idx] = root.hs;
             uint64_t code;
@@ -468,12 +474,20 @@ void solve_one_bnb(const hvp_system& S, const hvp::Consts& C, int role, const do
         nxt.clear();
         for (const Node& p : lvl) {
             if (hvp::bnb_pruned(p.lb, inc)) continue;
+            int nch = 0;
+            for (int r = 0; r < S.n_regions; ++r) {
+                double a, b;
+                nch += hvp::bnb_child(S, C, k - 1, p.lo, p.hi, r, &a, &b) ? 1 : 0;
+            }
+#pragma omp atomic
+            g_bnb_nch[k - 1][nch < 7 ? nch : 7] += 1;
             for (int r = 0; r < S.n_regions; ++r) {
                 Node c;
                 if (!hvp::bnb_child(S, C, k - 1, p.lo, p.hi, r, &c.lo, &c.hi)) continue;
                 c.code = hvp::code_with(p.code, k - 1, r);
                 c.lb = p.lb;
                 c.hs = p.hs;
+                c.pit = p.pit;
                 nxt.push_back(c);
             }
         }
@@ -488,6 +502,11 @@ void solve_one_bnb(const hvp_system& S, const hvp::Consts& C, int role, const do
             double lb;
             const double plb = c.lb;  // the parent's bound (min_1_norm: kept by an unresolved leaf)
             const bool good = qp(c.code, k, c.lo, c.hi, lb, c.y, &c.hs);
+            if (C.l1) {
+#pragma omp atomic
+                g_lp_pc[c.pit < 31 ? c.pit : 31][last_it < 31 ? last_it : 31] += 1;
+                c.pit = last_it;
+            }
             c.stat = good ? 0 : HVP_MAXITER;
             c.lb = good ? lb : (k < N ? -1e300 : 1e300);
             if (!good && C.l1) {
@@ -683,6 +702,16 @@ void hvp_hostref_reset_admm_warm() {
 void hvp_hostref_admm_warm_stats(long long* out) {
     for (int i = 0; i < 4; ++i) out[i] = g_admm_warm_stats[i];
     for (int i = 0; i < 4; ++i) out[4 + i] = g_admm_rec_stats[i];
+}
+// unpruned branch-and-bound nodes by depth (0..16) and children (0..7+) since the last call (17 x 8)
+void hvp_hostref_bnb_children(long long* out) {
+    for (int i = 0; i < 17; ++i)
+        for (int j = 0; j < 8; ++j) out[i * 8 + j] = g_bnb_nch[i][j], g_bnb_nch[i][j] = 0;
+}
+// the (parent pivots, child pivots) histogram of the min_1_norm node LPs since the last call (32 x 32)
+void hvp_hostref_lp_parent_child(long long* out) {
+    for (int i = 0; i < 32; ++i)
+        for (int j = 0; j < 32; ++j) out[i * 32 + j] = g_lp_pc[i][j], g_lp_pc[i][j] = 0;
 }
 void hvp_hostref_lp_hist(long long* out) {
     for (int i = 0; i < 64; ++i) out[i] = g_lp_hist[i], g_lp_hist[i] = 0;

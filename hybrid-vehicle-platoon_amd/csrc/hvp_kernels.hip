@@ -642,7 +642,9 @@ int hvp_get_stats(hvp_handle* h, hvp_stats* out) {
         for (int k = 1; k <= h->prob.N; ++k)
             for (int b = 0; b < nb; ++b)
                 n += (int64_t)std::min(b == 0 ? lv[k] : lv[(1 + b) * M + k], b + 1 < nb ? seg : cap - (nb - 1) * seg);
-        out->n_candidates = n;
+        // less the pass-through nodes (counter[6]): listed, but their parent's QP is theirs
+        // (hvp_lane.h bnb_put_children kPassFlag)
+        out->n_candidates = n - (int64_t)c[6];
         // QP time = K_bnb_root + every K_bnb_bound launch (the expand / select kernels excluded)
         float sum = 0.f;
         for (int k = 0; k <= h->prob.N; ++k) {

@@ -262,6 +262,7 @@ struct L1Wave {
     bool pon[NPS];
     double pg[NPS][N], pe0[NPS], pw[NPS], pal[NPS], pt[NPS], ps1[NPS], ps2[NPS], pl1[NPS], pl2[NPS];
     double pds1[NPS], pdl1[NPS], pds2[NPS], pdl2[NPS], pdt[NPS];
+    bool rel = false;  // primal residuals relative to the row's constant, |rp| / (1 + |h|) (L1AdmmWave)
 
     __device__ void clear() {
 #pragma unroll
@@ -330,7 +331,7 @@ struct L1Wave {
             const double rc = hs[q] * hl[q] + (corr ? hds[q] * hdl[q] : 0.0) - sigmu;
             const double rho = (hl[q] * rp - rc) / hs[q], coef = -(hl[q] + rho);
             gap += hs[q] * hl[q];
-            rpm = fmax(rpm, fabs(rp));
+            rpm = fmax(rpm, rel ? fabs(rp) / (1.0 + fabs(hh[q])) : fabs(rp));
 #pragma unroll
             for (int a = 0; a < N; ++a) {
                 rdy[a] += hl[q] * hg[q][a];
@@ -358,7 +359,7 @@ struct L1Wave {
             const double coef = -(pl1[q] - al * pl2[q]) - (rho1 - al * rho2) - m * rhst / mt;
             gap += ps1[q] * pl1[q] + ps2[q] * pl2[q];
             obj += pw[q] * pt[q];
-            rpm = fmax(rpm, fmax(fabs(rp1), fabs(rp2)));
+            rpm = fmax(rpm, fmax(fabs(rp1), fabs(rp2)) / (rel ? 1.0 + fabs(pe0[q]) : 1.0));
             rdm = fmax(rdm, fabs(rdt));
 #pragma unroll
             for (int a = 0; a < N; ++a) {
@@ -589,6 +590,7 @@ struct L1AdmmWave {
     L1Wave<N> W;
     bool gon;
     double rho, c[2], q[2], dc[2];  // the group's copies (p, v) and linear terms y - rho z
+    double k0;                      // constant of the ADMM terms: y'(c - z) + rho/2 |c - z|^2 = rho/2 c'c + q'c + k0
     bool qon[NQ];
     double qg[NQ][N], qh[NQ][2], qe0[NQ], qw[NQ], qal[NQ], qt[NQ], qs1[NQ], qs2[NQ], ql1[NQ], ql2[NQ];
     double qds1[NQ], qdl1[NQ], qds2[NQ], qdl2[NQ], qdt[NQ];
@@ -598,6 +600,7 @@ struct L1AdmmWave {
     __device__ bool load(const hvp_system& S, const hvp::Consts& C, int rl, const double* prm, uint64_t code, int K,
                          double rlo, double rhi, int lane, int& mh, int& mp, int& mg) {
         const bool ok = W.load(S, C, rl & HVP_ROLE_TRACK_LEADER, prm, code, K, rlo, rhi, lane, mh, mp, 8);
+        W.rel = true;
         constexpr int K1 = N + 1;
         const int side = lane / K1, k = lane % K1;
         gon = lane < 2 * K1 && (rl & (side == 0 ? HVP_ROLE_SAFE_FRONT : HVP_ROLE_SAFE_BACK)) != 0;
@@ -613,7 +616,7 @@ struct L1AdmmWave {
 #pragma unroll
             for (int a = 0; a < N; ++a) qg[j][a] = 0.0;
         }
-        c[0] = c[1] = q[0] = q[1] = dc[0] = dc[1] = 0.0;
+        c[0] = c[1] = q[0] = q[1] = dc[0] = dc[1] = k0 = 0.0;
         if (gon) {
             const double* yy = hvp::admm_y(prm, side, N);
             const double* zz = hvp::admm_z(prm, side, N);
@@ -621,6 +624,7 @@ struct L1AdmmWave {
             for (int i = 0; i < 2; ++i) {
                 c[i] = zz[i * K1 + k] - yy[i * K1 + k] / rho;  // the ADMM term's own minimiser
                 q[i] = yy[i * K1 + k] - rho * zz[i * K1 + k];
+                k0 += 0.5 * rho * zz[i * K1 + k] * zz[i * K1 + k] - yy[i * K1 + k] * zz[i * K1 + k];
             }
             const bool tr = (rl & (side == 0 ? HVP_ROLE_TRACK_FRONT : HVP_ROLE_TRACK_BACK)) != 0;
             const double ts = S.ts, P1 = prm[0] + ts * prm[1];
@@ -728,7 +732,7 @@ struct L1AdmmWave {
             if (acc) {
                 gap += qs1[j] * ql1[j] + qs2[j] * ql2[j];
                 obj += qw[j] * qt[j];
-                rpm = fmax(rpm, fmax(fabs(P.rp1), fabs(P.rp2)));
+                rpm = fmax(rpm, fmax(fabs(P.rp1), fabs(P.rp2)) / (1.0 + fabs(qe0[j])));
                 rdm = fmax(rdm, fabs(P.rdt));
 #pragma unroll
                 for (int a = 0; a < N; ++a) {
@@ -749,7 +753,8 @@ struct L1AdmmWave {
         i11 = a00 / det;
         if (acc) {
             rdm = fmax(rdm, fmax(fabs(rd0), fabs(rd1)));
-            obj += fabs(0.5 * rho * (c[0] * c[0] + c[1] * c[1]) + q[0] * c[0] + q[1] * c[1]);
+            // the objective itself (the ADMM terms are small near the optimum, c ~ z): the gap test's scale
+            obj += 0.5 * rho * (c[0] * c[0] + c[1] * c[1]) + q[0] * c[0] + q[1] * c[1] + k0;
             // Schur complement of the copy block: K -= A_yc A^-1 A_cy, rhs -= A_yc A^-1 rc
             const double w0 = i00 * rc0 + i01 * rc1, w1 = i01 * rc0 + i11 * rc1;
 #pragma unroll
@@ -890,6 +895,7 @@ __device__ int l1_admm_wave_solve(L1AdmmWave<N>& A, double* y, double v0, int mh
     if (A.gon) wmx = fmax(wmx, fmax(fabs(A.q[0]), fabs(A.q[1])));
     hsc = wave_max(hsc);
     wmx = wave_max(wmx);
+    double ybest[N], best_rdm = 1e300;
     for (iters = 0; iters < max_iter; ++iters) {
         double acc[kL1Red<N>];
 #pragma unroll
@@ -905,7 +911,19 @@ __device__ int l1_admm_wave_solve(L1AdmmWave<N>& A, double* y, double v0, int mh
         rdm = wave_max(rdm);
 #pragma unroll
         for (int i = 0; i < N; ++i) rdm = fmax(rdm, fabs(rdy[i]));
-        if (rpm <= 1e-10 * hsc && rdm <= 1e-10 * wmx && gap <= 1e-12 * fmax(1.0, fabs(obj))) return hvp::L1_OK;
+        // (primal residuals relative to each row's constant, W.rel; the objective's own scale)
+        if (rpm <= 1e-11 && rdm <= 1e-10 * wmx && gap <= 1e-12 * fmax(1.0, fabs(obj))) return hvp::L1_OK;
+        // Past primal convergence the dual residual of some nodes oscillates (0.2 .. 7 at wmx = 1e4
+        // for 100 iterations: admm_l1_local_ct_N5 instance 5, profiles/r06r.log) while y, the copies
+        // and the objective stay put.  The iterate with the smallest dual residual among those within
+        // a looser test is kept and returned when the strict test is never met (the copies are
+        // re-priced exactly from y, copy_exact).
+        const bool loose = rpm <= 1e-9 && rdm <= 1e-8 * wmx && gap <= 1e-10 * fmax(1.0, fabs(obj));
+        if (loose && rdm < best_rdm) {
+            best_rdm = rdm;
+#pragma unroll
+            for (int i = 0; i < N; ++i) ybest[i] = y[i];
+        }
         const double mu = gap / mtot;
         hvp::cholesky_l1<N>(K);
         double dy[N];
@@ -978,6 +996,11 @@ __device__ int l1_admm_wave_solve(L1AdmmWave<N>& A, double* y, double v0, int mh
             A.ql1[j] += ad * A.qdl1[j];
             A.ql2[j] += ad * A.qdl2[j];
         }
+    }
+    if (best_rdm < 1e300) {  // (wave-uniform: the residuals are wave reductions)
+#pragma unroll
+        for (int i = 0; i < N; ++i) y[i] = ybest[i];
+        return hvp::L1_OK;
     }
     return l1_wave_cert<N>(W, red, lane, ylo, yhi);
 }
@@ -1238,10 +1261,19 @@ __device__ inline unsigned long long node_prio(const Workspace& ws, uint64_t cod
 // The slots of a failed reservation below its segment's end are marked dead (-1), which the
 // next kernels sweep.
 // CLAIM: the 16-lane path's k_bnb_expand, the only writer whose levels can have node records
+// pass >= 0 (the decentralised lane path's fused levels, a parent whose QP succeeded, lv < N): a
+// single child whose region's band holds the parent's whole interval of v_{lv-1} has the parent's
+// QP (kPassFlag below) and is written as a pass-through node carrying `pass` (the parent's active-set
+// steps, its children's bucket).  Returns 1 when it wrote one.
+constexpr uint64_t kPassFlag = 1ull << 63;  // codes of N <= 8 steps use 32 bits
+constexpr uint64_t kPassCode = (1ull << 56) - 1;
+#ifndef HVP_REFILL_BYVAL
+#define HVP_REFILL_BYVAL 1  // (k_bnb_bound_refill's body; only the default one reads pass-through nodes)
+#endif
 template <bool CLAIM = false>
-__device__ inline void bnb_put_children(const Workspace& ws, int lv, unsigned long long off, unsigned long long limit,
+__device__ inline int bnb_put_children(const Workspace& ws, int lv, unsigned long long off, unsigned long long limit,
                                         unsigned mask, int inst, const hvp_system& S, const hvp::Consts& C,
-                                        uint64_t code, double lo, double hi, double plb) {
+                                        uint64_t code, double lo, double hi, double plb, int pass = -1) {
     const int nc = __popc(mask), d = lv & 1;
     if (off + nc > limit) {
         for (unsigned long long t = off; t < limit && t < off + nc; ++t) ws.nd_inst[d][t] = -1;
@@ -1267,23 +1299,28 @@ __device__ inline void bnb_put_children(const Workspace& ws, int lv, unsigned lo
         }
         if (!placed) {
             atomicOr(&ws.inst_flag[inst], 2);
-            return;
+            return 0;
         }
     }
-    int j = 0;
+    int j = 0, passed = 0;
     for (int r = 0; r < S.n_regions; ++r) {
         if (!((mask >> r) & 1u)) continue;
         double a, b;
         hvp::bnb_child(S, C, lv - 1, lo, hi, r, &a, &b);
-        const uint64_t cc = hvp::code_with(code, lv - 1, r);
+        uint64_t cc = hvp::code_with(code, lv - 1, r);
+        if (HVP_REFILL_BYVAL && ws.pass && pass >= 0 && nc == 1 && lo >= S.vlo[r] && hi <= S.vhi[r]) {
+            cc |= kPassFlag | ((uint64_t)(pass < 127 ? pass : 127) << 56);
+            passed = 1;
+        }
         ws.nd_inst[d][off + j] = inst;
         ws.nd_code[d][off + j] = cc;
         if (CLAIM && ws.nclaim) atomicMax(&ws.nclaim[node_index(ws, inst, lv, cc)], node_prio(ws, cc));
         ws.nd_lo[d][off + j] = a;
         ws.nd_hi[d][off + j] = b;
-        ws.nd_lb[d][off + j] = plb;  // inherited: kept by a leaf whose QP fails
+        ws.nd_lb[d][off + j] = plb;  // inherited: kept by a leaf whose QP fails (a pass-through node's bound)
         ++j;
     }
+    return passed;
 }
 
 // wave-level reservation of nc slots per lane in level lv's list (an inclusive scan, one atomic
@@ -1448,7 +1485,7 @@ __global__ __launch_bounds__(kBnbBlock<N>) HVP_LANE_OCC void k_bnb_root(int B, c
     ws.nd_hi[0][i] = v0;
     double inc = __longlong_as_double(0x7ff0000000000000ll);  // +inf: no incumbent
     double lb = -1e300;
-    int nodes = 0, iters = 0;
+    int nodes = 0, iters = 0, root_steps = 0;
     if (ok) {
         hvp::LaneQp<N, LdsMem<N, BS>> q;
         q.mem.lane = threadIdx.x;
@@ -1456,6 +1493,7 @@ __global__ __launch_bounds__(kBnbBlock<N>) HVP_LANE_OCC void k_bnb_root(int B, c
         int it = bnb_qp<N, BS, ADMM>(q, S, C, rl, prm, 0, 0, v0, v0, c0);
         ++nodes;
         iters += it >= 0 ? it : -1 - it;
+        root_steps = it;
         if (it >= 0) {
             lb = c0;
             double ystar[N];
@@ -1497,8 +1535,10 @@ __global__ __launch_bounds__(kBnbBlock<N>) HVP_LANE_OCC void k_bnb_root(int B, c
                 // the root's children all go to bucket 0 (LevelList; level 1 is the smallest level,
                 // and a bucket choice here measured 3x slower in this kernel: r03v)
                 const unsigned long long off = atomicAdd(&ws.lvl[1], (unsigned long long)__popc(mask));
-                bnb_put_children(ws, 1, off, (unsigned long long)ws.cap >> ws.split_shift, mask, i, S, C, 0, v0,
-                                 v0, lb);
+                // (a pass-through child when it has the root's QP: k_bnb_bound_refill)
+                if (bnb_put_children(ws, 1, off, (unsigned long long)ws.cap >> ws.split_shift, mask, i, S, C, 0, v0,
+                                     v0, lb, 1 < N && lb > -1e300 ? root_steps : -1))
+                    atomicAdd(&ws.counter[6], 1ull);
             }
         }
     }
@@ -2577,7 +2617,8 @@ __global__ __launch_bounds__(kBnbBlock<N>) HVP_LP_OCC void k_lp_bound_refill(int
 }
 
 // lane stages of the refill kernels
-enum { RS_IDLE = 0, RS_SCAN = 1, RS_STEP = 2, RS_FAIL = 3, RS_OPT = 4 };
+// RS_PASS: a pass-through node (bnb_put_children kPassFlag), finished without a QP
+enum { RS_IDLE = 0, RS_SCAN = 1, RS_STEP = 2, RS_FAIL = 3, RS_OPT = 4, RS_PASS = 5 };
 
 // one active-set trip of a busy lane (RS_SCAN / RS_STEP); finished lanes end in RS_FAIL / RS_OPT
 template <int N, class Q>
@@ -2632,10 +2673,10 @@ void k_bnb_bound_refill(int k, const hvp_system* __restrict__ systems, const int
     q.mem.lane = threadIdx.x;
     hvp::GiLane<N> g;
     long long t = -1;  // node of the lane
-    int inst = 0, stage = RS_IDLE, fail = 0;
+    int inst = 0, stage = RS_IDLE, fail = 0;  // (RS_PASS: fail holds the pass-through node's steps)
     uint64_t code = 0;
     bool exhausted = false;
-    unsigned long long iter_sum = 0;
+    unsigned long long iter_sum = 0, pass_n = 0;
 #ifdef HVP_REFILL_PROF  // diagnostics build: event / trip cycles and busy lane-trips per wave
     unsigned long long pf_ev = 0, pf_all = 0, pf_busy = 0, pf_trips = 0, pf_wb = 0, pf_cl = 0, pf_dc = 0, pf_rs = 0;
     const unsigned long long pf_t0 = __builtin_amdgcn_s_memtime();
@@ -2663,13 +2704,25 @@ void k_bnb_bound_refill(int k, const hvp_system* __restrict__ systems, const int
             // ---- event: write the finished lanes' results, then refill every free lane
             unsigned cmask = 0;  // children of a finished bound node (k_bnb_expand's work, fused)
             double clb = 0.0;
-            if (done) {
+            int csteps = 0;      // the finished node's active-set steps (its children's bucket)
+            if (done && stage == RS_PASS) {
+                // a pass-through node: its QP is its parent's (bound inherited in nd_lb), so only its
+                // children are written.  A tree node all the same (nodes_out, the NodeCount
+                // analogue); hvp_stats.n_candidates counts QPs and leaves it out (counter[6])
+                stage = RS_IDLE;
+                atomicAdd(&ws.nodes[inst], 1);
+                clb = ws.nd_lb[dst][t];
+                csteps = fail;
+                if (!(ws.inst_flag[inst] & 2) && !hvp::bnb_pruned(clb, inc_of(ws, inst)))
+                    cmask = bnb_children(systems[sys[inst]], C, k, ws.nd_lo[dst][t], ws.nd_hi[dst][t]);
+            } else if (done) {
                 const int st = stage == RS_OPT ? g.verify(C, nullptr) : fail;
                 const bool ok = st == hvp::GI_OK;
                 const double c = ok ? hvp::direct_cost<N>(q, systems[sys[inst]], C, role[inst],
                                                           params + (size_t)inst * C.stride, code, k)
                                     : 0.0;
                 iter_sum += (unsigned long long)g.iter;
+                csteps = ok ? g.iter : -1;
 #ifdef HVP_REFILL_PROF
                 {
                     const double cc = __builtin_amdgcn_readfirstlane(__double_as_longlong(c) & 0xffffffff);
@@ -2688,10 +2741,10 @@ void k_bnb_bound_refill(int k, const hvp_system* __restrict__ systems, const int
             if (k < N) {
                 unsigned long long limit;
                 const unsigned long long off =
-                    split_reserve(ws, k + 1, __popc(cmask), done ? g.iter : 0, lane, limit);
+                    split_reserve(ws, k + 1, __popc(cmask), csteps > 0 ? csteps : 0, lane, limit);
                 if (cmask)
-                    bnb_put_children(ws, k + 1, off, limit, cmask, inst, systems[sys[inst]], C, code,
-                                     ws.nd_lo[dst][t], ws.nd_hi[dst][t], clb);
+                    pass_n += bnb_put_children(ws, k + 1, off, limit, cmask, inst, systems[sys[inst]], C, code,
+                                               ws.nd_lo[dst][t], ws.nd_hi[dst][t], clb, k + 1 < N ? csteps : -1);
 #ifdef HVP_REFILL_PROF
                 pf_rs += __builtin_amdgcn_s_memtime() - pf_e0;
 #endif
@@ -2721,10 +2774,17 @@ void k_bnb_bound_refill(int k, const hvp_system* __restrict__ systems, const int
                     } else {
                         t = mine;
                         code = ws.nd_code[dst][mine];
-                        setup_node<N>(q, systems[sys[inst]], C, ws, inst, role[inst], params + (size_t)inst * C.stride,
-                                      code, k, ws.nd_lo[dst][mine], ws.nd_hi[dst][mine]);
-                        stage = g.init(q) == hvp::GI_OK ? RS_SCAN : RS_FAIL;
-                        fail = hvp::GI_FAIL_CHOL;
+                        if (code & kPassFlag) {  // its parent's QP: finished at the next event
+                            fail = (int)((code >> 56) & 127);
+                            code &= kPassCode;
+                            stage = RS_PASS;
+                        } else {
+                            setup_node<N>(q, systems[sys[inst]], C, ws, inst, role[inst],
+                                          params + (size_t)inst * C.stride, code, k, ws.nd_lo[dst][mine],
+                                          ws.nd_hi[dst][mine]);
+                            stage = g.init(q) == hvp::GI_OK ? RS_SCAN : RS_FAIL;
+                            fail = hvp::GI_FAIL_CHOL;
+                        }
                     }
                 }
             }
@@ -2735,8 +2795,12 @@ void k_bnb_bound_refill(int k, const hvp_system* __restrict__ systems, const int
         if (stage == RS_SCAN || stage == RS_STEP) gi_trip<N>(q, g, C, stage, fail);
     }
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) iter_sum += __shfl_down(iter_sum, off, 64);
+    for (int off = 32; off > 0; off >>= 1) {
+        iter_sum += __shfl_down(iter_sum, off, 64);
+        pass_n += __shfl_down(pass_n, off, 64);
+    }
     if (lane == 0 && iter_sum) atomicAdd(&ws.counter[1], iter_sum);
+    if (lane == 0 && pass_n) atomicAdd(&ws.counter[6], pass_n);  // pass-through nodes (no QP; hvp_get_stats)
 #ifdef HVP_REFILL_PROF
     pf_all = __builtin_amdgcn_s_memtime() - pf_t0;
     if (lane == 0) {  // the claim slots of levels > N are free (prof builds need N <= 8)
@@ -3548,6 +3612,8 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
     ws.split = fused ? (want >= 4 ? 4 : (want >= 2 ? 2 : 1)) : 1;
     ws.split_shift = ws.split == 4 ? 2 : (ws.split == 2 ? 1 : 0);
     h->last_split = ws.split;
+    const char* pt = std::getenv("HVP_PASS_THROUGH");
+    ws.pass = !(pt && pt[0] == '0');
     if (fused) {
         // the refill kernel's workspace descriptors ([0] the level lists, [1] the dive list in
         // place of level N's), uploaded when they change

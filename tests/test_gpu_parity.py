@@ -343,3 +343,30 @@ def test_root_refill_equals_root_kernel(gpu_available, monkeypatch):
     assert s.stats().n_candidates == ca
     for k in a:
         assert torch.equal(a[k], b[k]), k
+
+
+def test_pass_through_nodes_keep_the_answers(gpu_available, monkeypatch):
+    """configs[1] at bench size with and without the pass-through nodes (round 6, hvp_lane.h
+    bnb_put_children kPassFlag; HVP_PASS_THROUGH=0): a child whose region's band holds its parent's
+    whole velocity interval has its parent's QP, so it is not solved again.  Same sequences and
+    statuses, costs and controls to rounding, and at least 5 % fewer QPs (hvp_stats.n_candidates)."""
+    import torch
+
+    import bench
+
+    n, S = 10, 16384
+    params, roles = bench.make_inputs(range(S), n, N)
+    dev = torch.device("cuda", 0)
+    tp, tr = torch.from_numpy(params).to(dev), torch.from_numpy(roles).to(dev)
+    ts = torch.zeros(len(roles), dtype=torch.int32, device=dev)
+    s = _solver([_gear_system()])
+    a = {k: v.cpu().numpy() for k, v in s.solve_device(ts, tr, tp).items()}
+    ca = s.stats().n_candidates
+    monkeypatch.setenv("HVP_PASS_THROUGH", "0")
+    b = {k: v.cpu().numpy() for k, v in s.solve_device(ts, tr, tp).items()}
+    cb = s.stats().n_candidates
+    assert (a["status"] == 0).all() and np.array_equal(a["status"], b["status"])
+    assert np.array_equal(a["region"], b["region"])
+    assert np.all(np.abs(a["cost"] - b["cost"]) <= 1e-12 * np.maximum(1.0, np.abs(b["cost"])))
+    assert np.abs(a["u"] - b["u"]).max() <= 1e-9
+    assert ca <= 0.95 * cb, (ca, cb)
