@@ -1566,7 +1566,7 @@ __global__ __launch_bounds__(kCoopBlock) HVP_COOP_OCC void k_bnb_root_coop(int B
                                                               const int32_t* __restrict__ sys,
                                                               const int32_t* __restrict__ role,
                                                               const double* __restrict__ params, hvp::Consts C,
-                                                              Workspace ws) {
+                                                              Workspace ws, int leaf_list) {
     __shared__ hvp::coop::GroupLds lds[kCoopGroups];
     const int g = threadIdx.x / hvp::coop::G, t = threadIdx.x % hvp::coop::G;
     const int i = blockIdx.x * kCoopGroups + g;
@@ -1610,7 +1610,29 @@ __global__ __launch_bounds__(kCoopBlock) HVP_COOP_OCC void k_bnb_root_coop(int B
             }
             dive_ok = hvp::coop::bcast(dive_ok, 0);
             code = hvp::coop::bcast(code, 0);
-            if (dive_ok) {
+            if (leaf_list) {
+                // the incumbent leaves (the dive's, the hint's) as a list of their own, solved by
+                // k_bnb_leaf_coop: here every group solves exactly one QP, its root
+                if (t == 0) {
+                    uint64_t hc = 0;
+                    const int hok = ws.hint && hint_code<N>(ws, i, S, C, v0, &hc) && (!dive_ok || hc != code) ? 1 : 0;
+                    if (dive_ok + hok) {
+                        const unsigned long long o = atomicAdd(&ws.counter[7], (unsigned long long)(dive_ok + hok));
+                        if (dive_ok) {
+                            ws.nd_inst[1][o] = i;
+                            ws.nd_code[1][o] = code;
+                            ws.nd_lo[1][o] = 0.0;
+                        }
+                        if (hok) {
+                            ws.nd_inst[1][o + dive_ok] = i;
+                            ws.nd_code[1][o + dive_ok] = hc;
+                            // one writer per record: a hint whose slot is the dive's solves without it
+                            ws.nd_lo[1][o + dive_ok] =
+                                dive_ok && ws.nclaim && node_slot(hc, ws.nslots) == node_slot(code, ws.nslots) ? 1.0 : 0.0;
+                        }
+                    }
+                }
+            } else if (dive_ok) {
                 double c1 = 0.0;
                 Rec* w1 = ws.nclaim ? recs + node_index(ws, i, N, code) : nullptr;
                 st = hvp::coop::solve_qp<N, Rec>(L, lds[g], S, C, rl, prm, code, N, kGiMaxIter<N>, it, &c1, nullptr,
@@ -1619,7 +1641,7 @@ __global__ __launch_bounds__(kCoopBlock) HVP_COOP_OCC void k_bnb_root_coop(int B
                 iters += it;
                 if (st == hvp::GI_OK) inc = c1;
             }
-            if (ws.hint) {  // see hint_code (set for the ADMM and decentralised forms only)
+            if (!leaf_list && ws.hint) {  // see hint_code (set for the ADMM and decentralised forms only)
                 unsigned long long hc = 0;
                 int hok = 0;
                 if (t == 0) {
@@ -1654,6 +1676,47 @@ __global__ __launch_bounds__(kCoopBlock) HVP_COOP_OCC void k_bnb_root_coop(int B
         ws.iters[i] = iters;
         atomicAdd(&ws.counter[3], (unsigned long long)nodes);
         atomicAdd(&ws.counter[1], (unsigned long long)iters);
+    }
+}
+
+// The incumbent leaves of k_bnb_root_coop's list (leaf_list): the greedy dive's sequence and the hint's
+// (the previous ADMM iteration's / time step's winner), one QP per 16-lane group, grid-stride over
+// the list.  Run inline after each root (round 5) a group solved one to three QPs while the other
+// three groups of its wave waited for the longest chain (lane utilisation 0.26).  Same
+// QPs, same node records (a leaf owns its depth-N slot; a hint that shares the dive's slot solves
+// cold), same incumbents (atomicMin of the leaves' costs).  The list lives in level 1's node arrays,
+// which k_bnb_expand fills only afterwards; its length is counter[7].
+template <int N>
+__global__ __launch_bounds__(kCoopBlock) HVP_COOP_OCC void k_bnb_leaf_coop(const hvp_system* __restrict__ systems,
+                                                              const int32_t* __restrict__ sys,
+                                                              const int32_t* __restrict__ role,
+                                                              const double* __restrict__ params, hvp::Consts C,
+                                                              Workspace ws) {
+    __shared__ hvp::coop::GroupLds lds[kCoopGroups];
+    const int g = threadIdx.x / hvp::coop::G, t = threadIdx.x % hvp::coop::G;
+    const long long total = (long long)ws.counter[7];
+    using Rec = hvp::coop::WarmRec<N>;
+    for (long long q = (long long)blockIdx.x * kCoopGroups + g; q < total; q += (long long)gridDim.x * kCoopGroups) {
+        const int inst = ws.nd_inst[1][q];
+        const uint64_t code = ws.nd_code[1][q];
+        const hvp_system& S = systems[sys[inst]];
+        const int rl = role[inst];
+        const double* prm = params + (size_t)inst * C.stride;
+        Rec* w = ws.nclaim && ws.nd_lo[1][q] == 0.0 ? reinterpret_cast<Rec*>(ws.nrec) + node_index(ws, inst, N, code)
+                                                   : nullptr;
+        hvp::coop::Lane<N> L;
+        double c = 0.0;
+        int it = 0;
+        const int st = hvp::coop::solve_qp<N, Rec>(L, lds[g], S, C, rl, prm, code, N, kGiMaxIter<N>, it, &c, nullptr, 0.0,
+                                                   -1.0, w, w != nullptr,
+                                                   ((uint64_t)(uint32_t)sys[inst] << 32) | (uint32_t)rl);
+        if (t == 0) {
+            atomicAdd(&ws.nodes[inst], 1);
+            atomicAdd(&ws.iters[inst], it);
+            atomicAdd(&ws.counter[3], 1ull);
+            atomicAdd(&ws.counter[1], (unsigned long long)it);
+            if (st == hvp::GI_OK) atomicMin(&ws.inc[inst], cost_key(c));
+        }
     }
 }
 
@@ -3705,8 +3768,19 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
             hipLaunchKernelGGL((k_l1_root<N, false>), dim3(g_l1), dim3(kL1BlockOf<N>), 0, st, B, h->d_sys, sys, role,
                                params, h->C, ws);
     } else if constexpr (kCoop<N>) {
+        // the roots, then their incumbent leaves as a list (k_bnb_leaf_coop; HVP_COOP_LEAF_LIST=0: each
+        // root's group solves its leaves right after it, A/B); the list needs 2 B slots of level 1
+        const char* ll = std::getenv("HVP_COOP_LEAF_LIST");
+        const int leaf_list = !(ll && ll[0] == '0') && ws.cap >= 2LL * B ? 1 : 0;
         hipLaunchKernelGGL(k_bnb_root_coop<N>, dim3((B + kCoopGroups - 1) / kCoopGroups), dim3(kCoopBlock), 0, st, B,
-                           h->d_sys, sys, role, params, h->C, ws);
+                           h->d_sys, sys, role, params, h->C, ws, leaf_list);
+        if (leaf_list) {
+            HIP_TRY(hipGetLastError());
+            const int g_leaf = (int)std::min<long long>((2LL * B + kCoopGroups - 1) / kCoopGroups,
+                                                        (long long)h->n_cu * 32);
+            hipLaunchKernelGGL(k_bnb_leaf_coop<N>, dim3(g_leaf), dim3(kCoopBlock), 0, st, h->d_sys, sys, role, params,
+                               h->C, ws);
+        }
     } else {
         if (h->C.form == HVP_FORM_ADMM) {
             hipLaunchKernelGGL((k_bnb_root<N, true>), dim3((B + BS - 1) / BS), dim3(BS), lds, st, B, h->d_sys, sys,

@@ -426,6 +426,45 @@ def test_node_records_keep_the_answers(gpu_available, monkeypatch):
 
 
 @pytest.mark.gpu
+def test_coop_leaf_list_keeps_the_answers(gpu_available, monkeypatch):
+    """configs[2] at its own size per platoon (n = 10, N = 10, 20 ADMM iterations, 2 closed-loop
+    steps, y carried), 64 platoons: the incumbent leaves (greedy dive, previous iteration's winner)
+    as a list of their own after the roots (round 6, hvp_lane.h k_bnb_leaf_coop) against each root's
+    group solving them inline (HVP_COOP_LEAF_LIST=0).  Same QPs with the same node records, so the
+    same regions, controls and trajectories to 1e-9 and the same QP counts (to 0.1 %: a hint that
+    shares the dive's record slot now starts cold)."""
+    import torch
+
+    from hvp.admm import AdmmEngine, admm_problem
+
+    n, N, P, iters = 10, 10, 64, 20
+    states = np.stack([O.env_initial_state(n, s).astype(float) for s in range(P)])
+    roles = [O.role_bits(i, n) for i in range(n)] * P
+    lead = np.stack([3000.0 + 20.0 * np.arange(N + 1), np.full(N + 1, 20.0)])
+
+    def run(flag):
+        monkeypatch.setenv("HVP_COOP_LEAF_LIST", flag)
+        eng = AdmmEngine(admm_problem(N, 0.5), [_system()], np.zeros(P * n, np.int32), roles, n, P)
+        eng.set_leader(lead)
+        outs, qps, st = [], [], states
+        for t in range(2):
+            o = eng.step(st, iters, on_solve=lambda s: qps.append(int(s.stats().n_candidates)))
+            torch.cuda.synchronize()
+            outs.append({k: v.cpu().numpy().copy() for k, v in o.items()})
+            st = outs[-1]["x"][:, :, 1].reshape(P, 2 * n)
+        return outs, qps
+
+    inline, q_in = run("0")
+    listed, q_li = run("1")
+    for a, b in zip(listed, inline):
+        assert (a["status"] == 0).all() and np.array_equal(a["region"], b["region"])
+        for k in ("u", "x", "x_front", "x_back"):
+            if k in a:
+                assert np.abs(a[k] - b[k]).max() <= 1e-9, k
+    assert abs(sum(q_li) - sum(q_in)) <= 1e-3 * sum(q_in), (sum(q_li), sum(q_in))
+
+
+@pytest.mark.gpu
 def test_node_records_repeatable_at_scale(gpu_available):
     """Half of C3's bench size (512 platoons of n = 10, N = 10, 20 ADMM iterations, 2 closed-loop
     steps) twice on fresh engines: every iteration's QP count and the final outputs bit-identical.
