@@ -81,8 +81,8 @@ struct Workspace {
     int split = 1;                               // buckets per level list (hvp_lane.h LevelList; > 1
                                                  // per launch for the decentralised lane path)
     int split_shift = 0;                         // log2(split): a bucket's segment is cap >> split_shift
-    int pass = 1;                                // pass-through nodes (hvp_lane.h bnb_put_children;
-                                                 // HVP_PASS_THROUGH=0 turns them off, A/B)
+    int pass = 0;                                // pass-through nodes (hvp_lane.h bnb_put_children;
+                                                 // HVP_PASS_THROUGH=1 turns them on, launch_bnb)
     // naive-ADMM node records (16-lane path, 8 < N <= 12; hvp_lane.h node_index): the final hinge
     // states, active set and factors of every tree node's QP, for the same node in the next solve
     void* nrec = nullptr;                        // [max_batch][N + 1][nslots] hvp::coop::WarmRec<N>

@@ -3675,8 +3675,12 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
     ws.split = fused ? (want >= 4 ? 4 : (want >= 2 ? 2 : 1)) : 1;
     ws.split_shift = ws.split == 4 ? 2 : (ws.split == 2 ? 1 : 0);
     h->last_split = ws.split;
+    // pass-through nodes (bnb_put_children): off by default -- 12 % fewer QPs at C2 but no faster,
+    // in any of three forms (a pass node holding its lane for a generation; finished inside the
+    // claim; compacted out of the level by a pre-pass kernel): profiles/r06n, r06w, r06x.
+    // HVP_PASS_THROUGH=1 turns them on
     const char* pt = std::getenv("HVP_PASS_THROUGH");
-    ws.pass = !(pt && pt[0] == '0');
+    ws.pass = pt && pt[0] == '1';
     if (fused) {
         // the refill kernel's workspace descriptors ([0] the level lists, [1] the dive list in
         // place of level N's), uploaded when they change

@@ -347,9 +347,10 @@ def test_root_refill_equals_root_kernel(gpu_available, monkeypatch):
 
 def test_pass_through_nodes_keep_the_answers(gpu_available, monkeypatch):
     """configs[1] at bench size with and without the pass-through nodes (round 6, hvp_lane.h
-    bnb_put_children kPassFlag; HVP_PASS_THROUGH=0): a child whose region's band holds its parent's
-    whole velocity interval has its parent's QP, so it is not solved again.  Same sequences and
-    statuses, costs and controls to rounding, and at least 5 % fewer QPs (hvp_stats.n_candidates)."""
+    bnb_put_children kPassFlag; HVP_PASS_THROUGH=1, off by default: no faster):
+    a child whose region's band holds its parent's whole velocity interval has its parent's QP, so
+    it is not solved again.  Same sequences and statuses, costs and controls to rounding, and at
+    least 5 % fewer QPs (hvp_stats.n_candidates)."""
     import torch
 
     import bench
@@ -360,6 +361,7 @@ def test_pass_through_nodes_keep_the_answers(gpu_available, monkeypatch):
     tp, tr = torch.from_numpy(params).to(dev), torch.from_numpy(roles).to(dev)
     ts = torch.zeros(len(roles), dtype=torch.int32, device=dev)
     s = _solver([_gear_system()])
+    monkeypatch.setenv("HVP_PASS_THROUGH", "1")
     a = {k: v.cpu().numpy() for k, v in s.solve_device(ts, tr, tp).items()}
     ca = s.stats().n_candidates
     monkeypatch.setenv("HVP_PASS_THROUGH", "0")
