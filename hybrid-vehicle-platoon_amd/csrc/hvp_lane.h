@@ -211,6 +211,25 @@ __device__ inline void lds_rows_sum32(double* red, int lane, int m) {
     if (lane < m) red[lane * 65 + 64] = acc;
 }
 
+// M values in chunks of 32 rows (lds_rows_sum32 for every chunk, whatever M)
+template <int M>
+__device__ inline void wave_sum_lds32(double* v, double* red, int lane) {
+#pragma unroll
+    for (int c0 = 0; c0 < M; c0 += 32) {
+        constexpr int CH = 32;
+#pragma unroll
+        for (int j = 0; j < CH; ++j)
+            if (c0 + j < M) red[j * 65 + lane] = v[c0 + j];
+        lds_wave_sync();
+        lds_rows_sum32(red, lane, M - c0 < CH ? M - c0 : CH);
+        lds_wave_sync();
+#pragma unroll
+        for (int j = 0; j < CH; ++j)
+            if (c0 + j < M) v[c0 + j] = red[j * 65 + 64];
+        lds_wave_sync();
+    }
+}
+
 template <int M>
 __device__ inline void wave_sum_lds(double* v, double* red, int lane) {
     if constexpr (M <= 64) {
@@ -233,34 +252,49 @@ __device__ inline void wave_sum_lds(double* v, double* red, int lane) {
         for (int j = 0; j < M; ++j) v[j] = red[j * 65 + 64];
         lds_wave_sync();  // the buffer is reused by the next reduction
     } else {
-#pragma unroll
-        for (int c0 = 0; c0 < M; c0 += 32) {
-            constexpr int CH = 32;
-#pragma unroll
-            for (int j = 0; j < CH; ++j)
-                if (c0 + j < M) red[j * 65 + lane] = v[c0 + j];
-            lds_wave_sync();
-            lds_rows_sum32(red, lane, M - c0 < CH ? M - c0 : CH);
-            lds_wave_sync();
-#pragma unroll
-            for (int j = 0; j < CH; ++j)
-                if (c0 + j < M) v[c0 + j] = red[j * 65 + 64];
-            lds_wave_sync();
-        }
+        wave_sum_lds32<M>(v, red, lane);
     }
 }
 
+// A lane's row vectors in LDS: component a of slot q at base[(q N + a) 64] (the wave's 64 lanes
+// interleaved, so a wave's read of one component is one conflict-free 512-byte row).  The vectors
+// are constant through an LP's iterations; held in registers they pushed the wave solver to ~2 KB
+// of scratch per lane at N = 10 (spilled state reloaded every iteration).
+struct LdsRow {
+    double* p;
+    __device__ double& operator[](int a) const { return p[a * 64]; }
+};
+template <int N>
+struct LdsRows {
+    double* base;
+    __device__ LdsRow operator[](int q) const { return LdsRow{base + q * N * 64}; }
+};
+}  // namespace hvp_k
+namespace hvp {
+template <int N>
+__device__ inline double l1_dot(const hvp_k::LdsRow& g, const double* y) {  // l1_dot's order
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) s += g[i] * y[i];
+    return s;
+}
+}  // namespace hvp
+namespace hvp_k {
+
 // One LP per wavefront: lane l owns hard rows l, l + 64 (8N - 2 <= 126) and pairs l, l + 64,
-// l + 128 (10N <= 160) in registers.
+// l + 128 (10N <= 160): their scalars in registers, their row vectors in LDS (LdsRows; the wave's
+// area of kL1GSlots x N x 64 doubles after its reduction rows, kL1LdsAll).
 template <int N>
 struct L1Wave {
     static constexpr int NHS = (8 * N - 2 + 63) / 64;  // hard-row slots per lane
     static constexpr int NPS = (10 * N + 63) / 64;     // pair slots per lane
     static constexpr int NT = N * (N + 1) / 2;
     bool hon[NHS];
-    double hg[NHS][N], hh[NHS], hs[NHS], hl[NHS], hds[NHS], hdl[NHS];
+    LdsRows<N> hg;
+    double hh[NHS], hs[NHS], hl[NHS], hds[NHS], hdl[NHS];
     bool pon[NPS];
-    double pg[NPS][N], pe0[NPS], pw[NPS], pal[NPS], pt[NPS], ps1[NPS], ps2[NPS], pl1[NPS], pl2[NPS];
+    LdsRows<N> pg;
+    double pe0[NPS], pw[NPS], pal[NPS], pt[NPS], ps1[NPS], ps2[NPS], pl1[NPS], pl2[NPS];
     double pds1[NPS], pdl1[NPS], pds2[NPS], pdl2[NPS], pdt[NPS];
     bool rel = false;  // primal residuals relative to the row's constant, |rp| / (1 + |h|) (L1AdmmWave)
 
@@ -286,9 +320,11 @@ struct L1Wave {
     }
 
     // the rows of the LP of (prm, code) relaxed after K steps (hvp_l1.h l1_rows) that map to this
-    // lane; false when the constant p_1 row is violated
+    // lane (row vectors into gbuf, the wave's LDS row area); false when the constant p_1 row is violated
     __device__ bool load(const hvp_system& S, const hvp::Consts& C, int rl, const double* prm, uint64_t code, int K,
-                         double rlo, double rhi, int lane, int& mh, int& mp, int xl_blk = 4) {
+                         double rlo, double rhi, int lane, int& mh, int& mp, double* gbuf, int xl_blk = 4) {
+        hg.base = gbuf + lane;
+        pg.base = gbuf + NHS * N * 64 + lane;
         clear();
         return hvp::l1_rows<N>(
             S, C, rl, prm, code, K, rlo, rhi, mh, mp,
@@ -319,15 +355,15 @@ struct L1Wave {
             xl_blk);
     }
 
-    // this lane's share of: residuals (gap, obj, rd_y, max |rp|, max |rd_t|) when res, and the
-    // Newton system (K when withK, rhs for targets rc = s l [+ ds dl - sigmu when corr])
-    __device__ void contrib(const double* y, bool corr, double sigmu, bool withK, double* K, double* rhs, double& gap,
-                            double& obj, double* rdy, double& rpm, double& rdm) const {
+    // this lane's share of: residuals (gap, obj, rd_y, max |rp|, max |rd_t|) and the Newton right-hand
+    // side (targets rc = s l [+ ds dl - sigmu when corr]); the matrix is kpart's
+    __device__ void contrib(const double* y, bool corr, double sigmu, double* rhs, double& gap, double& obj,
+                            double* rdy, double& rpm, double& rdm) const {
 #pragma unroll
         for (int q = 0; q < NHS; ++q) {
             if (!hon[q]) continue;
             const double gy = hvp::l1_dot<N>(hg[q], y);
-            const double rp = gy + hs[q] - hh[q], D = hl[q] / hs[q];
+            const double rp = gy + hs[q] - hh[q];
             const double rc = hs[q] * hl[q] + (corr ? hds[q] * hdl[q] : 0.0) - sigmu;
             const double rho = (hl[q] * rp - rc) / hs[q], coef = -(hl[q] + rho);
             gap += hs[q] * hl[q];
@@ -336,10 +372,6 @@ struct L1Wave {
             for (int a = 0; a < N; ++a) {
                 rdy[a] += hl[q] * hg[q][a];
                 rhs[a] += coef * hg[q][a];
-                if (withK) {
-#pragma unroll
-                    for (int c = 0; c <= a; ++c) K[hvp::tri(a, c)] += D * hg[q][a] * hg[q][c];
-                }
             }
         }
 #pragma unroll
@@ -355,7 +387,6 @@ struct L1Wave {
             const double rdt = pw[q] - pl1[q] - pl2[q];
             const double rhst = -rdt + rho1 + rho2;
             const double mt = D1 + D2, m = al * D2 - D1;
-            const double ce = D1 * D2 * (1.0 + al) * (1.0 + al) / mt;
             const double coef = -(pl1[q] - al * pl2[q]) - (rho1 - al * rho2) - m * rhst / mt;
             gap += ps1[q] * pl1[q] + ps2[q] * pl2[q];
             obj += pw[q] * pt[q];
@@ -365,9 +396,51 @@ struct L1Wave {
             for (int a = 0; a < N; ++a) {
                 rdy[a] += (pl1[q] - al * pl2[q]) * pg[q][a];
                 rhs[a] += coef * pg[q][a];
-                if (withK) {
+            }
+        }
+    }
+
+    // The Newton matrix K = sum_r D_r g_r g_r' is assembled in chunks of its packed triangle
+    // (hvp::tri order): weights() takes contrib's per-row D (hard rows) / ce (pairs) of the current
+    // iterate, kpart<E0, CH> adds this lane's rows to entries [E0, E0 + CH).  With contrib's
+    // expressions and per-entry order, so the matrix is the one a single pass over K built; but only
+    // CH accumulators are live at a time instead of the whole triangle (l1_newton_factor).
+    struct Wts {
+        double dh[NHS], dp[NPS];
+    };
+    __device__ void weights(const double* /*y*/, Wts& w) const {
 #pragma unroll
-                    for (int c = 0; c <= a; ++c) K[hvp::tri(a, c)] += ce * pg[q][a] * pg[q][c];
+        for (int q = 0; q < NHS; ++q) w.dh[q] = hl[q] / hs[q];
+#pragma unroll
+        for (int q = 0; q < NPS; ++q) {
+            const double al = pal[q], D1 = pl1[q] / ps1[q], D2 = pl2[q] / ps2[q];
+            const double mt = D1 + D2;
+            w.dp[q] = D1 * D2 * (1.0 + al) * (1.0 + al) / mt;
+        }
+    }
+    template <int E0, int CH>
+    __device__ void kpart(const Wts& w, double* kc) const {
+#pragma unroll
+        for (int q = 0; q < NHS; ++q) {
+            if (!hon[q]) continue;
+#pragma unroll
+            for (int a = 0; a < N; ++a) {
+#pragma unroll
+                for (int c = 0; c <= a; ++c) {
+                    const int e = hvp::tri(a, c) - E0;
+                    if (e >= 0 && e < CH) kc[e] += w.dh[q] * hg[q][a] * hg[q][c];
+                }
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < NPS; ++q) {
+            if (!pon[q]) continue;
+#pragma unroll
+            for (int a = 0; a < N; ++a) {
+#pragma unroll
+                for (int c = 0; c <= a; ++c) {
+                    const int e = hvp::tri(a, c) - E0;
+                    if (e >= 0 && e < CH) kc[e] += w.dp[q] * pg[q][a] * pg[q][c];
                 }
             }
         }
@@ -422,7 +495,70 @@ struct L1Wave {
 // Returns L1_OK, L1_INFEASIBLE (Farkas certificate of the hard rows over the velocity box
 // [ylo, yhi], hvp_l1.h l1_farkas) or L1_FAIL; y (uniform) holds the iterate.
 template <int N>
-constexpr int kL1Red = 2 + 2 * N + N * (N + 1) / 2;  // gap, obj, rd_y, rhs, K
+constexpr int kL1Res = 2 + 2 * N;  // gap, obj, rd_y, rhs: one LDS all-reduce per iteration
+template <int N>
+constexpr int kL1NT = N * (N + 1) / 2;  // the Newton matrix's packed triangle
+// A wave's LDS buffer: kL1Rows reduction rows of 65 doubles (the residuals and the K chunks in
+// rows of at most 32 values, l1_wave_cert's N + 2), then the K area of kL1NT doubles that holds the
+// assembled matrix and then its factor (the chol_solve calls of an iteration read it from there).
+constexpr int l1_rows_of(int n) {
+    const int nt = n * (n + 1) / 2 < 32 ? n * (n + 1) / 2 : 32, res = 2 + 2 * n < 32 ? 2 + 2 * n : 32;
+    const int r = nt > res ? nt : res;
+    return r > n + 2 ? r : n + 2;
+}
+template <int N>
+constexpr int kL1Rows = l1_rows_of(N);
+template <int N>
+constexpr int kL1KOff = kL1Rows<N> * 65;
+template <int N>
+constexpr int kL1Lds = kL1KOff<N> + kL1NT<N>;
+template <int N>
+constexpr int kL1GSlots = L1Wave<N>::NHS + L1Wave<N>::NPS;
+template <int N, bool ADMM = false>
+constexpr int kL1LdsAll = kL1Lds<N> + (kL1GSlots<N> + (ADMM ? 3 : 0)) * N * 64;  // doubles per wave: + the row vectors
+
+// Newton matrix of the current iterate (R: L1Wave or L1AdmmWave; all lanes call it) into the K
+// area, factored there (cholesky_l1): the lanes' shares of each chunk of 32 entries are summed
+// through the reduction rows (lds_rows_sum32, as wave_sum_lds32 sums them), every lane loads the
+// matrix, factors it redundantly, and lane 0 stores the factor.  Only one chunk of accumulators and
+// then the triangle are live in registers, never both next to the row state (the one-pass form
+// held 2 + 2N + N(N+1)/2 partial sums and spilled ~3 KB per lane at N = 10).
+template <int N, int E0, class R>
+__device__ inline void l1_k_chunks(const R& rows, const typename R::Wts& w, double* red, int lane) {
+    if constexpr (E0 < kL1NT<N>) {
+        constexpr int CH = kL1NT<N> - E0 < 32 ? kL1NT<N> - E0 : 32;
+        double kc[CH];
+#pragma unroll
+        for (int e = 0; e < CH; ++e) kc[e] = 0.0;
+        rows.template kpart<E0, CH>(w, kc);
+#pragma unroll
+        for (int e = 0; e < CH; ++e) red[e * 65 + lane] = kc[e];
+        lds_wave_sync();
+        lds_rows_sum32(red, lane, CH);
+        lds_wave_sync();
+        if (lane < CH) red[kL1KOff<N> + E0 + lane] = red[lane * 65 + 64];
+        lds_wave_sync();
+        l1_k_chunks<N, E0 + 32>(rows, w, red, lane);
+    }
+}
+template <int N, class R>
+__device__ inline const double* l1_newton_factor(const R& rows, const double* y, double* red, int lane) {
+    typename R::Wts w;
+    rows.weights(y, w);
+    l1_k_chunks<N, 0>(rows, w, red, lane);
+    double* KA = red + kL1KOff<N>;
+    double K[kL1NT<N>];
+#pragma unroll
+    for (int i = 0; i < kL1NT<N>; ++i) K[i] = KA[i];
+    hvp::cholesky_l1<N>(K);
+    lds_wave_sync();  // every lane has read the matrix
+    if (lane == 0) {
+#pragma unroll
+        for (int i = 0; i < kL1NT<N>; ++i) KA[i] = K[i];
+    }
+    lds_wave_sync();
+    return KA;
+}
 
 template <int N>
 __device__ int l1_wave_cert(const L1Wave<N>& W, double* red, int lane, double ylo, double yhi) {
@@ -471,16 +607,15 @@ __device__ int l1_wave_solve(L1Wave<N>& W, double* y, double v0, int mh, int mp,
     hsc = wave_max(hsc);
     wmx = wave_max(wmx);
     for (iters = 0; iters < max_iter; ++iters) {
-        // acc = [gap, obj, rd_y (N), rhs (N), K (NT)]: one LDS all-reduce
-        double acc[kL1Red<N>];
+        // acc = [gap, obj, rd_y (N), rhs (N)]: one LDS all-reduce; the matrix after the stop test
+        double acc[kL1Res<N>];
 #pragma unroll
-        for (int i = 0; i < kL1Red<N>; ++i) acc[i] = 0.0;
+        for (int i = 0; i < kL1Res<N>; ++i) acc[i] = 0.0;
         double* rdy = acc + 2;
         double* rhs = acc + 2 + N;
-        double* K = acc + 2 + 2 * N;
         double rpm = 0.0, rdm = 0.0;
-        W.contrib(y, false, 0.0, true, K, rhs, acc[0], acc[1], rdy, rpm, rdm);
-        wave_sum_lds<kL1Red<N>>(acc, red, lane);
+        W.contrib(y, false, 0.0, rhs, acc[0], acc[1], rdy, rpm, rdm);
+        wave_sum_lds32<kL1Res<N>>(acc, red, lane);
         const double gap = acc[0], obj = acc[1];
         rpm = wave_max(rpm);
         rdm = wave_max(rdm);
@@ -488,7 +623,7 @@ __device__ int l1_wave_solve(L1Wave<N>& W, double* y, double v0, int mh, int mp,
         for (int i = 0; i < N; ++i) rdm = fmax(rdm, fabs(rdy[i]));
         if (rpm <= 1e-10 * hsc && rdm <= 1e-10 * wmx && gap <= 1e-12 * fmax(1.0, fabs(obj))) return hvp::L1_OK;
         const double mu = gap / mtot;
-        hvp::cholesky_l1<N>(K);
+        const double* K = l1_newton_factor<N>(W, y, red, lane);  // the factor, in LDS
         double dy[N];
         hvp::chol_solve<N>(K, rhs, dy);
         double ap = 1.0, ad = 1.0;
@@ -516,7 +651,7 @@ __device__ int l1_wave_solve(L1Wave<N>& W, double* y, double v0, int mh, int mp,
 #pragma unroll
             for (int i = 0; i < N; ++i) rhs2[i] = dum[i] = 0.0;
             double g2 = 0.0, o2 = 0.0, r2 = 0.0, d2 = 0.0;
-            W.contrib(y, corr, sm, false, K, rhs2, g2, o2, dum, r2, d2);
+            W.contrib(y, corr, sm, rhs2, g2, o2, dum, r2, d2);
             wave_sum_lds<N>(rhs2, red, lane);
             hvp::chol_solve<N>(K, rhs2, dy);
             ap = 1.0 / 0.995;
@@ -564,7 +699,7 @@ __device__ int l1_node_lp(const hvp_system& S, const hvp::Consts& C, int rl, con
     }
     L1Wave<N> W;
     int mh = 0, mp = 0;
-    W.load(S, C, rl, prm, code, K, rlo, rhi, lane, mh, mp);
+    W.load(S, C, rl, prm, code, K, rlo, rhi, lane, mh, mp, red + kL1Lds<N>);
     const int st = l1_wave_solve<N>(W, y, prm[1], mh, mp, C.max_iter, iters, red, lane, S.vmin, S.vmax);
     cost = COST && st == hvp::L1_OK ? hvp::l1_direct_cost<N>(y, S, C, rl, prm, code, K, rlo, rhi) : 0.0;
     return st;
@@ -592,14 +727,16 @@ struct L1AdmmWave {
     double rho, c[2], q[2], dc[2];  // the group's copies (p, v) and linear terms y - rho z
     double k0;                      // constant of the ADMM terms: y'(c - z) + rho/2 |c - z|^2 = rho/2 c'c + q'c + k0
     bool qon[NQ];
-    double qg[NQ][N], qh[NQ][2], qe0[NQ], qw[NQ], qal[NQ], qt[NQ], qs1[NQ], qs2[NQ], ql1[NQ], ql2[NQ];
+    LdsRows<N> qg;  // the pairs' row vectors in y (LDS, after the own rows' slots)
+    double qh[NQ][2], qe0[NQ], qw[NQ], qal[NQ], qt[NQ], qs1[NQ], qs2[NQ], ql1[NQ], ql2[NQ];
     double qds1[NQ], qdl1[NQ], qds2[NQ], qdl2[NQ], qdt[NQ];
 
     // the own rows (hard rows, leader tracking, inputs: l1_rows with the ADMM params layout) and this
     // lane's copy group; mg = pairs of every group of the wave
     __device__ bool load(const hvp_system& S, const hvp::Consts& C, int rl, const double* prm, uint64_t code, int K,
-                         double rlo, double rhi, int lane, int& mh, int& mp, int& mg) {
-        const bool ok = W.load(S, C, rl & HVP_ROLE_TRACK_LEADER, prm, code, K, rlo, rhi, lane, mh, mp, 8);
+                         double rlo, double rhi, int lane, int& mh, int& mp, int& mg, double* gbuf) {
+        const bool ok = W.load(S, C, rl & HVP_ROLE_TRACK_LEADER, prm, code, K, rlo, rhi, lane, mh, mp, gbuf, 8);
+        qg.base = gbuf + kL1GSlots<N> * N * 64 + lane;
         W.rel = true;
         constexpr int K1 = N + 1;
         const int side = lane / K1, k = lane % K1;
@@ -698,8 +835,8 @@ struct L1AdmmWave {
     }
 
     // the group's copy block A = rho I + sum ce h h' (inverse), A_cy dy (when dy), and rc = -(rho c + q)
-    // + sum coef h; also adds the group's pair terms to K / rhs / residuals when acc
-    __device__ void group_block(const double* y, const double* dy, bool corr, double sigmu, bool withK, double* K,
+    // + sum coef h; also adds the group's pair terms to rhs / residuals when acc (the matrix: kpart)
+    __device__ void group_block(const double* y, const double* dy, bool corr, double sigmu,
                                 double* rhs, double& gap, double& obj, double* rdy, double& rpm, double& rdm, bool acc,
                                 double& i00, double& i01, double& i11, double& rc0, double& rc1, double& ad0,
                                 double& ad1) const {
@@ -740,10 +877,6 @@ struct L1AdmmWave {
                     rhs[a] += P.coef * qg[j][a];
                     acy[0][a] += P.ce * h0 * qg[j][a];
                     acy[1][a] += P.ce * h1 * qg[j][a];
-                    if (withK) {
-#pragma unroll
-                        for (int b = 0; b <= a; ++b) K[hvp::tri(a, b)] += P.ce * qg[j][a] * qg[j][b];
-                    }
                 }
             }
         }
@@ -755,35 +888,86 @@ struct L1AdmmWave {
             rdm = fmax(rdm, fmax(fabs(rd0), fabs(rd1)));
             // the objective itself (the ADMM terms are small near the optimum, c ~ z): the gap test's scale
             obj += 0.5 * rho * (c[0] * c[0] + c[1] * c[1]) + q[0] * c[0] + q[1] * c[1] + k0;
-            // Schur complement of the copy block: K -= A_yc A^-1 A_cy, rhs -= A_yc A^-1 rc
+            // Schur complement of the copy block: rhs -= A_yc A^-1 rc (K -= A_yc A^-1 A_cy: kpart)
             const double w0 = i00 * rc0 + i01 * rc1, w1 = i01 * rc0 + i11 * rc1;
 #pragma unroll
-            for (int a = 0; a < N; ++a) {
-                rhs[a] -= acy[0][a] * w0 + acy[1][a] * w1;
-                if (withK) {
-                    const double u0 = i00 * acy[0][a] + i01 * acy[1][a], u1 = i01 * acy[0][a] + i11 * acy[1][a];
-#pragma unroll
-                    for (int b = 0; b <= a; ++b) K[hvp::tri(a, b)] -= u0 * acy[0][b] + u1 * acy[1][b];
-                }
-            }
+            for (int a = 0; a < N; ++a) rhs[a] -= acy[0][a] * w0 + acy[1][a] * w1;
         }
     }
 
-    __device__ void contrib(const double* y, bool corr, double sigmu, bool withK, double* K, double* rhs, double& gap,
-                            double& obj, double* rdy, double& rpm, double& rdm) const {
-        W.contrib(y, corr, sigmu, withK, K, rhs, gap, obj, rdy, rpm, rdm);
+    __device__ void contrib(const double* y, bool corr, double sigmu, double* rhs, double& gap, double& obj,
+                            double* rdy, double& rpm, double& rdm) const {
+        W.contrib(y, corr, sigmu, rhs, gap, obj, rdy, rpm, rdm);
         if (!gon) return;
         double i00, i01, i11, rc0, rc1, ad0, ad1;
-        group_block(y, nullptr, corr, sigmu, withK, K, rhs, gap, obj, rdy, rpm, rdm, true, i00, i01, i11, rc0, rc1, ad0,
-                    ad1);
+        group_block(y, nullptr, corr, sigmu, rhs, gap, obj, rdy, rpm, rdm, true, i00, i01, i11, rc0, rc1, ad0, ad1);
+    }
+
+    // the Newton matrix in chunks (L1Wave::kpart): the own rows' weights, then per copy group its
+    // pairs' ce and the copy block's inverse and A_cy (group_block's, at the predictor's corr =
+    // false, sigmu = 0), whose Schur complement K -= A_yc A^-1 A_cy follows the pairs' terms
+    struct Wts {
+        typename L1Wave<N>::Wts w;
+        double ce[NQ], i00, i01, i11, acy[2][N];
+    };
+    __device__ void weights(const double* y, Wts& g) const {
+        W.weights(y, g.w);
+        double a00 = rho, a01 = 0.0, a11 = rho;
+#pragma unroll
+        for (int a = 0; a < N; ++a) g.acy[0][a] = g.acy[1][a] = 0.0;
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) {
+            g.ce[j] = 0.0;
+            if (!qon[j]) continue;
+            const PairTerms P = pair_terms(j, hvp::l1_dot<N>(qg[j], y) + hc(j, c), false, 0.0);
+            const double h0 = qh[j][0], h1 = qh[j][1];
+            a00 += P.ce * h0 * h0;
+            a01 += P.ce * h0 * h1;
+            a11 += P.ce * h1 * h1;
+            g.ce[j] = P.ce;
+#pragma unroll
+            for (int a = 0; a < N; ++a) {
+                g.acy[0][a] += P.ce * h0 * qg[j][a];
+                g.acy[1][a] += P.ce * h1 * qg[j][a];
+            }
+        }
+        const double det = a00 * a11 - a01 * a01;
+        g.i00 = a11 / det;
+        g.i01 = -a01 / det;
+        g.i11 = a00 / det;
+    }
+    template <int E0, int CH>
+    __device__ void kpart(const Wts& g, double* kc) const {
+        W.template kpart<E0, CH>(g.w, kc);
+        if (!gon) return;
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) {
+            if (!qon[j]) continue;
+#pragma unroll
+            for (int a = 0; a < N; ++a) {
+#pragma unroll
+                for (int b = 0; b <= a; ++b) {
+                    const int e = hvp::tri(a, b) - E0;
+                    if (e >= 0 && e < CH) kc[e] += g.ce[j] * qg[j][a] * qg[j][b];
+                }
+            }
+        }
+#pragma unroll
+        for (int a = 0; a < N; ++a) {
+            const double u0 = g.i00 * g.acy[0][a] + g.i01 * g.acy[1][a], u1 = g.i01 * g.acy[0][a] + g.i11 * g.acy[1][a];
+#pragma unroll
+            for (int b = 0; b <= a; ++b) {
+                const int e = hvp::tri(a, b) - E0;
+                if (e >= 0 && e < CH) kc[e] -= u0 * g.acy[0][b] + u1 * g.acy[1][b];
+            }
+        }
     }
 
     __device__ void directions(const double* y, const double* dy, bool corr, double sigmu, double& ap, double& ad) {
         W.directions(y, dy, corr, sigmu, ap, ad);
         if (!gon) return;
         double i00, i01, i11, rc0, rc1, ad0, ad1, dum = 0.0;
-        group_block(y, dy, corr, sigmu, false, nullptr, nullptr, dum, dum, nullptr, dum, dum, false, i00, i01, i11, rc0,
-                    rc1, ad0, ad1);
+        group_block(y, dy, corr, sigmu, nullptr, dum, dum, nullptr, dum, dum, false, i00, i01, i11, rc0, rc1, ad0, ad1);
         dc[0] = i00 * (rc0 - ad0) + i01 * (rc1 - ad1);
         dc[1] = i01 * (rc0 - ad0) + i11 * (rc1 - ad1);
         // every pair's terms from the stored (predictor) directions first, then the new directions
@@ -897,15 +1081,14 @@ __device__ int l1_admm_wave_solve(L1AdmmWave<N>& A, double* y, double v0, int mh
     wmx = wave_max(wmx);
     double ybest[N], best_rdm = 1e300;
     for (iters = 0; iters < max_iter; ++iters) {
-        double acc[kL1Red<N>];
+        double acc[kL1Res<N>];
 #pragma unroll
-        for (int i = 0; i < kL1Red<N>; ++i) acc[i] = 0.0;
+        for (int i = 0; i < kL1Res<N>; ++i) acc[i] = 0.0;
         double* rdy = acc + 2;
         double* rhs = acc + 2 + N;
-        double* K = acc + 2 + 2 * N;
         double rpm = 0.0, rdm = 0.0;
-        A.contrib(y, false, 0.0, true, K, rhs, acc[0], acc[1], rdy, rpm, rdm);
-        wave_sum_lds<kL1Red<N>>(acc, red, lane);
+        A.contrib(y, false, 0.0, rhs, acc[0], acc[1], rdy, rpm, rdm);
+        wave_sum_lds32<kL1Res<N>>(acc, red, lane);
         const double gap = acc[0], obj = acc[1];
         rpm = wave_max(rpm);
         rdm = wave_max(rdm);
@@ -925,7 +1108,7 @@ __device__ int l1_admm_wave_solve(L1AdmmWave<N>& A, double* y, double v0, int mh
             for (int i = 0; i < N; ++i) ybest[i] = y[i];
         }
         const double mu = gap / mtot;
-        hvp::cholesky_l1<N>(K);
+        const double* K = l1_newton_factor<N>(A, y, red, lane);  // the factor, in LDS
         double dy[N];
         hvp::chol_solve<N>(K, rhs, dy);
         double ap = 1.0, ad = 1.0;
@@ -956,7 +1139,7 @@ __device__ int l1_admm_wave_solve(L1AdmmWave<N>& A, double* y, double v0, int mh
 #pragma unroll
             for (int i = 0; i < N; ++i) rhs2[i] = dum[i] = 0.0;
             double g2 = 0.0, o2 = 0.0, r2 = 0.0, d2 = 0.0;
-            A.contrib(y, corr, sm, false, K, rhs2, g2, o2, dum, r2, d2);
+            A.contrib(y, corr, sm, rhs2, g2, o2, dum, r2, d2);
             wave_sum_lds<N>(rhs2, red, lane);
             hvp::chol_solve<N>(K, rhs2, dy);
             ap = 1.0 / 0.995;
@@ -1020,7 +1203,7 @@ __device__ int l1_admm_node_lp(const hvp_system& S, const hvp::Consts& C, int rl
     }
     L1AdmmWave<N> A;
     int mh = 0, mp = 0, mg = 0;
-    A.load(S, C, rl, prm, code, K, rlo, rhi, lane, mh, mp, mg);
+    A.load(S, C, rl, prm, code, K, rlo, rhi, lane, mh, mp, mg, red + kL1Lds<N>);
     const int st = l1_admm_wave_solve<N>(A, y, prm[1], mh, mp, mg, C.max_iter, iters, red, lane, S.vmin, S.vmax);
     cost = 0.0;
     if (st == hvp::L1_OK) {
@@ -1041,14 +1224,19 @@ __device__ int l1_admm_node_lp(const hvp_system& S, const hvp::Consts& C, int rl
 
 constexpr int kL1Block = 256;
 template <int N>
-constexpr int kL1BlockOf = N <= HVP_MAX_N_ENUM ? kL1Block : 128;  // LDS: kRedRows x 65 doubles per wave
+constexpr int kL1BlockOf = N <= HVP_MAX_N_ENUM ? kL1Block : 128;  // LDS: kL1LdsAll doubles per wave
+// the naive-ADMM form: one wave per block (one wave per SIMD by registers; its copy groups' row
+// vectors make a wave's LDS ~41 KB at N = 8, ~53 KB at N = 10: three or four blocks of one wave fit a
+// CU where blocks of two or four waves would leave SIMDs idle or not fit at all)
+template <int N, bool ADMM>
+constexpr int kL1BlockOfA = ADMM ? 64 : kL1BlockOf<N>;
 
 template <int N>
 __global__ __launch_bounds__(kL1Block) void k_qp_l1(const hvp_system* __restrict__ systems,
                                                     const int32_t* __restrict__ sys, const int32_t* __restrict__ role,
                                                     const double* __restrict__ params, hvp::Consts C, Workspace ws) {
     static_assert(8 * N - 2 <= 64, "enumeration: one hard row per lane");
-    __shared__ double s_red[kL1Block / 64][kRedRows<kL1Red<N>> * 65];
+    __shared__ double s_red[kL1Block / 64][kL1LdsAll<N>];
     const unsigned long long reserved = ws.counter[0];
     const long long total = (long long)(reserved < (unsigned long long)ws.cap ? reserved : ws.cap);
     const int lane = threadIdx.x & 63;
@@ -1915,12 +2103,12 @@ __device__ inline int l1_any_node_lp(const hvp_system& S, const hvp::Consts& C, 
 }
 
 template <int N, bool ADMM>
-__global__ __launch_bounds__(kL1BlockOf<N>) __attribute__((amdgpu_waves_per_eu(kL1WavesOf<N, ADMM>))) void k_l1_root(int B, const hvp_system* __restrict__ systems,
+__global__ __launch_bounds__((kL1BlockOfA<N, ADMM>)) __attribute__((amdgpu_waves_per_eu(kL1WavesOf<N, ADMM>))) void k_l1_root(int B, const hvp_system* __restrict__ systems,
                                                            const int32_t* __restrict__ sys,
                                                            const int32_t* __restrict__ role,
                                                            const double* __restrict__ params, hvp::Consts C,
                                                            Workspace ws) {
-    __shared__ double s_red[kL1BlockOf<N> / 64][kRedRows<kL1Red<N>> * 65];
+    __shared__ double s_red[kL1BlockOfA<N, ADMM> / 64][kL1LdsAll<N, ADMM>];
     double* red = s_red[threadIdx.x >> 6];
     const int lane = threadIdx.x & 63;
     const long long nwaves = ((long long)gridDim.x * blockDim.x) >> 6;
@@ -1987,12 +2175,12 @@ __global__ __launch_bounds__(kL1BlockOf<N>) __attribute__((amdgpu_waves_per_eu(k
 }
 
 template <int N, bool ADMM>
-__global__ __launch_bounds__(kL1BlockOf<N>) __attribute__((amdgpu_waves_per_eu(kL1WavesOf<N, ADMM>))) void k_l1_bound(int k, const hvp_system* __restrict__ systems,
+__global__ __launch_bounds__((kL1BlockOfA<N, ADMM>)) __attribute__((amdgpu_waves_per_eu(kL1WavesOf<N, ADMM>))) void k_l1_bound(int k, const hvp_system* __restrict__ systems,
                                                             const int32_t* __restrict__ sys,
                                                             const int32_t* __restrict__ role,
                                                             const double* __restrict__ params, hvp::Consts C,
                                                             Workspace ws) {
-    __shared__ double s_red[kL1BlockOf<N> / 64][kRedRows<kL1Red<N>> * 65];
+    __shared__ double s_red[kL1BlockOfA<N, ADMM> / 64][kL1LdsAll<N, ADMM>];
     double* red = s_red[threadIdx.x >> 6];
     const int lane = threadIdx.x & 63;
     const int dst = k & 1;
@@ -2040,13 +2228,13 @@ __global__ __launch_bounds__(kL1BlockOf<N>) __attribute__((amdgpu_waves_per_eu(k
 // leaf, the same iterate) and the lanes that own the copy groups write them.  After k_bnb_finish
 // (which zeroes the copies of instances without an optimal answer).
 template <int N>
-__global__ __launch_bounds__(kL1BlockOf<N>) __attribute__((amdgpu_waves_per_eu(1))) void k_l1_admm_write(int B, const hvp_system* __restrict__ systems,
+__global__ __launch_bounds__((kL1BlockOfA<N, true>)) __attribute__((amdgpu_waves_per_eu(1))) void k_l1_admm_write(int B, const hvp_system* __restrict__ systems,
                                                                  const int32_t* __restrict__ sys,
                                                                  const int32_t* __restrict__ role,
                                                                  const double* __restrict__ params, hvp::Consts C,
                                                                  Workspace ws, double* __restrict__ xf_out,
                                                                  double* __restrict__ xb_out) {
-    __shared__ double s_red[kL1BlockOf<N> / 64][kRedRows<kL1Red<N>> * 65];
+    __shared__ double s_red[kL1BlockOfA<N, true> / 64][kL1LdsAll<N, true>];
     double* red = s_red[threadIdx.x >> 6];
     const int lane = threadIdx.x & 63;
     const long long nwaves = ((long long)gridDim.x * blockDim.x) >> 6;
@@ -3766,7 +3954,7 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
         }
     } else if (h->C.l1) {
         if (l1_admm)
-            hipLaunchKernelGGL((k_l1_root<N, true>), dim3(g_l1), dim3(kL1BlockOf<N>), 0, st, B, h->d_sys, sys, role, params,
+            hipLaunchKernelGGL((k_l1_root<N, true>), dim3(g_l1 * kL1BlockOf<N> / kL1BlockOfA<N, true>), dim3(kL1BlockOfA<N, true>), 0, st, B, h->d_sys, sys, role, params,
                                h->C, ws);
         else
             hipLaunchKernelGGL((k_l1_root<N, false>), dim3(g_l1), dim3(kL1BlockOf<N>), 0, st, B, h->d_sys, sys, role,
@@ -3842,7 +4030,7 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
             }
         } else if (h->C.l1) {
             if (l1_admm)
-                hipLaunchKernelGGL((k_l1_bound<N, true>), dim3(g_l1), dim3(kL1BlockOf<N>), 0, st, k, h->d_sys, sys, role,
+                hipLaunchKernelGGL((k_l1_bound<N, true>), dim3(g_l1 * kL1BlockOf<N> / kL1BlockOfA<N, true>), dim3(kL1BlockOfA<N, true>), 0, st, k, h->d_sys, sys, role,
                                    params, h->C, ws);
             else
                 hipLaunchKernelGGL((k_l1_bound<N, false>), dim3(g_l1), dim3(kL1BlockOf<N>), 0, st, k, h->d_sys, sys, role,
@@ -3895,8 +4083,9 @@ int launch_bnb(hvp_handle* h, int B, const int32_t* sys, const int32_t* role, co
                        xb_out);
     HIP_TRY(hipGetLastError());
     if (l1_admm && (xf_out || xb_out)) {
-        hipLaunchKernelGGL(k_l1_admm_write<N>, dim3(std::max(1, std::min((B + 1) / 2, h->n_cu * 4))),
-                           dim3(kL1BlockOf<N>), 0, st, B, h->d_sys, sys, role, params, h->C, ws, xf_out, xb_out);
+        constexpr int wpb = kL1BlockOfA<N, true> / 64;  // waves per block, one instance per wave
+        hipLaunchKernelGGL(k_l1_admm_write<N>, dim3(std::max(1, std::min((B + wpb - 1) / wpb, h->n_cu * 8 / wpb))),
+                           dim3(kL1BlockOfA<N, true>), 0, st, B, h->d_sys, sys, role, params, h->C, ws, xf_out, xb_out);
         HIP_TRY(hipGetLastError());
     }
     HIP_TRY(hipEventRecord(h->ev1, st));
