@@ -17,6 +17,8 @@ for w in "${W[@]}"; do
     admm_n10_N10_P512) bash profiles/run_profiles.sh "$O/$w" --controller admm --n 10 --N 10 --platoons 512 --steps 1 --warmup 1 --no-cpu --streams 1 ;;
     gadmm_n20_N10_P2048) bash profiles/run_profiles.sh "$O/$w" --controller gadmm --n 20 --N 10 --platoons 2048 --steps 1 --warmup 0 --no-cpu --streams 1 ;;
     cent_n10_N5_P4096) bash profiles/run_profiles.sh "$O/$w" --controller cent --n 10 --N 5 --platoons 4096 --steps 1 --warmup 0 --no-cpu --streams 1 ;;
+    # naive-ADMM min_1_norm (the wave interior point): the bench line's 64 platoons on 2 engines
+    admm_n10_N10_l1_P32) bash profiles/run_profiles.sh "$O/$w" --controller admm --cost l1 --n 10 --N 10 --platoons 32 --steps 1 --warmup 0 --no-cpu --streams 1 ;;
     *) echo "unknown workload $w"; exit 2 ;;
   esac
 done
