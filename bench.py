@@ -479,6 +479,8 @@ def bench_admm(args, world: int, rank: int, local: int, dist) -> None:
     if rank == 0 and not args.no_cpu and args.cpu_budget > 0 and world == 1 and quadratic:
         result["cpu_baseline"] = cpu_baseline_admm(n, N, iters, min(args.cpu_budget, 20.0), cpu_threads())
         result["cpu_baseline_1core"] = cpu_baseline_admm(n, N, iters, min(args.cpu_budget, 20.0) * 0.5, 1)
+    elif rank == 0 and not args.no_cpu and args.cpu_budget > 0 and world == 1:
+        result["cpu_baseline"] = cpu_baseline_admm_l1(n, N, iters, min(args.cpu_budget, 20.0), cpu_threads())
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist:
@@ -529,6 +531,44 @@ def cpu_baseline_admm(n: int, N: int, iters: int, budget_s: float, threads: int 
     return {"value": sum(r[0] / r[1] for r in res), "unit": "platoon-timesteps/s", "cores": threads, "kind": "port",
             "sample": f"{done} platoon steps x {iters} ADMM iterations x {n} local MIQPs (N={N}), oracle, "
                       f"{max(r[1] for r in res):.1f} s on {threads} core(s)"}
+
+
+def _admm_l1_worker(n: int, N: int, budget_s: float, seed0: int):
+    """Local min_1_norm MILPs of the first ADMM iteration (the oracle coordinator's own parameter rows:
+    warm-start blocks of a fresh coordinator, vehicles in order, platoon after platoon), one at a time
+    until the budget is spent (at least one)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    sysd = O.gear_pwa_system(800.0)
+    lead = np.stack([3000.0 + 20.0 * np.arange(N + 1), np.full(N + 1, 20.0)])
+    done, seed, t0 = 0, seed0, time.perf_counter()
+    while done == 0 or time.perf_counter() - t0 < budget_s:
+        c = O.AdmmCoordinator(sysd, O.Cfg(), N, n, quadratic=False)
+        c.set_leader_x(lead)
+        x = O.env_initial_state(n, seed).astype(float).reshape(n, 2)
+        for i in range(n):
+            b = c.blocks[i]
+            p = O.admm_params(x[i], b["yf"], b["zf"], b["yb"], b["zb"], b["xl"])
+            O.solve_admm_miqp(sysd, O.Cfg(), N, c.roles[i], c.rho, p, 200, False)
+            done += 1
+            if time.perf_counter() - t0 >= budget_s:
+                break
+        seed += 1
+    return done, time.perf_counter() - t0
+
+
+def cpu_baseline_admm_l1(n: int, N: int, iters: int, budget_s: float, threads: int = 1):
+    """naive-ADMM min_1_norm on the oracle: a platoon step is iters x n local MILPs (~20 s each at
+    N = 10 on one core, so a whole step is far beyond a bounded sample); the sample times first-iteration
+    local MILPs and scales their rate by 1 / (iters n)."""
+    res = run_cpu_workers(_admm_l1_worker, (n, N), threads, budget_s, 40_000_000)
+    done = sum(r[0] for r in res)
+    rate = sum(r[0] / r[1] for r in res)
+    return {"value": rate / (iters * n), "unit": "platoon-timesteps/s", "cores": threads, "kind": "port",
+            "sample": f"{done} local min_1_norm MILPs (N={N}) of the first ADMM iteration, oracle, "
+                      f"{max(r[1] for r in res):.1f} s on {threads} core(s); rate / ({iters} iterations x {n} "
+                      f"vehicles) per platoon step"}
 
 
 def gadmm_qp_bytes(N: int) -> int:
