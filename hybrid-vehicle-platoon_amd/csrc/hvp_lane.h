@@ -1188,6 +1188,13 @@ __device__ int l1_admm_wave_solve(L1AdmmWave<N>& A, double* y, double v0, int mh
     return l1_wave_cert<N>(W, red, lane, ylo, yhi);
 }
 
+// The naive-ADMM form's LDS buffer (reduction rows, K area, row vectors) as a module-scope variable:
+// its kernels run one wave per block (kL1BlockOfA), and the node LP below is an outlined function of
+// three kernels; reached through this variable its LDS accesses stay ds_* instructions (through the
+// kernels' pointer argument the callee saw a generic pointer: flat instructions).
+template <int N>
+__shared__ double g_l1_admm_lds[kL1LdsAll<N, true>];
+
 // one (node) LP of the naive-ADMM min_1_norm form, as l1_node_lp; xf_o / xb_o (optional, the
 // instance's (2, N+1) rows): the optimal copies, written by the lanes that own them
 template <int N>
@@ -1201,6 +1208,7 @@ __device__ int l1_admm_node_lp(const hvp_system& S, const hvp::Consts& C, int rl
         for (int i = 0; i < N; ++i) y[i] = prm[1];
         return hvp::L1_INFEASIBLE;
     }
+    red = g_l1_admm_lds<N>;  // the caller's buffer (one wave per block), with its address space
     L1AdmmWave<N> A;
     int mh = 0, mp = 0, mg = 0;
     A.load(S, C, rl, prm, code, K, rlo, rhi, lane, mh, mp, mg, red + kL1Lds<N>);
@@ -2108,8 +2116,8 @@ __global__ __launch_bounds__((kL1BlockOfA<N, ADMM>)) __attribute__((amdgpu_waves
                                                            const int32_t* __restrict__ role,
                                                            const double* __restrict__ params, hvp::Consts C,
                                                            Workspace ws) {
-    __shared__ double s_red[kL1BlockOfA<N, ADMM> / 64][kL1LdsAll<N, ADMM>];
-    double* red = s_red[threadIdx.x >> 6];
+    __shared__ double s_red[kL1BlockOfA<N, ADMM> / 64][ADMM ? 1 : kL1LdsAll<N, ADMM>];
+    double* red = ADMM ? g_l1_admm_lds<N> : s_red[threadIdx.x >> 6];
     const int lane = threadIdx.x & 63;
     const long long nwaves = ((long long)gridDim.x * blockDim.x) >> 6;
     if (blockIdx.x == 0 && threadIdx.x == 0) ws.lvl[0] = (unsigned long long)B;
@@ -2180,8 +2188,8 @@ __global__ __launch_bounds__((kL1BlockOfA<N, ADMM>)) __attribute__((amdgpu_waves
                                                             const int32_t* __restrict__ role,
                                                             const double* __restrict__ params, hvp::Consts C,
                                                             Workspace ws) {
-    __shared__ double s_red[kL1BlockOfA<N, ADMM> / 64][kL1LdsAll<N, ADMM>];
-    double* red = s_red[threadIdx.x >> 6];
+    __shared__ double s_red[kL1BlockOfA<N, ADMM> / 64][ADMM ? 1 : kL1LdsAll<N, ADMM>];
+    double* red = ADMM ? g_l1_admm_lds<N> : s_red[threadIdx.x >> 6];
     const int lane = threadIdx.x & 63;
     const int dst = k & 1;
     const unsigned long long nn = ws.lvl[k];
@@ -2234,8 +2242,7 @@ __global__ __launch_bounds__((kL1BlockOfA<N, true>)) __attribute__((amdgpu_waves
                                                                  const double* __restrict__ params, hvp::Consts C,
                                                                  Workspace ws, double* __restrict__ xf_out,
                                                                  double* __restrict__ xb_out) {
-    __shared__ double s_red[kL1BlockOfA<N, true> / 64][kL1LdsAll<N, true>];
-    double* red = s_red[threadIdx.x >> 6];
+    double* red = g_l1_admm_lds<N>;  // one wave per block
     const int lane = threadIdx.x & 63;
     const long long nwaves = ((long long)gridDim.x * blockDim.x) >> 6;
     for (long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6; i < B; i += nwaves) {
